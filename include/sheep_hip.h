@@ -1,0 +1,185 @@
+/*
+ * sheep_hip.h — C ABI of libsheep_hip.so, the MI355X (gfx950) implementation of Sheep's
+ * map/reduce partitioning path:
+ *
+ *   degree sequence -> relabel -> per-shard elimination tree (map) -> tree merge
+ *   (reduce) -> partition_tree downward assignment + ECV(down)/balance evaluator.
+ *
+ * Plain pointers and sizes only.  "_dev" pointers are device (HBM) pointers on the
+ * context's device; every call is asynchronous on the context's stream unless it
+ * returns a host-side value (documented per call), in which case it synchronises.
+ *
+ * Every entry point returns SHEEP_OK (0) or a negative status; sheep_last_error()
+ * returns the message of the calling thread's last failure.  The reference throws
+ * (std::bad_alloc / std::out_of_range) or asserts in the corresponding places; the
+ * façade in sheep_amd/include/sheep/sheep.hpp maps these codes back to the same
+ * behaviour.
+ *
+ * Reference interfaces replaced (chan150/sheep, file:line):
+ *   sheep_degree_count            sequence.h:65-78  (mpiSequence local degrees; LLAMA
+ *                                 out_degree, graph_wrapper.h:87-89) and
+ *                                 sequence.h:95-107 (fileSequence degree loop)
+ *   sheep_sequence_from_degrees   sequence.h:80-92 / :109-121 (compact + (deg,vid) sort)
+ *   sheep_positions               jtree.h:113,142-143 (vid -> jnid index)
+ *   sheep_build_tree              jtree.h:111-122 + jtree.cpp:66-145 (JTree map step)
+ *   sheep_merge_trees             jnode.cpp:174-201 (JNodeTable::merge) and the
+ *                                 per-hop op of mpi_merge, jnode.cpp:203-250
+ *   sheep_kids_create/_destroy    jnode.h:190-204 (makeKids; the persistent kid table)
+ *   sheep_partition               partition.cpp:50-67 + :86-157 (Partition ctor,
+ *                                 forwardPartition) and partition.h:135-143 (print counts)
+ *   sheep_evaluate                partition.cpp:428-473 + :475-521 (both evaluators)
+ *   sheep_facts                   jnode.cpp:256-290 (JNodeTable::Facts)
+ *   sheep_rmat_generate           (new) synthetic Graph500-style RMAT .dat records
+ */
+#ifndef SHEEP_HIP_H
+#define SHEEP_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SHEEP_OK 0
+#define SHEEP_ERR_ARG (-1)     /* bad argument (null pointer, size mismatch)          */
+#define SHEEP_ERR_HIP (-2)     /* HIP runtime error (no device, launch failure, ...)  */
+#define SHEEP_ERR_RANGE (-3)   /* reference would throw std::out_of_range (.at())    */
+#define SHEEP_ERR_PACK (-4)    /* forwardPartition would never terminate             */
+#define SHEEP_ERR_ALLOC (-5)   /* device allocation failed (reference: bad_alloc)     */
+
+#define SHEEP_INVALID_ID 0xFFFFFFFFu /* INVALID_VID / INVALID_JNID, defs.h:82 jnode.h:43 */
+#define SHEEP_INVALID_PART ((int16_t)-1) /* INVALID_PART, partition.h:44 */
+
+/* .dat record, 12 bytes: struct xs1 (readerwriter.h:36-40). */
+typedef struct {
+  uint32_t tail;
+  uint32_t head;
+  float weight;
+} sheep_xs1;
+
+/* One tree node, 8 bytes: JNodeTable::JNode (jnode.h:56-69); .tre = u32 end_id + these. */
+typedef struct {
+  uint32_t parent;
+  uint32_t pst_weight;
+} sheep_jnode;
+
+/* Degree-count semantics. */
+enum {
+  SHEEP_DEGREE_LLAMA = 0,    /* LLAMA out_degree: self-loop counted once            */
+  SHEEP_DEGREE_FILE_DAT = 1, /* fileSequence over XS1: +1 per endpoint, self-loop +2,
+                                last record counted twice (readerwriter.h:138-146)  */
+  SHEEP_DEGREE_FILE_NET = 2  /* fileSequence over SNAP text: +1 per endpoint         */
+};
+
+typedef struct sheep_ctx sheep_ctx;
+typedef struct sheep_kids sheep_kids;
+
+typedef struct {
+  int32_t created;          /* max part + 1 ("Actually created %d partitions.")     */
+  uint64_t first_size;      /* count of part 0 over the vid-indexed vector          */
+  uint64_t second_size;     /* count of part 1                                      */
+  uint64_t max_component;   /* (size_t)((total / k) * balance)                      */
+  uint64_t total_weight;
+  uint64_t packing_nodes;   /* nodes where first-fit-decreasing packing ran         */
+  uint64_t heavy_nodes;     /* |{v : subtree weight > max_component}|               */
+} sheep_partition_info;
+
+typedef struct {
+  uint64_t edges_cut, vcom_vol, max_vertex_bal, ecv_hash, max_hash_bal;
+  uint64_t ecv_down, max_down_bal, ecv_up, max_up_bal;
+  uint64_t edges;  /* getEdges() = adjacency entries / 2 (graph_wrapper.h:79-81) */
+  uint64_t nodes;  /* getNodes() = slots with degree != 0                       */
+} sheep_eval;
+
+typedef struct {
+  uint64_t width, root_cnt, vert_height, edge_height, vert_cnt, edge_cnt, halo_id, core_id, fill;
+} sheep_facts_t;
+
+/* ---- context ------------------------------------------------------------------- */
+const char *sheep_last_error(void);
+/* hip_stream may be NULL (the context creates its own stream). */
+int sheep_ctx_create(int device, void *hip_stream, sheep_ctx **out);
+int sheep_ctx_destroy(sheep_ctx *ctx);
+int sheep_ctx_sync(sheep_ctx *ctx);
+void *sheep_ctx_stream(sheep_ctx *ctx);
+int sheep_malloc(sheep_ctx *ctx, size_t bytes, void **dev_out);
+int sheep_free(sheep_ctx *ctx, void *dev);
+int sheep_memcpy_h2d(sheep_ctx *ctx, void *dst_dev, const void *src_host, size_t bytes);
+int sheep_memcpy_d2h(sheep_ctx *ctx, void *dst_host, const void *src_dev, size_t bytes);
+/* Device-side timing of the last instrumented kernel class:
+ * name = "relabel" | "degree" | ...; returns accumulated ms and launch count since reset. */
+int sheep_timer_enable(sheep_ctx *ctx, int on);
+int sheep_timer_get(sheep_ctx *ctx, const char *name, double *ms, uint64_t *launches);
+int sheep_timer_reset(sheep_ctx *ctx);
+
+/* ---- degree sequence --------------------------------------------------------------
+ * Adds this shard's degrees into deg_dev[0, deg_cap) (caller zeroes it once; shards
+ * accumulate, or are summed with an all-reduce).  *max_slot_out (host, synchronises)
+ * = 1 + max vid seen (LLAMA max_nodes()).  Fails with SHEEP_ERR_RANGE if a vid >= deg_cap. */
+int sheep_degree_count(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec, int mode,
+                       uint32_t *deg_dev, uint64_t deg_cap, uint64_t *max_slot_out);
+
+/* seq_dev[0,n) = slots with deg != 0 sorted by (degree, vid); pos_dev[0, vs) = jnid of
+ * each slot or SHEEP_INVALID_ID.  *n_out (host, synchronises). */
+int sheep_sequence_from_degrees(sheep_ctx *ctx, const uint32_t *deg_dev, uint64_t vs,
+                                uint32_t *seq_dev, uint32_t *pos_dev, uint64_t *n_out);
+
+/* pos_dev[0, pos_size) from an arbitrary sequence (readSequence path); pos_size must be
+ * max(seq)+1.  Duplicate vids: SHEEP_ERR_ARG (the reference asserts, jtree.h:166). */
+int sheep_positions(sheep_ctx *ctx, const uint32_t *seq_dev, uint64_t n, uint32_t *pos_dev,
+                    uint64_t pos_size);
+
+/* ---- map: per-shard elimination tree ---------------------------------------------
+ * tree_dev[0,n): Liu's elimination tree of this shard's records under the order pos
+ * (parent INVALID = root) and pst_weight = #later neighbours.  Records whose endpoint
+ * is >= pos_size while the other endpoint is sequenced -> SHEEP_ERR_RANGE
+ * (jtree.cpp:75 index.at). */
+int sheep_build_tree(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec,
+                     const uint32_t *pos_dev, uint64_t pos_size, uint64_t n,
+                     sheep_jnode *tree_dev);
+
+/* ---- reduce: merge two trees over the same n ------------------------------------ */
+int sheep_merge_trees(sheep_ctx *ctx, const sheep_jnode *a_dev, const sheep_jnode *b_dev,
+                      uint64_t n, sheep_jnode *out_dev);
+
+/* ---- partition ------------------------------------------------------------------ */
+int sheep_kids_create(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n,
+                      sheep_kids **out);
+int sheep_kids_destroy(sheep_kids *kids);
+/* parts_vid_dev[0, pos_size) (pos_size = max(seq)+1) receives the vid-indexed parts
+ * (SHEEP_INVALID_PART for unsequenced slots).  info is host (synchronises). */
+int sheep_partition(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n,
+                    const uint32_t *seq_dev, uint64_t pos_size, sheep_kids *kids, int16_t k,
+                    double balance, int vtx_weight, int pst_weight, int16_t *parts_vid_dev,
+                    sheep_partition_info *info);
+
+/* ---- evaluators: both partition.cpp evaluators over one graph (all records) -------
+ * what: bitmask SHEEP_EVAL_GRAPH (edges cut, Vcom vol, vertex balance, ECV(hash) +
+ * balance), SHEEP_EVAL_DOWN (ECV(down) + balance), SHEEP_EVAL_UP; 0 = all.
+ * Ratios are printed by the caller from these counts and getEdges()/getNodes(). */
+#define SHEEP_EVAL_GRAPH 1
+#define SHEEP_EVAL_DOWN 2
+#define SHEEP_EVAL_UP 4
+int sheep_evaluate(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec,
+                   const uint32_t *pos_dev, uint64_t pos_size, const int16_t *parts_vid_dev,
+                   int what, sheep_eval *out);
+
+/* ---- tree facts (TREEFAQS) -------------------------------------------------------- */
+int sheep_facts(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n, sheep_facts_t *out);
+
+/* ---- synthetic input ---------------------------------------------------------------
+ * Graph500-parameter RMAT (A,B,C,D = .57,.19,.19,.05, no per-level noise), vertex
+ * labels permuted by a seeded Feistel bijection, self-loops and duplicate pairs
+ * removed, orientation tail > head, records sorted by (tail, head), weight 1.0f.
+ * out_dev needs capacity (ef << scale) records; *nrec_out (host) = records kept.
+ * sheep_rmat_generate_host is the identical generator on the CPU (for .dat files). */
+int sheep_rmat_generate(sheep_ctx *ctx, int scale, int edgefactor, uint64_t seed,
+                        sheep_xs1 *out_dev, uint64_t cap, uint64_t *nrec_out);
+int sheep_rmat_generate_host(int scale, int edgefactor, uint64_t seed, sheep_xs1 *out_host,
+                             uint64_t cap, uint64_t *nrec_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHEEP_HIP_H */

@@ -1,0 +1,149 @@
+// =====================================================================================
+//  ref_harness.cpp — drives the REFERENCE's own lib/ code (compiled from
+//  /root/reference/lib where it lies; nothing is copied) to produce golden fixtures.
+//
+//  TEST INFRASTRUCTURE ONLY (oracle/).  Built by oracle/ref/Makefile into oracle/_ref/.
+//
+//  What is reference code here: JTree (jtree.h/.cpp), JNodeTable incl. merge, Facts,
+//  save/load (jnode.h/.cpp), FastUnionFind (unionfind.h), Partition incl.
+//  forwardPartition, evaluate(graph), evaluate(graph, seq), print,
+//  writePartitionedGraph (partition.h/.cpp), degreeSequence / fileSequence /
+//  readSequence / writeSequence (sequence.h), XS1Reader / SNAPReader (readerwriter.h).
+//
+//  What is ours: HarnessGraph, an implementation of the reference's GraphType template
+//  concept (getMaxVid/getNodes/getEdges/isNode/getDeg/getNodeItr/getEdgeItr — the
+//  concept LLAMAGraph and SNAPGraph implement, graph_wrapper.h:71-162).  LLAMA itself
+//  is un-vendored (README:3-8); we do NOT provide a llama.h.  `#undef USE_LLAMA` after
+//  defs.h keeps graph_wrapper.h from naming it, exactly as a USE_SNAP build would.
+//  HarnessGraph restates LLAMA's load semantics (undirected doubling, self-loop stored
+//  once, degree-0 slots not nodes) — see DESIGN.md §Oracle for what is pinned.
+// =====================================================================================
+#include <cstdint>
+#include <cstring>
+#include "defs.h"
+#undef USE_LLAMA
+#include "jtree.h"
+#include "partition.h"
+#include "sequence.h"
+
+#include <cstdio>
+#include <fstream>
+#include <string>
+#include <vector>
+
+class HarnessGraph {
+  std::vector<uint64_t> off;
+  std::vector<vid_t> adj;
+  vid_t max_nodes = 0;
+  size_t num_nodes = 0;
+
+ public:
+  HarnessGraph(char const *filename, size_t part = 0, size_t num_parts = 0) {
+    std::vector<vid_t> t, h;
+    vid_t X, Y;
+    if (strcmp(".dat", filename + strlen(filename) - 4) == 0) {
+      std::ifstream s(filename, std::ios::binary);
+      xs1 rec;
+      while (s.read((char *)&rec, sizeof rec)) { t.push_back(rec.tail); h.push_back(rec.head); }
+    } else {
+      std::ifstream s(filename);
+      while ((s >> X) && (s >> Y)) { t.push_back(X); h.push_back(Y); }
+    }
+    size_t R = t.size(), beg = 0, end = R;
+    if (num_parts != 0) { beg = (part - 1) * R / num_parts; end = part * R / num_parts; }
+    for (size_t i = beg; i < end; ++i) max_nodes = std::max(max_nodes, std::max(t[i], h[i]) + 1);
+    off.assign((size_t)max_nodes + 2, 0);
+    for (size_t i = beg; i < end; ++i) { off[t[i] + 1]++; if (t[i] != h[i]) off[h[i] + 1]++; }
+    for (size_t v = 0; v <= max_nodes; ++v) off[v + 1] += off[v];
+    adj.resize(off[max_nodes]);
+    std::vector<uint64_t> cur(off.begin(), off.end() - 1);
+    for (size_t i = beg; i < end; ++i) {
+      adj[cur[t[i]]++] = h[i];
+      if (t[i] != h[i]) adj[cur[h[i]]++] = t[i];
+    }
+    for (vid_t v = 0; v < max_nodes; ++v) if (getDeg(v) != 0) ++num_nodes;
+  }
+  vid_t getMaxVid() const { return max_nodes; }
+  size_t getNodes() const { return num_nodes; }
+  size_t getEdges() const { return adj.size() / 2; }
+  bool isNode(vid_t X) const { return X < max_nodes && getDeg(X) != 0; }
+  size_t getDeg(vid_t X) const { return X < max_nodes ? off[X + 1] - off[X] : 0; }
+
+  class NodeItr {
+    HarnessGraph const *g; vid_t n;
+   public:
+    NodeItr(HarnessGraph const *gr) : g(gr), n(0) { while (n != g->max_nodes && g->getDeg(n) == 0) ++n; }
+    vid_t operator*() const { return n; }
+    vid_t operator++() { do { ++n; } while (n != g->max_nodes && g->getDeg(n) == 0); return n; }
+    bool isEnd() const { return n == g->max_nodes; }
+  };
+  class EdgeItr {
+    HarnessGraph const *g; uint64_t e, end;
+   public:
+    EdgeItr(HarnessGraph const *gr, vid_t X) : g(gr), e(gr->off[X]), end(gr->off[X + 1]) {}
+    vid_t operator*() const { return g->adj[e]; }
+    vid_t operator++() { ++e; return e < end ? g->adj[e] : INVALID_VID; }
+    bool isEnd() const { return e == end; }
+  };
+  NodeItr getNodeItr() const { return NodeItr(this); }
+  EdgeItr getEdgeItr(vid_t X) const { return EdgeItr(this, X); }
+};
+
+static void dump_parts(Partition const &p, char const *path) {
+  std::ofstream o(path, std::ios::binary | std::ios::trunc);
+  o.write((char const *)p.parts.data(), p.parts.size() * sizeof(part_t));
+}
+
+static int usage() {
+  fprintf(stderr,
+          "ref_harness seq G OUT_SEQ                      degreeSequence (LLAMA degrees)\n"
+          "ref_harness tree G SEQ|- OUT_TRE [p/k]         JTree (+ partial load), TREEFAQS\n"
+          "ref_harness part G SEQ|- TREE PARTS_PREFIX k.. partition_tree -f -g flow + parts dumps\n"
+          "ref_harness write G SEQ|- TREE k PREFIX        Partition + graph-based writePartitionedGraph\n");
+  return 1;
+}
+
+int main(int argc, char **argv) {
+  if (argc < 2) return usage();
+  std::string cmd = argv[1];
+  if (cmd == "seq" && argc == 4) {
+    HarnessGraph g(argv[2]);
+    writeSequence(degreeSequence(g), argv[3]);
+    return 0;
+  }
+  if (cmd == "tree" && (argc == 5 || argc == 6)) {
+    size_t part = 0, num_parts = 0;
+    if (argc == 6) sscanf(argv[5], "%zu/%zu", &part, &num_parts);
+    HarnessGraph g(argv[2], part, num_parts);
+    std::vector<vid_t> seq = strcmp(argv[3], "-") == 0 ? degreeSequence(g) : readSequence(argv[3]);
+    JTree tree(g, seq);
+    tree.jnodes.save(argv[4]);
+    tree.jnodes.getFacts().print();
+    return 0;
+  }
+  if (cmd == "part" && argc >= 7) {
+    HarnessGraph g(argv[2]);
+    std::vector<vid_t> seq = strcmp(argv[3], "-") == 0 ? degreeSequence(g) : readSequence(argv[3]);
+    JNodeTable jnodes(argv[4]);
+    jnodes.getFacts().print();
+    for (int i = 6; i < argc; ++i) {
+      short const k = atoi(argv[i]);
+      Partition part(seq, jnodes, k, 1.03, false, true, false);
+      part.print();
+      part.evaluate(g, seq);
+      std::string path = std::string(argv[5]) + "k" + argv[i] + ".parts";
+      dump_parts(part, path.c_str());
+    }
+    return 0;
+  }
+  if (cmd == "write" && argc == 7) {
+    HarnessGraph g(argv[2]);
+    std::vector<vid_t> seq = strcmp(argv[3], "-") == 0 ? degreeSequence(g) : readSequence(argv[3]);
+    JNodeTable jnodes(argv[4]);
+    Partition part(seq, jnodes, (short)atoi(argv[5]), 1.03, false, true, false);
+    part.print();
+    part.writePartitionedGraph(g, seq, argv[6]);
+    return 0;
+  }
+  return usage();
+}

@@ -1,0 +1,479 @@
+"""sheep_amd — MI355X implementation of Sheep's map/reduce partitioning path.
+
+Python mirror of the reference's lib/ interfaces (chan150/sheep) over the C ABI of
+``sheep_amd/lib/libsheep_hip.so`` (declared in ``include/sheep_hip.h``):
+
+=========================  ======================================================
+reference (file:line)      here
+=========================  ======================================================
+mpiSequence / degreeSeq.   :func:`degree_sequence`  (sequence.h:52-93)
+fileSequence               :func:`degree_sequence` ``mode='dat'|'net'``  (:95-128)
+JTree(graph, seq)          :func:`build_tree`  (jtree.h:111-122, jtree.cpp:66-145)
+JNodeTable::merge          :func:`merge_trees`  (jnode.cpp:174-201)
+JNodeTable::makeKids       :class:`KidTable`  (jnode.h:190-204)
+Partition(seq,jnodes,k..)  :func:`partition`  (partition.cpp:50-157)
+Partition::print           :meth:`PartitionResult.print_text`  (partition.h:135-143)
+Partition::evaluate        :func:`evaluate`  (partition.cpp:428-521)
+JNodeTable::Facts          :func:`facts`  (jnode.cpp:256-290)
+=========================  ======================================================
+
+Device memory is torch-allocated (``torch.cuda``), streams are torch's current
+stream; every computation runs in the HIP kernels of libsheep_hip.so.  There is NO
+CPU fallback: importing this package without the built library, or calling it without
+a GPU, raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libsheep_hip.so")
+
+INVALID_ID = 0xFFFFFFFF
+INVALID_PART = -1
+DEGREE_MODES = {"llama": 0, "dat": 1, "net": 2}
+EVAL_GRAPH, EVAL_DOWN, EVAL_UP = 1, 2, 4
+
+_ERRORS = {-1: ValueError, -2: RuntimeError, -3: IndexError, -4: RuntimeError, -5: MemoryError}
+
+
+class SheepError(RuntimeError):
+    pass
+
+
+class _PartInfo(ctypes.Structure):
+    _fields_ = [("created", ctypes.c_int32), ("first_size", ctypes.c_uint64), ("second_size", ctypes.c_uint64),
+                ("max_component", ctypes.c_uint64), ("total_weight", ctypes.c_uint64),
+                ("packing_nodes", ctypes.c_uint64), ("heavy_nodes", ctypes.c_uint64)]
+
+
+class _Eval(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_uint64) for f in (
+        "edges_cut", "vcom_vol", "max_vertex_bal", "ecv_hash", "max_hash_bal", "ecv_down", "max_down_bal",
+        "ecv_up", "max_up_bal", "edges", "nodes")]
+
+
+class _Facts(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_uint64) for f in (
+        "width", "root_cnt", "vert_height", "edge_height", "vert_cnt", "edge_cnt", "halo_id", "core_id", "fill")]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libsheep_hip.so (fails loudly: there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is not built; run `make hip` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    P, U64, I32, I16, D = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int16, ctypes.c_double
+    sig = {
+        "sheep_last_error": ([], ctypes.c_char_p),
+        "sheep_ctx_create": ([I32, P, ctypes.POINTER(P)], I32),
+        "sheep_ctx_destroy": ([P], I32),
+        "sheep_ctx_sync": ([P], I32),
+        "sheep_ctx_stream": ([P], P),
+        "sheep_malloc": ([P, ctypes.c_size_t, ctypes.POINTER(P)], I32),
+        "sheep_free": ([P, P], I32),
+        "sheep_memcpy_h2d": ([P, P, P, ctypes.c_size_t], I32),
+        "sheep_memcpy_d2h": ([P, P, P, ctypes.c_size_t], I32),
+        "sheep_timer_enable": ([P, I32], I32),
+        "sheep_timer_get": ([P, ctypes.c_char_p, ctypes.POINTER(D), ctypes.POINTER(U64)], I32),
+        "sheep_timer_reset": ([P], I32),
+        "sheep_degree_count": ([P, P, U64, I32, P, U64, ctypes.POINTER(U64)], I32),
+        "sheep_sequence_from_degrees": ([P, P, U64, P, P, ctypes.POINTER(U64)], I32),
+        "sheep_positions": ([P, P, U64, P, U64], I32),
+        "sheep_build_tree": ([P, P, U64, P, U64, U64, P], I32),
+        "sheep_merge_trees": ([P, P, P, U64, P], I32),
+        "sheep_kids_create": ([P, P, U64, ctypes.POINTER(P)], I32),
+        "sheep_kids_destroy": ([P], I32),
+        "sheep_partition": ([P, P, U64, P, U64, P, I16, D, I32, I32, P, ctypes.POINTER(_PartInfo)], I32),
+        "sheep_evaluate": ([P, P, U64, P, U64, P, I32, ctypes.POINTER(_Eval)], I32),
+        "sheep_facts": ([P, P, U64, ctypes.POINTER(_Facts)], I32),
+        "sheep_rmat_generate": ([P, I32, I32, U64, P, U64, ctypes.POINTER(U64)], I32),
+        "sheep_rmat_generate_host": ([I32, I32, U64, P, U64, ctypes.POINTER(U64)], I32),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        msg = lib().sheep_last_error().decode(errors="replace")
+        raise _ERRORS.get(rc, SheepError)(f"sheep_hip error {rc}: {msg}")
+
+
+def _ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+class Context:
+    """One device + the torch current stream (so torch and sheep kernels stay ordered)."""
+
+    def __init__(self, device: int = 0, stream=None):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("sheep_amd needs a HIP device (torch.cuda.is_available() is False)")
+        self.device = device
+        torch.cuda.set_device(device)
+        s = stream if stream is not None else torch.cuda.current_stream(device)
+        self._stream = s
+        h = ctypes.c_void_p()
+        _check(lib().sheep_ctx_create(device, ctypes.c_void_p(s.cuda_stream), ctypes.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().sheep_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        _check(lib().sheep_ctx_sync(self.handle))
+
+    # device-side kernel timers (HIP events on the context stream)
+    def timing(self, on: bool = True):
+        _check(lib().sheep_timer_enable(self.handle, int(on)))
+
+    def timer(self, name: str):
+        ms, n = ctypes.c_double(), ctypes.c_uint64()
+        _check(lib().sheep_timer_get(self.handle, name.encode(), ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def timer_reset(self):
+        _check(lib().sheep_timer_reset(self.handle))
+
+
+_default_ctx: Context | None = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _dev_u32(n: int):
+    t = _torch()
+    return t.empty(max(int(n), 1), dtype=t.int32, device="cuda")
+
+
+def records_to_device(tail: np.ndarray, head: np.ndarray, weight: np.ndarray | None = None):
+    """XS1 records (12 bytes: u32 tail, u32 head, f32 weight) as a [R,3] int32 device tensor."""
+    t = _torch()
+    R = len(tail)
+    host = np.empty((R, 3), dtype=np.uint32)
+    host[:, 0] = tail
+    host[:, 1] = head
+    host[:, 2] = (np.ones(R, np.float32) if weight is None else np.asarray(weight, np.float32)).view(np.uint32)
+    return t.from_numpy(host.view(np.int32)).to("cuda")
+
+
+def to_numpy_u32(x) -> np.ndarray:
+    return x.detach().cpu().numpy().view(np.uint32)
+
+
+# ---------------------------------------------------------------------------------
+# sequence.h
+# ---------------------------------------------------------------------------------
+@dataclass
+class Sequence:
+    seq: object          # device int32 tensor [n] (u32 vids)
+    pos: object          # device int32 tensor [pos_size] (u32 jnids, INVALID elsewhere)
+    n: int
+    pos_size: int        # max(seq) + 1 (jtree.h:113) for readSequence; max_nodes for degree seqs
+
+    def numpy(self) -> np.ndarray:
+        return to_numpy_u32(self.seq[: self.n])
+
+
+def degree_count(records, nrec: int | None = None, mode: str = "llama", deg=None, vs_cap: int | None = None,
+                 ctx: Context | None = None):
+    """Accumulate one shard's degrees into `deg` (device u32); returns (deg, max_slot)."""
+    ctx = ctx or default_context()
+    t = _torch()
+    nrec = records.shape[0] if nrec is None else nrec
+    if deg is None:
+        vs_cap = vs_cap or (1 << 32) - 1
+        raise ValueError("pass a zeroed degree tensor `deg` of the vertex-slot capacity")
+    ms = ctypes.c_uint64()
+    _check(lib().sheep_degree_count(ctx.handle, _ptr(records), nrec, DEGREE_MODES[mode], _ptr(deg), deg.numel(),
+                                    ctypes.byref(ms)))
+    return deg, ms.value
+
+
+def sequence_from_degrees(deg, vs: int, ctx: Context | None = None) -> Sequence:
+    ctx = ctx or default_context()
+    seq, pos = _dev_u32(vs), _dev_u32(vs)
+    n = ctypes.c_uint64()
+    _check(lib().sheep_sequence_from_degrees(ctx.handle, _ptr(deg), vs, _ptr(seq), _ptr(pos), ctypes.byref(n)))
+    return Sequence(seq, pos, n.value, vs)
+
+
+def degree_sequence(records, mode: str = "llama", vs_cap: int | None = None, ctx: Context | None = None) -> Sequence:
+    """degreeSequence / mpiSequence (mode 'llama') or fileSequence ('dat' / 'net')."""
+    ctx = ctx or default_context()
+    t = _torch()
+    nrec = records.shape[0]
+    if vs_cap is None:
+        vs_cap = int(records[:, :2].max().item()) + 1 if nrec else 1
+        vs_cap = vs_cap if vs_cap > 0 else (1 << 32) - 1
+    deg = t.zeros(max(vs_cap, 1), dtype=t.int32, device="cuda")
+    _, vs = degree_count(records, nrec, mode, deg, ctx=ctx)
+    return sequence_from_degrees(deg, vs, ctx)
+
+
+def sequence_from_host(seq: np.ndarray, ctx: Context | None = None) -> Sequence:
+    """readSequence path (sequence.h:159-168): an arbitrary sequence -> seq/pos on device."""
+    ctx = ctx or default_context()
+    t = _torch()
+    seq = np.asarray(seq, dtype=np.uint32)
+    n = len(seq)
+    pos_size = int(seq.max()) + 1 if n else 0
+    d_seq = t.from_numpy(seq.view(np.int32).copy()).to("cuda") if n else _dev_u32(1)
+    pos = _dev_u32(pos_size)
+    _check(lib().sheep_positions(ctx.handle, _ptr(d_seq), n, _ptr(pos), pos_size))
+    return Sequence(d_seq, pos, n, pos_size)
+
+
+# ---------------------------------------------------------------------------------
+# jtree / jnode
+# ---------------------------------------------------------------------------------
+def build_tree(records, seq: Sequence, nrec: int | None = None, ctx: Context | None = None):
+    """JTree(graph, seq): device tensor [n, 2] int32 = JNode {parent, pst_weight}."""
+    ctx = ctx or default_context()
+    t = _torch()
+    nrec = records.shape[0] if nrec is None else nrec
+    tree = t.empty((max(seq.n, 1), 2), dtype=t.int32, device="cuda")
+    _check(lib().sheep_build_tree(ctx.handle, _ptr(records), nrec, _ptr(seq.pos), seq.pos_size, seq.n, _ptr(tree)))
+    return tree[: seq.n]
+
+
+def merge_trees(a, b, ctx: Context | None = None):
+    """JNodeTable::merge(lhs, rhs): Liu over the union of both parent-edge sets."""
+    ctx = ctx or default_context()
+    t = _torch()
+    n = a.shape[0]
+    if b.shape[0] != n:
+        raise ValueError("trees of different sizes")
+    out = t.empty((max(n, 1), 2), dtype=t.int32, device="cuda")
+    _check(lib().sheep_merge_trees(ctx.handle, _ptr(a), _ptr(b), n, _ptr(out)))
+    return out[:n]
+
+
+def tree_to_device(parent: np.ndarray, pst: np.ndarray):
+    t = _torch()
+    host = np.stack([np.asarray(parent, np.uint32), np.asarray(pst, np.uint32)], axis=1)
+    return t.from_numpy(host.view(np.int32).copy()).to("cuda")
+
+
+def tree_to_numpy(tree):
+    a = to_numpy_u32(tree).reshape(-1, 2)
+    return a[:, 0].copy(), a[:, 1].copy()
+
+
+class KidTable:
+    """makeKids (jnode.h:190-204): kid lists kept on the device; forwardPartition's
+    in-place std::sort of a packing node's kids persists across k (partition.cpp:104-106)."""
+
+    def __init__(self, tree, ctx: Context | None = None):
+        self.ctx = ctx or default_context()
+        self.n = tree.shape[0]
+        h = ctypes.c_void_p()
+        _check(lib().sheep_kids_create(self.ctx.handle, _ptr(tree), self.n, ctypes.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().sheep_kids_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class PartitionResult:
+    parts: object            # device int16 tensor, vid-indexed, size max(seq)+1
+    num_parts: int           # the k asked for
+    created: int
+    first_size: int
+    second_size: int
+    max_component: int
+    total_weight: int
+    packing_nodes: int
+    heavy_nodes: int
+
+    def print_text(self) -> str:   # partition.h:135-143
+        return (f"Actually created {self.created} partitions.\n"
+                f"First two partition sizes: {self.first_size} and {self.second_size}\n")
+
+    def numpy(self) -> np.ndarray:
+        return self.parts.detach().cpu().numpy()
+
+
+def partition(seq: Sequence, tree, k: int, balance: float = 1.03, vtx_weight: bool = False,
+              pst_weight: bool = True, kids: KidTable | None = None, ctx: Context | None = None) -> PartitionResult:
+    """Partition(seq, jnodes, k, balance, vtx, pst, pre=false) + forwardPartition."""
+    ctx = ctx or default_context()
+    t = _torch()
+    kids = kids or KidTable(tree, ctx)
+    pos_size = seq.pos_size
+    parts = t.empty(max(pos_size, 1), dtype=t.int16, device="cuda")
+    info = _PartInfo()
+    _check(lib().sheep_partition(ctx.handle, _ptr(tree), tree.shape[0], _ptr(seq.seq), pos_size, kids.handle,
+                                 int(k), float(balance), int(vtx_weight), int(pst_weight), _ptr(parts),
+                                 ctypes.byref(info)))
+    return PartitionResult(parts[:pos_size], int(k), info.created, info.first_size, info.second_size,
+                           info.max_component, info.total_weight, info.packing_nodes, info.heavy_nodes)
+
+
+@dataclass
+class EvalResult:
+    edges_cut: int
+    vcom_vol: int
+    max_vertex_bal: int
+    ecv_hash: int
+    max_hash_bal: int
+    ecv_down: int
+    max_down_bal: int
+    ecv_up: int
+    max_up_bal: int
+    edges: int
+    nodes: int
+
+    def text(self, num_parts: int, with_seq: bool = True) -> str:
+        """The reference's printf lines (partition.cpp:468-472, 517-520), byte for byte."""
+        E, N = self.edges, self.nodes
+        Ek, Nk = E // num_parts, N // num_parts
+        f = lambda a, b: _cfmt(a, b)
+        s = (f"edges cut: {self.edges_cut} ({f(self.edges_cut, E)}%)\n"
+             f"Vcom. vol: {self.vcom_vol} ({f(self.vcom_vol, E)}%)\n"
+             f"  balance: {self.max_vertex_bal} ({f(self.max_vertex_bal, Nk)}%)\n"
+             f"ECV(hash): {self.ecv_hash} ({f(self.ecv_hash, E)}%)\n"
+             f"  balance: {self.max_hash_bal} ({f(self.max_hash_bal, Ek)}%)\n")
+        if with_seq:
+            s += (f"ECV(down): {self.ecv_down} ({f(self.ecv_down, E)}%)\n"
+                  f"  balance: {self.max_down_bal} ({f(self.max_down_bal, Ek)}%)\n"
+                  f"ECV(up)  : {self.ecv_up} ({f(self.ecv_up, E)}%)\n"
+                  f"  balance: {self.max_up_bal} ({f(self.max_up_bal, Ek)}%)\n")
+        return s
+
+
+def _cfmt(a: int, b: int) -> str:
+    """C printf("%f", (double)a / b) including inf/nan spellings."""
+    if b == 0:
+        return "inf" if a > 0 else "-nan"
+    return "%f" % (a / b)
+
+
+def evaluate(records, seq: Sequence, parts, what: int = 0, nrec: int | None = None,
+             ctx: Context | None = None) -> EvalResult:
+    ctx = ctx or default_context()
+    nrec = records.shape[0] if nrec is None else nrec
+    out = _Eval()
+    _check(lib().sheep_evaluate(ctx.handle, _ptr(records), nrec, _ptr(seq.pos), seq.pos_size, _ptr(parts), what,
+                                ctypes.byref(out)))
+    return EvalResult(*[getattr(out, f) for f, _ in _Eval._fields_])
+
+
+@dataclass
+class Facts:
+    width: int
+    root_cnt: int
+    vert_height: int
+    edge_height: int
+    vert_cnt: int
+    edge_cnt: int
+    halo_id: int
+    core_id: int
+    fill: int
+
+    def text(self) -> str:   # jnode.h:285-291
+        return (f"TREEFAQS: width:{self.width}\troots:{self.root_cnt}\n"
+                f"\tvheight:{self.vert_height}\teheight:{self.edge_height}\n"
+                f"\tverts:{self.vert_cnt}\tedges:{self.edge_cnt}\n"
+                f"\thalo:{self.halo_id}\tcore:{self.core_id}\n"
+                f"\tfill:{self.fill}\n")
+
+
+def facts(tree, ctx: Context | None = None) -> Facts:
+    ctx = ctx or default_context()
+    out = _Facts()
+    _check(lib().sheep_facts(ctx.handle, _ptr(tree), tree.shape[0], ctypes.byref(out)))
+    return Facts(*[getattr(out, f) for f, _ in _Facts._fields_])
+
+
+# ---------------------------------------------------------------------------------
+# synthetic input
+# ---------------------------------------------------------------------------------
+def rmat(scale: int, edgefactor: int = 16, seed: int = 1, ctx: Context | None = None):
+    """Graph500-parameter RMAT records generated in HBM: [R, 3] int32 device tensor."""
+    ctx = ctx or default_context()
+    t = _torch()
+    cap = edgefactor << scale
+    out = t.empty((cap, 3), dtype=t.int32, device="cuda")
+    n = ctypes.c_uint64()
+    _check(lib().sheep_rmat_generate(ctx.handle, scale, edgefactor, seed, _ptr(out), cap, ctypes.byref(n)))
+    return out[: n.value]
+
+
+def rmat_host(scale: int, edgefactor: int = 16, seed: int = 1) -> np.ndarray:
+    """The same generator on the CPU: structured array of XS1 records (for .dat files)."""
+    cap = edgefactor << scale
+    buf = np.empty(cap * 3, dtype=np.uint32)
+    n = ctypes.c_uint64()
+    _check(lib().sheep_rmat_generate_host(scale, edgefactor, seed, buf.ctypes.data, cap, ctypes.byref(n)))
+    return buf[: 3 * n.value].reshape(-1, 3)
+
+
+XS1 = np.dtype([("tail", "<u4"), ("head", "<u4"), ("weight", "<f4")])
+
+
+def read_dat(path: str) -> np.ndarray:
+    return np.fromfile(path, dtype=XS1)
+
+
+def read_net(path: str) -> np.ndarray:
+    """SNAPReader (readerwriter.h:166-178): whitespace-separated pairs, stop at the first
+    incomplete pair."""
+    toks = open(path).read().split()
+    vals = []
+    for tok in toks:
+        try:
+            vals.append(int(tok))
+        except ValueError:
+            break
+    if len(vals) % 2:
+        vals = vals[:-1]
+    a = np.array(vals, dtype=np.uint64).reshape(-1, 2)
+    rec = np.zeros(len(a), dtype=XS1)
+    rec["tail"] = a[:, 0]
+    rec["head"] = a[:, 1]
+    rec["weight"] = 1.0
+    return rec

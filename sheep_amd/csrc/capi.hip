@@ -1,0 +1,261 @@
+// capi.hip — the extern "C" boundary of libsheep_hip.so (declared in include/sheep_hip.h).
+// Exceptions never cross it: every entry point maps sheep::Error / std::exception to a
+// status code and a thread-local message.
+#include <cstring>
+#include <string>
+
+#include "common.hpp"
+#include "tree_tour.hpp"
+
+struct sheep_ctx {
+  sheep::Ctx c;
+};
+
+namespace sheep {
+static thread_local std::string g_last_error;
+void set_error(const char *msg) { g_last_error = msg; }
+
+void degree_count(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap, uint64_t *max_slot);
+uint64_t sequence_from_degrees(Ctx &c, const uint32_t *deg, uint64_t vs, uint32_t *seq, uint32_t *pos);
+void positions(Ctx &c, const uint32_t *seq, uint64_t n, uint32_t *pos, uint64_t pos_size);
+void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size, uint64_t n,
+                      sheep_jnode *tree);
+void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n, sheep_jnode *out);
+void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t *seq, uint64_t pos_size,
+                    sheep_kids *k, int16_t np, double balance, int vtx, int pstw, int16_t *parts_vid,
+                    sheep_partition_info *info);
+void evaluate(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
+              const int16_t *parts, int what, sheep_eval *out);
+void tree_facts(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_facts_t *out);
+uint64_t rmat_generate(Ctx &c, int scale, int ef, uint64_t seed, sheep_xs1 *out, uint64_t cap);
+uint64_t rmat_generate_host(int scale, int ef, uint64_t seed, sheep_xs1 *out, uint64_t cap);
+}  // namespace sheep
+
+using sheep::Error;
+
+#define API_BEGIN try {
+#define API_END                                                          \
+  }                                                                      \
+  catch (const sheep::Error &e) { sheep::set_error(e.what()); return e.code; } \
+  catch (const std::bad_alloc &e) { sheep::set_error("bad_alloc"); return SHEEP_ERR_ALLOC; } \
+  catch (const std::exception &e) { sheep::set_error(e.what()); return SHEEP_ERR_HIP; } \
+  return SHEEP_OK;
+
+#define NEED(cond, msg) \
+  if (!(cond)) throw sheep::Error(SHEEP_ERR_ARG, msg)
+
+extern "C" {
+
+const char *sheep_last_error(void) { return sheep::g_last_error.c_str(); }
+
+int sheep_ctx_create(int device, void *hip_stream, sheep_ctx **out) {
+  API_BEGIN
+  NEED(out, "null out");
+  int ndev = 0;
+  HIP_CHECK(hipGetDeviceCount(&ndev));
+  NEED(device >= 0 && device < ndev, "no such HIP device");
+  HIP_CHECK(hipSetDevice(device));
+  sheep_ctx *x = new sheep_ctx();
+  x->c.device = device;
+  if (hip_stream) {
+    x->c.stream = (hipStream_t)hip_stream;
+  } else {
+    HIP_CHECK(hipStreamCreateWithFlags(&x->c.stream, hipStreamNonBlocking));
+    x->c.own_stream = true;
+  }
+  HIP_CHECK(hipHostMalloc((void **)&x->c.h_scalars, sheep::Ctx::NSCALARS * sizeof(uint64_t), hipHostMallocDefault));
+  HIP_CHECK(hipMalloc((void **)&x->c.d_scalars, sheep::Ctx::NSCALARS * sizeof(uint64_t)));
+  *out = x;
+  API_END
+}
+
+int sheep_ctx_destroy(sheep_ctx *ctx) {
+  API_BEGIN
+  if (!ctx) return SHEEP_OK;
+  sheep::Ctx &c = ctx->c;
+  HIP_CHECK(hipSetDevice(c.device));
+  if (c.stream) HIP_CHECK(hipStreamSynchronize(c.stream));
+  for (auto &kv : c.ws) if (kv.second.p) hipFree(kv.second.p);
+  for (auto &kv : c.timers) for (auto &p : kv.second.pending) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
+  for (hipEvent_t e : c.event_pool) hipEventDestroy(e);
+  if (c.h_scalars) hipHostFree(c.h_scalars);
+  if (c.d_scalars) hipFree(c.d_scalars);
+  if (c.own_stream) hipStreamDestroy(c.stream);
+  delete ctx;
+  API_END
+}
+
+int sheep_ctx_sync(sheep_ctx *ctx) {
+  API_BEGIN
+  NEED(ctx, "null ctx");
+  ctx->c.sync();
+  API_END
+}
+
+void *sheep_ctx_stream(sheep_ctx *ctx) { return ctx ? (void *)ctx->c.stream : nullptr; }
+
+int sheep_malloc(sheep_ctx *ctx, size_t bytes, void **dev_out) {
+  API_BEGIN
+  NEED(ctx && dev_out, "null argument");
+  HIP_CHECK(hipSetDevice(ctx->c.device));
+  HIP_CHECK(hipMalloc(dev_out, bytes ? bytes : 1));
+  API_END
+}
+
+int sheep_free(sheep_ctx *ctx, void *dev) {
+  API_BEGIN
+  NEED(ctx, "null ctx");
+  if (dev) HIP_CHECK(hipFree(dev));
+  API_END
+}
+
+int sheep_memcpy_h2d(sheep_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  API_BEGIN
+  NEED(ctx, "null ctx");
+  if (bytes) {
+    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->c.stream));
+    ctx->c.sync();
+  }
+  API_END
+}
+
+int sheep_memcpy_d2h(sheep_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  API_BEGIN
+  NEED(ctx, "null ctx");
+  if (bytes) {
+    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->c.stream));
+    ctx->c.sync();
+  }
+  API_END
+}
+
+int sheep_timer_enable(sheep_ctx *ctx, int on) {
+  API_BEGIN
+  NEED(ctx, "null ctx");
+  ctx->c.timing = on != 0;
+  API_END
+}
+
+int sheep_timer_get(sheep_ctx *ctx, const char *name, double *ms, uint64_t *launches) {
+  API_BEGIN
+  NEED(ctx && name && ms && launches, "null argument");
+  ctx->c.collect_timers();
+  auto it = ctx->c.timers.find(name);
+  *ms = it == ctx->c.timers.end() ? 0.0 : it->second.ms;
+  *launches = it == ctx->c.timers.end() ? 0 : it->second.launches;
+  API_END
+}
+
+int sheep_timer_reset(sheep_ctx *ctx) {
+  API_BEGIN
+  NEED(ctx, "null ctx");
+  ctx->c.collect_timers();
+  ctx->c.timers.clear();
+  API_END
+}
+
+int sheep_degree_count(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap,
+                       uint64_t *max_slot_out) {
+  API_BEGIN
+  NEED(ctx && (rec || !nrec) && deg && max_slot_out, "null argument");
+  sheep::degree_count(ctx->c, rec, nrec, mode, deg, cap, max_slot_out);
+  API_END
+}
+
+int sheep_sequence_from_degrees(sheep_ctx *ctx, const uint32_t *deg, uint64_t vs, uint32_t *seq, uint32_t *pos,
+                                uint64_t *n_out) {
+  API_BEGIN
+  NEED(ctx && (deg || !vs) && n_out, "null argument");
+  *n_out = sheep::sequence_from_degrees(ctx->c, deg, vs, seq, pos);
+  API_END
+}
+
+int sheep_positions(sheep_ctx *ctx, const uint32_t *seq, uint64_t n, uint32_t *pos, uint64_t pos_size) {
+  API_BEGIN
+  NEED(ctx && (seq || !n) && (pos || !pos_size), "null argument");
+  sheep::positions(ctx->c, seq, n, pos, pos_size);
+  API_END
+}
+
+int sheep_build_tree(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
+                     uint64_t n, sheep_jnode *tree) {
+  API_BEGIN
+  NEED(ctx && (rec || !nrec) && (pos || !pos_size) && (tree || !n), "null argument");
+  NEED(n < 0xFFFFFFFFull, "tree too large for 32-bit node ids");
+  sheep::relabel_and_tree(ctx->c, rec, nrec, pos, pos_size, n, tree);
+  API_END
+}
+
+int sheep_merge_trees(sheep_ctx *ctx, const sheep_jnode *a, const sheep_jnode *b, uint64_t n, sheep_jnode *out) {
+  API_BEGIN
+  NEED(ctx && ((a && b && out) || !n), "null argument");
+  sheep::merge_trees(ctx->c, a, b, n, out);
+  API_END
+}
+
+int sheep_kids_create(sheep_ctx *ctx, const sheep_jnode *tree, uint64_t n, sheep_kids **out) {
+  API_BEGIN
+  NEED(ctx && out && (tree || !n), "null argument");
+  sheep_kids *k = new sheep_kids();
+  try {
+    sheep::build_kids(ctx->c, tree, n, k);
+  } catch (...) {
+    hipFree(k->parent); hipFree(k->koff); hipFree(k->kids);
+    delete k;
+    throw;
+  }
+  *out = k;
+  API_END
+}
+
+int sheep_kids_destroy(sheep_kids *k) {
+  API_BEGIN
+  if (!k) return SHEEP_OK;
+  if (k->ctx) k->ctx->sync();
+  hipFree(k->parent);
+  hipFree(k->koff);
+  hipFree(k->kids);
+  delete k;
+  API_END
+}
+
+int sheep_partition(sheep_ctx *ctx, const sheep_jnode *tree, uint64_t n, const uint32_t *seq, uint64_t pos_size,
+                    sheep_kids *kids, int16_t k, double balance, int vtx_weight, int pst_weight, int16_t *parts_vid,
+                    sheep_partition_info *info) {
+  API_BEGIN
+  NEED(ctx && kids && info && ((tree && seq) || !n) && (parts_vid || !pos_size), "null argument");
+  sheep::partition_tree(ctx->c, tree, n, seq, pos_size, kids, k, balance, vtx_weight, pst_weight, parts_vid, info);
+  API_END
+}
+
+int sheep_evaluate(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
+                   const int16_t *parts_vid, int what, sheep_eval *out) {
+  API_BEGIN
+  NEED(ctx && out && (rec || !nrec) && ((pos && parts_vid) || !pos_size), "null argument");
+  sheep::evaluate(ctx->c, rec, nrec, pos, pos_size, parts_vid, what, out);
+  API_END
+}
+
+int sheep_facts(sheep_ctx *ctx, const sheep_jnode *tree, uint64_t n, sheep_facts_t *out) {
+  API_BEGIN
+  NEED(ctx && out && (tree || !n), "null argument");
+  sheep::tree_facts(ctx->c, tree, n, out);
+  API_END
+}
+
+int sheep_rmat_generate(sheep_ctx *ctx, int scale, int ef, uint64_t seed, sheep_xs1 *out, uint64_t cap,
+                        uint64_t *nrec_out) {
+  API_BEGIN
+  NEED(ctx && out && nrec_out, "null argument");
+  *nrec_out = sheep::rmat_generate(ctx->c, scale, ef, seed, out, cap);
+  API_END
+}
+
+int sheep_rmat_generate_host(int scale, int ef, uint64_t seed, sheep_xs1 *out, uint64_t cap, uint64_t *nrec_out) {
+  API_BEGIN
+  NEED(out && nrec_out, "null argument");
+  *nrec_out = sheep::rmat_generate_host(scale, ef, seed, out, cap);
+  API_END
+}
+
+}  // extern "C"

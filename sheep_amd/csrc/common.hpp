@@ -1,0 +1,161 @@
+// common.hpp — shared host/device plumbing for libsheep_hip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "sheep_hip.h"
+
+namespace sheep {
+
+constexpr uint32_t INVALID = 0xFFFFFFFFu;
+constexpr int WAVE = 64;     // CDNA wavefront
+constexpr int BLOCK = 256;   // 4 waves per workgroup
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIP_CHECK(expr)                                                                   \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess)                                                                 \
+      throw ::sheep::Error(_e == hipErrorOutOfMemory ? SHEEP_ERR_ALLOC : SHEEP_ERR_HIP,   \
+                           std::string(#expr) + ": " + hipGetErrorString(_e));            \
+  } while (0)
+
+#define LAUNCH_CHECK() HIP_CHECK(hipGetLastError())
+
+// Grid for a grid-stride streaming kernel: enough workgroups to fill 256 CUs x 8.
+inline unsigned grid_for(uint64_t items, unsigned per_block = BLOCK, unsigned cap = 256 * 8) {
+  uint64_t g = (items + per_block - 1) / per_block;
+  if (g == 0) g = 1;
+  return (unsigned)(g < cap ? g : cap);
+}
+
+// Per-context state: device, stream, grow-only named workspaces, pinned scalars, timers.
+struct Ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+
+  struct Buf { void *p = nullptr; size_t bytes = 0; };
+  std::map<std::string, Buf> ws;
+
+  uint64_t *h_scalars = nullptr;   // pinned host mirror
+  uint64_t *d_scalars = nullptr;   // device scalars (counters / flags)
+  static constexpr int NSCALARS = 64;
+
+  bool timing = false;
+  struct Timer { std::vector<std::pair<hipEvent_t, hipEvent_t>> pending; double ms = 0; uint64_t launches = 0; };
+  std::map<std::string, Timer> timers;
+  std::vector<hipEvent_t> event_pool;
+
+  void *get(const std::string &name, size_t bytes) {
+    Buf &b = ws[name];
+    if (b.bytes < bytes) {
+      if (b.p) HIP_CHECK(hipFree(b.p));
+      b.p = nullptr;
+      size_t want = bytes + bytes / 8 + 256;
+      HIP_CHECK(hipMalloc(&b.p, want));
+      b.bytes = want;
+    }
+    return b.p;
+  }
+  template <typename T> T *get_as(const std::string &name, size_t count) {
+    return (T *)get(name, count * sizeof(T));
+  }
+  void sync() { HIP_CHECK(hipStreamSynchronize(stream)); }
+
+  hipEvent_t ev() {
+    if (!event_pool.empty()) { hipEvent_t e = event_pool.back(); event_pool.pop_back(); return e; }
+    hipEvent_t e; HIP_CHECK(hipEventCreate(&e)); return e;
+  }
+  void collect_timers() {
+    for (auto &kv : timers) {
+      for (auto &p : kv.second.pending) {
+        float ms = 0;
+        HIP_CHECK(hipEventSynchronize(p.second));
+        HIP_CHECK(hipEventElapsedTime(&ms, p.first, p.second));
+        kv.second.ms += ms;
+        kv.second.launches++;
+        event_pool.push_back(p.first);
+        event_pool.push_back(p.second);
+      }
+      kv.second.pending.clear();
+    }
+  }
+};
+
+// Brackets one instrumented launch with HIP events on the context stream.
+struct TimedRegion {
+  Ctx &c; const char *name; hipEvent_t a = nullptr, b = nullptr;
+  TimedRegion(Ctx &ctx, const char *n) : c(ctx), name(n) {
+    if (c.timing) { a = c.ev(); b = c.ev(); HIP_CHECK(hipEventRecord(a, c.stream)); }
+  }
+  ~TimedRegion() {
+    if (c.timing) {
+      if (hipEventRecord(b, c.stream) == hipSuccess) c.timers[name].pending.push_back({a, b});
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------------
+// Device helpers
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  unsigned l = __lane_id();
+  return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+template <typename T> __device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <typename T> __device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { T w = __shfl_xor(v, o, 64); v = w > v ? w : v; }
+  return v;
+}
+template <typename T> __device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { T w = __shfl_xor(v, o, 64); v = w < v ? w : v; }
+  return v;
+}
+
+// Wave-aggregated append: every lane with `pred` gets a unique slot in [0, *counter).
+__device__ __forceinline__ uint64_t wave_append(bool pred, unsigned long long *counter) {
+  uint64_t mask = __ballot(pred);
+  uint64_t base = 0;
+  if (mask == 0) return 0;
+  int leader = __ffsll((unsigned long long)mask) - 1;
+  if ((int)__lane_id() == leader) base = atomicAdd(counter, (unsigned long long)__popcll(mask));
+  base = __shfl(base, leader, 64);
+  return base + __popcll(mask & lanemask_lt());
+}
+
+}  // namespace sheep
+
+// Host entry points shared between translation units.
+namespace sheep {
+void set_error(const char *msg);
+// scan.hip
+void scan_exclusive_u32(Ctx &c, const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total_dev);
+void scan_exclusive_u64(Ctx &c, const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *total_dev);
+// radix.hip — stable LSD sort of (key, value) pairs on bits [0, end_bit); results end
+// in (keys, vals); alt buffers are scratch of the same size.
+void radix_sort_pairs_u32(Ctx &c, uint32_t *keys, uint32_t *vals, uint64_t n, int end_bit,
+                          uint32_t *keys_alt, uint32_t *vals_alt);
+void radix_sort_keys_u64(Ctx &c, uint64_t *keys, uint64_t n, int end_bit, uint64_t *keys_alt);
+// etree.hip
+void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent);
+}  // namespace sheep

@@ -1,0 +1,371 @@
+// etree.hip — map step (relabel + pst + per-shard elimination tree) and the reduce
+// step (pairwise tree merge), both on one GPU kernel family.
+//
+// Reference: JTree::insert (jtree.cpp:66-110) runs Liu's algorithm sequentially: for
+// X in order, every earlier neighbour's union-find representative gets parent X
+// (jnode.h:158-162, unionfind.h:82-102); later neighbours count into pst_weight.
+// JNodeTable::merge (jnode.cpp:174-201) re-runs Liu over the union of two parent
+// edge sets.
+//
+// MI355X formulation (no sequential sweep).  With vertices numbered by sequence
+// position, parent(x) = min{ v > x : v adjacent to C_x } where C_x is x's component
+// in G[0..x].  We compute it by divide and conquer over the position range, all
+// subproblems of one level at once:
+//   subproblem [l,r), split mid:  light = both ends < mid,  cross = lo < mid <= hi.
+//   * union-find over the light edges (hook smaller root under larger: the root of a
+//     component is its maximum = its "top" t);
+//   * for every cross edge (a,b): t = top(a); m_t = min b  (atomicMin)  -> parent(t) = m_t;
+//   * contract: (a,b) -> (m_t, b); drop it when b == m_t; dedup contracted pairs.
+//   After the level every live edge lies inside one half; recurse.
+// Every vertex gets its parent at the one level where it is the top of a light
+// component with a cross edge; vertices never assigned are roots.  The result is the
+// unique elimination tree of (edge multiset, order) — identical to Liu's.  Level
+// ranges are dyadic in a monotone spread of [0,n) onto [0,2^L) so halves are balanced.
+#include "common.hpp"
+
+namespace sheep {
+namespace {
+
+constexpr uint64_t DEAD = ~0ull;
+
+__device__ __forceinline__ uint32_t spread(uint32_t x, uint32_t clo) { return x + __umulhi(x, clo); }
+
+// ---- union-find (values only move up: parent[x] > x) ------------------------------
+// Concurrent phase: agent-scope relaxed loads (L1 bypass) + CAS hooking; a CAS failure
+// returns the fresh value and the loop climbs from there, so stale reads only cost
+// retries, never correctness (hook target is always > the hooked root -> acyclic).
+__device__ __forceinline__ uint32_t ld_rlx(uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_rlx(uint32_t *p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t find_conc(uint32_t *uf, uint32_t x) {
+  uint32_t p = ld_rlx(&uf[x]);
+  while (p != x) {
+    uint32_t gp = ld_rlx(&uf[p]);
+    if (gp == p) return p;
+    st_rlx(&uf[x], gp);
+    x = gp;
+    p = ld_rlx(&uf[x]);
+  }
+  return x;
+}
+__device__ __forceinline__ void union_conc(uint32_t *uf, uint32_t a, uint32_t b) {
+  uint32_t ra = find_conc(uf, a), rb = find_conc(uf, b);
+  while (ra != rb) {
+    if (ra > rb) { uint32_t t = ra; ra = rb; rb = t; }
+    uint32_t old = atomicCAS(&uf[ra], ra, rb);
+    if (old == ra) return;
+    ra = find_conc(uf, old);
+    rb = find_conc(uf, rb);
+  }
+}
+// Read-only phase (after a kernel boundary): plain loads + path halving.
+__device__ __forceinline__ uint32_t find_plain(uint32_t *uf, uint32_t x) {
+  uint32_t p = uf[x];
+  while (p != x) {
+    uint32_t gp = uf[p];
+    if (gp == p) return p;
+    uf[x] = gp;
+    x = gp;
+    p = uf[x];
+  }
+  return x;
+}
+
+__device__ __forceinline__ uint32_t hash64(uint64_t k) {
+  k ^= k >> 33; k *= 0xff51afd7ed558ccdull; k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ull; k ^= k >> 33;
+  return (uint32_t)k;
+}
+
+// ---- relabel + pst (jtree.cpp:72-91) -------------------------------------------------
+// One record = one undirected pair.  Both endpoints sequenced: pst[lo]++ and a tree
+// edge (lo,hi).  One endpoint sequenced, the other a slot < pos_size but absent from
+// the sequence: its index stays INVALID forever -> POSTORDER for the sequenced one.
+// A neighbour >= pos_size of a sequenced vertex -> index.at() throws -> error flag.
+__global__ __launch_bounds__(BLOCK) void k_relabel(const sheep_xs1 *__restrict__ rec, uint64_t nrec,
+                                                   const uint32_t *__restrict__ pos, uint64_t pos_size,
+                                                   uint32_t *__restrict__ pst, uint64_t *__restrict__ edges,
+                                                   unsigned long long *__restrict__ counter,
+                                                   unsigned long long *__restrict__ err) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const uint64_t iters = (nrec + stride - 1) / stride;
+  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  bool bad = false;
+  for (uint64_t it = 0; it < iters; ++it, i += stride) {
+    bool emit = false;
+    uint64_t e = 0;
+    if (i < nrec) {
+      sheep_xs1 r = rec[i];
+      uint32_t t = r.tail, h = r.head;
+      if (t != h) {
+        uint32_t pt = t < pos_size ? pos[t] : INVALID;
+        uint32_t ph = h < pos_size ? pos[h] : INVALID;
+        bool tin = pt != INVALID, hin = ph != INVALID;
+        if ((tin && h >= pos_size) || (hin && t >= pos_size)) bad = true;
+        else if (tin && hin) {
+          uint32_t lo = pt < ph ? pt : ph, hi = pt < ph ? ph : pt;
+          atomicAdd(&pst[lo], 1u);
+          e = ((uint64_t)hi << 32) | lo;
+          emit = true;
+        } else if (tin) atomicAdd(&pst[pt], 1u);
+        else if (hin) atomicAdd(&pst[ph], 1u);
+      }
+    }
+    uint64_t slot = wave_append(emit, counter);
+    if (emit) edges[slot] = e;
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(err, 1ull);
+}
+
+// ---- one D&C level ---------------------------------------------------------------
+__global__ __launch_bounds__(BLOCK) void k_reset(uint32_t *__restrict__ uf, uint32_t *__restrict__ mt, uint64_t n) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
+    uf[i] = (uint32_t)i;
+    mt[i] = INVALID;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_union_light(const uint64_t *__restrict__ edges, uint64_t m, int s,
+                                                       uint32_t clo, uint32_t *uf) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) {
+    uint64_t e = edges[i];
+    if (e == DEAD) continue;
+    uint32_t a = (uint32_t)e, b = (uint32_t)(e >> 32);
+    uint32_t ya = spread(a, clo), yb = spread(b, clo);
+    if (((ya ^ yb) >> s) == 0 && ((yb >> s) & 1) == 0) union_conc(uf, a, b);
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_cross_min(const uint64_t *__restrict__ edges, uint64_t m, int s,
+                                                     uint32_t clo, uint32_t *uf, uint32_t *__restrict__ mt,
+                                                     uint32_t *__restrict__ xidx, uint32_t *__restrict__ xtop,
+                                                     unsigned long long *__restrict__ counter) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const uint64_t iters = (m + stride - 1) / stride;
+  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (uint64_t it = 0; it < iters; ++it, i += stride) {
+    bool cross = false;
+    uint32_t t = 0;
+    if (i < m) {
+      uint64_t e = edges[i];
+      if (e != DEAD) {
+        uint32_t a = (uint32_t)e, b = (uint32_t)(e >> 32);
+        uint32_t ya = spread(a, clo), yb = spread(b, clo);
+        if (((ya ^ yb) >> s) == 1) {
+          cross = true;
+          t = find_plain(uf, a);
+          atomicMin(&mt[t], b);
+        }
+      }
+    }
+    uint64_t slot = wave_append(cross, counter);
+    if (cross) { xidx[slot] = (uint32_t)i; xtop[slot] = t; }
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_cross_apply(uint64_t *__restrict__ edges, const uint32_t *__restrict__ xidx,
+                                                       const uint32_t *__restrict__ xtop, uint64_t nx,
+                                                       const uint32_t *__restrict__ mt, uint32_t *__restrict__ parent,
+                                                       unsigned long long *__restrict__ table, uint32_t mask,
+                                                       unsigned long long *__restrict__ dead) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  uint32_t ndead = 0;
+  for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < nx; j += stride) {
+    uint32_t idx = xidx[j], t = xtop[j];
+    uint32_t m = mt[t];
+    parent[t] = m;   // every cross edge of t writes the same value
+    uint64_t e = edges[idx];
+    uint32_t b = (uint32_t)(e >> 32);
+    if (b == m) { edges[idx] = DEAD; ++ndead; continue; }
+    uint64_t ne = ((uint64_t)b << 32) | m;
+    // lossy dedup of contracted pairs: bounded linear probing; on overflow keep the edge
+    uint32_t h = hash64(ne) & mask;
+    bool dup = false;
+    for (int probe = 0; probe < 16; ++probe) {
+      unsigned long long old = atomicCAS(&table[h], DEAD, (unsigned long long)ne);
+      if (old == DEAD) break;
+      if (old == ne) { dup = true; break; }
+      h = (h + 1) & mask;
+    }
+    if (dup) { edges[idx] = DEAD; ++ndead; }
+    else edges[idx] = ne;
+  }
+  ndead = wave_sum(ndead);
+  if ((threadIdx.x & 63) == 0 && ndead) atomicAdd(dead, (unsigned long long)ndead);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_compact_edges(const uint64_t *__restrict__ in, uint64_t m,
+                                                         uint64_t *__restrict__ out, unsigned long long *__restrict__ counter) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const uint64_t iters = (m + stride - 1) / stride;
+  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (uint64_t it = 0; it < iters; ++it, i += stride) {
+    uint64_t e = i < m ? in[i] : DEAD;
+    bool live = e != DEAD;
+    uint64_t slot = wave_append(live, counter);
+    if (live) out[slot] = e;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_tree_edges(const sheep_jnode *__restrict__ a, const sheep_jnode *__restrict__ b,
+                                                      uint64_t n, uint64_t *__restrict__ edges,
+                                                      unsigned long long *__restrict__ counter,
+                                                      uint32_t *__restrict__ pst_out, unsigned long long *__restrict__ err) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const uint64_t iters = (n + stride - 1) / stride;
+  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  bool bad = false;
+  for (uint64_t it = 0; it < iters; ++it, i += stride) {
+    uint32_t pa = INVALID, pb = INVALID;
+    if (i < n) {
+      sheep_jnode x = a[i], y = b[i];
+      pa = x.parent; pb = y.parent;
+      pst_out[i] = x.pst_weight + y.pst_weight;
+      // a parent must be a later, existing node (jnode.cpp kids(current) via makeKids)
+      if ((pa != INVALID && (pa <= i || pa >= n)) || (pb != INVALID && (pb <= i || pb >= n))) {
+        bad = true; pa = pb = INVALID;
+      }
+    }
+    bool ea = pa != INVALID, eb = pb != INVALID && pb != pa;
+    uint64_t sa = wave_append(ea, counter);
+    if (ea) edges[sa] = ((uint64_t)pa << 32) | (uint32_t)i;
+    uint64_t sb = wave_append(eb, counter);
+    if (eb) edges[sb] = ((uint64_t)pb << 32) | (uint32_t)i;
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(err, 1ull);
+}
+
+__global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t *__restrict__ pst, uint64_t n,
+                            sheep_jnode *__restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
+    sheep_jnode j;
+    j.parent = parent[i];
+    j.pst_weight = pst[i];
+    out[i] = j;
+  }
+}
+
+}  // namespace
+
+void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
+
+// Elimination tree of `m` edges ((hi<<32)|lo, lo < hi < n).  `edges` is consumed.
+void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent) {
+  fill_u32(c, parent, n, INVALID);
+  if (n < 2 || m == 0) return;
+  if (m >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "too many edges for one shard");
+  int L = 0;
+  while ((1ull << L) < n) ++L;
+  // spread(x) = floor(x * c / 2^32), c = floor(2^(32+L) / n) in [2^32, 2^33): monotone,
+  // injective on [0,n), image in [0, 2^L).
+  unsigned __int128 cfull = (((unsigned __int128)1) << (32 + L)) / n;
+  uint32_t clo = (uint32_t)(cfull - (((unsigned __int128)1) << 32));
+
+  uint32_t *uf = c.get_as<uint32_t>("et_uf", n);
+  uint32_t *mt = c.get_as<uint32_t>("et_mt", n);
+  uint32_t *xidx = c.get_as<uint32_t>("et_xidx", m);
+  uint32_t *xtop = c.get_as<uint32_t>("et_xtop", m);
+  uint64_t *alt = c.get_as<uint64_t>("et_alt", m);
+  unsigned long long *d = (unsigned long long *)c.d_scalars;
+  uint64_t *cur = edges;
+  uint64_t live = m, dead = 0;
+  for (int lvl = 0; lvl < L && live > 0; ++lvl) {
+    const int s = L - 1 - lvl;
+    const unsigned g = grid_for(live);
+    hipLaunchKernelGGL(k_reset, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, uf, mt, n);
+    LAUNCH_CHECK();
+    {
+      TimedRegion tr(c, "etree_union");
+      hipLaunchKernelGGL(k_union_light, dim3(g), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, live, s, clo, uf);
+      LAUNCH_CHECK();
+    }
+    HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
+    {
+      TimedRegion tr(c, "etree_cross");
+      hipLaunchKernelGGL(k_cross_min, dim3(g), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, live, s, clo, uf, mt,
+                         xidx, xtop, d);
+      LAUNCH_CHECK();
+    }
+    HIP_CHECK(hipMemcpyAsync(c.h_scalars, d, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+    uint64_t nx = c.h_scalars[0];
+    if (nx) {
+      uint64_t cap = 1024;
+      while (cap < 2 * nx && cap < (1ull << 27)) cap <<= 1;
+      unsigned long long *table = c.get_as<unsigned long long>("et_hash", cap);
+      HIP_CHECK(hipMemsetAsync(table, 0xFF, cap * sizeof(uint64_t), c.stream));
+      TimedRegion tr(c, "etree_apply");
+      hipLaunchKernelGGL(k_cross_apply, dim3(grid_for(nx)), dim3(BLOCK), 0, c.stream, cur, xidx, xtop, nx, mt, parent,
+                         table, (uint32_t)(cap - 1), d + 1);
+      LAUNCH_CHECK();
+      HIP_CHECK(hipMemcpyAsync(c.h_scalars + 1, d + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+      c.sync();
+      dead += c.h_scalars[1];
+    }
+    if (dead * 4 >= live && dead) {   // compact once a quarter of the list is dead
+      HIP_CHECK(hipMemsetAsync(d + 2, 0, sizeof(uint64_t), c.stream));
+      uint64_t *out = cur == edges ? alt : edges;
+      hipLaunchKernelGGL(k_compact_edges, dim3(grid_for(live)), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, live,
+                         out, d + 2);
+      LAUNCH_CHECK();
+      cur = out;
+      live -= dead;
+      dead = 0;
+    }
+  }
+}
+
+void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
+                      uint64_t n, sheep_jnode *tree) {
+  uint32_t *pst = c.get_as<uint32_t>("bt_pst", n ? n : 1);
+  uint32_t *parent = c.get_as<uint32_t>("bt_parent", n ? n : 1);
+  HIP_CHECK(hipMemsetAsync(pst, 0, n * sizeof(uint32_t), c.stream));
+  uint64_t *edges = c.get_as<uint64_t>("bt_edges", nrec ? nrec : 1);
+  unsigned long long *d = (unsigned long long *)c.d_scalars + 8;
+  HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
+  if (nrec) {
+    TimedRegion tr(c, "relabel");
+    hipLaunchKernelGGL(k_relabel, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos, pos_size, pst,
+                       edges, d, d + 1);
+    LAUNCH_CHECK();
+  }
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 8, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  if (c.h_scalars[9]) throw Error(SHEEP_ERR_RANGE, "vector::_M_range_check: neighbour vid beyond the sequence's index (jtree.cpp:75)");
+  uint64_t m = c.h_scalars[8];
+  {
+    TimedRegion tr(c, "etree");
+    etree_from_edges(c, edges, m, n, parent);
+  }
+  if (n) {
+    hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, tree);
+    LAUNCH_CHECK();
+  }
+}
+
+void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n, sheep_jnode *out) {
+  if (n == 0) return;
+  uint32_t *pst = c.get_as<uint32_t>("mg_pst", n);
+  uint32_t *parent = c.get_as<uint32_t>("mg_parent", n);
+  uint64_t *edges = c.get_as<uint64_t>("mg_edges", 2 * n);
+  unsigned long long *d = (unsigned long long *)c.d_scalars + 10;
+  HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
+  hipLaunchKernelGGL(k_tree_edges, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, a, b, n, edges, d, pst, d + 1);
+  LAUNCH_CHECK();
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 10, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  if (c.h_scalars[11]) throw Error(SHEEP_ERR_ARG, "merge: a parent is not a later node of the tree");
+  {
+    TimedRegion tr(c, "merge");
+    etree_from_edges(c, edges, c.h_scalars[10], n, parent);
+  }
+  hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);
+  LAUNCH_CHECK();
+}
+
+}  // namespace sheep

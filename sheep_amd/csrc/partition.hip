@@ -1,0 +1,628 @@
+// partition.hip — Partition(seq, jnodes, k, balance, vtx, pst, pre) (partition.cpp:50-67)
+// with forwardPartition (partition.cpp:86-157), and JNodeTable::Facts (jnode.cpp:256-290).
+//
+// forwardPartition walks ids ascending: cb[id] += w(id); if cb[id] > max it std::sorts
+// the kids by cb (descending; the kid table keeps that order for the next k) and
+// first-fit packs unassigned kids into bins until cb[id] <= max; then cb[parent] +=
+// cb[id].  A descending pass pushes parts down and packs roots into the highest bin
+// that fits.
+//
+// GPU formulation:
+//   1. subtree sums S(v) on the GPU (Euler tour + prefix sums; tree_tour.hip);
+//   2. only H = {v : S(v) > max} can ever pack (cb <= S), and H is ancestor-closed;
+//      outside H, cb == S.  The GPU hands the host H in ascending order with
+//      L(v) = w(v) + sum of S over v's non-H kids and the rank of v's parent;
+//   3. the host replays the ascending pass over H only, running the packing steps with
+//      the reference's own std::sort/first-fit on the current kid order (kid segments
+//      of packing nodes are fetched and written back, so the order persists across k);
+//   4. roots are packed host-side in descending id order (cb(root) known);
+//   5. the GPU pushes parts down: every node takes the part of its innermost assigned
+//      ancestor-or-self (assigned = packed kids + roots), found by binary search over
+//      the assigned nodes' Euler-tour intervals (laminar), then re-indexes jnid -> vid.
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "tree_tour.hpp"
+
+namespace sheep {
+namespace {
+
+__global__ void k_weights(const sheep_jnode *__restrict__ tree, uint64_t n, int vtx, int pstw,
+                          uint64_t *__restrict__ w, unsigned long long *__restrict__ total) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  uint64_t s = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
+    uint64_t x = (vtx ? 1ull : 0ull) + (pstw ? (uint64_t)tree[i].pst_weight : 0ull);
+    w[i] = x;
+    s += x;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(total, (unsigned long long)s);
+}
+
+// tour-order value array for a sum channel: val[tU[c]] = up(c), val[tD[c]] = down(c)
+__global__ void k_tour_vals(const uint32_t *__restrict__ tD, const uint32_t *__restrict__ tU, uint64_t n,
+                            const uint64_t *__restrict__ up, const uint64_t *__restrict__ down_or_null,
+                            int mode, uint64_t *__restrict__ val) {
+  // mode 0: D = 0, U = up[c];   mode 1: D = +up[c], U = -up[c];   mode 2: D = +1, U = -1
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t c = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; c < n; c += stride) {
+    uint32_t d = tD[c];
+    if (d == INVALID) continue;
+    uint64_t x = mode == 2 ? 1ull : up[c];
+    if (mode == 0) { val[d] = 0; val[tU[c]] = x; }
+    else { val[d] = x; val[tU[c]] = (uint64_t)0 - x; }
+  }
+}
+
+__global__ void k_subtree(const uint32_t *__restrict__ parent, const uint32_t *__restrict__ tD,
+                          const uint32_t *__restrict__ tU, uint64_t n, const uint64_t *__restrict__ w,
+                          const uint64_t *__restrict__ E, uint64_t *__restrict__ S) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t c = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; c < n; c += stride) {
+    if (parent[c] == INVALID) { S[c] = w[c]; continue; }
+    S[c] = E[tU[c]] + w[c] - E[tD[c]];
+  }
+}
+__global__ void k_root_sums(const uint32_t *__restrict__ parent, uint64_t n, uint64_t *__restrict__ S) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t c = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; c < n; c += stride) {
+    uint32_t p = parent[c];
+    if (p != INVALID && parent[p] == INVALID) atomicAdd((unsigned long long *)&S[p], (unsigned long long)S[c]);
+  }
+}
+
+// order-preserving compaction of {v : pred(v)}, pred 0: S(v) > max (H);  1: root
+constexpr int P_ITEMS = 8, P_TILE = BLOCK * P_ITEMS;
+__device__ __forceinline__ bool pred_of(int which, uint64_t i, const uint64_t *S, uint64_t mx, const uint32_t *parent) {
+  return which == 0 ? S[i] > mx : parent[i] == INVALID;
+}
+__global__ void k_pred_count(int which, const uint64_t *__restrict__ S, uint64_t mx, const uint32_t *__restrict__ parent,
+                             uint64_t n, uint32_t *__restrict__ bcnt) {
+  __shared__ uint32_t s[BLOCK / WAVE];
+  uint64_t base = (uint64_t)blockIdx.x * P_TILE;
+  uint32_t c = 0;
+  for (int j = 0; j < P_ITEMS; ++j) {
+    uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
+    if (i < n && pred_of(which, i, S, mx, parent)) ++c;
+  }
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+__global__ void k_pred_write(int which, const uint64_t *__restrict__ S, uint64_t mx, const uint32_t *__restrict__ parent,
+                             uint64_t n, const uint32_t *__restrict__ boff, uint32_t *__restrict__ ids,
+                             uint32_t *__restrict__ rank) {
+  __shared__ uint32_t wc[BLOCK / WAVE];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t base = (uint64_t)blockIdx.x * P_TILE;
+  uint32_t running = boff[blockIdx.x];
+  for (int j = 0; j < P_ITEMS; ++j) {
+    uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
+    bool f = i < n && pred_of(which, i, S, mx, parent);
+    uint64_t m = __ballot(f);
+    if (lane == 0) wc[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t off = running;
+    for (int w = 0; w < wave; ++w) off += wc[w];
+    if (i < n && rank) rank[i] = f ? off + (uint32_t)__popcll(m & lanemask_lt()) : INVALID;
+    if (f) ids[off + __popcll(m & lanemask_lt())] = (uint32_t)i;
+    running += wc[0] + wc[1] + wc[2] + wc[3];
+    __syncthreads();
+  }
+}
+
+// For H nodes: L = w + sum of non-H kids' S; parent rank.
+__global__ void k_h_init(const uint32_t *__restrict__ hids, uint64_t nh, const uint64_t *__restrict__ w,
+                         const uint32_t *__restrict__ parent, const uint32_t *__restrict__ hrank,
+                         uint64_t *__restrict__ L, uint32_t *__restrict__ hpar) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t h = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; h < nh; h += stride) {
+    uint32_t v = hids[h];
+    L[h] = w[v];
+    uint32_t p = parent[v];
+    hpar[h] = p == INVALID ? INVALID : hrank[p];
+  }
+}
+__global__ void k_h_light(const uint32_t *__restrict__ parent, uint64_t n, const uint32_t *__restrict__ hrank,
+                          const uint64_t *__restrict__ S, uint64_t *__restrict__ L) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t c = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; c < n; c += stride) {
+    uint32_t p = parent[c];
+    if (p == INVALID || hrank[c] != INVALID) continue;
+    uint32_t hp = hrank[p];
+    if (hp != INVALID) atomicAdd((unsigned long long *)&L[hp], (unsigned long long)S[c]);
+  }
+}
+
+// kid segment values for one packing node
+__global__ void k_kid_info(const uint32_t *__restrict__ kids, uint32_t beg, uint32_t cnt,
+                           const uint64_t *__restrict__ S, const uint32_t *__restrict__ hrank,
+                           uint64_t *__restrict__ outS, uint32_t *__restrict__ outH) {
+  for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < cnt; j += gridDim.x * BLOCK) {
+    uint32_t kid = kids[beg + j];
+    outS[j] = S[kid];
+    outH[j] = hrank[kid];
+  }
+}
+
+// interval endpoints for assigned nodes: non-root -> [tD, tU]; root with kids ->
+// [tD(first kid), tU(last kid)]; root without kids -> none (INVALID)
+__global__ void k_intervals(const uint32_t *__restrict__ ids, uint64_t m, const uint32_t *__restrict__ parent,
+                            const uint32_t *__restrict__ koff, const uint32_t *__restrict__ kids,
+                            const uint32_t *__restrict__ tD, const uint32_t *__restrict__ tU,
+                            uint32_t *__restrict__ st, uint32_t *__restrict__ en) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) {
+    uint32_t v = ids[i];
+    if (parent[v] != INVALID) { st[i] = tD[v]; en[i] = tU[v]; }
+    else if (koff[v] < koff[v + 1]) { st[i] = tD[kids[koff[v]]]; en[i] = tU[kids[koff[v + 1] - 1]]; }
+    else { st[i] = INVALID; en[i] = INVALID; }
+  }
+}
+
+__global__ void k_push_down(const uint32_t *__restrict__ parent, const uint32_t *__restrict__ tD, uint64_t n,
+                            const uint32_t *__restrict__ ast, const uint32_t *__restrict__ aen,
+                            const int16_t *__restrict__ apart, const uint32_t *__restrict__ aencl, uint32_t na,
+                            int16_t *__restrict__ parts, unsigned long long *__restrict__ err) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride) {
+    if (parent[v] == INVALID) continue;   // roots are scattered directly
+    uint32_t p = tD[v];
+    uint32_t lo = 0, hi = na;              // last interval with start <= p
+    while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (ast[mid] <= p) lo = mid + 1; else hi = mid; }
+    if (lo == 0) { atomicAdd(err, 1ull); continue; }
+    uint32_t j = lo - 1;
+    while (j != INVALID && aen[j] < p) j = aencl[j];
+    if (j == INVALID) { atomicAdd(err, 1ull); continue; }
+    parts[v] = apart[j];
+  }
+}
+
+__global__ void k_scatter_parts(const uint32_t *__restrict__ ids, const int16_t *__restrict__ pv, uint64_t m,
+                                int16_t *__restrict__ parts) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) parts[ids[i]] = pv[i];
+}
+
+__global__ void k_fill_i16(int16_t *__restrict__ p, uint64_t n, int16_t v) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+
+__global__ void k_parts_to_vid(const uint32_t *__restrict__ seq, uint64_t n, const int16_t *__restrict__ parts,
+                               int16_t *__restrict__ pv, unsigned long long *__restrict__ cnt) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  uint64_t c0 = 0, c1 = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
+    int16_t p = parts[i];
+    pv[seq[i]] = p;
+    c0 += p == 0;
+    c1 += p == 1;
+  }
+  c0 = wave_sum(c0);
+  c1 = wave_sum(c1);
+  if ((threadIdx.x & 63) == 0) {
+    if (c0) atomicAdd(&cnt[0], (unsigned long long)c0);
+    if (c1) atomicAdd(&cnt[1], (unsigned long long)c1);
+  }
+}
+
+// ---- facts ---------------------------------------------------------------------------
+__global__ void k_facts_basic(const sheep_jnode *__restrict__ tree, uint64_t n, unsigned long long *__restrict__ f) {
+  // f[0] = sum pst, f[1] = max pst, f[2] = roots, f[3] = min id with pst > 2 (width > 3)
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  uint64_t s = 0, mx = 0, r = 0, halo = ~0ull;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
+    sheep_jnode j = tree[i];
+    s += j.pst_weight;
+    mx = j.pst_weight > mx ? j.pst_weight : mx;
+    r += j.parent == INVALID;
+    if (j.pst_weight > 2 && i < halo) halo = i;
+  }
+  s = wave_sum(s); mx = wave_max(mx); r = wave_sum(r); halo = wave_min(halo);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&f[0], (unsigned long long)s);
+    atomicMax(&f[1], (unsigned long long)mx);
+    atomicAdd(&f[2], (unsigned long long)r);
+    atomicMin(&f[3], (unsigned long long)halo);
+  }
+}
+// depth(c) = E1[tD] + 1;  path(c) = E2[tD] + pst(c);  per-root best path via the root
+// segment index (roots with kids are chained in ascending order, their starts ascend)
+__global__ void k_facts_paths(const uint32_t *__restrict__ parent, const uint32_t *__restrict__ tD, uint64_t n,
+                              const uint64_t *__restrict__ E1, const uint64_t *__restrict__ E2,
+                              const uint64_t *__restrict__ pst64, const uint32_t *__restrict__ rstart, uint32_t nrk,
+                              unsigned long long *__restrict__ best, unsigned long long *__restrict__ maxdepth) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  uint64_t md = 0;
+  for (uint64_t c = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; c < n; c += stride) {
+    if (parent[c] == INVALID) continue;
+    uint32_t p = tD[c];
+    uint64_t depth = E1[p] + 1;
+    md = depth > md ? depth : md;
+    uint64_t path = E2[p] + pst64[c];
+    uint32_t lo = 0, hi = nrk;
+    while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (rstart[mid] <= p) lo = mid + 1; else hi = mid; }
+    atomicMax(&best[lo - 1], (unsigned long long)path);
+  }
+  md = wave_max(md);
+  if ((threadIdx.x & 63) == 0 && md) atomicMax(maxdepth, (unsigned long long)md);
+}
+__global__ void k_root_starts(const uint32_t *__restrict__ rk, uint64_t nrk, const uint32_t *__restrict__ koff,
+                              const uint32_t *__restrict__ kids, const uint32_t *__restrict__ tD,
+                              uint32_t *__restrict__ rstart) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nrk; i += stride)
+    rstart[i] = tD[kids[koff[rk[i]]]];
+}
+__global__ void k_root_eheight(const uint32_t *__restrict__ rk, uint64_t nrk, const sheep_jnode *__restrict__ tree,
+                               const unsigned long long *__restrict__ best, unsigned long long *__restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  uint64_t m = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nrk; i += stride) {
+    uint64_t e = (uint64_t)tree[rk[i]].pst_weight + best[i];
+    m = e > m ? e : m;
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(out, (unsigned long long)m);
+}
+__global__ void k_pst64(const sheep_jnode *__restrict__ tree, uint64_t n, uint64_t *__restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) out[i] = tree[i].pst_weight;
+}
+
+template <typename T> void d2h(Ctx &c, T *h, const T *d, uint64_t cnt) {
+  if (cnt) HIP_CHECK(hipMemcpyAsync(h, d, cnt * sizeof(T), hipMemcpyDeviceToHost, c.stream));
+}
+template <typename T> void h2d(Ctx &c, T *d, const T *h, uint64_t cnt) {
+  if (cnt) HIP_CHECK(hipMemcpyAsync(d, h, cnt * sizeof(T), hipMemcpyHostToDevice, c.stream));
+}
+
+// order-preserving compaction; returns count; rank optional
+uint64_t compact_pred(Ctx &c, int which, const uint64_t *S, uint64_t mx, const uint32_t *parent, uint64_t n,
+                      uint32_t *ids, uint32_t *rank, const char *tag) {
+  uint64_t nb = (n + P_TILE - 1) / P_TILE;
+  uint32_t *bcnt = c.get_as<uint32_t>(std::string("pc_bcnt_") + tag, nb);
+  hipLaunchKernelGGL(k_pred_count, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, which, S, mx, parent, n, bcnt);
+  LAUNCH_CHECK();
+  uint32_t *tot = (uint32_t *)(c.d_scalars + 30);
+  HIP_CHECK(hipMemsetAsync(c.d_scalars + 30, 0, sizeof(uint64_t), c.stream));
+  scan_exclusive_u32(c, bcnt, bcnt, nb, tot);
+  hipLaunchKernelGGL(k_pred_write, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, which, S, mx, parent, n, bcnt, ids,
+                     rank);
+  LAUNCH_CHECK();
+  d2h(c, c.h_scalars + 30, c.d_scalars + 30, 1);
+  c.sync();
+  return (uint32_t)c.h_scalars[30];
+}
+
+}  // namespace
+
+void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
+
+void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t *seq, uint64_t pos_size,
+                    sheep_kids *k, int16_t np, double balance, int vtx, int pstw, int16_t *parts_vid,
+                    sheep_partition_info *info) {
+  if (np <= 0) throw Error(SHEEP_ERR_ARG, "number of parts must be positive");
+  if (!k || k->n != n) throw Error(SHEEP_ERR_ARG, "kid table does not belong to this tree");
+  *info = sheep_partition_info();
+  if (pos_size) {
+    hipLaunchKernelGGL(k_fill_i16, dim3(grid_for(pos_size)), dim3(BLOCK), 0, c.stream, parts_vid, pos_size,
+                       SHEEP_INVALID_PART);
+    LAUNCH_CHECK();
+  }
+  if (n == 0) { c.sync(); return; }
+  TimedRegion tr_all(c, "partition");
+
+  // 1. weights and max_component (partition.cpp:54-57)
+  uint64_t *w = c.get_as<uint64_t>("pt_w", n);
+  unsigned long long *d = (unsigned long long *)c.d_scalars + 32;
+  HIP_CHECK(hipMemsetAsync(d, 0, 4 * sizeof(uint64_t), c.stream));
+  hipLaunchKernelGGL(k_weights, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, tree, n, vtx, pstw, w, d);
+  LAUNCH_CHECK();
+
+  // 2. Euler tour + subtree sums
+  Tour t;
+  build_tour(c, k, t);
+  d2h(c, c.h_scalars + 32, c.d_scalars + 32, 1);
+  c.sync();
+  const uint64_t total = c.h_scalars[32];
+  const uint64_t max_component = (uint64_t)((double)(total / (uint64_t)(int64_t)np) * balance);
+  info->total_weight = total;
+  info->max_component = max_component;
+  uint64_t *S = c.get_as<uint64_t>("pt_S", n);
+  if (t.A) {
+    uint64_t *val = c.get_as<uint64_t>("pt_tourval", t.A);
+    hipLaunchKernelGGL(k_tour_vals, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, t.tD, t.tU, n, (const uint64_t *)w,
+                       (const uint64_t *)nullptr, 0, val);
+    LAUNCH_CHECK();
+    scan_exclusive_u64(c, val, val, t.A, nullptr);
+    hipLaunchKernelGGL(k_subtree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, k->parent, t.tD, t.tU, n,
+                       (const uint64_t *)w, (const uint64_t *)val, S);
+    LAUNCH_CHECK();
+  } else {
+    HIP_CHECK(hipMemcpyAsync(S, w, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, c.stream));
+  }
+  hipLaunchKernelGGL(k_root_sums, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, k->parent, n, S);
+  LAUNCH_CHECK();
+
+  // 3. heavy set H (ascending), L, parent ranks
+  uint32_t *hids = c.get_as<uint32_t>("pt_hids", n), *hrank = c.get_as<uint32_t>("pt_hrank", n);
+  const uint64_t nh = compact_pred(c, 0, S, max_component, k->parent, n, hids, hrank, "h");
+  info->heavy_nodes = nh;
+  std::vector<uint32_t> h_ids(nh), h_par(nh);
+  std::vector<uint64_t> h_L(nh);
+  if (nh) {
+    uint64_t *L = c.get_as<uint64_t>("pt_L", nh);
+    uint32_t *hpar = c.get_as<uint32_t>("pt_hpar", nh);
+    hipLaunchKernelGGL(k_h_init, dim3(grid_for(nh)), dim3(BLOCK), 0, c.stream, hids, nh, (const uint64_t *)w,
+                       k->parent, hrank, L, hpar);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_h_light, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, k->parent, n, hrank,
+                       (const uint64_t *)S, L);
+    LAUNCH_CHECK();
+    d2h(c, h_ids.data(), hids, nh);
+    d2h(c, h_par.data(), hpar, nh);
+    d2h(c, h_L.data(), L, nh);
+  }
+  // roots (ascending) with S and hrank
+  uint32_t *rids = c.get_as<uint32_t>("pt_roots", n);
+  const uint64_t nroots = compact_pred(c, 1, S, 0, k->parent, n, rids, nullptr, "r");
+  std::vector<uint32_t> r_ids(nroots), r_h(nroots);
+  std::vector<uint64_t> r_S(nroots);
+  {
+    uint64_t *rS = c.get_as<uint64_t>("pt_rS", nroots);
+    uint32_t *rH = c.get_as<uint32_t>("pt_rH", nroots);
+    // gather S (as two u32 halves) and hrank for the roots
+    gather_u32(c, hrank, rids, nroots, rH);
+    std::vector<uint32_t> tmp;
+    d2h(c, r_ids.data(), rids, nroots);
+    d2h(c, r_h.data(), rH, nroots);
+    c.sync();
+    // S for roots: small, fetch individually through a gathered staging buffer
+    std::vector<uint64_t> idx64(nroots);
+    if (nroots) {
+      // stage: rS[i] = S[rids[i]] via 2 x u32 gathers on the S array viewed as u32 pairs
+      uint32_t *lo = c.get_as<uint32_t>("pt_rSlo", nroots), *hi = c.get_as<uint32_t>("pt_rShi", nroots);
+      uint32_t *i2 = c.get_as<uint32_t>("pt_ridx2", 2 * nroots);
+      std::vector<uint32_t> h_i2(2 * nroots);
+      for (uint64_t i = 0; i < nroots; ++i) { h_i2[i] = 2 * r_ids[i]; h_i2[nroots + i] = 2 * r_ids[i] + 1; }
+      h2d(c, i2, h_i2.data(), 2 * nroots);
+      gather_u32(c, (const uint32_t *)S, i2, nroots, lo);
+      gather_u32(c, (const uint32_t *)S, i2 + nroots, nroots, hi);
+      std::vector<uint32_t> hl(nroots), hh(nroots);
+      d2h(c, hl.data(), lo, nroots);
+      d2h(c, hh.data(), hi, nroots);
+      c.sync();
+      for (uint64_t i = 0; i < nroots; ++i) r_S[i] = ((uint64_t)hh[i] << 32) | hl[i];
+    }
+    (void)rS;
+  }
+  c.sync();
+
+  // 4. host replay of the ascending pass over H (partition.cpp:97-135)
+  std::vector<uint64_t> part_size;
+  std::vector<uint64_t> cbH(nh, 0), acc(nh, 0);
+  std::vector<uint32_t> asg_ids;
+  std::vector<int16_t> asg_part;
+  uint64_t *kS = nullptr;
+  uint32_t *kH = nullptr;
+  std::vector<uint32_t> seg, segH;
+  std::vector<uint64_t> segS;
+  std::vector<uint32_t> koff_pair(2);
+  for (uint64_t h = 0; h < nh; ++h) {
+    uint64_t cb = h_L[h] + acc[h];
+    const uint32_t v = h_ids[h];
+    if (cb > max_component) {
+      info->packing_nodes++;
+      d2h(c, koff_pair.data(), k->koff + v, 2);
+      c.sync();
+      const uint32_t beg = koff_pair[0], cnt = koff_pair[1] - koff_pair[0];
+      seg.resize(cnt); segH.resize(cnt); segS.resize(cnt);
+      if (cnt) {
+        kS = c.get_as<uint64_t>("pt_kS", cnt);
+        kH = c.get_as<uint32_t>("pt_kH", cnt);
+        hipLaunchKernelGGL(k_kid_info, dim3(grid_for(cnt)), dim3(BLOCK), 0, c.stream, k->kids, beg, cnt,
+                           (const uint64_t *)S, hrank, kS, kH);
+        LAUNCH_CHECK();
+        d2h(c, seg.data(), k->kids + beg, cnt);
+        d2h(c, segS.data(), kS, cnt);
+        d2h(c, segH.data(), kH, cnt);
+        c.sync();
+      }
+      // cb of each kid: final cb for H kids (already processed: kid < v), S otherwise
+      std::vector<uint64_t> kidcb(cnt);
+      std::vector<uint32_t> order(cnt);
+      for (uint32_t j = 0; j < cnt; ++j) {
+        kidcb[j] = segH[j] != INVALID ? cbH[segH[j]] : segS[j];
+        order[j] = j;
+      }
+      // std::sort on the current kid order with the reference comparator (:104-106).
+      // Sorting indices with a comparator on kidcb is the same sort on the same keys.
+      std::sort(order.begin(), order.end(), [&kidcb](uint32_t a, uint32_t b) { return kidcb[a] > kidcb[b]; });
+      std::vector<uint32_t> sorted(cnt);
+      std::vector<uint64_t> scb(cnt);
+      for (uint32_t j = 0; j < cnt; ++j) { sorted[j] = seg[order[j]]; scb[j] = kidcb[order[j]]; }
+      h2d(c, k->kids + beg, sorted.data(), cnt);
+      std::vector<char> done(cnt, 0);
+      do {
+        for (uint32_t j = 0; cb > max_component && j < cnt; ++j) {
+          if (scb[j] > max_component) throw Error(SHEEP_ERR_PACK, "forwardPartition: kid exceeds max_component");
+          if (done[j]) continue;
+          for (size_t p = 0; p != part_size.size(); ++p) {
+            if (part_size[p] + scb[j] <= max_component) {
+              cb -= scb[j];
+              part_size[p] += scb[j];
+              done[j] = 1;
+              asg_ids.push_back(sorted[j]);
+              asg_part.push_back((int16_t)p);
+              break;
+            }
+          }
+        }
+        if (cb > max_component) {
+          bool any = false;
+          for (uint32_t j = 0; j < cnt; ++j) any |= !done[j];
+          if (!any || part_size.size() >= 32767)
+            throw Error(SHEEP_ERR_PACK, "forwardPartition: node weight exceeds max_component (reference loops forever)");
+          part_size.push_back(0);
+        }
+      } while (cb > max_component);
+    }
+    cbH[h] = cb;
+    if (h_par[h] != INVALID) acc[h_par[h]] += cb;
+  }
+  // 5. descending pass: roots into the highest bin that fits (:146-152)
+  std::vector<int16_t> root_part(nroots);
+  for (uint64_t ri = nroots; ri-- > 0;) {
+    uint64_t cb = r_h[ri] != INVALID ? cbH[r_h[ri]] : r_S[ri];
+    int16_t got = -1;
+    while (got < 0) {
+      for (long p = (long)part_size.size() - 1; p != -1; --p) {
+        if (part_size[p] + cb <= max_component) { part_size[p] += cb; got = (int16_t)p; break; }
+      }
+      if (got < 0) {
+        if (part_size.size() >= 32767) throw Error(SHEEP_ERR_PACK, "forwardPartition: root cannot be packed");
+        part_size.push_back(0);
+      }
+    }
+    root_part[ri] = got;
+  }
+  info->created = (int32_t)part_size.size();
+
+  // 6. push down: assigned = packed kids + roots, as laminar tour intervals
+  const uint64_t na = asg_ids.size() + nroots;
+  std::vector<uint32_t> all_ids(asg_ids);
+  all_ids.insert(all_ids.end(), r_ids.begin(), r_ids.end());
+  std::vector<int16_t> all_part(asg_part);
+  all_part.insert(all_part.end(), root_part.begin(), root_part.end());
+  int16_t *parts = c.get_as<int16_t>("pt_parts", n);
+  {
+    uint32_t *aid = c.get_as<uint32_t>("pt_aid", na);
+    int16_t *ap = c.get_as<int16_t>("pt_ap", na);
+    h2d(c, aid, all_ids.data(), na);
+    h2d(c, ap, all_part.data(), na);
+    hipLaunchKernelGGL(k_scatter_parts, dim3(grid_for(na)), dim3(BLOCK), 0, c.stream, aid, ap, na, parts);
+    LAUNCH_CHECK();
+    uint32_t *st = c.get_as<uint32_t>("pt_ast", na), *en = c.get_as<uint32_t>("pt_aen", na);
+    hipLaunchKernelGGL(k_intervals, dim3(grid_for(na)), dim3(BLOCK), 0, c.stream, aid, na, k->parent, k->koff,
+                       k->kids, t.tD, t.tU, st, en);
+    LAUNCH_CHECK();
+    std::vector<uint32_t> hs(na), he(na);
+    d2h(c, hs.data(), st, na);
+    d2h(c, he.data(), en, na);
+    c.sync();
+    std::vector<uint32_t> ord;
+    ord.reserve(na);
+    for (uint32_t i = 0; i < na; ++i) if (hs[i] != INVALID) ord.push_back(i);
+    std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
+      return hs[a] != hs[b] ? hs[a] < hs[b] : he[a] > he[b];
+    });
+    const uint32_t m = (uint32_t)ord.size();
+    std::vector<uint32_t> sst(m), sen(m), encl(m);
+    std::vector<int16_t> sp(m);
+    std::vector<uint32_t> stack;
+    for (uint32_t i = 0; i < m; ++i) {
+      sst[i] = hs[ord[i]]; sen[i] = he[ord[i]]; sp[i] = all_part[ord[i]];
+      while (!stack.empty() && sen[stack.back()] < sst[i]) stack.pop_back();
+      encl[i] = stack.empty() ? INVALID : stack.back();
+      stack.push_back(i);
+    }
+    if (m) {
+      uint32_t *dst_ = c.get_as<uint32_t>("pt_sst", m), *den = c.get_as<uint32_t>("pt_sen", m);
+      uint32_t *dencl = c.get_as<uint32_t>("pt_encl", m);
+      int16_t *dsp = c.get_as<int16_t>("pt_sp", m);
+      h2d(c, dst_, sst.data(), m);
+      h2d(c, den, sen.data(), m);
+      h2d(c, dencl, encl.data(), m);
+      h2d(c, dsp, sp.data(), m);
+      unsigned long long *e = (unsigned long long *)c.d_scalars + 36;
+      HIP_CHECK(hipMemsetAsync(e, 0, sizeof(uint64_t), c.stream));
+      hipLaunchKernelGGL(k_push_down, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, k->parent, t.tD, n, dst_, den, dsp,
+                         dencl, m, parts, e);
+      LAUNCH_CHECK();
+      d2h(c, c.h_scalars + 36, c.d_scalars + 36, 1);
+    }
+  }
+  // 7. jnid -> vid (:62-66) and print counts (partition.h:138-139)
+  unsigned long long *cnt = (unsigned long long *)c.d_scalars + 38;
+  HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(uint64_t), c.stream));
+  hipLaunchKernelGGL(k_parts_to_vid, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, seq, n, parts, parts_vid, cnt);
+  LAUNCH_CHECK();
+  d2h(c, c.h_scalars + 38, c.d_scalars + 38, 2);
+  c.sync();
+  if (asg_ids.size() + nroots && c.h_scalars[36]) throw Error(SHEEP_ERR_HIP, "partition push-down: unassigned node");
+  info->first_size = c.h_scalars[38];
+  info->second_size = c.h_scalars[39];
+}
+
+void tree_facts(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_facts_t *out) {
+  *out = sheep_facts_t();
+  out->halo_id = INVALID;
+  out->core_id = INVALID;
+  if (n == 0) return;
+  unsigned long long *f = (unsigned long long *)c.d_scalars + 40;
+  HIP_CHECK(hipMemsetAsync(f, 0, 8 * sizeof(uint64_t), c.stream));
+  HIP_CHECK(hipMemsetAsync(f + 3, 0xFF, sizeof(uint64_t), c.stream));
+  hipLaunchKernelGGL(k_facts_basic, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, tree, n, f);
+  LAUNCH_CHECK();
+  sheep_kids k;
+  build_kids(c, tree, n, &k);
+  Tour t;
+  uint64_t maxdepth = 0, eheight = 0;
+  try {
+    build_tour(c, &k, t);
+    uint64_t *pst64 = c.get_as<uint64_t>("fx_pst", n);
+    hipLaunchKernelGGL(k_pst64, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, tree, n, pst64);
+    LAUNCH_CHECK();
+    unsigned long long *best = nullptr;
+    if (t.A) {
+      uint64_t *E1 = c.get_as<uint64_t>("fx_E1", t.A), *E2 = c.get_as<uint64_t>("fx_E2", t.A);
+      hipLaunchKernelGGL(k_tour_vals, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, t.tD, t.tU, n,
+                         (const uint64_t *)pst64, (const uint64_t *)nullptr, 2, E1);
+      LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_tour_vals, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, t.tD, t.tU, n,
+                         (const uint64_t *)pst64, (const uint64_t *)nullptr, 1, E2);
+      LAUNCH_CHECK();
+      scan_exclusive_u64(c, E1, E1, t.A, nullptr);
+      scan_exclusive_u64(c, E2, E2, t.A, nullptr);
+      uint32_t *rstart = c.get_as<uint32_t>("fx_rstart", t.nrk);
+      hipLaunchKernelGGL(k_root_starts, dim3(grid_for(t.nrk)), dim3(BLOCK), 0, c.stream, t.rk, t.nrk, k.koff, k.kids,
+                         t.tD, rstart);
+      LAUNCH_CHECK();
+      best = c.get_as<unsigned long long>("fx_best", t.nrk);
+      HIP_CHECK(hipMemsetAsync(best, 0, t.nrk * sizeof(uint64_t), c.stream));
+      hipLaunchKernelGGL(k_facts_paths, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, k.parent, t.tD, n,
+                         (const uint64_t *)E1, (const uint64_t *)E2, (const uint64_t *)pst64, rstart,
+                         (uint32_t)t.nrk, best, f + 4);
+      LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_root_eheight, dim3(grid_for(t.nrk)), dim3(BLOCK), 0, c.stream, t.rk, t.nrk, tree,
+                         (const unsigned long long *)best, f + 5);
+      LAUNCH_CHECK();
+    }
+    HIP_CHECK(hipMemcpyAsync(c.h_scalars + 40, c.d_scalars + 40, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+    maxdepth = c.h_scalars[44];
+    eheight = c.h_scalars[45];
+  } catch (...) {
+    hipFree(k.parent); hipFree(k.koff); hipFree(k.kids);
+    throw;
+  }
+  HIP_CHECK(hipFree(k.parent)); HIP_CHECK(hipFree(k.koff)); HIP_CHECK(hipFree(k.kids));
+  const uint64_t sum = c.h_scalars[40], mx = c.h_scalars[41], roots = c.h_scalars[42], halo = c.h_scalars[43];
+  out->vert_cnt = n;
+  out->edge_cnt = sum;
+  out->width = 1 + mx;
+  out->fill = 0;
+  out->root_cnt = roots;
+  out->vert_height = maxdepth + 1;   // a root alone has vheight 1
+  // kidless roots: eheight = own pst
+  out->edge_height = eheight;
+  out->halo_id = halo == ~0ull ? INVALID : halo;
+  out->core_id = 0;
+}
+
+}  // namespace sheep

@@ -1,0 +1,156 @@
+// radix.hip — stable LSD radix sort (8-bit digits) for the degree sequence
+// (key = degree, value = vid), the kid table (key = parent, value = id) and the RMAT
+// generator's dedup (64-bit keys).
+//
+// Per pass: (1) per-tile digit histogram, (2) exclusive scan of the digit-major
+// histogram, (3) per-tile stable ranking with wave ballots (64-lane peer masks),
+// LDS staging into tile-sorted order, then contiguous-run stores.
+#include "common.hpp"
+
+namespace sheep {
+namespace {
+
+constexpr int R_ITEMS = 16;
+constexpr int R_TILE = BLOCK * R_ITEMS;   // 4096 keys per workgroup
+constexpr int RADIX = 256;
+
+// 64-lane mask of the valid lanes whose digit equals mine.
+__device__ __forceinline__ uint64_t digit_peers(bool valid, uint32_t d) {
+  uint64_t peers = __ballot(valid);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    bool bit = (d >> b) & 1;
+    uint64_t bb = __ballot(bit);
+    peers &= bit ? bb : ~bb;
+  }
+  return peers;
+}
+
+template <typename K>
+__global__ __launch_bounds__(BLOCK) void k_hist(const K *__restrict__ keys, uint64_t n, int shift,
+                                                uint32_t ntiles, uint32_t *__restrict__ hist) {
+  __shared__ uint32_t h[RADIX];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t base = (uint64_t)blockIdx.x * R_TILE;
+  for (int j = 0; j < R_ITEMS; ++j) {
+    uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
+    bool valid = i < n;
+    uint32_t d = valid ? (uint32_t)((keys[i] >> shift) & (RADIX - 1)) : 0;
+    uint64_t peers = digit_peers(valid, d);
+    if (valid && (peers & lanemask_lt()) == 0) atomicAdd(&h[d], (uint32_t)__popcll(peers));
+  }
+  __syncthreads();
+  hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+template <typename K, bool VALS>
+__global__ __launch_bounds__(BLOCK) void k_scatter(const K *__restrict__ kin, const uint32_t *__restrict__ vin,
+                                                   K *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                   uint64_t n, int shift, uint32_t ntiles,
+                                                   const uint32_t *__restrict__ offsets) {
+  __shared__ uint32_t run[RADIX];
+  __shared__ uint32_t wcnt[BLOCK / WAVE][RADIX];
+  __shared__ uint32_t dstart[RADIX];
+  __shared__ uint32_t wtot[BLOCK / WAVE];
+  __shared__ K skeys[R_TILE];
+  __shared__ uint32_t svals[VALS ? R_TILE : 1];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  run[t] = 0;
+  for (int w = 0; w < BLOCK / WAVE; ++w) wcnt[w][t] = 0;
+  __syncthreads();
+
+  const uint64_t base = (uint64_t)blockIdx.x * R_TILE;
+  K key[R_ITEMS];
+  uint32_t val[R_ITEMS];
+  uint32_t rank[R_ITEMS];
+  for (int j = 0; j < R_ITEMS; ++j) {
+    uint64_t i = base + (uint64_t)j * BLOCK + t;
+    bool valid = i < n;
+    key[j] = valid ? kin[i] : K(0);
+    if (VALS) val[j] = valid ? vin[i] : 0u;
+    uint32_t d = (uint32_t)((key[j] >> shift) & (RADIX - 1));
+    uint64_t peers = digit_peers(valid, d);
+    uint32_t lrank = (uint32_t)__popcll(peers & lanemask_lt());
+    if (valid && lrank == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    if (valid) {
+      uint32_t before = run[d];
+      for (int w = 0; w < wave; ++w) before += wcnt[w][d];
+      rank[j] = before + lrank;
+    }
+    __syncthreads();
+    uint32_t add = 0;
+    for (int w = 0; w < BLOCK / WAVE; ++w) { add += wcnt[w][t]; wcnt[w][t] = 0; }
+    run[t] += add;
+    __syncthreads();
+  }
+  // tile-local digit starts (exclusive scan of run[] over the 256 digits)
+  uint32_t v = run[t], inc = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) wtot[wave] = inc;
+  __syncthreads();
+  uint32_t woff = 0;
+  for (int w = 0; w < wave; ++w) woff += wtot[w];
+  dstart[t] = woff + inc - v;
+  __syncthreads();
+  for (int j = 0; j < R_ITEMS; ++j) {
+    uint64_t i = base + (uint64_t)j * BLOCK + t;
+    if (i < n) {
+      uint32_t d = (uint32_t)((key[j] >> shift) & (RADIX - 1));
+      uint32_t lp = dstart[d] + rank[j];
+      skeys[lp] = key[j];
+      if (VALS) svals[lp] = val[j];
+    }
+  }
+  __syncthreads();
+  uint32_t cnt = (uint32_t)((n - base) < (uint64_t)R_TILE ? (n - base) : (uint64_t)R_TILE);
+  for (uint32_t idx = t; idx < cnt; idx += BLOCK) {
+    K k = skeys[idx];
+    uint32_t d = (uint32_t)((k >> shift) & (RADIX - 1));
+    uint64_t g = (uint64_t)offsets[(uint64_t)d * ntiles + blockIdx.x] + (idx - dstart[d]);
+    kout[g] = k;
+    if (VALS) vout[g] = svals[idx];
+  }
+}
+
+template <typename K, bool VALS>
+void radix_sort_impl(Ctx &c, K *keys, uint32_t *vals, uint64_t n, int end_bit, K *kalt, uint32_t *valt) {
+  if (n <= 1 || end_bit <= 0) return;
+  if (n >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "radix sort: n >= 2^32");
+  uint32_t ntiles = (uint32_t)((n + R_TILE - 1) / R_TILE);
+  uint32_t *hist = c.get_as<uint32_t>("radix_hist", (uint64_t)RADIX * ntiles);
+  K *src = keys, *dst = kalt;
+  uint32_t *vs = vals, *vd = valt;
+  int passes = 0;
+  for (int shift = 0; shift < end_bit; shift += 8, ++passes) {
+    hipLaunchKernelGGL(k_hist<K>, dim3(ntiles), dim3(BLOCK), 0, c.stream, (const K *)src, n, shift, ntiles, hist);
+    LAUNCH_CHECK();
+    scan_exclusive_u32(c, hist, hist, (uint64_t)RADIX * ntiles, nullptr);
+    hipLaunchKernelGGL((k_scatter<K, VALS>), dim3(ntiles), dim3(BLOCK), 0, c.stream, (const K *)src,
+                       (const uint32_t *)vs, dst, vd, n, shift, ntiles, (const uint32_t *)hist);
+    LAUNCH_CHECK();
+    std::swap(src, dst);
+    std::swap(vs, vd);
+  }
+  if (src != keys) {
+    HIP_CHECK(hipMemcpyAsync(keys, src, n * sizeof(K), hipMemcpyDeviceToDevice, c.stream));
+    if (VALS) HIP_CHECK(hipMemcpyAsync(vals, vs, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
+  }
+}
+
+}  // namespace
+
+void radix_sort_pairs_u32(Ctx &c, uint32_t *keys, uint32_t *vals, uint64_t n, int end_bit,
+                          uint32_t *keys_alt, uint32_t *vals_alt) {
+  radix_sort_impl<uint32_t, true>(c, keys, vals, n, end_bit, keys_alt, vals_alt);
+}
+void radix_sort_keys_u64(Ctx &c, uint64_t *keys, uint64_t n, int end_bit, uint64_t *keys_alt) {
+  radix_sort_impl<uint64_t, false>(c, keys, nullptr, n, end_bit, keys_alt, nullptr);
+}
+
+}  // namespace sheep

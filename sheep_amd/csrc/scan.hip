@@ -1,0 +1,114 @@
+// scan.hip — device-wide exclusive prefix sums (reduce -> scan block sums -> apply).
+// Tiles of 256 threads x 8 items staged through LDS; coalesced (striped) global
+// loads/stores, blocked per-thread sums, wave shuffles for the block scan.
+#include "common.hpp"
+
+namespace sheep {
+namespace {
+
+constexpr int SCAN_ITEMS = 8;
+constexpr int SCAN_TILE = BLOCK * SCAN_ITEMS;
+
+template <typename T> __device__ __forceinline__ T block_exclusive_scan(T v, T *lds_wave, T &block_total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  T inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) lds_wave[wave] = inc;
+  __syncthreads();
+  T wave_off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < BLOCK / WAVE; ++w) {
+    T s = lds_wave[w];
+    if (w < wave) wave_off += s;
+    tot += s;
+  }
+  block_total = tot;
+  return wave_off + inc - v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(BLOCK) void k_reduce(const T *__restrict__ in, uint64_t n, T *__restrict__ sums) {
+  __shared__ T lds[BLOCK / WAVE];
+  uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+  T s = 0;
+#pragma unroll
+  for (int j = 0; j < SCAN_ITEMS; ++j) {
+    uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
+    if (i < n) s += in[i];
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T t = 0;
+    for (int w = 0; w < BLOCK / WAVE; ++w) t += lds[w];
+    sums[blockIdx.x] = t;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(BLOCK) void k_apply(const T *__restrict__ in, T *__restrict__ out, uint64_t n,
+                                                 const T *__restrict__ block_off, T *__restrict__ total) {
+  __shared__ T tile[SCAN_TILE];
+  __shared__ T lds_wave[BLOCK / WAVE];
+  uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+#pragma unroll
+  for (int j = 0; j < SCAN_ITEMS; ++j) {
+    uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
+    tile[j * BLOCK + threadIdx.x] = i < n ? in[i] : T(0);
+  }
+  __syncthreads();
+  T local[SCAN_ITEMS];
+  T s = 0;
+#pragma unroll
+  for (int j = 0; j < SCAN_ITEMS; ++j) { local[j] = tile[threadIdx.x * SCAN_ITEMS + j]; s += local[j]; }
+  T block_total;
+  T ex = block_exclusive_scan(s, lds_wave, block_total);
+  T off = block_off ? block_off[blockIdx.x] : T(0);
+  ex += off;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < SCAN_ITEMS; ++j) { tile[threadIdx.x * SCAN_ITEMS + j] = ex; ex += local[j]; }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < SCAN_ITEMS; ++j) {
+    uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
+    if (i < n) out[i] = tile[j * BLOCK + threadIdx.x];
+  }
+  if (total && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *total = off + block_total;
+}
+
+template <typename T>
+void scan_rec(Ctx &c, const T *in, T *out, uint64_t n, T *total_dev, int depth) {
+  if (n == 0) {
+    if (total_dev) HIP_CHECK(hipMemsetAsync(total_dev, 0, sizeof(T), c.stream));
+    return;
+  }
+  uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+  if (nb > 0x7FFFFFFFull) throw Error(SHEEP_ERR_ARG, "scan too large");
+  T *sums = nullptr;
+  if (nb > 1) {
+    sums = c.get_as<T>("scan_sums_" + std::to_string(depth) + (sizeof(T) == 8 ? "_64" : "_32"), nb);
+    hipLaunchKernelGGL(k_reduce<T>, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, in, n, sums);
+    LAUNCH_CHECK();
+    scan_rec<T>(c, sums, sums, nb, nullptr, depth + 1);
+  }
+  hipLaunchKernelGGL(k_apply<T>, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, in, out, n,
+                     (const T *)sums, total_dev);
+  LAUNCH_CHECK();
+}
+
+}  // namespace
+
+void scan_exclusive_u32(Ctx &c, const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total_dev) {
+  scan_rec<uint32_t>(c, in, out, n, total_dev, 0);
+}
+void scan_exclusive_u64(Ctx &c, const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *total_dev) {
+  scan_rec<uint64_t>(c, in, out, n, total_dev, 0);
+}
+
+}  // namespace sheep

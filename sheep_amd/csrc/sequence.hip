@@ -1,0 +1,175 @@
+// sequence.hip — degree counting and the (degree, vid) degree sequence.
+//
+//   k_degree            sequence.h:70-78 (mpiSequence local degrees = LLAMA out_degree:
+//                       self-loop once, graph_wrapper.h:87-89) and sequence.h:99-107
+//                       (fileSequence: +1 per endpoint per record; XS1 last record twice)
+//   k_compact_*         sequence.h:80-83 (slots with degree != 0, ascending vid)
+//   radix_sort_pairs    sequence.h:85-91 (sort by degree; stable, so ties keep vid order)
+//   k_scatter_pos       jtree.h:113,142-143 (vid -> jnid index; INVALID elsewhere)
+//
+// Layout in HBM: records are the 12-byte XS1 AoS exactly as on disk; degree/pos are
+// dense u32 arrays over vertex slots; seq is a dense u32 array over jnids.
+#include "common.hpp"
+
+namespace sheep {
+namespace {
+
+__global__ __launch_bounds__(BLOCK) void k_degree(const sheep_xs1 *__restrict__ rec, uint64_t nrec, int mode,
+                                                  uint32_t *__restrict__ deg, uint64_t cap,
+                                                  unsigned long long *__restrict__ d_max,
+                                                  unsigned long long *__restrict__ d_err) {
+  uint32_t lmax = 0;
+  bool bad = false;
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nrec; i += stride) {
+    sheep_xs1 r = rec[i];
+    uint32_t t = r.tail, h = r.head;
+    if (t >= cap || h >= cap) { bad = true; continue; }
+    uint32_t inc = (mode == SHEEP_DEGREE_FILE_DAT && i == nrec - 1) ? 2u : 1u;
+    if (mode == SHEEP_DEGREE_LLAMA && t == h) {
+      atomicAdd(&deg[t], 1u);
+    } else {
+      atomicAdd(&deg[t], inc);
+      atomicAdd(&deg[h], inc);
+    }
+    uint32_t m = (t > h ? t : h) + 1;
+    lmax = m > lmax ? m : lmax;
+  }
+  lmax = wave_max(lmax);
+  if ((threadIdx.x & 63) == 0 && lmax) atomicMax(d_max, (unsigned long long)lmax);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(d_err, 1ull);
+}
+
+constexpr int C_ITEMS = 8;
+constexpr int C_TILE = BLOCK * C_ITEMS;
+
+__global__ __launch_bounds__(BLOCK) void k_compact_count(const uint32_t *__restrict__ deg, uint64_t vs,
+                                                         uint32_t *__restrict__ block_cnt,
+                                                         unsigned long long *__restrict__ d_maxdeg) {
+  __shared__ uint32_t s[BLOCK / WAVE];
+  uint64_t base = (uint64_t)blockIdx.x * C_TILE;
+  uint32_t cnt = 0, mx = 0;
+  for (int j = 0; j < C_ITEMS; ++j) {
+    uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
+    if (i < vs) { uint32_t d = deg[i]; cnt += d != 0; mx = d > mx ? d : mx; }
+  }
+  cnt = wave_sum(cnt);
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) { s[threadIdx.x >> 6] = cnt; if (mx) atomicMax(d_maxdeg, (unsigned long long)mx); }
+  __syncthreads();
+  if (threadIdx.x == 0) block_cnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+
+// Order-preserving compaction: (key = degree, value = vid) for every non-zero slot.
+__global__ __launch_bounds__(BLOCK) void k_compact_write(const uint32_t *__restrict__ deg, uint64_t vs,
+                                                         const uint32_t *__restrict__ block_off,
+                                                         uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+  __shared__ uint32_t wcount[BLOCK / WAVE];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t base = (uint64_t)blockIdx.x * C_TILE;
+  uint32_t running = block_off[blockIdx.x];
+  for (int j = 0; j < C_ITEMS; ++j) {
+    uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
+    uint32_t d = i < vs ? deg[i] : 0;
+    uint64_t m = __ballot(d != 0);
+    if (lane == 0) wcount[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t off = running;
+    for (int w = 0; w < wave; ++w) off += wcount[w];
+    if (d != 0) {
+      uint32_t o = off + (uint32_t)__popcll(m & lanemask_lt());
+      keys[o] = d;
+      vals[o] = (uint32_t)i;
+    }
+    running += wcount[0] + wcount[1] + wcount[2] + wcount[3];
+    __syncthreads();
+  }
+}
+
+__global__ void k_fill_u32(uint32_t *p, uint64_t n, uint32_t v) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+
+__global__ void k_scatter_pos(const uint32_t *__restrict__ seq, uint64_t n, uint32_t *__restrict__ pos) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) pos[seq[i]] = (uint32_t)i;
+}
+
+// readSequence path: arbitrary vids; detect out-of-range and duplicates.
+__global__ void k_scatter_pos_checked(const uint32_t *__restrict__ seq, uint64_t n, uint32_t *__restrict__ pos,
+                                      uint64_t pos_size, unsigned long long *__restrict__ d_err) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
+    uint32_t v = seq[i];
+    if (v >= pos_size) { atomicAdd(d_err, 1ull); continue; }
+    if (atomicExch(&pos[v], (uint32_t)i) != INVALID) atomicAdd(d_err, 1ull);
+  }
+}
+
+}  // namespace
+
+void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_fill_u32, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, p, n, v);
+  LAUNCH_CHECK();
+}
+
+void degree_count(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap,
+                  uint64_t *max_slot) {
+  if (mode < 0 || mode > 2) throw Error(SHEEP_ERR_ARG, "bad degree mode");
+  unsigned long long *d = (unsigned long long *)c.d_scalars;
+  HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
+  if (nrec) {
+    TimedRegion tr(c, "degree");
+    hipLaunchKernelGGL(k_degree, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, mode, deg, cap, d, d + 1);
+    LAUNCH_CHECK();
+  }
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  if (c.h_scalars[1]) throw Error(SHEEP_ERR_RANGE, "degree count: vertex id >= degree capacity");
+  *max_slot = c.h_scalars[0];
+}
+
+uint64_t sequence_from_degrees(Ctx &c, const uint32_t *deg, uint64_t vs, uint32_t *seq, uint32_t *pos) {
+  TimedRegion tr(c, "sequence");
+  fill_u32(c, pos, vs, INVALID);
+  if (vs == 0) return 0;
+  uint64_t nb = (vs + C_TILE - 1) / C_TILE;
+  uint32_t *bcnt = c.get_as<uint32_t>("seq_bcnt", nb + 1);
+  unsigned long long *d = (unsigned long long *)c.d_scalars;
+  HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
+  hipLaunchKernelGGL(k_compact_count, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, deg, vs, bcnt, d);
+  LAUNCH_CHECK();
+  scan_exclusive_u32(c, bcnt, bcnt, nb, (uint32_t *)(c.d_scalars + 1));
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  uint64_t maxdeg = c.h_scalars[0];
+  uint64_t n = (uint32_t)c.h_scalars[1];
+  if (n == 0) return 0;
+  uint32_t *keys = c.get_as<uint32_t>("seq_keys", n), *kalt = c.get_as<uint32_t>("seq_kalt", n);
+  uint32_t *valt = c.get_as<uint32_t>("seq_valt", n);
+  hipLaunchKernelGGL(k_compact_write, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, deg, vs, bcnt, keys, seq);
+  LAUNCH_CHECK();
+  int bits = 0;
+  while (bits < 32 && (maxdeg >> bits)) ++bits;
+  radix_sort_pairs_u32(c, keys, seq, n, bits, kalt, valt);
+  hipLaunchKernelGGL(k_scatter_pos, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, seq, n, pos);
+  LAUNCH_CHECK();
+  return n;
+}
+
+void positions(Ctx &c, const uint32_t *seq, uint64_t n, uint32_t *pos, uint64_t pos_size) {
+  fill_u32(c, pos, pos_size, INVALID);
+  unsigned long long *d = (unsigned long long *)c.d_scalars;
+  HIP_CHECK(hipMemsetAsync(d, 0, sizeof(uint64_t), c.stream));
+  if (n) {
+    hipLaunchKernelGGL(k_scatter_pos_checked, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, seq, n, pos, pos_size, d);
+    LAUNCH_CHECK();
+  }
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars, d, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  if (c.h_scalars[0]) throw Error(SHEEP_ERR_ARG, "sequence has duplicate or out-of-range vids");
+}
+
+}  // namespace sheep

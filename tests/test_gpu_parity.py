@@ -1,0 +1,164 @@
+"""GPU parity: every stage of the HIP path, called through the C ABI, against the
+reference's golden fixtures (tests/golden, produced by oracle/_ref) and, at sizes the
+golden files do not cover, against the CPU oracle.  Bit-exact throughout (integer /
+index work)."""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import (GRAPHS, golden_part_text, golden_parts, golden_records, golden_seq, golden_tree, ks)
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev_records(rec):
+    import sheep_amd
+    return sheep_amd.records_to_device(rec["tail"], rec["head"], rec["weight"])
+
+
+def _tree_np(tree):
+    import sheep_amd
+    return sheep_amd.tree_to_numpy(tree)
+
+
+@pytest.mark.parametrize("scale,seed", [(10, 10), (14, 14), (17, 3)])
+def test_rmat_gpu_matches_host(gpu_ctx, scale, seed):
+    import sheep_amd
+    d = sheep_amd.to_numpy_u32(sheep_amd.rmat(scale, 16, seed)).reshape(-1, 3)
+    h = sheep_amd.rmat_host(scale, 16, seed)
+    assert d.shape == h.shape and np.array_equal(d, h)
+
+
+@pytest.mark.parametrize("name", GRAPHS)
+@pytest.mark.parametrize("mode,kind", [("llama", "seq"), ("dat", "fileseq")])
+def test_degree_sequence(gpu_ctx, name, mode, kind):
+    import sheep_amd
+    rec = golden_records(name)
+    s = sheep_amd.degree_sequence(_dev_records(rec), mode=mode)
+    assert np.array_equal(s.numpy(), golden_seq(name, kind))
+    # pos is the inverse permutation, INVALID on degree-0 slots
+    pos = sheep_amd.to_numpy_u32(s.pos[: s.pos_size])
+    seq = s.numpy()
+    assert np.array_equal(pos[seq], np.arange(len(seq), dtype=np.uint32))
+    assert np.count_nonzero(pos != 0xFFFFFFFF) == len(seq)
+
+
+@pytest.mark.parametrize("name", GRAPHS)
+def test_tree(gpu_ctx, name):
+    import sheep_amd
+    rec = golden_records(name)
+    s = sheep_amd.sequence_from_host(golden_seq(name))
+    p, w = _tree_np(sheep_amd.build_tree(_dev_records(rec), s))
+    gp, gw = golden_tree(name)
+    assert np.array_equal(p, gp), "parent"
+    assert np.array_equal(w, gw), "pst_weight"
+
+
+@pytest.mark.parametrize("name", GRAPHS)
+def test_partial_trees_and_merge(gpu_ctx, name):
+    """graph2tree -l 1/2, 2/2 (contiguous record halves) + merge_trees."""
+    import sheep_amd
+    rec = golden_records(name)
+    R = len(rec)
+    s = sheep_amd.sequence_from_host(golden_seq(name))
+    d = _dev_records(rec)
+    trees = []
+    for part, which in ((1, "h1.tre"), (2, "h2.tre")):
+        beg, end = (part - 1) * R // 2, part * R // 2
+        t = sheep_amd.build_tree(d[beg:end], s)
+        p, w = _tree_np(t)
+        gp, gw = golden_tree(name, which)
+        assert np.array_equal(p, gp) and np.array_equal(w, gw), which
+        trees.append(t)
+    p, w = _tree_np(sheep_amd.merge_trees(*trees))
+    gp, gw = golden_tree(name, "merge.tre")
+    assert np.array_equal(p, gp) and np.array_equal(w, gw)
+
+
+@pytest.mark.parametrize("name", GRAPHS)
+def test_partition_evaluate_facts(gpu_ctx, name):
+    """partition_tree -f -g SEQ TREE k1 k2 ...: one kid table for all k (the FFD sort
+    order persists across k), printed lines byte-exact."""
+    import sheep_amd
+    rec = golden_records(name)
+    s = sheep_amd.sequence_from_host(golden_seq(name))
+    gp, gw = golden_tree(name)
+    tree = sheep_amd.tree_to_device(gp, gw)
+    facts_txt, blocks = golden_part_text(name)
+    assert sheep_amd.facts(tree).text() == facts_txt
+    kids = sheep_amd.KidTable(tree)
+    d = _dev_records(rec)
+    for k, block in zip(ks(name), blocks):
+        res = sheep_amd.partition(s, tree, k, kids=kids)
+        assert np.array_equal(res.numpy(), golden_parts(name, k)), f"k={k}"
+        ev = sheep_amd.evaluate(d, s, res.parts)
+        assert res.print_text() + ev.text(k) == block, f"k={k}"
+
+
+@pytest.mark.parametrize("scale,seed,k", [(16, 5, 16), (18, 7, 64)])
+def test_rmat_vs_oracle(gpu_ctx, scale, seed, k):
+    """Beyond the committed fixtures: the whole path on larger RMAT graphs vs the oracle."""
+    import sheep_amd
+    d = sheep_amd.rmat(scale, 16, seed)
+    h = sheep_amd.to_numpy_u32(d).reshape(-1, 3)
+    t_, h_ = h[:, 0], h[:, 1]
+    s = sheep_amd.degree_sequence(d)
+    seq = oracle.sequence(t_, h_)
+    assert np.array_equal(s.numpy(), seq)
+    tree = sheep_amd.build_tree(d, s)
+    p, w = _tree_np(tree)
+    op, ow = oracle.build_tree(t_, h_, seq)
+    assert np.array_equal(p, op) and np.array_equal(w, ow)
+    assert sheep_amd.facts(tree).__dict__ == oracle.facts(op, ow)
+    res = sheep_amd.partition(s, tree, k)
+    oparts, oinfo = oracle.partition(op, ow, seq, k)
+    assert np.array_equal(res.numpy(), oparts)
+    assert res.created == oinfo["created"]
+    ev = sheep_amd.evaluate(d, s, res.parts)
+    oev = oracle.evaluate(t_, h_, seq, oparts)
+    assert ev.__dict__ == oev
+
+
+def test_shards_merge_to_whole_tree(gpu_ctx):
+    """Shard independence: 4 contiguous shards, pairwise merges == the whole tree."""
+    import sheep_amd
+    d = sheep_amd.rmat(18, 16, 11)
+    s = sheep_amd.degree_sequence(d)
+    whole = _tree_np(sheep_amd.build_tree(d, s))
+    R = d.shape[0]
+    parts = [sheep_amd.build_tree(d[i * R // 4:(i + 1) * R // 4], s) for i in range(4)]
+    m = sheep_amd.merge_trees(sheep_amd.merge_trees(parts[0], parts[1]), sheep_amd.merge_trees(parts[2], parts[3]))
+    p, w = _tree_np(m)
+    assert np.array_equal(p, whole[0]) and np.array_equal(w, whole[1])
+
+
+def test_unsequenced_and_out_of_range(gpu_ctx):
+    """A neighbour missing from the sequence counts as POSTORDER forever (jtree.cpp:84-90);
+    a neighbour beyond max(seq) makes index.at() throw (jtree.cpp:75)."""
+    import sheep_amd
+    rec = golden_records("edge")
+    seq = golden_seq("edge")
+    drop = seq[seq != 3]                    # vertex 3 unsequenced, max(seq) unchanged
+    s = sheep_amd.sequence_from_host(drop)
+    p, w = _tree_np(sheep_amd.build_tree(_dev_records(rec), s))
+    op, ow = oracle.build_tree(rec["tail"], rec["head"], drop)
+    assert np.array_equal(p, op) and np.array_equal(w, ow)
+    short = seq[seq < 10]                   # max(seq) = 9 while record (10, 0) exists
+    s2 = sheep_amd.sequence_from_host(short)
+    with pytest.raises(IndexError):
+        sheep_amd.build_tree(_dev_records(rec), s2)
+
+
+def test_empty_and_tiny(gpu_ctx):
+    import sheep_amd
+    import torch
+    # one record, a self-loop: one node, no tree edge, pst 0
+    rec = np.zeros(1, dtype=[("tail", "<u4"), ("head", "<u4"), ("weight", "<f4")])
+    rec["tail"] = rec["head"] = 4
+    d = _dev_records(rec)
+    s = sheep_amd.degree_sequence(d)
+    assert list(s.numpy()) == [4]
+    p, w = _tree_np(sheep_amd.build_tree(d, s))
+    assert list(p) == [0xFFFFFFFF] and list(w) == [0]
+    res = sheep_amd.partition(s, sheep_amd.tree_to_device(p, w), 2)
+    assert res.created == 1
