@@ -7,7 +7,7 @@
 HIPCC   ?= /opt/rocm/bin/hipcc
 ARCH    ?= gfx950
 JOBS    ?= 8
-HIPFLAGS:= --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable \
+HIPFLAGS:= --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable -Wno-unused-value \
            -Iinclude -Isheep_amd/csrc
 HIPSRC  := $(wildcard sheep_amd/csrc/*.hip)
 HIPOBJ  := $(patsubst sheep_amd/csrc/%.hip,build/hip/%.o,$(HIPSRC))

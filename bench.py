@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""bench.py — Sheep's map/reduce partitioning path on MI355X (BASELINE.json metric).
+
+One step = the whole hot path over one synthetic graph already resident in HBM:
+
+  degree count (per edge shard) -> [RCCL all-reduce of degrees] -> degree sequence
+  -> per-shard elimination tree (map) -> [log2(N) send/recv rounds + tree merge]
+  -> makeKids + partition_tree forwardPartition (k parts) on rank 0
+
+(reference: graph2tree.cpp:161-216 `-ir` + partition_tree.cpp:130-143).
+Every computation runs in libsheep_hip.so's HIP kernels; the CPU oracle is only timed
+as the `cpu_baseline` leg (rank 0, N=1) on a bounded sample.
+
+    python bench.py [--gpus N --steps K --warmup W --scale 26 --ef 16 --k 64]
+
+For N > 1 launch with torch.distributed.run (one process per GPU, RCCL over xGMI).
+The graph is fixed as N grows (edge shards of one RMAT graph): "scaling": "strong".
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level table)
+# Leaf regions (one kernel or one fused kernel family per launch); aggregates such as
+# "etree" / "partition" / "sequence" are reported in phases but not rooflined.
+LEAF = ("degree", "relabel", "etree_union", "etree_cross", "etree_apply", "evaluate")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scale", type=int, default=26)
+    ap.add_argument("--ef", type=int, default=16)
+    ap.add_argument("--k", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=None, help="RMAT seed (default: the scale, SURVEY §8d)")
+    ap.add_argument("--cpu-scale", type=int, default=22, help="RMAT scale of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    import sheep_amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and world > 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    seed = a.scale if a.seed is None else a.seed
+
+    ctx = sheep_amd.Context(local)
+    rec = sheep_amd.rmat(a.scale, a.ef, seed, ctx=ctx)          # whole graph, identical on every rank
+    R = rec.shape[0]
+    beg, end = rank * R // world, (rank + 1) * R // world      # contiguous edge shard (graph2tree -l)
+    shard = rec[beg:end]
+    vs_cap = 1 << a.scale
+    deg = torch.zeros(vs_cap, dtype=torch.int32, device="cuda")
+    mx = torch.zeros(1, dtype=torch.int64, device="cuda")
+
+    def step():
+        deg.zero_()
+        _, max_slot = sheep_amd.degree_count(shard, mode="llama", deg=deg, ctx=ctx)
+        vs = max_slot
+        if world > 1:                                           # sequence.h:72,78 MPI_Allreduce
+            mx.fill_(max_slot)
+            dist.all_reduce(deg, op=dist.ReduceOp.SUM)
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            vs = int(mx.item())
+        s = sheep_amd.sequence_from_degrees(deg, vs, ctx=ctx)
+        tree = sheep_amd.build_tree(shard, s, ctx=ctx)
+        r = 1
+        while r < world:                                        # binomial reduce to rank 0 (jnode.cpp:241)
+            if rank % (2 * r) == r:
+                dist.send(tree, rank - r)
+            elif rank % (2 * r) == 0 and rank + r < world:
+                other = torch.empty_like(tree)
+                dist.recv(other, rank + r)
+                tree = sheep_amd.merge_trees(tree, other, ctx=ctx)
+            r *= 2
+        res = None
+        if rank == 0:
+            kids = sheep_amd.KidTable(tree, ctx)
+            res = sheep_amd.partition(s, tree, a.k, kids=kids, ctx=ctx)
+            kids.close()
+        return s, tree, res
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        step()
+    barrier()
+    ctx.timing(True)
+    ctx.timer_reset()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        s, tree, res = step()
+    barrier()
+    t = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([t], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+
+    # per-region device timings (HIP events on the context stream)
+    phases = {}
+    for name in ctx.timer_names():
+        ms, launches, nbytes = ctx.timer(name)
+        phases[name] = {"ms_per_step": round(ms / a.steps, 4), "launches": launches, "alg_bytes": nbytes}
+    ctx.timing(False)
+    roof = None
+    leaf = [(phases[n]["ms_per_step"], n) for n in LEAF if n in phases and phases[n]["launches"]]
+    if leaf:
+        _, dom = max(leaf)
+        p = phases[dom]
+        ms_launch = p["ms_per_step"] * a.steps / p["launches"]
+        b_launch = p["alg_bytes"] / p["launches"]
+        ach = b_launch / (ms_launch * 1e-3) / 1e9
+        roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "alg_bytes_per_launch": int(b_launch), "ms_per_launch": round(ms_launch, 4)}
+
+    out = None
+    if rank == 0:
+        n = s.n
+        b_alg = 32 * R + 14 * s.pos_size + 20 * n
+        value = R * a.steps / t
+        out = {
+            "metric": "edges/s seq+tree+partition",
+            "value": round(value, 1),
+            "unit": "edges/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1e3 * t / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (Graph500 RMAT, seeded, self-loops/duplicates removed)",
+            "config": {"workload": f"RMAT-{a.scale} ef{a.ef}, k={a.k}", "records": R, "vertex_slots": s.pos_size,
+                       "tree_nodes": n, "k": a.k, "created": res.created, "seed": seed,
+                       "parallelism": f"edge-shards x{world}"},
+            "path_roofline": {"alg_bytes": b_alg, "achieved_GBs": round(b_alg * a.steps / t / 1e9, 2),
+                              "frac": round(b_alg * a.steps / t / 1e9 / (HBM_PEAK_GBS * world), 4)},
+            "roofline": roof,
+            "phases": phases,
+        }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(a, ctx)
+    del rec, shard
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def cpu_baseline(a, ctx):
+    """The oracle (CPU restatement of the reference, oracle/sheep_oracle.cpp) on a
+    bounded sample: RMAT-<cpu-scale> from the same generator, seq + tree + partition,
+    one core.  Test infrastructure timed as a baseline; never the measured path."""
+    import numpy as np
+    import sheep_amd
+    import oracle
+    sc = a.cpu_scale
+    d = sheep_amd.rmat(sc, a.ef, sc, ctx=ctx)
+    h = sheep_amd.to_numpy_u32(d).reshape(-1, 3)
+    del d
+    tail, head = np.ascontiguousarray(h[:, 0]), np.ascontiguousarray(h[:, 1])
+    t0 = time.perf_counter()
+    seq = oracle.sequence(tail, head)
+    p, w = oracle.build_tree(tail, head, seq)
+    oracle.partition(p, w, seq, a.k)
+    t = time.perf_counter() - t0
+    return {"value": round(len(tail) / t, 1), "unit": "edges/s", "cores": 1, "kind": "port",
+            "sample": f"RMAT-{sc} ef{a.ef} seed {sc} ({len(tail)} records), seq+tree+partition k={a.k}, "
+                      f"oracle/sheep_oracle.cpp single-threaded, {t:.2f} s"}
+
+
+if __name__ == "__main__":
+    main()

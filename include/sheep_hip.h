@@ -98,7 +98,11 @@ typedef struct {
 
 /* ---- context ------------------------------------------------------------------- */
 const char *sheep_last_error(void);
-/* hip_stream may be NULL (the context creates its own stream). */
+/* Every call of the context is issued on `hip_stream` as given — NULL is the device's
+ * null stream (PyTorch's default stream), so callers that share buffers with other
+ * work order it simply by passing the stream that work runs on.  SHEEP_OWN_STREAM makes
+ * the context create (and destroy) a non-blocking stream of its own. */
+#define SHEEP_OWN_STREAM ((void *)(intptr_t)-1)
 int sheep_ctx_create(int device, void *hip_stream, sheep_ctx **out);
 int sheep_ctx_destroy(sheep_ctx *ctx);
 int sheep_ctx_sync(sheep_ctx *ctx);
@@ -107,11 +111,15 @@ int sheep_malloc(sheep_ctx *ctx, size_t bytes, void **dev_out);
 int sheep_free(sheep_ctx *ctx, void *dev);
 int sheep_memcpy_h2d(sheep_ctx *ctx, void *dst_dev, const void *src_host, size_t bytes);
 int sheep_memcpy_d2h(sheep_ctx *ctx, void *dst_host, const void *src_dev, size_t bytes);
-/* Device-side timing of the last instrumented kernel class:
- * name = "relabel" | "degree" | ...; returns accumulated ms and launch count since reset. */
+/* Device-side timing per instrumented region (HIP events on the context stream; see
+ * DESIGN.md §Measurement): name = "degree" | "relabel" | "etree" | ...; returns the
+ * accumulated ms, launch count and algorithmic bytes since the last reset. */
 int sheep_timer_enable(sheep_ctx *ctx, int on);
-int sheep_timer_get(sheep_ctx *ctx, const char *name, double *ms, uint64_t *launches);
+int sheep_timer_get(sheep_ctx *ctx, const char *name, double *ms, uint64_t *launches,
+                    uint64_t *alg_bytes);
 int sheep_timer_reset(sheep_ctx *ctx);
+/* Names of every region timed since the last reset, comma-separated, into buf[cap]. */
+int sheep_timer_names(sheep_ctx *ctx, char *buf, size_t cap);
 
 /* ---- degree sequence --------------------------------------------------------------
  * Adds this shard's degrees into deg_dev[0, deg_cap) (caller zeroes it once; shards

@@ -85,8 +85,9 @@ def lib() -> ctypes.CDLL:
         "sheep_memcpy_h2d": ([P, P, P, ctypes.c_size_t], I32),
         "sheep_memcpy_d2h": ([P, P, P, ctypes.c_size_t], I32),
         "sheep_timer_enable": ([P, I32], I32),
-        "sheep_timer_get": ([P, ctypes.c_char_p, ctypes.POINTER(D), ctypes.POINTER(U64)], I32),
+        "sheep_timer_get": ([P, ctypes.c_char_p, ctypes.POINTER(D), ctypes.POINTER(U64), ctypes.POINTER(U64)], I32),
         "sheep_timer_reset": ([P], I32),
+        "sheep_timer_names": ([P, ctypes.c_char_p, ctypes.c_size_t], I32),
         "sheep_degree_count": ([P, P, U64, I32, P, U64, ctypes.POINTER(U64)], I32),
         "sheep_sequence_from_degrees": ([P, P, U64, P, P, ctypes.POINTER(U64)], I32),
         "sheep_positions": ([P, P, U64, P, U64], I32),
@@ -152,9 +153,15 @@ class Context:
         _check(lib().sheep_timer_enable(self.handle, int(on)))
 
     def timer(self, name: str):
-        ms, n = ctypes.c_double(), ctypes.c_uint64()
-        _check(lib().sheep_timer_get(self.handle, name.encode(), ctypes.byref(ms), ctypes.byref(n)))
-        return ms.value, n.value
+        """(ms, launches, algorithmic bytes) accumulated for one instrumented region."""
+        ms, n, b = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().sheep_timer_get(self.handle, name.encode(), ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b)))
+        return ms.value, n.value, b.value
+
+    def timer_names(self) -> list:
+        buf = ctypes.create_string_buffer(4096)
+        _check(lib().sheep_timer_names(self.handle, buf, 4096))
+        return [x for x in buf.value.decode().split(",") if x]
 
     def timer_reset(self):
         _check(lib().sheep_timer_reset(self.handle))

@@ -57,7 +57,7 @@ int sheep_ctx_create(int device, void *hip_stream, sheep_ctx **out) {
   HIP_CHECK(hipSetDevice(device));
   sheep_ctx *x = new sheep_ctx();
   x->c.device = device;
-  if (hip_stream) {
+  if (hip_stream != SHEEP_OWN_STREAM) {
     x->c.stream = (hipStream_t)hip_stream;
   } else {
     HIP_CHECK(hipStreamCreateWithFlags(&x->c.stream, hipStreamNonBlocking));
@@ -74,7 +74,7 @@ int sheep_ctx_destroy(sheep_ctx *ctx) {
   if (!ctx) return SHEEP_OK;
   sheep::Ctx &c = ctx->c;
   HIP_CHECK(hipSetDevice(c.device));
-  if (c.stream) HIP_CHECK(hipStreamSynchronize(c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
   for (auto &kv : c.ws) if (kv.second.p) hipFree(kv.second.p);
   for (auto &kv : c.timers) for (auto &p : kv.second.pending) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
   for (hipEvent_t e : c.event_pool) hipEventDestroy(e);
@@ -136,13 +136,25 @@ int sheep_timer_enable(sheep_ctx *ctx, int on) {
   API_END
 }
 
-int sheep_timer_get(sheep_ctx *ctx, const char *name, double *ms, uint64_t *launches) {
+int sheep_timer_get(sheep_ctx *ctx, const char *name, double *ms, uint64_t *launches, uint64_t *alg_bytes) {
   API_BEGIN
   NEED(ctx && name && ms && launches, "null argument");
   ctx->c.collect_timers();
   auto it = ctx->c.timers.find(name);
-  *ms = it == ctx->c.timers.end() ? 0.0 : it->second.ms;
-  *launches = it == ctx->c.timers.end() ? 0 : it->second.launches;
+  const bool none = it == ctx->c.timers.end();
+  *ms = none ? 0.0 : it->second.ms;
+  *launches = none ? 0 : it->second.launches;
+  if (alg_bytes) *alg_bytes = none ? 0 : it->second.bytes;
+  API_END
+}
+
+int sheep_timer_names(sheep_ctx *ctx, char *buf, size_t cap) {
+  API_BEGIN
+  NEED(ctx && buf && cap, "null argument");
+  std::string s;
+  for (auto &kv : ctx->c.timers) { if (!s.empty()) s += ','; s += kv.first; }
+  NEED(s.size() < cap, "buffer too small");
+  memcpy(buf, s.c_str(), s.size() + 1);
   API_END
 }
 

@@ -53,7 +53,7 @@ struct Ctx {
   static constexpr int NSCALARS = 64;
 
   bool timing = false;
-  struct Timer { std::vector<std::pair<hipEvent_t, hipEvent_t>> pending; double ms = 0; uint64_t launches = 0; };
+  struct Timer { std::vector<std::pair<hipEvent_t, hipEvent_t>> pending; double ms = 0; uint64_t launches = 0; uint64_t bytes = 0; };
   std::map<std::string, Timer> timers;
   std::vector<hipEvent_t> event_pool;
 
@@ -93,11 +93,15 @@ struct Ctx {
   }
 };
 
-// Brackets one instrumented launch with HIP events on the context stream.
+// Brackets one instrumented launch with HIP events on the context stream.  `bytes` is
+// the launch's ALGORITHMIC traffic, summed per timer name.
 struct TimedRegion {
   Ctx &c; const char *name; hipEvent_t a = nullptr, b = nullptr;
-  TimedRegion(Ctx &ctx, const char *n) : c(ctx), name(n) {
-    if (c.timing) { a = c.ev(); b = c.ev(); HIP_CHECK(hipEventRecord(a, c.stream)); }
+  TimedRegion(Ctx &ctx, const char *n, uint64_t bytes = 0) : c(ctx), name(n) {
+    if (c.timing) {
+      c.timers[name].bytes += bytes;
+      a = c.ev(); b = c.ev(); HIP_CHECK(hipEventRecord(a, c.stream));
+    }
   }
   ~TimedRegion() {
     if (c.timing) {

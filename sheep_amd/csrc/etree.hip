@@ -280,13 +280,13 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
     hipLaunchKernelGGL(k_reset, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, uf, mt, n);
     LAUNCH_CHECK();
     {
-      TimedRegion tr(c, "etree_union");
+      TimedRegion tr(c, "etree_union", 8 * live);
       hipLaunchKernelGGL(k_union_light, dim3(g), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, live, s, clo, uf);
       LAUNCH_CHECK();
     }
     HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
     {
-      TimedRegion tr(c, "etree_cross");
+      TimedRegion tr(c, "etree_cross", 8 * live);
       hipLaunchKernelGGL(k_cross_min, dim3(g), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, live, s, clo, uf, mt,
                          xidx, xtop, d);
       LAUNCH_CHECK();
@@ -299,7 +299,7 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
       while (cap < 2 * nx && cap < (1ull << 27)) cap <<= 1;
       unsigned long long *table = c.get_as<unsigned long long>("et_hash", cap);
       HIP_CHECK(hipMemsetAsync(table, 0xFF, cap * sizeof(uint64_t), c.stream));
-      TimedRegion tr(c, "etree_apply");
+      TimedRegion tr(c, "etree_apply", 28 * nx);
       hipLaunchKernelGGL(k_cross_apply, dim3(grid_for(nx)), dim3(BLOCK), 0, c.stream, cur, xidx, xtop, nx, mt, parent,
                          table, (uint32_t)(cap - 1), d + 1);
       LAUNCH_CHECK();
@@ -329,7 +329,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   unsigned long long *d = (unsigned long long *)c.d_scalars + 8;
   HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
   if (nrec) {
-    TimedRegion tr(c, "relabel");
+    TimedRegion tr(c, "relabel", 20 * nrec);   // record + 2 pos gathers
     hipLaunchKernelGGL(k_relabel, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos, pos_size, pst,
                        edges, d, d + 1);
     LAUNCH_CHECK();
@@ -339,7 +339,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   if (c.h_scalars[9]) throw Error(SHEEP_ERR_RANGE, "vector::_M_range_check: neighbour vid beyond the sequence's index (jtree.cpp:75)");
   uint64_t m = c.h_scalars[8];
   {
-    TimedRegion tr(c, "etree");
+    TimedRegion tr(c, "etree", 8 * m);
     etree_from_edges(c, edges, m, n, parent);
   }
   if (n) {
@@ -361,7 +361,7 @@ void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n,
   c.sync();
   if (c.h_scalars[11]) throw Error(SHEEP_ERR_ARG, "merge: a parent is not a later node of the tree");
   {
-    TimedRegion tr(c, "merge");
+    TimedRegion tr(c, "merge", 16 * n);
     etree_from_edges(c, edges, c.h_scalars[10], n, parent);
   }
   hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);

@@ -165,7 +165,8 @@ void evaluate(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, 
   unsigned long long *bal = c.get_as<unsigned long long>("ev_bal", 4 * (uint64_t)nparts);
   HIP_CHECK(hipMemsetAsync(bal, 0, 4 * (uint64_t)nparts * sizeof(uint64_t), c.stream));
   {
-    TimedRegion tr(c, "evaluate");
+    // B_eval: record read + 2 pos + 2 part gathers, bitset write + read
+    TimedRegion tr(c, "evaluate", 28 * nrec + 8 * words);
     if (nrec) {
       hipLaunchKernelGGL(k_eval_records, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos, pos_size,
                          parts, what, W, nparts, bd, bu, bh, bv, bal, scal, scal + 8);

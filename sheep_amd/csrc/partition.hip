@@ -148,17 +148,31 @@ __global__ void k_kid_info(const uint32_t *__restrict__ kids, uint32_t beg, uint
   }
 }
 
-// interval endpoints for assigned nodes: non-root -> [tD, tU]; root with kids ->
-// [tD(first kid), tU(last kid)]; root without kids -> none (INVALID)
+// Tour interval of every root with kids: [tD(first kid), tU(last kid)] in the kid order
+// the tour was built from.  Taken before the host replay re-sorts kid segments.
+__global__ void k_root_intervals(const uint32_t *__restrict__ rk, uint64_t nrk, const uint32_t *__restrict__ koff,
+                                 const uint32_t *__restrict__ kids, const uint32_t *__restrict__ tD,
+                                 const uint32_t *__restrict__ tU, uint32_t *__restrict__ rst,
+                                 uint32_t *__restrict__ ren) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nrk; i += stride) {
+    uint32_t v = rk[i];
+    rst[v] = tD[kids[koff[v]]];
+    ren[v] = tU[kids[koff[v + 1] - 1]];
+  }
+}
+
+// interval endpoints for assigned nodes: non-root -> [tD, tU]; root with kids -> its
+// tour segment; root without kids -> none (INVALID)
 __global__ void k_intervals(const uint32_t *__restrict__ ids, uint64_t m, const uint32_t *__restrict__ parent,
-                            const uint32_t *__restrict__ koff, const uint32_t *__restrict__ kids,
-                            const uint32_t *__restrict__ tD, const uint32_t *__restrict__ tU,
-                            uint32_t *__restrict__ st, uint32_t *__restrict__ en) {
+                            const uint32_t *__restrict__ koff, const uint32_t *__restrict__ rst,
+                            const uint32_t *__restrict__ ren, const uint32_t *__restrict__ tD,
+                            const uint32_t *__restrict__ tU, uint32_t *__restrict__ st, uint32_t *__restrict__ en) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) {
     uint32_t v = ids[i];
     if (parent[v] != INVALID) { st[i] = tD[v]; en[i] = tU[v]; }
-    else if (koff[v] < koff[v + 1]) { st[i] = tD[kids[koff[v]]]; en[i] = tU[kids[koff[v + 1] - 1]]; }
+    else if (koff[v] < koff[v + 1]) { st[i] = rst[v]; en[i] = ren[v]; }
     else { st[i] = INVALID; en[i] = INVALID; }
   }
 }
@@ -315,7 +329,7 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
     LAUNCH_CHECK();
   }
   if (n == 0) { c.sync(); return; }
-  TimedRegion tr_all(c, "partition");
+  TimedRegion tr_all(c, "partition", 12 * n + 2 * pos_size);   // tree + seq read, parts write
 
   // 1. weights and max_component (partition.cpp:54-57)
   uint64_t *w = c.get_as<uint64_t>("pt_w", n);
@@ -334,6 +348,12 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   info->total_weight = total;
   info->max_component = max_component;
   uint64_t *S = c.get_as<uint64_t>("pt_S", n);
+  uint32_t *rst = c.get_as<uint32_t>("pt_rst", n), *ren = c.get_as<uint32_t>("pt_ren", n);
+  if (t.nrk) {
+    hipLaunchKernelGGL(k_root_intervals, dim3(grid_for(t.nrk)), dim3(BLOCK), 0, c.stream, t.rk, t.nrk, k->koff,
+                       k->kids, t.tD, t.tU, rst, ren);
+    LAUNCH_CHECK();
+  }
   if (t.A) {
     uint64_t *val = c.get_as<uint64_t>("pt_tourval", t.A);
     hipLaunchKernelGGL(k_tour_vals, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, t.tD, t.tU, n, (const uint64_t *)w,
@@ -447,6 +467,7 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
       std::vector<uint64_t> scb(cnt);
       for (uint32_t j = 0; j < cnt; ++j) { sorted[j] = seg[order[j]]; scb[j] = kidcb[order[j]]; }
       h2d(c, k->kids + beg, sorted.data(), cnt);
+      c.sync();   // `sorted` is a pageable host buffer that dies with this iteration
       std::vector<char> done(cnt, 0);
       do {
         for (uint32_t j = 0; cb > max_component && j < cnt; ++j) {
@@ -509,7 +530,7 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
     LAUNCH_CHECK();
     uint32_t *st = c.get_as<uint32_t>("pt_ast", na), *en = c.get_as<uint32_t>("pt_aen", na);
     hipLaunchKernelGGL(k_intervals, dim3(grid_for(na)), dim3(BLOCK), 0, c.stream, aid, na, k->parent, k->koff,
-                       k->kids, t.tD, t.tU, st, en);
+                       (const uint32_t *)rst, (const uint32_t *)ren, t.tD, t.tU, st, en);
     LAUNCH_CHECK();
     std::vector<uint32_t> hs(na), he(na);
     d2h(c, hs.data(), st, na);
@@ -545,6 +566,7 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
                          dencl, m, parts, e);
       LAUNCH_CHECK();
       d2h(c, c.h_scalars + 36, c.d_scalars + 36, 1);
+      c.sync();   // the staged host vectors die with this block
     }
   }
   // 7. jnid -> vid (:62-66) and print counts (partition.h:138-139)

@@ -121,7 +121,7 @@ void degree_count(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_
   unsigned long long *d = (unsigned long long *)c.d_scalars;
   HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
   if (nrec) {
-    TimedRegion tr(c, "degree");
+    TimedRegion tr(c, "degree", 12 * nrec);   // one read of the 12-B records
     hipLaunchKernelGGL(k_degree, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, mode, deg, cap, d, d + 1);
     LAUNCH_CHECK();
   }
@@ -132,7 +132,7 @@ void degree_count(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_
 }
 
 uint64_t sequence_from_degrees(Ctx &c, const uint32_t *deg, uint64_t vs, uint32_t *seq, uint32_t *pos) {
-  TimedRegion tr(c, "sequence");
+  TimedRegion tr(c, "sequence", 8 * vs);   // degree read + pos write
   fill_u32(c, pos, vs, INVALID);
   if (vs == 0) return 0;
   uint64_t nb = (vs + C_TILE - 1) / C_TILE;

@@ -125,8 +125,9 @@ __global__ void k_pick_rulers(const uint32_t *__restrict__ parent, uint64_t n, u
 __global__ void k_walk(const uint32_t *__restrict__ rulers, uint64_t nr, const uint32_t *__restrict__ succ,
                        const uint32_t *__restrict__ rid, uint32_t *__restrict__ owner, uint32_t *__restrict__ loff,
                        uint32_t *__restrict__ rlen, uint32_t *__restrict__ rnext) {
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t r = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; r < nr; r += stride) {
+  // launched with 64-thread workgroups (one wave: the walks are long dependent chains)
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nr; r += stride) {
     uint32_t cur = rulers[r], local = 0, nx;
     const uint32_t cap = (uint32_t)(2 * (nr + 1) * 64 + 2);   // > any list length: guards a corrupt list
     while (local < cap) {
