@@ -136,6 +136,47 @@ template <typename T> __device__ __forceinline__ T wave_min(T v) {
   return v;
 }
 
+// Workgroup-aggregated append: reserves `cnt` consecutive slots for every thread with
+// ONE device atomic per workgroup call (a single hot counter takes ~0.1 G atomics/s, so
+// per-wave appends serialise a streaming kernel).  Every thread of the workgroup must
+// call it (it synchronises the workgroup); returns the thread's first slot.  Slots are
+// handed out in thread order within the call.
+__device__ __forceinline__ uint64_t block_reserve(uint32_t cnt, unsigned long long *counter) {
+  __shared__ uint32_t s_w[BLOCK / WAVE];
+  __shared__ unsigned long long s_base;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t inc = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) s_w[wave] = inc;
+  __syncthreads();
+  uint32_t woff = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < BLOCK / WAVE; ++w) {
+    uint32_t x = s_w[w];
+    if (w < wave) woff += x;
+    tot += x;
+  }
+  if (threadIdx.x == 0) s_base = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
+  __syncthreads();
+  const uint64_t first = s_base + woff + inc - cnt;
+  __syncthreads();   // s_w / s_base are reused by the next call
+  return first;
+}
+
+// Tiles for streaming kernels that append: BLOCK threads x TILE_ITEMS items, items
+// strided by BLOCK so each load instruction is coalesced.
+constexpr int TILE_ITEMS = 8;
+constexpr int TILE = BLOCK * TILE_ITEMS;
+inline unsigned grid_tiles(uint64_t items, unsigned cap = 256 * 8) {
+  uint64_t t = (items + TILE - 1) / TILE;
+  if (t == 0) t = 1;
+  return (unsigned)(t < cap ? t : cap);
+}
+
 // Wave-aggregated append: every lane with `pred` gets a unique slot in [0, *counter).
 __device__ __forceinline__ uint64_t wave_append(bool pred, unsigned long long *counter) {
   uint64_t mask = __ballot(pred);

@@ -21,6 +21,8 @@
 // component with a cross edge; vertices never assigned are roots.  The result is the
 // unique elimination tree of (edge multiset, order) — identical to Liu's.  Level
 // ranges are dyadic in a monotone spread of [0,n) onto [0,2^L) so halves are balanced.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace sheep {
@@ -89,32 +91,38 @@ __global__ __launch_bounds__(BLOCK) void k_relabel(const sheep_xs1 *__restrict__
                                                    uint32_t *__restrict__ pst, uint64_t *__restrict__ edges,
                                                    unsigned long long *__restrict__ counter,
                                                    unsigned long long *__restrict__ err) {
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  const uint64_t iters = (nrec + stride - 1) / stride;
-  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const uint64_t ntiles = (nrec + TILE - 1) / TILE;
   bool bad = false;
-  for (uint64_t it = 0; it < iters; ++it, i += stride) {
-    bool emit = false;
-    uint64_t e = 0;
-    if (i < nrec) {
-      sheep_xs1 r = rec[i];
-      uint32_t t = r.tail, h = r.head;
-      if (t != h) {
-        uint32_t pt = t < pos_size ? pos[t] : INVALID;
-        uint32_t ph = h < pos_size ? pos[h] : INVALID;
-        bool tin = pt != INVALID, hin = ph != INVALID;
-        if ((tin && h >= pos_size) || (hin && t >= pos_size)) bad = true;
-        else if (tin && hin) {
-          uint32_t lo = pt < ph ? pt : ph, hi = pt < ph ? ph : pt;
-          atomicAdd(&pst[lo], 1u);
-          e = ((uint64_t)hi << 32) | lo;
-          emit = true;
-        } else if (tin) atomicAdd(&pst[pt], 1u);
-        else if (hin) atomicAdd(&pst[ph], 1u);
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    uint64_t ev[TILE_ITEMS];
+    uint32_t flags = 0;
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
+      ev[j] = 0;
+      if (i >= nrec) continue;
+      const sheep_xs1 r = rec[i];
+      const uint32_t t = r.tail, h = r.head;
+      if (t == h) continue;
+      const uint32_t pt = t < pos_size ? pos[t] : INVALID;
+      const uint32_t ph = h < pos_size ? pos[h] : INVALID;
+      const bool tin = pt != INVALID, hin = ph != INVALID;
+      if ((tin && h >= pos_size) || (hin && t >= pos_size)) { bad = true; continue; }
+      if (tin && hin) {
+        const uint32_t lo = pt < ph ? pt : ph, hi = pt < ph ? ph : pt;
+        atomicAdd(&pst[lo], 1u);
+        ev[j] = ((uint64_t)hi << 32) | lo;
+        flags |= 1u << j;
+      } else if (tin) {
+        atomicAdd(&pst[pt], 1u);
+      } else if (hin) {
+        atomicAdd(&pst[ph], 1u);
       }
     }
-    uint64_t slot = wave_append(emit, counter);
-    if (emit) edges[slot] = e;
+    uint64_t slot = block_reserve((uint32_t)__popc(flags), counter);
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j)
+      if (flags & (1u << j)) edges[slot++] = ev[j];
   }
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(err, 1ull);
 }
@@ -144,26 +152,51 @@ __global__ __launch_bounds__(BLOCK) void k_cross_min(const uint64_t *__restrict_
                                                      uint32_t clo, uint32_t *uf, uint32_t *__restrict__ mt,
                                                      uint32_t *__restrict__ xidx, uint32_t *__restrict__ xtop,
                                                      unsigned long long *__restrict__ counter) {
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  const uint64_t iters = (m + stride - 1) / stride;
-  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  for (uint64_t it = 0; it < iters; ++it, i += stride) {
-    bool cross = false;
-    uint32_t t = 0;
-    if (i < m) {
-      uint64_t e = edges[i];
-      if (e != DEAD) {
-        uint32_t a = (uint32_t)e, b = (uint32_t)(e >> 32);
-        uint32_t ya = spread(a, clo), yb = spread(b, clo);
-        if (((ya ^ yb) >> s) == 1) {
-          cross = true;
-          t = find_plain(uf, a);
-          atomicMin(&mt[t], b);
+  const uint64_t ntiles = (m + TILE - 1) / TILE;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    uint32_t tops[TILE_ITEMS];
+    uint32_t flags = 0;
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
+      bool cross = false;
+      uint32_t t = 0, b = 0;
+      if (i < m) {
+        const uint64_t e = edges[i];
+        if (e != DEAD) {
+          const uint32_t a = (uint32_t)e;
+          b = (uint32_t)(e >> 32);
+          const uint32_t ya = spread(a, clo), yb = spread(b, clo);
+          if (((ya ^ yb) >> s) == 1) {
+            cross = true;
+            t = find_plain(uf, a);
+          }
         }
       }
+      tops[j] = t;
+      if (cross) flags |= 1u << j;
+      // m_t = min b over t's cross edges.  Power-law graphs send most cross edges of a
+      // level to one giant component's top, so combine in the wave first (lanes sharing
+      // the first cross lane's top) and skip atomics a plain read already shows useless
+      // (mt only decreases, so a stale read is >= the true value: skipping stays exact).
+      const uint64_t cm = __ballot(cross);
+      if (cm) {
+        const int first = __ffsll((unsigned long long)cm) - 1;
+        const uint32_t t0 = __shfl(t, first, 64);
+        const bool same = cross && t == t0;
+        const uint32_t v = wave_min(same ? b : INVALID);
+        if ((int)__lane_id() == first && v < mt[t0]) atomicMin(&mt[t0], v);
+        if (cross && !same && b < mt[t]) atomicMin(&mt[t], b);
+      }
     }
-    uint64_t slot = wave_append(cross, counter);
-    if (cross) { xidx[slot] = (uint32_t)i; xtop[slot] = t; }
+    uint64_t slot = block_reserve((uint32_t)__popc(flags), counter);
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j)
+      if (flags & (1u << j)) {
+        xidx[slot] = (uint32_t)(tile * TILE + (uint64_t)j * BLOCK + threadIdx.x);
+        xtop[slot] = tops[j];
+        ++slot;
+      }
   }
 }
 
@@ -200,14 +233,20 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(uint64_t *__restrict__ ed
 
 __global__ __launch_bounds__(BLOCK) void k_compact_edges(const uint64_t *__restrict__ in, uint64_t m,
                                                          uint64_t *__restrict__ out, unsigned long long *__restrict__ counter) {
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  const uint64_t iters = (m + stride - 1) / stride;
-  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  for (uint64_t it = 0; it < iters; ++it, i += stride) {
-    uint64_t e = i < m ? in[i] : DEAD;
-    bool live = e != DEAD;
-    uint64_t slot = wave_append(live, counter);
-    if (live) out[slot] = e;
+  const uint64_t ntiles = (m + TILE - 1) / TILE;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    uint64_t ev[TILE_ITEMS];
+    uint32_t flags = 0;
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
+      ev[j] = i < m ? in[i] : DEAD;
+      if (ev[j] != DEAD) flags |= 1u << j;
+    }
+    uint64_t slot = block_reserve((uint32_t)__popc(flags), counter);
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j)
+      if (flags & (1u << j)) out[slot++] = ev[j];
   }
 }
 
@@ -215,26 +254,37 @@ __global__ __launch_bounds__(BLOCK) void k_tree_edges(const sheep_jnode *__restr
                                                       uint64_t n, uint64_t *__restrict__ edges,
                                                       unsigned long long *__restrict__ counter,
                                                       uint32_t *__restrict__ pst_out, unsigned long long *__restrict__ err) {
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  const uint64_t iters = (n + stride - 1) / stride;
-  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const uint64_t ntiles = (n + TILE - 1) / TILE;
   bool bad = false;
-  for (uint64_t it = 0; it < iters; ++it, i += stride) {
-    uint32_t pa = INVALID, pb = INVALID;
-    if (i < n) {
-      sheep_jnode x = a[i], y = b[i];
-      pa = x.parent; pb = y.parent;
-      pst_out[i] = x.pst_weight + y.pst_weight;
-      // a parent must be a later, existing node (jnode.cpp kids(current) via makeKids)
-      if ((pa != INVALID && (pa <= i || pa >= n)) || (pb != INVALID && (pb <= i || pb >= n))) {
-        bad = true; pa = pb = INVALID;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    uint64_t ea[TILE_ITEMS], eb[TILE_ITEMS];
+    uint32_t fa = 0, fb = 0;
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
+      uint32_t pa = INVALID, pb = INVALID;
+      if (i < n) {
+        const sheep_jnode x = a[i], y = b[i];
+        pa = x.parent;
+        pb = y.parent;
+        pst_out[i] = x.pst_weight + y.pst_weight;
+        // a parent must be a later, existing node (jnode.cpp kids(current) via makeKids)
+        if ((pa != INVALID && (pa <= i || pa >= n)) || (pb != INVALID && (pb <= i || pb >= n))) {
+          bad = true;
+          pa = pb = INVALID;
+        }
       }
+      ea[j] = ((uint64_t)pa << 32) | (uint32_t)i;
+      eb[j] = ((uint64_t)pb << 32) | (uint32_t)i;
+      if (pa != INVALID) fa |= 1u << j;
+      if (pb != INVALID && pb != pa) fb |= 1u << j;
     }
-    bool ea = pa != INVALID, eb = pb != INVALID && pb != pa;
-    uint64_t sa = wave_append(ea, counter);
-    if (ea) edges[sa] = ((uint64_t)pa << 32) | (uint32_t)i;
-    uint64_t sb = wave_append(eb, counter);
-    if (eb) edges[sb] = ((uint64_t)pb << 32) | (uint32_t)i;
+    uint64_t slot = block_reserve((uint32_t)(__popc(fa) + __popc(fb)), counter);
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      if (fa & (1u << j)) edges[slot++] = ea[j];
+      if (fb & (1u << j)) edges[slot++] = eb[j];
+    }
   }
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(err, 1ull);
 }
@@ -253,6 +303,8 @@ __global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t 
 }  // namespace
 
 void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
+
+static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
 
 // Elimination tree of `m` edges ((hi<<32)|lo, lo < hi < n).  `edges` is consumed.
 void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent) {
@@ -287,7 +339,7 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
     HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
     {
       TimedRegion tr(c, "etree_cross", 8 * live);
-      hipLaunchKernelGGL(k_cross_min, dim3(g), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, live, s, clo, uf, mt,
+      hipLaunchKernelGGL(k_cross_min, dim3(grid_tiles(live)), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, live, s, clo, uf, mt,
                          xidx, xtop, d);
       LAUNCH_CHECK();
     }
@@ -307,10 +359,11 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
       c.sync();
       dead += c.h_scalars[1];
     }
+    if (g_debug_etree) fprintf(stderr, "etree lvl %d s %d live %lu cross %lu dead %lu\n", lvl, s, (unsigned long)live, (unsigned long)nx, (unsigned long)dead);
     if (dead * 4 >= live && dead) {   // compact once a quarter of the list is dead
       HIP_CHECK(hipMemsetAsync(d + 2, 0, sizeof(uint64_t), c.stream));
       uint64_t *out = cur == edges ? alt : edges;
-      hipLaunchKernelGGL(k_compact_edges, dim3(grid_for(live)), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, live,
+      hipLaunchKernelGGL(k_compact_edges, dim3(grid_tiles(live)), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, live,
                          out, d + 2);
       LAUNCH_CHECK();
       cur = out;
@@ -330,7 +383,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
   if (nrec) {
     TimedRegion tr(c, "relabel", 20 * nrec);   // record + 2 pos gathers
-    hipLaunchKernelGGL(k_relabel, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos, pos_size, pst,
+    hipLaunchKernelGGL(k_relabel, dim3(grid_tiles(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos, pos_size, pst,
                        edges, d, d + 1);
     LAUNCH_CHECK();
   }
@@ -355,7 +408,7 @@ void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n,
   uint64_t *edges = c.get_as<uint64_t>("mg_edges", 2 * n);
   unsigned long long *d = (unsigned long long *)c.d_scalars + 10;
   HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
-  hipLaunchKernelGGL(k_tree_edges, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, a, b, n, edges, d, pst, d + 1);
+  hipLaunchKernelGGL(k_tree_edges, dim3(grid_tiles(n)), dim3(BLOCK), 0, c.stream, a, b, n, edges, d, pst, d + 1);
   LAUNCH_CHECK();
   HIP_CHECK(hipMemcpyAsync(c.h_scalars + 10, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();

@@ -14,6 +14,26 @@
 namespace sheep {
 namespace {
 
+// Adds w into cnt[key] for every lane whose key != INVALID, with one atomic per run of
+// equal keys in consecutive lanes (records sorted by tail, as generated and as many
+// edge lists are stored, make tail runs long; a hub's endpoints collapse too).
+__device__ __forceinline__ void run_add(uint32_t *cnt, uint32_t key, uint32_t w) {
+  const int lane = (int)__lane_id();
+  const uint32_t prev = __shfl_up(key, 1, 64);
+  const bool start = key != INVALID && (lane == 0 || prev != key);
+  const uint64_t starts = __ballot(start);
+  const uint32_t rid = (uint32_t)__popcll(starts & ((lane == 63) ? ~0ull : ((2ull << lane) - 1)));
+  uint32_t v = key != INVALID ? w : 0;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_down(v, o, 64);
+    const uint32_t ro = __shfl_down(rid, o, 64);
+    const uint32_t ko = __shfl_down(key, o, 64);
+    if (lane + o < 64 && ro == rid && ko == key) v += u;
+  }
+  if (start && v) atomicAdd(&cnt[key], v);
+}
+
 __global__ __launch_bounds__(BLOCK) void k_degree(const sheep_xs1 *__restrict__ rec, uint64_t nrec, int mode,
                                                   uint32_t *__restrict__ deg, uint64_t cap,
                                                   unsigned long long *__restrict__ d_max,
@@ -21,19 +41,25 @@ __global__ __launch_bounds__(BLOCK) void k_degree(const sheep_xs1 *__restrict__ 
   uint32_t lmax = 0;
   bool bad = false;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nrec; i += stride) {
-    sheep_xs1 r = rec[i];
-    uint32_t t = r.tail, h = r.head;
-    if (t >= cap || h >= cap) { bad = true; continue; }
-    uint32_t inc = (mode == SHEEP_DEGREE_FILE_DAT && i == nrec - 1) ? 2u : 1u;
-    if (mode == SHEEP_DEGREE_LLAMA && t == h) {
-      atomicAdd(&deg[t], 1u);
-    } else {
-      atomicAdd(&deg[t], inc);
-      atomicAdd(&deg[h], inc);
+  const uint64_t iters = (nrec + stride - 1) / stride;
+  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (uint64_t it = 0; it < iters; ++it, i += stride) {   // wave-uniform trip count
+    uint32_t kt = INVALID, kh = INVALID, inc = 1;
+    if (i < nrec) {
+      const sheep_xs1 r = rec[i];
+      const uint32_t t = r.tail, h = r.head;
+      if (t >= cap || h >= cap) {
+        bad = true;
+      } else {
+        inc = (mode == SHEEP_DEGREE_FILE_DAT && i == nrec - 1) ? 2u : 1u;
+        kt = t;
+        kh = (mode == SHEEP_DEGREE_LLAMA && t == h) ? INVALID : h;   // LLAMA: self-loop stored once
+        const uint32_t m = (t > h ? t : h) + 1;
+        lmax = m > lmax ? m : lmax;
+      }
     }
-    uint32_t m = (t > h ? t : h) + 1;
-    lmax = m > lmax ? m : lmax;
+    run_add(deg, kt, inc);
+    run_add(deg, kh, inc);
   }
   lmax = wave_max(lmax);
   if ((threadIdx.x & 63) == 0 && lmax) atomicMax(d_max, (unsigned long long)lmax);

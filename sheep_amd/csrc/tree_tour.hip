@@ -104,21 +104,32 @@ __device__ __forceinline__ bool hash_ruler(uint32_t a) {
   return (h & 63u) == 0;
 }
 
-__global__ void k_pick_rulers(const uint32_t *__restrict__ parent, uint64_t n, uint32_t head,
-                              uint32_t *__restrict__ rid, uint32_t *__restrict__ rulers,
-                              unsigned long long *__restrict__ counter) {
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+__global__ __launch_bounds__(BLOCK) void k_pick_rulers(const uint32_t *__restrict__ parent, uint64_t n, uint32_t head,
+                                                       uint32_t *__restrict__ rid, uint32_t *__restrict__ rulers,
+                                                       uint64_t cap, unsigned long long *__restrict__ counter) {
   const uint64_t total = 2 * n;
-  const uint64_t iters = (total + stride - 1) / stride;
-  uint64_t a = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  for (uint64_t it = 0; it < iters; ++it, a += stride) {
-    bool r = false;
-    if (a < total) {
-      uint32_t node = (uint32_t)(a < n ? a : a - n);
-      r = parent[node] != INVALID && (a == head || hash_ruler((uint32_t)a));
+  const uint64_t ntiles = (total + TILE - 1) / TILE;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    uint32_t flags = 0;
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      const uint64_t a = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
+      if (a < total) {
+        const uint32_t node = (uint32_t)(a < n ? a : a - n);
+        if (parent[node] != INVALID && (a == head || hash_ruler((uint32_t)a))) flags |= 1u << j;
+      }
     }
-    uint64_t slot = wave_append(r, counter);
-    if (r) { rid[a] = (uint32_t)slot; rulers[slot] = (uint32_t)a; }
+    uint64_t slot = block_reserve((uint32_t)__popc(flags), counter);
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j)
+      if (flags & (1u << j)) {
+        const uint32_t a = (uint32_t)(tile * TILE + (uint64_t)j * BLOCK + threadIdx.x);
+        if (slot < cap) {   // overflow is reported by the host (counter > cap)
+          rid[a] = (uint32_t)slot;
+          rulers[slot] = a;
+        }
+        ++slot;
+      }
   }
 }
 
@@ -265,15 +276,16 @@ void build_tour(Ctx &c, sheep_kids *k, Tour &t) {
   c.sync();
 
   uint32_t *rid = c.get_as<uint32_t>("tour_rid", 2 * n);
-  uint32_t *rulers = c.get_as<uint32_t>("tour_rulers", 2 * n / 16 + 1024);
+  const uint64_t rcap = 2 * n / 16 + 1024;   // expected 2n/64 hash-picked rulers
+  uint32_t *rulers = c.get_as<uint32_t>("tour_rulers", rcap);
   HIP_CHECK(hipMemsetAsync(d + 2, 0, sizeof(uint64_t), c.stream));
-  hipLaunchKernelGGL(k_pick_rulers, dim3(grid_for(2 * n)), dim3(BLOCK), 0, c.stream, k->parent, n, head, rid,
-                     rulers, d + 2);
+  hipLaunchKernelGGL(k_pick_rulers, dim3(grid_tiles(2 * n)), dim3(BLOCK), 0, c.stream, k->parent, n, head, rid,
+                     rulers, rcap, d + 2);
   LAUNCH_CHECK();
   HIP_CHECK(hipMemcpyAsync(c.h_scalars + 22, d + 2, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
   const uint64_t nr = c.h_scalars[22];
-  if (nr > 2 * n / 16 + 1024) throw Error(SHEEP_ERR_HIP, "tour: ruler overflow");
+  if (nr > rcap) throw Error(SHEEP_ERR_HIP, "tour: ruler overflow");
   uint32_t *owner = c.get_as<uint32_t>("tour_owner", 2 * n), *loff = c.get_as<uint32_t>("tour_loff", 2 * n);
   uint32_t *rlen = c.get_as<uint32_t>("tour_rlen", nr), *rnext = c.get_as<uint32_t>("tour_rnext", nr);
   uint32_t *rlen2 = c.get_as<uint32_t>("tour_rlen2", nr), *rnext2 = c.get_as<uint32_t>("tour_rnext2", nr);
