@@ -9,13 +9,15 @@
 //
 // GPU formulation:
 //   1. subtree sums S(v) on the GPU (Euler tour + prefix sums; tree_tour.hip);
-//   2. only H = {v : S(v) > max} can ever pack (cb <= S), and H is ancestor-closed;
-//      outside H, cb == S.  The GPU hands the host H in ascending order with
-//      L(v) = w(v) + sum of S over v's non-H kids and the rank of v's parent;
-//   3. the host replays the ascending pass over H only, running the packing steps with
-//      the reference's own std::sort/first-fit on the current kid order (kid segments
-//      of packing nodes are fetched and written back, so the order persists across k);
-//   4. roots are packed host-side in descending id order (cb(root) known);
+//   2. R(v) = cb(v) when the pass reaches v.  Only H = {v : S(v) > max} (ancestor-
+//      closed, R <= S) can pack, and the next packing node is the LOWEST id with
+//      R > max (everything below it is final).  One GPU pass over H per packing event
+//      subtracts the removed weight from the packed node and its ancestors (Euler-tour
+//      interval test) and finds the next such id;
+//   3. the host runs each packing with the reference's own std::sort on the node's
+//      current kid order plus first-fit (the sorted segment is written back, so the
+//      order persists across k like partition.cpp:104-106);
+//   4. roots are packed host-side in descending id order (their final R);
 //   5. the GPU pushes parts down: every node takes the part of its innermost assigned
 //      ancestor-or-self (assigned = packed kids + roots), found by binary search over
 //      the assigned nodes' Euler-tour intervals (laminar), then re-indexes jnid -> vid.
@@ -114,40 +116,6 @@ __global__ void k_pred_write(int which, const uint64_t *__restrict__ S, uint64_t
   }
 }
 
-// For H nodes: L = w + sum of non-H kids' S; parent rank.
-__global__ void k_h_init(const uint32_t *__restrict__ hids, uint64_t nh, const uint64_t *__restrict__ w,
-                         const uint32_t *__restrict__ parent, const uint32_t *__restrict__ hrank,
-                         uint64_t *__restrict__ L, uint32_t *__restrict__ hpar) {
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t h = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; h < nh; h += stride) {
-    uint32_t v = hids[h];
-    L[h] = w[v];
-    uint32_t p = parent[v];
-    hpar[h] = p == INVALID ? INVALID : hrank[p];
-  }
-}
-__global__ void k_h_light(const uint32_t *__restrict__ parent, uint64_t n, const uint32_t *__restrict__ hrank,
-                          const uint64_t *__restrict__ S, uint64_t *__restrict__ L) {
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t c = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; c < n; c += stride) {
-    uint32_t p = parent[c];
-    if (p == INVALID || hrank[c] != INVALID) continue;
-    uint32_t hp = hrank[p];
-    if (hp != INVALID) atomicAdd((unsigned long long *)&L[hp], (unsigned long long)S[c]);
-  }
-}
-
-// kid segment values for one packing node
-__global__ void k_kid_info(const uint32_t *__restrict__ kids, uint32_t beg, uint32_t cnt,
-                           const uint64_t *__restrict__ S, const uint32_t *__restrict__ hrank,
-                           uint64_t *__restrict__ outS, uint32_t *__restrict__ outH) {
-  for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < cnt; j += gridDim.x * BLOCK) {
-    uint32_t kid = kids[beg + j];
-    outS[j] = S[kid];
-    outH[j] = hrank[kid];
-  }
-}
-
 // Tour interval of every root with kids: [tD(first kid), tU(last kid)] in the kid order
 // the tour was built from.  Taken before the host replay re-sorts kid segments.
 __global__ void k_root_intervals(const uint32_t *__restrict__ rk, uint64_t nrk, const uint32_t *__restrict__ koff,
@@ -222,6 +190,52 @@ __global__ void k_parts_to_vid(const uint32_t *__restrict__ seq, uint64_t n, con
     if (c0) atomicAdd(&cnt[0], (unsigned long long)c0);
     if (c1) atomicAdd(&cnt[1], (unsigned long long)c1);
   }
+}
+
+// One packing event over H: the last packing (node v, tour position vpos, removed
+// weight delta) lowers R of v and of its ancestors; then the lowest id with R > max.
+__global__ __launch_bounds__(BLOCK) void k_pack_event(const uint32_t *__restrict__ hids, uint64_t nh,
+                                                      const uint32_t *__restrict__ hst, const uint32_t *__restrict__ hen,
+                                                      uint64_t *__restrict__ R, uint32_t v, uint32_t vpos,
+                                                      uint64_t delta, uint64_t maxc, uint32_t *__restrict__ next) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const uint64_t iters = (nh + stride - 1) / stride;
+  uint64_t h = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  uint32_t best = INVALID;
+  for (uint64_t it = 0; it < iters; ++it, h += stride) {
+    if (h >= nh) continue;
+    const uint32_t a = hids[h];
+    if (v != INVALID && a < v) continue;      // final: below the last packing node
+    uint64_t r = R[a];
+    if (delta && (a == v || (vpos != INVALID && hst[h] <= vpos && vpos <= hen[h]))) {
+      r -= delta;
+      R[a] = r;
+    }
+    if (r > maxc && (v == INVALID || a > v) && a < best) best = a;
+  }
+  best = wave_min(best);
+  if ((threadIdx.x & 63) == 0 && best != INVALID) atomicMin(next, best);
+}
+
+__global__ void k_event_info(uint32_t *__restrict__ ev, const uint32_t *__restrict__ koff,
+                             const uint32_t *__restrict__ parent, const uint32_t *__restrict__ tD) {
+  if (threadIdx.x != 0) return;
+  const uint32_t v = ev[0];
+  if (v == INVALID) return;
+  ev[1] = koff[v];
+  ev[2] = koff[v + 1];
+  ev[3] = parent[v] == INVALID ? INVALID : tD[v];
+}
+
+__global__ void k_kid_r(const uint32_t *__restrict__ kids, uint32_t beg, uint32_t cnt, const uint64_t *__restrict__ R,
+                        uint64_t *__restrict__ out) {
+  for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < cnt; j += gridDim.x * BLOCK) out[j] = R[kids[beg + j]];
+}
+
+__global__ void k_gather_r(const uint32_t *__restrict__ ids, uint64_t m, const uint64_t *__restrict__ R,
+                           uint64_t *__restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) out[i] = R[ids[i]];
 }
 
 // ---- facts ---------------------------------------------------------------------------
@@ -369,137 +383,121 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   hipLaunchKernelGGL(k_root_sums, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, k->parent, n, S);
   LAUNCH_CHECK();
 
-  // 3. heavy set H (ascending), L, parent ranks
-  uint32_t *hids = c.get_as<uint32_t>("pt_hids", n), *hrank = c.get_as<uint32_t>("pt_hrank", n);
-  const uint64_t nh = compact_pred(c, 0, S, max_component, k->parent, n, hids, hrank, "h");
+  // 3. packing events (partition.cpp:97-135).  R(v) = cb(v) when the ascending pass
+  // reaches v = S(v) minus what packings below v removed.  Ascending order means the
+  // next packing node is the LOWEST id with R > max: every node below it already has
+  // its final cb.  Only H = {v : S(v) > max} (ancestor-closed, R <= S) can pack, so each
+  // event is one pass over H: subtract the last packing's removed weight from the
+  // packed node and its ancestors (tour-interval test), then atomicMin the next id
+  // with R > max.  The host runs the packing itself with the reference's own
+  // std::sort on the node's current kid order and first-fit (order persists across k).
+  uint64_t *R = c.get_as<uint64_t>("pt_R", n);
+  HIP_CHECK(hipMemcpyAsync(R, S, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, c.stream));
+  uint32_t *hids = c.get_as<uint32_t>("pt_hids", n);
+  const uint64_t nh = compact_pred(c, 0, S, max_component, k->parent, n, hids, nullptr, "h");
   info->heavy_nodes = nh;
-  std::vector<uint32_t> h_ids(nh), h_par(nh);
-  std::vector<uint64_t> h_L(nh);
+  uint32_t *hst = c.get_as<uint32_t>("pt_hst", nh ? nh : 1), *hen = c.get_as<uint32_t>("pt_hen", nh ? nh : 1);
   if (nh) {
-    uint64_t *L = c.get_as<uint64_t>("pt_L", nh);
-    uint32_t *hpar = c.get_as<uint32_t>("pt_hpar", nh);
-    hipLaunchKernelGGL(k_h_init, dim3(grid_for(nh)), dim3(BLOCK), 0, c.stream, hids, nh, (const uint64_t *)w,
-                       k->parent, hrank, L, hpar);
+    hipLaunchKernelGGL(k_intervals, dim3(grid_for(nh)), dim3(BLOCK), 0, c.stream, hids, nh, k->parent, k->koff,
+                       (const uint32_t *)rst, (const uint32_t *)ren, t.tD, t.tU, hst, hen);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_h_light, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, k->parent, n, hrank,
-                       (const uint64_t *)S, L);
-    LAUNCH_CHECK();
-    d2h(c, h_ids.data(), hids, nh);
-    d2h(c, h_par.data(), hpar, nh);
-    d2h(c, h_L.data(), L, nh);
   }
-  // roots (ascending) with S and hrank
-  uint32_t *rids = c.get_as<uint32_t>("pt_roots", n);
-  const uint64_t nroots = compact_pred(c, 1, S, 0, k->parent, n, rids, nullptr, "r");
-  std::vector<uint32_t> r_ids(nroots), r_h(nroots);
-  std::vector<uint64_t> r_S(nroots);
-  {
-    uint64_t *rS = c.get_as<uint64_t>("pt_rS", nroots);
-    uint32_t *rH = c.get_as<uint32_t>("pt_rH", nroots);
-    // gather S (as two u32 halves) and hrank for the roots
-    gather_u32(c, hrank, rids, nroots, rH);
-    std::vector<uint32_t> tmp;
-    d2h(c, r_ids.data(), rids, nroots);
-    d2h(c, r_h.data(), rH, nroots);
-    c.sync();
-    // S for roots: small, fetch individually through a gathered staging buffer
-    std::vector<uint64_t> idx64(nroots);
-    if (nroots) {
-      // stage: rS[i] = S[rids[i]] via 2 x u32 gathers on the S array viewed as u32 pairs
-      uint32_t *lo = c.get_as<uint32_t>("pt_rSlo", nroots), *hi = c.get_as<uint32_t>("pt_rShi", nroots);
-      uint32_t *i2 = c.get_as<uint32_t>("pt_ridx2", 2 * nroots);
-      std::vector<uint32_t> h_i2(2 * nroots);
-      for (uint64_t i = 0; i < nroots; ++i) { h_i2[i] = 2 * r_ids[i]; h_i2[nroots + i] = 2 * r_ids[i] + 1; }
-      h2d(c, i2, h_i2.data(), 2 * nroots);
-      gather_u32(c, (const uint32_t *)S, i2, nroots, lo);
-      gather_u32(c, (const uint32_t *)S, i2 + nroots, nroots, hi);
-      std::vector<uint32_t> hl(nroots), hh(nroots);
-      d2h(c, hl.data(), lo, nroots);
-      d2h(c, hh.data(), hi, nroots);
-      c.sync();
-      for (uint64_t i = 0; i < nroots; ++i) r_S[i] = ((uint64_t)hh[i] << 32) | hl[i];
-    }
-    (void)rS;
-  }
-  c.sync();
-
-  // 4. host replay of the ascending pass over H (partition.cpp:97-135)
+  // ev[0] = next packing node (INVALID: none), ev[1..3] = koff[v], koff[v+1], tD(v)
+  uint32_t *ev = (uint32_t *)(c.d_scalars + 44);
+  uint32_t *h_ev = (uint32_t *)(c.h_scalars + 44);
   std::vector<uint64_t> part_size;
-  std::vector<uint64_t> cbH(nh, 0), acc(nh, 0);
   std::vector<uint32_t> asg_ids;
   std::vector<int16_t> asg_part;
-  uint64_t *kS = nullptr;
-  uint32_t *kH = nullptr;
-  std::vector<uint32_t> seg, segH;
-  std::vector<uint64_t> segS;
-  std::vector<uint32_t> koff_pair(2);
-  for (uint64_t h = 0; h < nh; ++h) {
-    uint64_t cb = h_L[h] + acc[h];
-    const uint32_t v = h_ids[h];
-    if (cb > max_component) {
-      info->packing_nodes++;
-      d2h(c, koff_pair.data(), k->koff + v, 2);
-      c.sync();
-      const uint32_t beg = koff_pair[0], cnt = koff_pair[1] - koff_pair[0];
-      seg.resize(cnt); segH.resize(cnt); segS.resize(cnt);
-      if (cnt) {
-        kS = c.get_as<uint64_t>("pt_kS", cnt);
-        kH = c.get_as<uint32_t>("pt_kH", cnt);
-        hipLaunchKernelGGL(k_kid_info, dim3(grid_for(cnt)), dim3(BLOCK), 0, c.stream, k->kids, beg, cnt,
-                           (const uint64_t *)S, hrank, kS, kH);
-        LAUNCH_CHECK();
-        d2h(c, seg.data(), k->kids + beg, cnt);
-        d2h(c, segS.data(), kS, cnt);
-        d2h(c, segH.data(), kH, cnt);
-        c.sync();
-      }
-      // cb of each kid: final cb for H kids (already processed: kid < v), S otherwise
-      std::vector<uint64_t> kidcb(cnt);
-      std::vector<uint32_t> order(cnt);
-      for (uint32_t j = 0; j < cnt; ++j) {
-        kidcb[j] = segH[j] != INVALID ? cbH[segH[j]] : segS[j];
-        order[j] = j;
-      }
-      // std::sort on the current kid order with the reference comparator (:104-106).
-      // Sorting indices with a comparator on kidcb is the same sort on the same keys.
-      std::sort(order.begin(), order.end(), [&kidcb](uint32_t a, uint32_t b) { return kidcb[a] > kidcb[b]; });
-      std::vector<uint32_t> sorted(cnt);
-      std::vector<uint64_t> scb(cnt);
-      for (uint32_t j = 0; j < cnt; ++j) { sorted[j] = seg[order[j]]; scb[j] = kidcb[order[j]]; }
+  std::vector<uint32_t> seg, order, sorted;
+  std::vector<uint64_t> segR, scb;
+  std::vector<char> done;
+  uint32_t v = INVALID, vpos = INVALID;
+  uint64_t delta = 0;
+  for (;;) {
+    HIP_CHECK(hipMemsetAsync(ev, 0xFF, sizeof(uint32_t), c.stream));
+    if (nh) {
+      hipLaunchKernelGGL(k_pack_event, dim3(grid_for(nh)), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh,
+                         (const uint32_t *)hst, (const uint32_t *)hen, R, v, vpos, delta, max_component, ev);
+      LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(k_event_info, dim3(1), dim3(WAVE), 0, c.stream, ev, k->koff, k->parent, t.tD);
+    LAUNCH_CHECK();
+    d2h(c, h_ev, (const uint32_t *)ev, 4);
+    c.sync();
+    v = h_ev[0];
+    if (v == INVALID) break;
+    info->packing_nodes++;
+    const uint32_t beg = h_ev[1], cnt = h_ev[2] - h_ev[1];
+    vpos = h_ev[3];
+    seg.resize(cnt); segR.resize(cnt);
+    if (cnt) {
+      uint64_t *kR = c.get_as<uint64_t>("pt_kR", cnt);
+      hipLaunchKernelGGL(k_kid_r, dim3(grid_for(cnt)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->kids, beg, cnt,
+                         (const uint64_t *)R, kR);
+      LAUNCH_CHECK();
+      d2h(c, seg.data(), (const uint32_t *)k->kids + beg, cnt);
+      d2h(c, segR.data(), (const uint64_t *)kR, cnt);
+    }
+    uint64_t cb = 0;
+    d2h(c, &cb, (const uint64_t *)R + v, 1);
+    c.sync();
+    const uint64_t cb0 = cb;
+    // std::sort on the current kid order with the reference comparator (:104-106);
+    // sorting positions with a comparator on their keys is the same sort.
+    order.resize(cnt);
+    for (uint32_t j = 0; j < cnt; ++j) order[j] = j;
+    std::sort(order.begin(), order.end(), [&segR](uint32_t a, uint32_t b) { return segR[a] > segR[b]; });
+    sorted.resize(cnt); scb.resize(cnt);
+    for (uint32_t j = 0; j < cnt; ++j) { sorted[j] = seg[order[j]]; scb[j] = segR[order[j]]; }
+    if (cnt) {
       h2d(c, k->kids + beg, sorted.data(), cnt);
-      c.sync();   // `sorted` is a pageable host buffer that dies with this iteration
-      std::vector<char> done(cnt, 0);
-      do {
-        for (uint32_t j = 0; cb > max_component && j < cnt; ++j) {
-          if (scb[j] > max_component) throw Error(SHEEP_ERR_PACK, "forwardPartition: kid exceeds max_component");
-          if (done[j]) continue;
-          for (size_t p = 0; p != part_size.size(); ++p) {
-            if (part_size[p] + scb[j] <= max_component) {
-              cb -= scb[j];
-              part_size[p] += scb[j];
-              done[j] = 1;
-              asg_ids.push_back(sorted[j]);
-              asg_part.push_back((int16_t)p);
-              break;
-            }
+      c.sync();   // `sorted` is a pageable host buffer reused by the next event
+    }
+    done.assign(cnt, 0);
+    do {
+      for (uint32_t j = 0; cb > max_component && j < cnt; ++j) {
+        if (scb[j] > max_component) throw Error(SHEEP_ERR_PACK, "forwardPartition: kid exceeds max_component");
+        if (done[j]) continue;
+        for (size_t p = 0; p != part_size.size(); ++p) {
+          if (part_size[p] + scb[j] <= max_component) {
+            cb -= scb[j];
+            part_size[p] += scb[j];
+            done[j] = 1;
+            asg_ids.push_back(sorted[j]);
+            asg_part.push_back((int16_t)p);
+            break;
           }
         }
-        if (cb > max_component) {
-          bool any = false;
-          for (uint32_t j = 0; j < cnt; ++j) any |= !done[j];
-          if (!any || part_size.size() >= 32767)
-            throw Error(SHEEP_ERR_PACK, "forwardPartition: node weight exceeds max_component (reference loops forever)");
-          part_size.push_back(0);
-        }
-      } while (cb > max_component);
-    }
-    cbH[h] = cb;
-    if (h_par[h] != INVALID) acc[h_par[h]] += cb;
+      }
+      if (cb > max_component) {
+        bool any = false;
+        for (uint32_t j = 0; j < cnt; ++j) any |= !done[j];
+        if (!any || part_size.size() >= 32767)
+          throw Error(SHEEP_ERR_PACK, "forwardPartition: node weight exceeds max_component (reference loops forever)");
+        part_size.push_back(0);
+      }
+    } while (cb > max_component);
+    delta = cb0 - cb;
   }
-  // 5. descending pass: roots into the highest bin that fits (:146-152)
+  // roots (ascending) with their final cb
+  uint32_t *rids = c.get_as<uint32_t>("pt_roots", n);
+  const uint64_t nroots = compact_pred(c, 1, S, 0, k->parent, n, rids, nullptr, "r");
+  std::vector<uint32_t> r_ids(nroots);
+  std::vector<uint64_t> r_cb(nroots);
+  if (nroots) {
+    uint64_t *rR = c.get_as<uint64_t>("pt_rR", nroots);
+    hipLaunchKernelGGL(k_gather_r, dim3(grid_for(nroots)), dim3(BLOCK), 0, c.stream, (const uint32_t *)rids, nroots,
+                       (const uint64_t *)R, rR);
+    LAUNCH_CHECK();
+    d2h(c, r_ids.data(), (const uint32_t *)rids, nroots);
+    d2h(c, r_cb.data(), (const uint64_t *)rR, nroots);
+    c.sync();
+  }
+
+  // 4. descending pass: roots into the highest bin that fits (:146-152)
   std::vector<int16_t> root_part(nroots);
   for (uint64_t ri = nroots; ri-- > 0;) {
-    uint64_t cb = r_h[ri] != INVALID ? cbH[r_h[ri]] : r_S[ri];
+    uint64_t cb = r_cb[ri];
     int16_t got = -1;
     while (got < 0) {
       for (long p = (long)part_size.size() - 1; p != -1; --p) {

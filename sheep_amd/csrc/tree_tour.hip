@@ -96,6 +96,11 @@ __global__ void k_rootnext(const uint32_t *__restrict__ rk, uint64_t nrk, const 
     rootnext[rk[i]] = i + 1 < nrk ? kids[koff[rk[i + 1]]] : INVALID;
 }
 
+__global__ void k_head(const uint32_t *__restrict__ rk, const uint32_t *__restrict__ koff,
+                       const uint32_t *__restrict__ kids, uint32_t *__restrict__ head) {
+  if (threadIdx.x == 0) head[0] = kids[koff[rk[0]]];
+}
+
 __device__ __forceinline__ bool hash_ruler(uint32_t a) {
   uint32_t h = a * 0x9E3779B1u;
   h ^= h >> 15;
@@ -266,14 +271,13 @@ void build_tour(Ctx &c, sheep_kids *k, Tour &t) {
                      rootnext, succ);
   LAUNCH_CHECK();
   // head = down arc into the first kid of the first root with kids
-  uint32_t first_rk = 0, head = 0;
-  HIP_CHECK(hipMemcpyAsync(&first_rk, rk, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+  uint32_t *dhead = (uint32_t *)(c.d_scalars + 24);
+  hipLaunchKernelGGL(k_head, dim3(1), dim3(WAVE), 0, c.stream, (const uint32_t *)rk, (const uint32_t *)k->koff,
+                     (const uint32_t *)k->kids, dhead);
+  LAUNCH_CHECK();
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 24, dhead, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
-  uint32_t koff_first = 0;
-  HIP_CHECK(hipMemcpyAsync(&koff_first, k->koff + first_rk, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
-  c.sync();
-  HIP_CHECK(hipMemcpyAsync(&head, k->kids + koff_first, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
-  c.sync();
+  const uint32_t head = (uint32_t)c.h_scalars[24];
 
   uint32_t *rid = c.get_as<uint32_t>("tour_rid", 2 * n);
   const uint64_t rcap = 2 * n / 16 + 1024;   // expected 2n/64 hash-picked rulers
@@ -296,15 +300,14 @@ void build_tour(Ctx &c, sheep_kids *k, Tour &t) {
     LAUNCH_CHECK();
   }
   uint32_t *sa = rlen, *na = rnext, *sb = rlen2, *nb2 = rnext2;
-  for (int it = 0; it < 40; ++it) {
-    HIP_CHECK(hipMemsetAsync(d + 3, 0, sizeof(uint64_t), c.stream));
+  // Wyllie jumping on ONE list of nr rulers: ceil(log2 nr) rounds, no host polling
+  int rounds = 0;
+  while ((1ull << rounds) < nr) ++rounds;
+  for (int it = 0; it < rounds; ++it) {
     hipLaunchKernelGGL(k_jump, dim3(grid_for(nr)), dim3(BLOCK), 0, c.stream, na, sa, nr, nb2, sb, d + 3);
     LAUNCH_CHECK();
     std::swap(sa, sb);
     std::swap(na, nb2);
-    HIP_CHECK(hipMemcpyAsync(c.h_scalars + 23, d + 3, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-    c.sync();
-    if (c.h_scalars[23] == 0) break;
   }
   hipLaunchKernelGGL(k_tpos, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, k->parent, n, owner, loff, sa,
                      (uint32_t)t.A, t.tD, t.tU);
