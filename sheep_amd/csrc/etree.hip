@@ -12,8 +12,8 @@
 // in G[0..x].  We compute it by divide and conquer over the position range, all
 // subproblems of one level at once:
 //   subproblem [l,r), split mid:  light = both ends < mid,  cross = lo < mid <= hi.
-//   * union-find over the light edges (hook smaller root under larger: the root of a
-//     component is its maximum = its "top" t);
+//   * union-find over the light edges (priority linking), then each component's
+//     maximum = its "top" t;
 //   * for every cross edge (a,b): t = top(a); m_t = min b  (atomicMin)  -> parent(t) = m_t;
 //   * contract: (a,b) -> (m_t, b); drop it when b == m_t; dedup contracted pairs.
 //   After the level every live edge lies inside one half; recurse.
@@ -32,49 +32,43 @@ constexpr uint64_t DEAD = ~0ull;
 
 __device__ __forceinline__ uint32_t spread(uint32_t x, uint32_t clo) { return x + __umulhi(x, clo); }
 
-// ---- union-find (values only move up: parent[x] > x) ------------------------------
-// Concurrent phase: agent-scope relaxed loads (L1 bypass) + CAS hooking; a CAS failure
-// returns the fresh value and the loop climbs from there, so stale reads only cost
-// retries, never correctness (hook target is always > the hooked root -> acyclic).
-__device__ __forceinline__ uint32_t ld_rlx(uint32_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_rlx(uint32_t *p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t find_conc(uint32_t *uf, uint32_t x) {
-  uint32_t p = ld_rlx(&uf[x]);
-  while (p != x) {
-    uint32_t gp = ld_rlx(&uf[p]);
-    if (gp == p) return p;
-    st_rlx(&uf[x], gp);
-    x = gp;
-    p = ld_rlx(&uf[x]);
-  }
-  return x;
-}
-__device__ __forceinline__ void union_conc(uint32_t *uf, uint32_t a, uint32_t b) {
-  uint32_t ra = find_conc(uf, a), rb = find_conc(uf, b);
-  while (ra != rb) {
-    if (ra > rb) { uint32_t t = ra; ra = rb; rb = t; }
-    uint32_t old = atomicCAS(&uf[ra], ra, rb);
-    if (old == ra) return;
-    ra = find_conc(uf, old);
-    rb = find_conc(uf, rb);
+// ---- union-find ---------------------------------------------------------------------
+// The forest is monotone: uf[x] only ever changes from x to a smaller root (CAS hook,
+// only on a current root, so no link is ever lost) or to a smaller ancestor (path
+// splitting), so every value a thread can read — even a stale L1 copy — is an ancestor
+// of x.  Plain loads/stores are therefore safe while other threads hook: a stale root
+// only makes its CAS fail, and the edge is simply kept for the next round.  The
+// component's top (its largest id, which the etree needs) is tracked separately.
+
+// Path splitting on two chains in lockstep (both loads in flight at once).
+__device__ __forceinline__ void find2(uint32_t *uf, uint32_t &x, uint32_t &y) {
+  uint32_t px = uf[x], py = uf[y];
+  while (px != x || py != y) {
+    if (px != x) {
+      const uint32_t g = uf[px];
+      if (g != px) uf[x] = g;
+      x = px;
+      px = g;
+    }
+    if (py != y) {
+      const uint32_t g = uf[py];
+      if (g != py) uf[y] = g;
+      y = py;
+      py = g;
+    }
   }
 }
-// Read-only phase (after a kernel boundary): plain loads + path halving.
 __device__ __forceinline__ uint32_t find_plain(uint32_t *uf, uint32_t x) {
   uint32_t p = uf[x];
   while (p != x) {
-    uint32_t gp = uf[p];
-    if (gp == p) return p;
-    uf[x] = gp;
-    x = gp;
-    p = uf[x];
+    const uint32_t g = uf[p];
+    if (g != p) uf[x] = g;
+    x = p;
+    p = g;
   }
   return x;
 }
+
 
 __device__ __forceinline__ uint32_t hash64(uint64_t k) {
   k ^= k >> 33; k *= 0xff51afd7ed558ccdull; k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ull; k ^= k >> 33;
@@ -128,89 +122,157 @@ __global__ __launch_bounds__(BLOCK) void k_relabel(const sheep_xs1 *__restrict__
 }
 
 // ---- one D&C level ---------------------------------------------------------------
-__global__ __launch_bounds__(BLOCK) void k_reset(uint32_t *__restrict__ uf, uint32_t *__restrict__ mt, uint64_t n) {
+__global__ __launch_bounds__(BLOCK) void k_reset(uint32_t *__restrict__ uf, uint32_t *__restrict__ mt,
+                                                 uint32_t *__restrict__ top, uint64_t n) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
     uf[i] = (uint32_t)i;
     mt[i] = INVALID;
+    top[i] = (uint32_t)i;
   }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_union_light(const uint64_t *__restrict__ edges, uint64_t m, int s,
-                                                       uint32_t clo, uint32_t *uf) {
+// top[root] = the component's largest id.  Every vertex of a non-singleton light
+// component is an endpoint of a light edge and its maximum is the hi end of one, so a
+// max over the light edges' hi ends suffices (singletons keep top = self).
+__global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict__ lbuf, uint64_t nl, uint32_t *uf,
+                                                     uint32_t *__restrict__ top) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) {
-    uint64_t e = edges[i];
-    if (e == DEAD) continue;
-    uint32_t a = (uint32_t)e, b = (uint32_t)(e >> 32);
-    uint32_t ya = spread(a, clo), yb = spread(b, clo);
-    if (((ya ^ yb) >> s) == 0 && ((yb >> s) & 1) == 0) union_conc(uf, a, b);
+  const uint64_t iters = (nl + stride - 1) / stride;
+  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (uint64_t it = 0; it < iters; ++it, i += stride) {   // wave-uniform trip count (ballots)
+    uint32_t r = 0, b = 0;
+    const bool live = i < nl;
+    if (live) {
+      const uint64_t e = lbuf[i];
+      b = (uint32_t)(e >> 32);
+      r = find_plain(uf, (uint32_t)e);
+    }
+    // top only grows: combine lanes sharing the first lane's root, skip useless atomics
+    const uint64_t lm = __ballot(live);
+    if (lm) {
+      const int first = __ffsll((unsigned long long)lm) - 1;
+      const uint32_t r0 = __shfl(r, first, 64);
+      const bool same = live && r == r0;
+      const uint32_t v = wave_max(same ? b : 0u);
+      if ((int)__lane_id() == first && v > top[r0]) atomicMax(&top[r0], v);
+      if (live && !same && b > top[r]) atomicMax(&top[r], b);
+    }
   }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_cross_min(const uint64_t *__restrict__ edges, uint64_t m, int s,
-                                                     uint32_t clo, uint32_t *uf, uint32_t *__restrict__ mt,
-                                                     uint32_t *__restrict__ xidx, uint32_t *__restrict__ xtop,
-                                                     unsigned long long *__restrict__ counter) {
+// One streaming pass classifies the live edges of a level: light (both ends in the
+// left half of their subproblem) -> the edge value into lbuf; cross -> its index into
+// xidx.  Edges inside a right half are left alone.  The dense lists keep every lane of
+// the union / find kernels busy (no divergence around dependent pointer chases).
+__global__ __launch_bounds__(BLOCK) void k_split(const uint64_t *__restrict__ edges, uint64_t m, int s, uint32_t clo,
+                                                 uint64_t *__restrict__ lbuf, uint32_t *__restrict__ xidx,
+                                                 unsigned long long *__restrict__ counters) {
   const uint64_t ntiles = (m + TILE - 1) / TILE;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    uint32_t tops[TILE_ITEMS];
-    uint32_t flags = 0;
+    uint64_t ev[TILE_ITEMS];
+    uint32_t fl = 0, fx = 0;
 #pragma unroll
     for (int j = 0; j < TILE_ITEMS; ++j) {
       const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
-      bool cross = false;
-      uint32_t t = 0, b = 0;
-      if (i < m) {
-        const uint64_t e = edges[i];
-        if (e != DEAD) {
-          const uint32_t a = (uint32_t)e;
-          b = (uint32_t)(e >> 32);
-          const uint32_t ya = spread(a, clo), yb = spread(b, clo);
-          if (((ya ^ yb) >> s) == 1) {
-            cross = true;
-            t = find_plain(uf, a);
-          }
-        }
-      }
-      tops[j] = t;
-      if (cross) flags |= 1u << j;
-      // m_t = min b over t's cross edges.  Power-law graphs send most cross edges of a
-      // level to one giant component's top, so combine in the wave first (lanes sharing
-      // the first cross lane's top) and skip atomics a plain read already shows useless
-      // (mt only decreases, so a stale read is >= the true value: skipping stays exact).
-      const uint64_t cm = __ballot(cross);
-      if (cm) {
-        const int first = __ffsll((unsigned long long)cm) - 1;
-        const uint32_t t0 = __shfl(t, first, 64);
-        const bool same = cross && t == t0;
-        const uint32_t v = wave_min(same ? b : INVALID);
-        if ((int)__lane_id() == first && v < mt[t0]) atomicMin(&mt[t0], v);
-        if (cross && !same && b < mt[t]) atomicMin(&mt[t], b);
-      }
+      ev[j] = i < m ? edges[i] : DEAD;
     }
-    uint64_t slot = block_reserve((uint32_t)__popc(flags), counter);
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      if (ev[j] == DEAD) continue;
+      const uint32_t ya = spread((uint32_t)ev[j], clo), yb = spread((uint32_t)(ev[j] >> 32), clo);
+      const uint32_t d = (ya ^ yb) >> s;
+      if (d == 0 && ((yb >> s) & 1) == 0) fl |= 1u << j;
+      else if (d == 1) fx |= 1u << j;
+    }
+    uint64_t sl = block_reserve((uint32_t)__popc(fl), counters);
+    uint64_t sx = block_reserve((uint32_t)__popc(fx), counters + 1);
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      if (fl & (1u << j)) lbuf[sl++] = ev[j];
+      if (fx & (1u << j)) xidx[sx++] = (uint32_t)(tile * TILE + (uint64_t)j * BLOCK + threadIdx.x);
+    }
+  }
+}
+
+// One hooking round over the unresolved light edges (Shiloach-Vishkin style, root =
+// smallest id): both roots; equal -> resolved; else ONE attempt to hook the larger
+// root under the smaller (CAS, succeeds only on a current root).  A failed attempt is
+// not retried here: the edge goes to `out` for the next round.  Retrying in place made
+// thousands of threads fight over a forming giant component's root (each failure =
+// another round trip); rounds instead resolve such a pile-up in a few passes.
+__global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict__ in, uint64_t nin, uint32_t *uf,
+                                                      uint64_t *__restrict__ out,
+                                                      unsigned long long *__restrict__ counter) {
+  const uint64_t ntiles = (nin + TILE - 1) / TILE;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    uint64_t ev[TILE_ITEMS];
+    uint32_t keep = 0;
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
+      ev[j] = i < nin ? in[i] : DEAD;
+    }
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      if (ev[j] == DEAD) continue;
+      uint32_t a = (uint32_t)ev[j], b = (uint32_t)(ev[j] >> 32);
+      find2(uf, a, b);
+      if (a == b) continue;
+      const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+      if (atomicCAS(&uf[hi], hi, lo) != hi) keep |= 1u << j;
+    }
+    uint64_t slot = block_reserve((uint32_t)__popc(keep), counter);
 #pragma unroll
     for (int j = 0; j < TILE_ITEMS; ++j)
-      if (flags & (1u << j)) {
-        xidx[slot] = (uint32_t)(tile * TILE + (uint64_t)j * BLOCK + threadIdx.x);
-        xtop[slot] = tops[j];
-        ++slot;
-      }
+      if (keep & (1u << j)) out[slot++] = ev[j];
+  }
+}
+
+// For every cross edge (a,b): r = root of a's light component; m_r = min b (atomicMin).
+__global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict__ edges,
+                                                      const uint32_t *__restrict__ xidx, uint64_t nx, uint32_t *uf,
+                                                      uint32_t *__restrict__ mt, uint32_t *__restrict__ xtop) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const uint64_t iters = (nx + stride - 1) / stride;
+  uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (uint64_t it = 0; it < iters; ++it, j += stride) {   // wave-uniform trip count (ballots)
+    const bool cross = j < nx;
+    uint32_t t = 0, b = 0;
+    if (cross) {
+      const uint64_t e = edges[xidx[j]];
+      b = (uint32_t)(e >> 32);
+      t = find_plain(uf, (uint32_t)e);
+      xtop[j] = t;
+    }
+    // Power-law graphs send most cross edges of a level to one giant component's top:
+    // combine in the wave first (lanes sharing the first lane's top) and skip atomics a
+    // plain read already shows useless (mt only decreases; a stale read is >= the true
+    // value, so skipping stays exact).
+    const uint64_t cm = __ballot(cross);
+    if (cm) {
+      const int first = __ffsll((unsigned long long)cm) - 1;
+      const uint32_t t0 = __shfl(t, first, 64);
+      const bool same = cross && t == t0;
+      const uint32_t v = wave_min(same ? b : INVALID);
+      if ((int)__lane_id() == first && v < mt[t0]) atomicMin(&mt[t0], v);
+      if (cross && !same && b < mt[t]) atomicMin(&mt[t], b);
+    }
   }
 }
 
 __global__ __launch_bounds__(BLOCK) void k_cross_apply(uint64_t *__restrict__ edges, const uint32_t *__restrict__ xidx,
                                                        const uint32_t *__restrict__ xtop, uint64_t nx,
-                                                       const uint32_t *__restrict__ mt, uint32_t *__restrict__ parent,
+                                                       const uint32_t *__restrict__ mt, const uint32_t *__restrict__ top,
+                                                       uint32_t *__restrict__ parent,
                                                        unsigned long long *__restrict__ table, uint32_t mask,
                                                        unsigned long long *__restrict__ dead) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   uint32_t ndead = 0;
   for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < nx; j += stride) {
-    uint32_t idx = xidx[j], t = xtop[j];
-    uint32_t m = mt[t];
-    parent[t] = m;   // every cross edge of t writes the same value
+    const uint32_t idx = xidx[j], r = xtop[j];
+    const uint32_t m = mt[r];
+    parent[top[r]] = m;   // every cross edge of the component writes the same value
     uint64_t e = edges[idx];
     uint32_t b = (uint32_t)(e >> 32);
     if (b == m) { edges[idx] = DEAD; ++ndead; continue; }
@@ -320,48 +382,72 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
 
   uint32_t *uf = c.get_as<uint32_t>("et_uf", n);
   uint32_t *mt = c.get_as<uint32_t>("et_mt", n);
+  uint32_t *top = c.get_as<uint32_t>("et_top", n);
   uint32_t *xidx = c.get_as<uint32_t>("et_xidx", m);
   uint32_t *xtop = c.get_as<uint32_t>("et_xtop", m);
   uint64_t *alt = c.get_as<uint64_t>("et_alt", m);
+  uint64_t *lbuf = c.get_as<uint64_t>("et_light", m);
   unsigned long long *d = (unsigned long long *)c.d_scalars;
   uint64_t *cur = edges;
   uint64_t live = m, dead = 0;
   for (int lvl = 0; lvl < L && live > 0; ++lvl) {
     const int s = L - 1 - lvl;
-    const unsigned g = grid_for(live);
-    hipLaunchKernelGGL(k_reset, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, uf, mt, n);
+    hipLaunchKernelGGL(k_reset, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, uf, mt, top, n);
     LAUNCH_CHECK();
+    HIP_CHECK(hipMemsetAsync(d, 0, 3 * sizeof(uint64_t), c.stream));
     {
-      TimedRegion tr(c, "etree_union", 8 * live);
-      hipLaunchKernelGGL(k_union_light, dim3(g), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, live, s, clo, uf);
+      TimedRegion tr(c, "etree_split", 8 * live);
+      hipLaunchKernelGGL(k_split, dim3(grid_tiles(live)), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, live, s,
+                         clo, lbuf, xidx, d);
       LAUNCH_CHECK();
     }
-    HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
-    {
-      TimedRegion tr(c, "etree_cross", 8 * live);
-      hipLaunchKernelGGL(k_cross_min, dim3(grid_tiles(live)), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, live, s, clo, uf, mt,
-                         xidx, xtop, d);
-      LAUNCH_CHECK();
-    }
-    HIP_CHECK(hipMemcpyAsync(c.h_scalars, d, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipMemcpyAsync(c.h_scalars, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
     c.sync();
-    uint64_t nx = c.h_scalars[0];
+    const uint64_t nl = c.h_scalars[0], nx = c.h_scalars[1];
+    if (nl) {
+      TimedRegion tr(c, "etree_union", 8 * nl);
+      const uint64_t *in = lbuf;
+      uint64_t nin = nl;
+      uint64_t *lwa = c.get_as<uint64_t>("et_lwa", nl), *lwb = c.get_as<uint64_t>("et_lwb", nl);
+      for (int round = 0; nin; ++round) {
+        uint64_t *out = (round & 1) ? lwb : lwa;
+        HIP_CHECK(hipMemsetAsync(d + 3, 0, sizeof(uint64_t), c.stream));
+        hipLaunchKernelGGL(k_hook_round, dim3(grid_tiles(nin)), dim3(BLOCK), 0, c.stream, in, nin, uf, out, d + 3);
+        LAUNCH_CHECK();
+        HIP_CHECK(hipMemcpyAsync(c.h_scalars + 3, d + 3, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+        c.sync();
+        nin = c.h_scalars[3];
+        in = out;
+        if (round > 4096) throw Error(SHEEP_ERR_HIP, "etree: union rounds do not converge");
+      }
+      hipLaunchKernelGGL(k_light_top, dim3(grid_for(nl)), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf, nl, uf, top);
+      LAUNCH_CHECK();
+    }
     if (nx) {
+      {
+        TimedRegion tr(c, "etree_cross", 16 * nx);
+        hipLaunchKernelGGL(k_cross_find, dim3(grid_for(nx)), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur,
+                           (const uint32_t *)xidx, nx, uf, mt, xtop);
+        LAUNCH_CHECK();
+      }
       uint64_t cap = 1024;
       while (cap < 2 * nx && cap < (1ull << 27)) cap <<= 1;
       unsigned long long *table = c.get_as<unsigned long long>("et_hash", cap);
       HIP_CHECK(hipMemsetAsync(table, 0xFF, cap * sizeof(uint64_t), c.stream));
       TimedRegion tr(c, "etree_apply", 28 * nx);
-      hipLaunchKernelGGL(k_cross_apply, dim3(grid_for(nx)), dim3(BLOCK), 0, c.stream, cur, xidx, xtop, nx, mt, parent,
-                         table, (uint32_t)(cap - 1), d + 1);
+      hipLaunchKernelGGL(k_cross_apply, dim3(grid_for(nx)), dim3(BLOCK), 0, c.stream, cur, xidx, xtop, nx, mt, top, parent,
+                         table, (uint32_t)(cap - 1), d + 2);
       LAUNCH_CHECK();
-      HIP_CHECK(hipMemcpyAsync(c.h_scalars + 1, d + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+      HIP_CHECK(hipMemcpyAsync(c.h_scalars + 2, d + 2, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
       c.sync();
-      dead += c.h_scalars[1];
+      dead += c.h_scalars[2];
     }
-    if (g_debug_etree) fprintf(stderr, "etree lvl %d s %d live %lu cross %lu dead %lu\n", lvl, s, (unsigned long)live, (unsigned long)nx, (unsigned long)dead);
+    if (g_debug_etree)
+      fprintf(stderr, "etree lvl %d s %d live %lu light %lu cross %lu dead %lu\n", lvl, s, (unsigned long)live,
+              (unsigned long)nl, (unsigned long)nx, (unsigned long)dead);
     if (dead * 4 >= live && dead) {   // compact once a quarter of the list is dead
       HIP_CHECK(hipMemsetAsync(d + 2, 0, sizeof(uint64_t), c.stream));
+      TimedRegion tr(c, "etree_compact", 16 * live);
       uint64_t *out = cur == edges ? alt : edges;
       hipLaunchKernelGGL(k_compact_edges, dim3(grid_tiles(live)), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, live,
                          out, d + 2);
