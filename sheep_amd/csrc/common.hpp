@@ -177,6 +177,24 @@ inline unsigned grid_tiles(uint64_t items, unsigned cap = 256 * 8) {
   return (unsigned)(t < cap ? t : cap);
 }
 
+// ---- sharded appends ------------------------------------------------------------------
+// Even one returning atomic per 2048-item tile saturates a single counter (~0.1 G/s):
+// a streaming pass over 1e9 edges would wait ~5 ms on it.  Tile t instead appends to
+// shard t % NSHARD (its own counter on its own 128-B line) inside the shard's region
+// of the output; shard k's region holds exactly the tiles t = k (mod NSHARD), so it
+// cannot overflow.  pack_shards() then moves the regions together (stable per shard).
+constexpr int NSHARD = 64;
+constexpr int SHARD_STRIDE = 16;   // u64 counters 128 B apart
+__host__ __device__ inline uint64_t shard_base(uint64_t ntiles, uint32_t k, uint32_t per_item) {
+  const uint64_t q = ntiles / NSHARD, r = ntiles % NSHARD;
+  return (uint64_t)TILE * per_item * (k * q + (k < r ? k : r));
+}
+__device__ __forceinline__ uint64_t shard_reserve(uint32_t cnt, unsigned long long *counters, uint64_t tile,
+                                                  uint64_t ntiles, uint32_t per_item) {
+  const uint32_t k = (uint32_t)(tile % NSHARD);
+  return shard_base(ntiles, k, per_item) + block_reserve(cnt, counters + (uint64_t)k * SHARD_STRIDE);
+}
+
 // Wave-aggregated append: every lane with `pred` gets a unique slot in [0, *counter).
 __device__ __forceinline__ uint64_t wave_append(bool pred, unsigned long long *counter) {
   uint64_t mask = __ballot(pred);
@@ -203,4 +221,10 @@ void radix_sort_pairs_u32(Ctx &c, uint32_t *keys, uint32_t *vals, uint64_t n, in
 void radix_sort_keys_u64(Ctx &c, uint64_t *keys, uint64_t n, int end_bit, uint64_t *keys_alt);
 // etree.hip
 void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent);
+// append.hip — sharded appends: counters (NSHARD * SHARD_STRIDE u64, zeroed), the pack
+// step returns the total and leaves the items contiguous in dst.
+unsigned long long *shard_counters(Ctx &c, const char *tag);
+template <typename T>
+uint64_t pack_shards(Ctx &c, const T *src, T *dst, uint64_t ntiles, uint32_t per_item,
+                     const unsigned long long *counters);
 }  // namespace sheep

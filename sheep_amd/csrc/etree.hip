@@ -83,17 +83,17 @@ __device__ __forceinline__ uint32_t hash64(uint64_t k) {
 __global__ __launch_bounds__(BLOCK) void k_relabel(const sheep_xs1 *__restrict__ rec, uint64_t nrec,
                                                    const uint32_t *__restrict__ pos, uint64_t pos_size,
                                                    uint32_t *__restrict__ pst, uint64_t *__restrict__ edges,
-                                                   unsigned long long *__restrict__ counter,
                                                    unsigned long long *__restrict__ err) {
+  // edges[i] = the relabelled tree edge of record i, or DEAD (no compaction: the first
+  // etree level skips holes, and self-loops / unsequenced endpoints are rare)
   const uint64_t ntiles = (nrec + TILE - 1) / TILE;
   bool bad = false;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     uint64_t ev[TILE_ITEMS];
-    uint32_t flags = 0;
 #pragma unroll
     for (int j = 0; j < TILE_ITEMS; ++j) {
       const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
-      ev[j] = 0;
+      ev[j] = DEAD;
       if (i >= nrec) continue;
       const sheep_xs1 r = rec[i];
       const uint32_t t = r.tail, h = r.head;
@@ -106,17 +106,17 @@ __global__ __launch_bounds__(BLOCK) void k_relabel(const sheep_xs1 *__restrict__
         const uint32_t lo = pt < ph ? pt : ph, hi = pt < ph ? ph : pt;
         atomicAdd(&pst[lo], 1u);
         ev[j] = ((uint64_t)hi << 32) | lo;
-        flags |= 1u << j;
       } else if (tin) {
         atomicAdd(&pst[pt], 1u);
       } else if (hin) {
         atomicAdd(&pst[ph], 1u);
       }
     }
-    uint64_t slot = block_reserve((uint32_t)__popc(flags), counter);
 #pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j)
-      if (flags & (1u << j)) edges[slot++] = ev[j];
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
+      if (i < nrec) edges[i] = ev[j];
+    }
   }
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(err, 1ull);
 }
@@ -167,7 +167,8 @@ __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict_
 // the union / find kernels busy (no divergence around dependent pointer chases).
 __global__ __launch_bounds__(BLOCK) void k_split(const uint64_t *__restrict__ edges, uint64_t m, int s, uint32_t clo,
                                                  uint64_t *__restrict__ lbuf, uint32_t *__restrict__ xidx,
-                                                 unsigned long long *__restrict__ counters) {
+                                                 unsigned long long *__restrict__ lcnt,
+                                                 unsigned long long *__restrict__ xcnt) {
   const uint64_t ntiles = (m + TILE - 1) / TILE;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     uint64_t ev[TILE_ITEMS];
@@ -185,8 +186,8 @@ __global__ __launch_bounds__(BLOCK) void k_split(const uint64_t *__restrict__ ed
       if (d == 0 && ((yb >> s) & 1) == 0) fl |= 1u << j;
       else if (d == 1) fx |= 1u << j;
     }
-    uint64_t sl = block_reserve((uint32_t)__popc(fl), counters);
-    uint64_t sx = block_reserve((uint32_t)__popc(fx), counters + 1);
+    uint64_t sl = shard_reserve((uint32_t)__popc(fl), lcnt, tile, ntiles, 1);
+    uint64_t sx = shard_reserve((uint32_t)__popc(fx), xcnt, tile, ntiles, 1);
 #pragma unroll
     for (int j = 0; j < TILE_ITEMS; ++j) {
       if (fl & (1u << j)) lbuf[sl++] = ev[j];
@@ -222,7 +223,7 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
       const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
       if (atomicCAS(&uf[hi], hi, lo) != hi) keep |= 1u << j;
     }
-    uint64_t slot = block_reserve((uint32_t)__popc(keep), counter);
+    uint64_t slot = shard_reserve((uint32_t)__popc(keep), counter, tile, ntiles, 1);
 #pragma unroll
     for (int j = 0; j < TILE_ITEMS; ++j)
       if (keep & (1u << j)) out[slot++] = ev[j];
@@ -289,8 +290,16 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(uint64_t *__restrict__ ed
     if (dup) { edges[idx] = DEAD; ++ndead; }
     else edges[idx] = ne;
   }
+  // one add per workgroup, spread over the shard counters (a single hot counter
+  // serialises ~1e5 adds per millisecond)
+  __shared__ uint32_t s_dead[BLOCK / WAVE];
   ndead = wave_sum(ndead);
-  if ((threadIdx.x & 63) == 0 && ndead) atomicAdd(dead, (unsigned long long)ndead);
+  if ((threadIdx.x & 63) == 0) s_dead[threadIdx.x >> 6] = ndead;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = s_dead[0] + s_dead[1] + s_dead[2] + s_dead[3];
+    if (t) atomicAdd(dead + (uint64_t)(blockIdx.x % NSHARD) * SHARD_STRIDE, (unsigned long long)t);
+  }
 }
 
 __global__ __launch_bounds__(BLOCK) void k_compact_edges(const uint64_t *__restrict__ in, uint64_t m,
@@ -305,48 +314,31 @@ __global__ __launch_bounds__(BLOCK) void k_compact_edges(const uint64_t *__restr
       ev[j] = i < m ? in[i] : DEAD;
       if (ev[j] != DEAD) flags |= 1u << j;
     }
-    uint64_t slot = block_reserve((uint32_t)__popc(flags), counter);
+    uint64_t slot = shard_reserve((uint32_t)__popc(flags), counter, tile, ntiles, 1);
 #pragma unroll
     for (int j = 0; j < TILE_ITEMS; ++j)
       if (flags & (1u << j)) out[slot++] = ev[j];
   }
 }
 
+// Parent edges of both trees, in place: edges[2i] from a, edges[2i+1] from b (DEAD when
+// absent or equal to a's).
 __global__ __launch_bounds__(BLOCK) void k_tree_edges(const sheep_jnode *__restrict__ a, const sheep_jnode *__restrict__ b,
                                                       uint64_t n, uint64_t *__restrict__ edges,
-                                                      unsigned long long *__restrict__ counter,
                                                       uint32_t *__restrict__ pst_out, unsigned long long *__restrict__ err) {
-  const uint64_t ntiles = (n + TILE - 1) / TILE;
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   bool bad = false;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    uint64_t ea[TILE_ITEMS], eb[TILE_ITEMS];
-    uint32_t fa = 0, fb = 0;
-#pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) {
-      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
-      uint32_t pa = INVALID, pb = INVALID;
-      if (i < n) {
-        const sheep_jnode x = a[i], y = b[i];
-        pa = x.parent;
-        pb = y.parent;
-        pst_out[i] = x.pst_weight + y.pst_weight;
-        // a parent must be a later, existing node (jnode.cpp kids(current) via makeKids)
-        if ((pa != INVALID && (pa <= i || pa >= n)) || (pb != INVALID && (pb <= i || pb >= n))) {
-          bad = true;
-          pa = pb = INVALID;
-        }
-      }
-      ea[j] = ((uint64_t)pa << 32) | (uint32_t)i;
-      eb[j] = ((uint64_t)pb << 32) | (uint32_t)i;
-      if (pa != INVALID) fa |= 1u << j;
-      if (pb != INVALID && pb != pa) fb |= 1u << j;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
+    const sheep_jnode x = a[i], y = b[i];
+    uint32_t pa = x.parent, pb = y.parent;
+    pst_out[i] = x.pst_weight + y.pst_weight;
+    // a parent must be a later, existing node (jnode.cpp kids(current) via makeKids)
+    if ((pa != INVALID && (pa <= i || pa >= n)) || (pb != INVALID && (pb <= i || pb >= n))) {
+      bad = true;
+      pa = pb = INVALID;
     }
-    uint64_t slot = block_reserve((uint32_t)(__popc(fa) + __popc(fb)), counter);
-#pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) {
-      if (fa & (1u << j)) edges[slot++] = ea[j];
-      if (fb & (1u << j)) edges[slot++] = eb[j];
-    }
+    edges[2 * i] = pa != INVALID ? ((uint64_t)pa << 32) | (uint32_t)i : DEAD;
+    edges[2 * i + 1] = pb != INVALID && pb != pa ? ((uint64_t)pb << 32) | (uint32_t)i : DEAD;
   }
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(err, 1ull);
 }
@@ -383,42 +375,49 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
   uint32_t *uf = c.get_as<uint32_t>("et_uf", n);
   uint32_t *mt = c.get_as<uint32_t>("et_mt", n);
   uint32_t *top = c.get_as<uint32_t>("et_top", n);
+  // scratch regions of sharded appends need whole tiles: m rounded up
+  const uint64_t mcap = (m + TILE - 1) / TILE * TILE;
   uint32_t *xidx = c.get_as<uint32_t>("et_xidx", m);
-  uint32_t *xtop = c.get_as<uint32_t>("et_xtop", m);
-  uint64_t *alt = c.get_as<uint64_t>("et_alt", m);
-  uint64_t *lbuf = c.get_as<uint64_t>("et_light", m);
+  uint32_t *xtop = c.get_as<uint32_t>("et_xtop", mcap);   // also the cross list's shard scratch
+  uint64_t *alt = c.get_as<uint64_t>("et_alt", mcap);     // shard scratch: light list, compaction
+  unsigned long long *lcnt = shard_counters(c, "light"), *xcnt = shard_counters(c, "cross");
+  unsigned long long *hcnt = shard_counters(c, "hook"), *ccnt = shard_counters(c, "compact");
+  unsigned long long *dcnt = shard_counters(c, "dead");
+  std::vector<uint64_t> h_dcnt(NSHARD * SHARD_STRIDE);
   unsigned long long *d = (unsigned long long *)c.d_scalars;
-  uint64_t *cur = edges;
   uint64_t live = m, dead = 0;
   for (int lvl = 0; lvl < L && live > 0; ++lvl) {
     const int s = L - 1 - lvl;
+    const uint64_t ntl = (live + TILE - 1) / TILE;
     hipLaunchKernelGGL(k_reset, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, uf, mt, top, n);
     LAUNCH_CHECK();
-    HIP_CHECK(hipMemsetAsync(d, 0, 3 * sizeof(uint64_t), c.stream));
+    HIP_CHECK(hipMemsetAsync(lcnt, 0, NSHARD * SHARD_STRIDE * sizeof(uint64_t), c.stream));
+    HIP_CHECK(hipMemsetAsync(xcnt, 0, NSHARD * SHARD_STRIDE * sizeof(uint64_t), c.stream));
+    uint64_t nl = 0, nx = 0;
+    uint64_t *lbuf = nullptr;
     {
       TimedRegion tr(c, "etree_split", 8 * live);
-      hipLaunchKernelGGL(k_split, dim3(grid_tiles(live)), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, live, s,
-                         clo, lbuf, xidx, d);
+      hipLaunchKernelGGL(k_split, dim3(grid_tiles(live)), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges, live, s,
+                         clo, alt, xtop, lcnt, xcnt);
       LAUNCH_CHECK();
+      // the dense light list must outlive the hook rounds (k_light_top reads it)
+      lbuf = c.get_as<uint64_t>("et_light", live);
+      nl = pack_shards<uint64_t>(c, alt, lbuf, ntl, 1, lcnt);
+      nx = pack_shards<uint32_t>(c, xtop, xidx, ntl, 1, xcnt);
     }
-    HIP_CHECK(hipMemcpyAsync(c.h_scalars, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-    c.sync();
-    const uint64_t nl = c.h_scalars[0], nx = c.h_scalars[1];
     if (nl) {
       TimedRegion tr(c, "etree_union", 8 * nl);
+      const uint64_t lcap = (nl + TILE - 1) / TILE * TILE;
+      uint64_t *scr = c.get_as<uint64_t>("et_lwa", lcap), *dst = c.get_as<uint64_t>("et_lwb", lcap);
       const uint64_t *in = lbuf;
       uint64_t nin = nl;
-      uint64_t *lwa = c.get_as<uint64_t>("et_lwa", nl), *lwb = c.get_as<uint64_t>("et_lwb", nl);
       for (int round = 0; nin; ++round) {
-        uint64_t *out = (round & 1) ? lwb : lwa;
-        HIP_CHECK(hipMemsetAsync(d + 3, 0, sizeof(uint64_t), c.stream));
-        hipLaunchKernelGGL(k_hook_round, dim3(grid_tiles(nin)), dim3(BLOCK), 0, c.stream, in, nin, uf, out, d + 3);
-        LAUNCH_CHECK();
-        HIP_CHECK(hipMemcpyAsync(c.h_scalars + 3, d + 3, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-        c.sync();
-        nin = c.h_scalars[3];
-        in = out;
         if (round > 4096) throw Error(SHEEP_ERR_HIP, "etree: union rounds do not converge");
+        HIP_CHECK(hipMemsetAsync(hcnt, 0, NSHARD * SHARD_STRIDE * sizeof(uint64_t), c.stream));
+        hipLaunchKernelGGL(k_hook_round, dim3(grid_tiles(nin)), dim3(BLOCK), 0, c.stream, in, nin, uf, scr, hcnt);
+        LAUNCH_CHECK();
+        nin = pack_shards<uint64_t>(c, scr, dst, (nin + TILE - 1) / TILE, 1, hcnt);
+        in = dst;
       }
       hipLaunchKernelGGL(k_light_top, dim3(grid_for(nl)), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf, nl, uf, top);
       LAUNCH_CHECK();
@@ -426,7 +425,7 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
     if (nx) {
       {
         TimedRegion tr(c, "etree_cross", 16 * nx);
-        hipLaunchKernelGGL(k_cross_find, dim3(grid_for(nx)), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur,
+        hipLaunchKernelGGL(k_cross_find, dim3(grid_for(nx)), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges,
                            (const uint32_t *)xidx, nx, uf, mt, xtop);
         LAUNCH_CHECK();
       }
@@ -435,25 +434,24 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
       unsigned long long *table = c.get_as<unsigned long long>("et_hash", cap);
       HIP_CHECK(hipMemsetAsync(table, 0xFF, cap * sizeof(uint64_t), c.stream));
       TimedRegion tr(c, "etree_apply", 28 * nx);
-      hipLaunchKernelGGL(k_cross_apply, dim3(grid_for(nx)), dim3(BLOCK), 0, c.stream, cur, xidx, xtop, nx, mt, top, parent,
-                         table, (uint32_t)(cap - 1), d + 2);
+      HIP_CHECK(hipMemsetAsync(dcnt, 0, NSHARD * SHARD_STRIDE * sizeof(uint64_t), c.stream));
+      hipLaunchKernelGGL(k_cross_apply, dim3(grid_for(nx)), dim3(BLOCK), 0, c.stream, edges, xidx, xtop, nx, mt, top,
+                         parent, table, (uint32_t)(cap - 1), dcnt);
       LAUNCH_CHECK();
-      HIP_CHECK(hipMemcpyAsync(c.h_scalars + 2, d + 2, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+      HIP_CHECK(hipMemcpyAsync(h_dcnt.data(), dcnt, h_dcnt.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
       c.sync();
-      dead += c.h_scalars[2];
+      for (int k = 0; k < NSHARD; ++k) dead += h_dcnt[(uint64_t)k * SHARD_STRIDE];
     }
     if (g_debug_etree)
       fprintf(stderr, "etree lvl %d s %d live %lu light %lu cross %lu dead %lu\n", lvl, s, (unsigned long)live,
               (unsigned long)nl, (unsigned long)nx, (unsigned long)dead);
     if (dead * 4 >= live && dead) {   // compact once a quarter of the list is dead
-      HIP_CHECK(hipMemsetAsync(d + 2, 0, sizeof(uint64_t), c.stream));
       TimedRegion tr(c, "etree_compact", 16 * live);
-      uint64_t *out = cur == edges ? alt : edges;
-      hipLaunchKernelGGL(k_compact_edges, dim3(grid_tiles(live)), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, live,
-                         out, d + 2);
+      HIP_CHECK(hipMemsetAsync(ccnt, 0, NSHARD * SHARD_STRIDE * sizeof(uint64_t), c.stream));
+      hipLaunchKernelGGL(k_compact_edges, dim3(grid_tiles(live)), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges,
+                         live, alt, ccnt);
       LAUNCH_CHECK();
-      cur = out;
-      live -= dead;
+      live = pack_shards<uint64_t>(c, alt, edges, ntl, 1, ccnt);
       dead = 0;
     }
   }
@@ -466,17 +464,17 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   HIP_CHECK(hipMemsetAsync(pst, 0, n * sizeof(uint32_t), c.stream));
   uint64_t *edges = c.get_as<uint64_t>("bt_edges", nrec ? nrec : 1);
   unsigned long long *d = (unsigned long long *)c.d_scalars + 8;
-  HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
+  HIP_CHECK(hipMemsetAsync(d + 1, 0, sizeof(uint64_t), c.stream));
   if (nrec) {
     TimedRegion tr(c, "relabel", 20 * nrec);   // record + 2 pos gathers
     hipLaunchKernelGGL(k_relabel, dim3(grid_tiles(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos, pos_size, pst,
-                       edges, d, d + 1);
+                       edges, d + 1);
     LAUNCH_CHECK();
   }
-  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 8, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 9, d + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
   if (c.h_scalars[9]) throw Error(SHEEP_ERR_RANGE, "vector::_M_range_check: neighbour vid beyond the sequence's index (jtree.cpp:75)");
-  uint64_t m = c.h_scalars[8];
+  const uint64_t m = nrec;   // edges[i] per record, DEAD holes included
   {
     TimedRegion tr(c, "etree", 8 * m);
     etree_from_edges(c, edges, m, n, parent);
@@ -493,15 +491,15 @@ void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n,
   uint32_t *parent = c.get_as<uint32_t>("mg_parent", n);
   uint64_t *edges = c.get_as<uint64_t>("mg_edges", 2 * n);
   unsigned long long *d = (unsigned long long *)c.d_scalars + 10;
-  HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
-  hipLaunchKernelGGL(k_tree_edges, dim3(grid_tiles(n)), dim3(BLOCK), 0, c.stream, a, b, n, edges, d, pst, d + 1);
+  HIP_CHECK(hipMemsetAsync(d + 1, 0, sizeof(uint64_t), c.stream));
+  hipLaunchKernelGGL(k_tree_edges, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, a, b, n, edges, pst, d + 1);
   LAUNCH_CHECK();
-  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 10, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 11, d + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
   if (c.h_scalars[11]) throw Error(SHEEP_ERR_ARG, "merge: a parent is not a later node of the tree");
   {
     TimedRegion tr(c, "merge", 16 * n);
-    etree_from_edges(c, edges, c.h_scalars[10], n, parent);
+    etree_from_edges(c, edges, 2 * n, n, parent);
   }
   hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);
   LAUNCH_CHECK();
