@@ -70,11 +70,6 @@ __device__ __forceinline__ uint32_t find_plain(uint32_t *uf, uint32_t x) {
 }
 
 
-__device__ __forceinline__ uint32_t hash64(uint64_t k) {
-  k ^= k >> 33; k *= 0xff51afd7ed558ccdull; k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ull; k ^= k >> 33;
-  return (uint32_t)k;
-}
-
 // ---- relabel + pst (jtree.cpp:72-91) -------------------------------------------------
 // One record = one undirected pair.  Both endpoints sequenced: pst[lo]++ and a tree
 // edge (lo,hi).  One endpoint sequenced, the other a slot < pos_size but absent from
@@ -123,12 +118,13 @@ __global__ __launch_bounds__(BLOCK) void k_relabel(const sheep_xs1 *__restrict__
 
 // ---- one D&C level ---------------------------------------------------------------
 __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t *__restrict__ uf, uint32_t *__restrict__ mt,
-                                                 uint32_t *__restrict__ top, uint64_t n) {
+                                                 uint32_t *__restrict__ top, uint32_t *__restrict__ claim, uint64_t n) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
     uf[i] = (uint32_t)i;
     mt[i] = INVALID;
     top[i] = (uint32_t)i;
+    claim[i] = INVALID;
   }
 }
 
@@ -230,6 +226,17 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
   }
 }
 
+// parent(top of every component with a cross edge) = m_r (jnode.h:158-162 adopt).
+__global__ __launch_bounds__(BLOCK) void k_assign_parents(const uint32_t *__restrict__ uf, const uint32_t *__restrict__ mt,
+                                                          const uint32_t *__restrict__ top, uint64_t n,
+                                                          uint32_t *__restrict__ parent) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride) {
+    const uint32_t m = mt[v];
+    if (m != INVALID && uf[v] == v) parent[top[v]] = m;
+  }
+}
+
 // For every cross edge (a,b): r = root of a's light component; m_r = min b (atomicMin).
 __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict__ edges,
                                                       const uint32_t *__restrict__ xidx, uint64_t nx, uint32_t *uf,
@@ -262,33 +269,32 @@ __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict
   }
 }
 
+// Contract every cross edge (a,b) -> (m_r, b) where r = a's light component; drop it
+// when b == m_r.  Dedup: claim[b] holds the first contracted lo seen for b; an edge that
+// finds its own m_r there is a duplicate of a kept edge and dies.  (Exact: only equal
+// (m_r, b) pairs die, and the claimant itself is kept.  Lossy: a second distinct m for
+// the same b is kept without a check — the common duplicates, a giant component's many
+// edges into one hub, all carry the same m.)  claim is n x u32, L3-resident, unlike a
+// global hash table of the pairs.
 __global__ __launch_bounds__(BLOCK) void k_cross_apply(uint64_t *__restrict__ edges, const uint32_t *__restrict__ xidx,
                                                        const uint32_t *__restrict__ xtop, uint64_t nx,
-                                                       const uint32_t *__restrict__ mt, const uint32_t *__restrict__ top,
-                                                       uint32_t *__restrict__ parent,
-                                                       unsigned long long *__restrict__ table, uint32_t mask,
+                                                       const uint32_t *__restrict__ mt, uint32_t *__restrict__ claim,
                                                        unsigned long long *__restrict__ dead) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   uint32_t ndead = 0;
   for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < nx; j += stride) {
     const uint32_t idx = xidx[j], r = xtop[j];
     const uint32_t m = mt[r];
-    parent[top[r]] = m;   // every cross edge of the component writes the same value
-    uint64_t e = edges[idx];
-    uint32_t b = (uint32_t)(e >> 32);
-    if (b == m) { edges[idx] = DEAD; ++ndead; continue; }
-    uint64_t ne = ((uint64_t)b << 32) | m;
-    // lossy dedup of contracted pairs: bounded linear probing; on overflow keep the edge
-    uint32_t h = hash64(ne) & mask;
-    bool dup = false;
-    for (int probe = 0; probe < 16; ++probe) {
-      unsigned long long old = atomicCAS(&table[h], DEAD, (unsigned long long)ne);
-      if (old == DEAD) break;
-      if (old == ne) { dup = true; break; }
-      h = (h + 1) & mask;
+    const uint64_t e = edges[idx];
+    const uint32_t b = (uint32_t)(e >> 32);
+    bool kill = b == m;
+    if (!kill) {
+      uint32_t c = claim[b];
+      if (c == INVALID) c = atomicCAS(&claim[b], INVALID, m);
+      kill = c == m;   // someone else's (m, b) is kept (our own successful CAS returned INVALID)
     }
-    if (dup) { edges[idx] = DEAD; ++ndead; }
-    else edges[idx] = ne;
+    if (kill) { edges[idx] = DEAD; ++ndead; }
+    else edges[idx] = ((uint64_t)b << 32) | m;
   }
   // one add per workgroup, spread over the shard counters (a single hot counter
   // serialises ~1e5 adds per millisecond)
@@ -375,6 +381,7 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
   uint32_t *uf = c.get_as<uint32_t>("et_uf", n);
   uint32_t *mt = c.get_as<uint32_t>("et_mt", n);
   uint32_t *top = c.get_as<uint32_t>("et_top", n);
+  uint32_t *claim = c.get_as<uint32_t>("et_claim", n);
   // scratch regions of sharded appends need whole tiles: m rounded up
   const uint64_t mcap = (m + TILE - 1) / TILE * TILE;
   uint32_t *xidx = c.get_as<uint32_t>("et_xidx", m);
@@ -389,7 +396,7 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
   for (int lvl = 0; lvl < L && live > 0; ++lvl) {
     const int s = L - 1 - lvl;
     const uint64_t ntl = (live + TILE - 1) / TILE;
-    hipLaunchKernelGGL(k_reset, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, uf, mt, top, n);
+    hipLaunchKernelGGL(k_reset, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, uf, mt, top, claim, n);
     LAUNCH_CHECK();
     HIP_CHECK(hipMemsetAsync(lcnt, 0, NSHARD * SHARD_STRIDE * sizeof(uint64_t), c.stream));
     HIP_CHECK(hipMemsetAsync(xcnt, 0, NSHARD * SHARD_STRIDE * sizeof(uint64_t), c.stream));
@@ -429,14 +436,13 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
                            (const uint32_t *)xidx, nx, uf, mt, xtop);
         LAUNCH_CHECK();
       }
-      uint64_t cap = 1024;
-      while (cap < 2 * nx && cap < (1ull << 27)) cap <<= 1;
-      unsigned long long *table = c.get_as<unsigned long long>("et_hash", cap);
-      HIP_CHECK(hipMemsetAsync(table, 0xFF, cap * sizeof(uint64_t), c.stream));
-      TimedRegion tr(c, "etree_apply", 28 * nx);
+      TimedRegion tr(c, "etree_apply", 20 * nx);
+      hipLaunchKernelGGL(k_assign_parents, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)uf,
+                         (const uint32_t *)mt, (const uint32_t *)top, n, parent);
+      LAUNCH_CHECK();
       HIP_CHECK(hipMemsetAsync(dcnt, 0, NSHARD * SHARD_STRIDE * sizeof(uint64_t), c.stream));
-      hipLaunchKernelGGL(k_cross_apply, dim3(grid_for(nx)), dim3(BLOCK), 0, c.stream, edges, xidx, xtop, nx, mt, top,
-                         parent, table, (uint32_t)(cap - 1), dcnt);
+      hipLaunchKernelGGL(k_cross_apply, dim3(grid_for(nx)), dim3(BLOCK), 0, c.stream, edges, xidx, xtop, nx, mt, claim,
+                         dcnt);
       LAUNCH_CHECK();
       HIP_CHECK(hipMemcpyAsync(h_dcnt.data(), dcnt, h_dcnt.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
       c.sync();
