@@ -219,6 +219,9 @@ void scan_exclusive_u64(Ctx &c, const uint64_t *in, uint64_t *out, uint64_t n, u
 void radix_sort_pairs_u32(Ctx &c, uint32_t *keys, uint32_t *vals, uint64_t n, int end_bit,
                           uint32_t *keys_alt, uint32_t *vals_alt);
 void radix_sort_keys_u64(Ctx &c, uint64_t *keys, uint64_t n, int end_bit, uint64_t *keys_alt);
+// hist.hip — cnt[key] += occurrences, keys bucketed through LDS (no scattered atomics)
+void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt);
+void histogram_edge_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t K, uint32_t *cnt);
 // etree.hip
 void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent);
 // append.hip — sharded appends: counters (NSHARD * SHARD_STRIDE u64, zeroed), the pack

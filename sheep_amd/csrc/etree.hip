@@ -99,8 +99,7 @@ __global__ __launch_bounds__(BLOCK) void k_relabel(const sheep_xs1 *__restrict__
       if ((tin && h >= pos_size) || (hin && t >= pos_size)) { bad = true; continue; }
       if (tin && hin) {
         const uint32_t lo = pt < ph ? pt : ph, hi = pt < ph ? ph : pt;
-        atomicAdd(&pst[lo], 1u);
-        ev[j] = ((uint64_t)hi << 32) | lo;
+        ev[j] = ((uint64_t)hi << 32) | lo;   // pst[lo]: histogram of the edges' lo (hist.hip)
       } else if (tin) {
         atomicAdd(&pst[pt], 1u);
       } else if (hin) {
@@ -481,6 +480,10 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   c.sync();
   if (c.h_scalars[9]) throw Error(SHEEP_ERR_RANGE, "vector::_M_range_check: neighbour vid beyond the sequence's index (jtree.cpp:75)");
   const uint64_t m = nrec;   // edges[i] per record, DEAD holes included
+  if (nrec) {
+    TimedRegion tr(c, "pst", 8 * nrec);
+    histogram_edge_lo(c, edges, m, n, pst);
+  }
   {
     TimedRegion tr(c, "etree", 8 * m);
     etree_from_edges(c, edges, m, n, parent);

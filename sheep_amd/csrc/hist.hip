@@ -1,0 +1,247 @@
+// hist.hip — large-range histograms without global random atomics.
+//
+// A histogram of N keys over [0, K) done with one device atomic per key runs at the
+// scattered-atomic rate (~2e10/s on MI355X: 1e9 heads of RMAT-26 took 40 ms, the pst
+// histogram 33 ms).  Here the keys are bucketed by their high bits into NB "fine"
+// buckets of W = 2^15 keys, so each bucket's counters fit one workgroup's LDS:
+//
+//   1. k_hist_count   per tile of T = 2^15 keys: LDS histogram over the NB buckets
+//                     -> tile_hist[bucket][tile]                      (reads the source)
+//   2. exclusive scan of tile_hist (bucket-major) -> every (bucket, tile) run's offset
+//   3. k_hist_scatter per tile: the keys again (32 per thread, in registers),
+//                     counting sort of (bucket, 15-bit local key) in LDS, each
+//                     bucket's run written contiguously as u16
+//   4. k_hist_final   one workgroup per (bucket, slice of <= 2^20 keys): LDS counters
+//                     over the bucket's W keys, then added into cnt[bucket*W + i]
+//
+// Traffic per key: two reads of the source + 2 B written + 2 B read back, all of it
+// coalesced (runs of ~T/NB u16), against one scattered RMW per key.
+#include <vector>
+
+#include "common.hpp"
+
+namespace sheep {
+namespace {
+
+constexpr int HB = 1024;        // threads per workgroup (one workgroup per CU: LDS-bound)
+constexpr int WBITS = 15;       // fine bucket width 2^15 keys
+constexpr uint32_t W = 1u << WBITS;
+constexpr uint32_t NO_KEY = 0xFFFFFFFFu;
+
+// ---- key sources ----------------------------------------------------------------
+// Heads of XS1 records (LLAMA degree: a self-loop's head is not counted again).
+// (The caller has range-checked every id against K before building the histogram.)
+struct HeadKeys {
+  const sheep_xs1 *rec;
+  int llama;
+  __device__ __forceinline__ uint32_t operator()(uint64_t i) const {
+    const sheep_xs1 r = rec[i];
+    return (llama && r.tail == r.head) ? NO_KEY : r.head;
+  }
+};
+// lo = low 32 bits of a (hi << 32 | lo) tree edge; DEAD edges carry no key.
+struct EdgeLoKeys {
+  const uint64_t *edges;
+  __device__ __forceinline__ uint32_t operator()(uint64_t i) const {
+    const uint64_t e = edges[i];
+    return e == ~0ull ? NO_KEY : (uint32_t)e;
+  }
+};
+
+constexpr int KPT = 32;                 // keys per thread in the scatter pass
+constexpr uint32_t TLOG = 15;           // tile = HB * KPT = 32768 keys
+constexpr uint32_t TKEYS = 1u << TLOG;
+static_assert(HB * KPT == (int)TKEYS, "tile shape");
+constexpr int CB = 256;                 // count pass: small workgroups, high occupancy
+constexpr int CPT = 8;                  // count pass keys per thread per step
+
+template <typename Src>
+__global__ __launch_bounds__(CB) void k_hist_count(Src src, uint64_t n, uint32_t nb, uint32_t *__restrict__ tile_hist,
+                                                   uint64_t ntiles) {
+  extern __shared__ uint32_t lds[];
+  for (uint32_t b = threadIdx.x; b < nb; b += CB) lds[b] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x << TLOG;
+  for (uint32_t step = 0; step < TKEYS; step += CB * CPT) {
+    uint32_t k[CPT];
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {   // all loads in flight before any LDS atomic
+      const uint64_t i = base + step + (uint64_t)j * CB + threadIdx.x;
+      k[j] = i < n ? src(i) : NO_KEY;
+    }
+#pragma unroll
+    for (int j = 0; j < CPT; ++j)
+      if (k[j] != NO_KEY) atomicAdd(&lds[k[j] >> WBITS], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += CB) tile_hist[(uint64_t)b * ntiles + blockIdx.x] = lds[b];
+}
+
+// Block-wide exclusive scan of a[0, nb) in LDS (nb <= 8 * HB), in place; returns total.
+__device__ uint32_t lds_exclusive_scan(uint32_t *a, uint32_t nb, uint32_t *wsum) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t per = (nb + HB - 1) / HB, b0 = threadIdx.x * per;
+  uint32_t v[8];
+  uint32_t s = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    v[q] = (q < (int)per && b0 + q < nb) ? a[b0 + q] : 0;
+    s += v[q];
+  }
+  uint32_t inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+  for (int w = 0; w < HB / WAVE; ++w) {
+    const uint32_t x = wsum[w];
+    if (w < wave) off += x;
+    tot += x;
+  }
+  uint32_t run = off + inc - s;
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    if (q < (int)per && b0 + q < nb) { a[b0 + q] = run; run += v[q]; }
+  __syncthreads();
+  return tot;
+}
+
+// Tile keys are held in registers (one source read); counting sort of (bucket, local)
+// in LDS; runs written with consecutive lanes.  stage[] carries bucket << 16 | local.
+template <typename Src>
+__global__ __launch_bounds__(HB) void k_hist_scatter(Src src, uint64_t n, uint32_t nb,
+                                                     const uint32_t *__restrict__ offsets, uint64_t ntiles,
+                                                     uint16_t *__restrict__ out) {
+  extern __shared__ uint32_t lds[];
+  uint32_t *cur = lds;              // nb: counts -> starts -> running cursors
+  uint32_t *start = lds + nb;       // nb: bucket starts inside the staged tile
+  uint32_t *wsum = lds + 2 * nb;    // HB / WAVE
+  uint32_t *stage = lds + 2 * nb + HB / WAVE;
+  for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x << TLOG;
+  uint32_t k[KPT];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const uint64_t i = base + (uint64_t)j * HB + threadIdx.x;
+    k[j] = i < n ? src(i) : NO_KEY;
+  }
+#pragma unroll
+  for (int j = 0; j < KPT; ++j)
+    if (k[j] != NO_KEY) atomicAdd(&cur[k[j] >> WBITS], 1u);
+  __syncthreads();
+  const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
+  for (uint32_t b = threadIdx.x; b < nb; b += HB) start[b] = cur[b];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < KPT; ++j)
+    if (k[j] != NO_KEY) {
+      const uint32_t b = k[j] >> WBITS;
+      stage[atomicAdd(&cur[b], 1u)] = (b << 16) | (k[j] & (W - 1));
+    }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < total; j += HB) {
+    const uint32_t x = stage[j], b = x >> 16;
+    out[offsets[(uint64_t)b * ntiles + blockIdx.x] + (j - start[b])] = (uint16_t)(x & 0xFFFF);
+  }
+}
+
+// One workgroup per chunk = (bucket, slice of its keys).  A bucket's keys can be very
+// skewed (pst: a few thousand positions own most lower endpoints; one bucket took
+// 21 ms alone on RMAT-26), so buckets are cut into slices of <= CHUNK keys; a bucket
+// with several slices adds its counts with atomics (one per nonzero counter per
+// slice), a single-slice bucket owns its range and adds plainly.
+struct Chunk {
+  uint64_t beg, end;
+  uint32_t bucket, shared;
+};
+constexpr uint64_t CHUNK = 1u << 20;
+
+__global__ __launch_bounds__(HB) void k_hist_final(const uint16_t *__restrict__ keys, const Chunk *__restrict__ chunks,
+                                                   uint64_t K, uint32_t *__restrict__ cnt) {
+  extern __shared__ uint32_t lds[];
+  const Chunk ch = chunks[blockIdx.x];
+  for (uint32_t i = threadIdx.x; i < W; i += HB) lds[i] = 0;
+  __syncthreads();
+  for (uint64_t i0 = ch.beg; i0 < ch.end; i0 += 8 * HB) {
+    uint32_t k[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
+      k[j] = i < ch.end ? keys[i] : NO_KEY;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (k[j] != NO_KEY) atomicAdd(&lds[k[j]], 1u);
+  }
+  __syncthreads();
+  const uint64_t k0 = (uint64_t)ch.bucket << WBITS;
+  for (uint32_t i = threadIdx.x; i < W; i += HB) {
+    const uint32_t v = lds[i];
+    if (!v || k0 + i >= K) continue;
+    if (ch.shared) atomicAdd(&cnt[k0 + i], v);
+    else cnt[k0 + i] += v;   // the bucket's only workgroup owns [k0, k0 + W)
+  }
+}
+
+template <typename Src>
+void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt) {
+  if (n == 0 || K == 0) return;
+  const uint32_t nb = (uint32_t)((K + W - 1) >> WBITS);
+  const uint64_t ntiles = (n + TKEYS - 1) >> TLOG;
+  if (ntiles * nb >= (1ull << 32) || n >= (1ull << 32)) throw Error(SHEEP_ERR_ARG, "histogram: too many keys");
+  const size_t lds_scatter = (2 * (size_t)nb + HB / WAVE + TKEYS) * 4;   // <= 160 KiB for nb <= 4096
+  if (lds_scatter > 160 * 1024) throw Error(SHEEP_ERR_ARG, "histogram: key range above 2^27");
+  static bool attr_set = false;   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
+  if (!attr_set) {
+    HIP_CHECK(hipFuncSetAttribute((const void *)k_hist_scatter<HeadKeys>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_CHECK(hipFuncSetAttribute((const void *)k_hist_scatter<EdgeLoKeys>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_CHECK(hipFuncSetAttribute((const void *)k_hist_final, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  uint32_t *tile_hist = c.get_as<uint32_t>("hist_tiles", ntiles * nb + 1);
+  uint16_t *keys = c.get_as<uint16_t>("hist_keys", n);
+  hipLaunchKernelGGL(k_hist_count<Src>, dim3((unsigned)ntiles), dim3(CB), nb * 4, c.stream, src, n, nb, tile_hist,
+                     ntiles);
+  LAUNCH_CHECK();
+  uint32_t *total = c.get_as<uint32_t>("hist_total", 1);
+  scan_exclusive_u32(c, tile_hist, tile_hist, ntiles * nb, total);
+  hipLaunchKernelGGL(k_hist_scatter<Src>, dim3((unsigned)ntiles), dim3(HB), lds_scatter, c.stream, src, n, nb,
+                     (const uint32_t *)tile_hist, ntiles, keys);
+  LAUNCH_CHECK();
+  // bucket starts (column 0 of the bucket-major offsets) -> chunk list
+  std::vector<uint32_t> bstart(nb + 1);
+  HIP_CHECK(hipMemcpy2DAsync(bstart.data(), sizeof(uint32_t), tile_hist, ntiles * sizeof(uint32_t), sizeof(uint32_t),
+                             nb, hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipMemcpyAsync(&bstart[nb], total, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  std::vector<Chunk> chunks;
+  for (uint32_t b = 0; b < nb; ++b) {
+    const uint64_t beg = bstart[b], end = bstart[b + 1];
+    if (beg == end) continue;
+    const uint32_t shared = end - beg > CHUNK;
+    for (uint64_t x = beg; x < end; x += CHUNK) chunks.push_back({x, x + CHUNK < end ? x + CHUNK : end, b, shared});
+  }
+  if (chunks.empty()) return;
+  Chunk *dch = c.get_as<Chunk>("hist_chunks", chunks.size());
+  HIP_CHECK(hipMemcpyAsync(dch, chunks.data(), chunks.size() * sizeof(Chunk), hipMemcpyHostToDevice, c.stream));
+  hipLaunchKernelGGL(k_hist_final, dim3((unsigned)chunks.size()), dim3(HB), W * 4, c.stream, (const uint16_t *)keys,
+                     (const Chunk *)dch, K, cnt);
+  LAUNCH_CHECK();
+  c.sync();   // `chunks` is a pageable host buffer
+}
+
+}  // namespace
+
+void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt) {
+  histogram_add(c, HeadKeys{rec, llama}, nrec, K, cnt);
+}
+void histogram_edge_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t K, uint32_t *cnt) {
+  histogram_add(c, EdgeLoKeys{edges}, m, K, cnt);
+}
+
+}  // namespace sheep

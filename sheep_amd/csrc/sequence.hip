@@ -58,8 +58,10 @@ __global__ __launch_bounds__(BLOCK) void k_degree(const sheep_xs1 *__restrict__ 
         lmax = m > lmax ? m : lmax;
       }
     }
+    // tails here (runs: records are usually stored sorted by tail); heads go through
+    // the LDS-bucketed histogram (hist.hip), except the FILE_DAT last record's extra
     run_add(deg, kt, inc);
-    run_add(deg, kh, inc);
+    if (inc == 2 && kh != INVALID) atomicAdd(&deg[kh], 1u);
   }
   lmax = wave_max(lmax);
   if ((threadIdx.x & 63) == 0 && lmax) atomicMax(d_max, (unsigned long long)lmax);
@@ -155,6 +157,10 @@ void degree_count(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_
   c.sync();
   if (c.h_scalars[1]) throw Error(SHEEP_ERR_RANGE, "degree count: vertex id >= degree capacity");
   *max_slot = c.h_scalars[0];
+  if (nrec) {
+    TimedRegion tr(c, "degree_heads", 12 * nrec);
+    histogram_heads(c, rec, nrec, mode == SHEEP_DEGREE_LLAMA, *max_slot, deg);
+  }
 }
 
 uint64_t sequence_from_degrees(Ctx &c, const uint32_t *deg, uint64_t vs, uint32_t *seq, uint32_t *pos) {
