@@ -13,7 +13,7 @@ HIPSRC  := $(wildcard sheep_amd/csrc/*.hip)
 HIPOBJ  := $(patsubst sheep_amd/csrc/%.hip,build/hip/%.o,$(HIPSRC))
 HIPHDR  := $(wildcard sheep_amd/csrc/*.hpp) include/sheep_hip.h
 LIB     := sheep_amd/lib/libsheep_hip.so
-CLIS    := graph2tree partition_tree merge_trees degree_sequence rmat_gen
+CLIS    := graph2tree partition_tree merge_trees degree_sequence
 CLIBIN  := $(addprefix sheep_amd/bin/,$(CLIS))
 CXX     ?= g++
 

@@ -1,0 +1,404 @@
+// sheep.hpp — C++ façade of libsheep_hip.so with the reference's lib/ names, so the
+// drop-in CLIs (sheep_amd/cli/) read like chan150/sheep's own graph2tree.cpp,
+// partition_tree.cpp, merge_trees.cpp and degree_sequence.cpp.
+//
+//   reference (file:line)                         here
+//   GraphWrapper / LLAMAGraph (graph_wrapper.h:43)  GraphWrapper   (records resident in HBM)
+//   degreeSequence / mpiSequence (sequence.h:52,65) degreeSequence (LLAMA degrees, on the GPU)
+//   fileSequence (sequence.h:95-128)              fileSequence   (file degrees, on the GPU)
+//   readSequence / writeSequence (:153-184)       readSequence / writeSequence (host text I/O)
+//   JNodeTable (jnode.h:48-297)                   JNodeTable     (host nodes + device mirror)
+//   JTree (jtree.h:111-122)                       JTree          (map step on the GPU)
+//   Partition (partition.h:51-188)                Partition      (forwardPartition + evaluators)
+//
+// Errors: the C ABI's status codes become the exceptions the reference throws in the
+// same places (std::bad_alloc for I/O and allocation, std::out_of_range for .at()).
+#pragma once
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "sheep_hip.h"
+
+namespace sheep {
+
+typedef uint32_t vid_t;   // defs.h:76 (LLAMA build)
+typedef uint32_t esize_t;
+typedef uint32_t jnid_t;  // jnode.h:42
+typedef int16_t part_t;   // partition.h:43
+constexpr vid_t INVALID_VID = 0xFFFFFFFFu;
+constexpr jnid_t INVALID_JNID = 0xFFFFFFFFu;
+constexpr part_t INVALID_PART = -1;
+
+inline void check(int rc) {
+  if (rc == SHEEP_OK) return;
+  const std::string msg = sheep_last_error();
+  if (rc == SHEEP_ERR_ALLOC) throw std::bad_alloc();
+  if (rc == SHEEP_ERR_RANGE) throw std::out_of_range(msg);
+  if (rc == SHEEP_ERR_ARG) throw std::invalid_argument(msg);
+  throw std::runtime_error(msg);
+}
+
+// One HIP device + a stream of its own, shared by everything in the process.
+// SHEEP_DEVICE selects the device (default 0).
+class Context {
+ public:
+  static Context &get() {
+    static Context c;
+    return c;
+  }
+  sheep_ctx *handle() const { return h_; }
+  void sync() const { check(sheep_ctx_sync(h_)); }
+  ~Context() { sheep_ctx_destroy(h_); }
+
+ private:
+  Context() {
+    const char *d = getenv("SHEEP_DEVICE");
+    check(sheep_ctx_create(d ? atoi(d) : 0, SHEEP_OWN_STREAM, &h_));
+  }
+  sheep_ctx *h_ = nullptr;
+};
+inline sheep_ctx *ctx() { return Context::get().handle(); }
+
+// Owning device buffer (move-only).
+template <typename T>
+class DeviceArray {
+ public:
+  DeviceArray() = default;
+  explicit DeviceArray(size_t n) : n_(n) {
+    void *p = nullptr;
+    check(sheep_malloc(ctx(), (n ? n : 1) * sizeof(T), &p));
+    p_ = (T *)p;
+  }
+  DeviceArray(DeviceArray &&o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }
+  DeviceArray &operator=(DeviceArray &&o) noexcept {
+    std::swap(p_, o.p_);
+    std::swap(n_, o.n_);
+    return *this;
+  }
+  DeviceArray(const DeviceArray &) = delete;
+  DeviceArray &operator=(const DeviceArray &) = delete;
+  ~DeviceArray() {
+    if (p_) sheep_free(ctx(), p_);
+  }
+  T *get() const { return p_; }
+  size_t size() const { return n_; }
+  void upload(const T *h, size_t cnt) { check(sheep_memcpy_h2d(ctx(), p_, h, cnt * sizeof(T))); }
+  void download(T *h, size_t cnt) const { check(sheep_memcpy_d2h(ctx(), h, p_, cnt * sizeof(T))); }
+
+ private:
+  T *p_ = nullptr;
+  size_t n_ = 0;
+};
+
+inline bool is_dat(const char *filename) {
+  const size_t l = strlen(filename);
+  return l >= 4 && strcmp(".dat", filename + l - 4) == 0;
+}
+
+// XS1 records of a .dat file, or pairs of a SNAP text file read the way SNAPReader does
+// (readerwriter.h:166-178: stop at the first pair that does not parse).
+inline std::vector<sheep_xs1> readRecords(const char *filename) {
+  std::vector<sheep_xs1> rec;
+  if (is_dat(filename)) {
+    FILE *f = fopen(filename, "rb");
+    if (!f) throw std::bad_alloc();   // the reference's loaders fail with bad_alloc / abort
+    fseek(f, 0, SEEK_END);
+    const long bytes = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    rec.resize((size_t)bytes / sizeof(sheep_xs1));
+    const size_t got = rec.empty() ? 0 : fread(rec.data(), sizeof(sheep_xs1), rec.size(), f);
+    fclose(f);
+    rec.resize(got);
+  } else {
+    std::ifstream s(filename);
+    if (!s) throw std::bad_alloc();
+    vid_t X, Y;
+    while ((s >> X) && (s >> Y)) rec.push_back(sheep_xs1{X, Y, 1.0f});
+  }
+  return rec;
+}
+
+// The graph of one (optionally partial, `part`/`num_parts` 1-indexed, contiguous record
+// ranges like LLAMA's partial load) edge file, resident in HBM.  LLAMA semantics:
+// undirected doubling, a self-loop stored once, degree-0 slots are not nodes.
+class GraphWrapper {
+ public:
+  GraphWrapper(const char *filename, size_t part = 0, size_t num_parts = 0) {
+    std::vector<sheep_xs1> all = readRecords(filename);
+    size_t beg = 0, end = all.size();
+    if (num_parts != 0) {
+      beg = (part - 1) * all.size() / num_parts;
+      end = part * all.size() / num_parts;
+    }
+    nrec_ = end - beg;
+    rec_ = DeviceArray<sheep_xs1>(nrec_);
+    if (nrec_) rec_.upload(all.data() + beg, nrec_);
+    uint64_t loops = 0;
+    for (size_t i = beg; i < end; ++i) {
+      max_nodes_ = std::max<uint64_t>(max_nodes_, (uint64_t)std::max(all[i].tail, all[i].head) + 1);
+      loops += all[i].tail == all[i].head;
+    }
+    edges_ = (2 * nrec_ - loops) / 2;   // max_edges / 2 (graph_wrapper.h:79-81)
+  }
+  size_t getMaxVid() const { return max_nodes_; }
+  size_t getEdges() const { return edges_; }
+  size_t getNodes() const;   // slots with degree != 0 (counted on the GPU)
+  const sheep_xs1 *records() const { return rec_.get(); }
+  uint64_t numRecords() const { return nrec_; }
+
+ private:
+  DeviceArray<sheep_xs1> rec_;
+  uint64_t nrec_ = 0, max_nodes_ = 0, edges_ = 0;
+  mutable int64_t nodes_ = -1;
+};
+
+// A sequence as the GPU path uses it: seq[n] and its inverse pos[pos_size] in HBM.
+struct DeviceSequence {
+  DeviceArray<uint32_t> seq, pos;
+  uint64_t n = 0, pos_size = 0;
+  std::vector<vid_t> host() const {
+    std::vector<vid_t> h(n);
+    if (n) seq.download(h.data(), n);
+    return h;
+  }
+};
+
+inline DeviceSequence sequenceFromDegrees(DeviceArray<uint32_t> &deg, uint64_t vs) {
+  DeviceSequence s;
+  s.seq = DeviceArray<uint32_t>(vs);
+  s.pos = DeviceArray<uint32_t>(vs);
+  check(sheep_sequence_from_degrees(ctx(), deg.get(), vs, s.seq.get(), s.pos.get(), &s.n));
+  s.pos_size = vs;
+  return s;
+}
+
+// degreeSequence (sequence.h:52-63): ascending (LLAMA degree, vid).
+inline DeviceSequence degreeSequence(const GraphWrapper &g) {
+  const uint64_t cap = std::max<uint64_t>(g.getMaxVid(), 1);
+  DeviceArray<uint32_t> deg(cap);
+  std::vector<uint32_t> zero(cap, 0);
+  deg.upload(zero.data(), cap);
+  uint64_t vs = 0;
+  check(sheep_degree_count(ctx(), g.records(), g.numRecords(), SHEEP_DEGREE_LLAMA, deg.get(), cap, &vs));
+  return sequenceFromDegrees(deg, vs);
+}
+
+inline size_t GraphWrapper::getNodes() const {
+  if (nodes_ < 0) nodes_ = (int64_t)degreeSequence(*this).n;
+  return (size_t)nodes_;
+}
+
+// fileSequence (sequence.h:95-128): degrees straight from the file records (self-loop
+// +2; XS1Reader hands the last record out twice, readerwriter.h:138-146).
+inline std::vector<vid_t> fileSequence(const char *filename) {
+  std::vector<sheep_xs1> all = readRecords(filename);
+  uint64_t cap = 1;
+  for (const sheep_xs1 &r : all) cap = std::max<uint64_t>(cap, (uint64_t)std::max(r.tail, r.head) + 1);
+  DeviceArray<sheep_xs1> rec(all.size());
+  if (!all.empty()) rec.upload(all.data(), all.size());
+  DeviceArray<uint32_t> deg(cap);
+  std::vector<uint32_t> zero(cap, 0);
+  deg.upload(zero.data(), cap);
+  uint64_t vs = 0;
+  check(sheep_degree_count(ctx(), rec.get(), all.size(), is_dat(filename) ? SHEEP_DEGREE_FILE_DAT : SHEEP_DEGREE_FILE_NET,
+                           deg.get(), cap, &vs));
+  return sequenceFromDegrees(deg, vs).host();
+}
+
+inline std::vector<vid_t> readSequence(const char *filename) {   // readTextSequence
+  std::vector<vid_t> seq;
+  std::ifstream stream(filename);
+  vid_t X;
+  while (stream >> X) seq.push_back(X);
+  return seq;
+}
+
+inline void writeSequence(const std::vector<vid_t> &seq, const char *filename) {   // writeTextSequence
+  FILE *f = fopen(filename, "w");
+  if (!f) throw std::runtime_error(std::string("cannot write ") + filename);
+  for (vid_t X : seq) fprintf(f, "%u\n", X);
+  fclose(f);
+}
+
+inline DeviceSequence uploadSequence(const std::vector<vid_t> &seq) {
+  DeviceSequence s;
+  s.n = seq.size();
+  s.pos_size = seq.empty() ? 0 : (uint64_t)*std::max_element(seq.begin(), seq.end()) + 1;   // jtree.h:113
+  s.seq = DeviceArray<uint32_t>(s.n);
+  if (s.n) s.seq.upload(seq.data(), s.n);
+  s.pos = DeviceArray<uint32_t>(s.pos_size);
+  check(sheep_positions(ctx(), s.seq.get(), s.n, s.pos.get(), s.pos_size));
+  return s;
+}
+
+// TREEFAQS (jnode.cpp:256-290, print jnode.h:285-291).
+struct Facts {
+  sheep_facts_t f;
+  void print() const {
+    printf("TREEFAQS: width:%zu\troots:%zu\n", (size_t)f.width, (size_t)f.root_cnt);
+    printf("\tvheight:%zu\teheight:%zu\n", (size_t)f.vert_height, (size_t)f.edge_height);
+    printf("\tverts:%zu\tedges:%zu\n", (size_t)f.vert_cnt, (size_t)f.edge_cnt);
+    printf("\thalo:%zu\tcore:%zu\n", (size_t)f.halo_id, (size_t)f.core_id);
+    printf("\tfill:%zu\n", (size_t)f.fill);
+  }
+};
+
+// JNodeTable: host nodes ([end_id] + max_id JNodes, the .tre layout) with a device
+// mirror and the persistent kid table (makeKids) made on demand.
+class JNodeTable {
+ public:
+  explicit JNodeTable(jnid_t max_jnids = 0) : nodes_(max_jnids, sheep_jnode{INVALID_JNID, 0}), end_id_(0) {}
+  explicit JNodeTable(const char *filename) {   // jnode.cpp:76-102 (load)
+    FILE *f = fopen(filename, "rb");
+    if (!f) throw std::bad_alloc();
+    fseek(f, 0, SEEK_END);
+    const long bytes = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    if (bytes < (long)sizeof(jnid_t)) { fclose(f); throw std::bad_alloc(); }
+    nodes_.resize(((size_t)bytes - sizeof(jnid_t)) / sizeof(sheep_jnode));
+    bool ok = fread(&end_id_, sizeof(jnid_t), 1, f) == 1;
+    ok = ok && (nodes_.empty() || fread(nodes_.data(), sizeof(sheep_jnode), nodes_.size(), f) == nodes_.size());
+    fclose(f);
+    if (!ok || end_id_ > nodes_.size()) throw std::bad_alloc();
+  }
+  JNodeTable(JNodeTable &&) = default;
+  JNodeTable &operator=(JNodeTable &&) = default;
+  ~JNodeTable() {
+    if (kids_) sheep_kids_destroy(kids_);
+  }
+
+  jnid_t size() const { return end_id_; }
+  jnid_t max_id() const { return (jnid_t)nodes_.size(); }
+  jnid_t parent(jnid_t id) const { return nodes_.at(id).parent; }
+  esize_t pst_weight(jnid_t id) const { return nodes_.at(id).pst_weight; }
+  std::vector<sheep_jnode> &nodes() { return nodes_; }
+
+  void save(const char *filename) const {   // jnode.cpp:164-168
+    FILE *f = fopen(filename, "wb");
+    if (!f) throw std::bad_alloc();
+    fwrite(&end_id_, sizeof(jnid_t), 1, f);
+    if (!nodes_.empty()) fwrite(nodes_.data(), sizeof(sheep_jnode), nodes_.size(), f);
+    fclose(f);
+  }
+
+  // The first end_id nodes in HBM (uploaded once; invalidated by assignments).
+  const sheep_jnode *device() const {
+    if (!dev_) {
+      dev_.reset(new DeviceArray<sheep_jnode>(end_id_));
+      if (end_id_) dev_->upload(nodes_.data(), end_id_);
+    }
+    return dev_->get();
+  }
+  // makeKids (jnode.h:190-204): kid lists in ascending id, kept on the device; the FFD
+  // sort order persists across Partition calls (partition.cpp:104-106).
+  sheep_kids *kids() const {
+    if (!kids_) check(sheep_kids_create(ctx(), device(), end_id_, &kids_));
+    return kids_;
+  }
+
+  // Result of a device computation: n nodes, end_id = n.
+  void assign_from_device(const DeviceArray<sheep_jnode> &d, jnid_t n, jnid_t max_id) {
+    nodes_.assign(std::max(n, max_id), sheep_jnode{INVALID_JNID, 0});
+    if (n) d.download(nodes_.data(), n);
+    end_id_ = n;
+    dev_.reset();
+    if (kids_) { sheep_kids_destroy(kids_); kids_ = nullptr; }
+  }
+
+  // merge (jnode.cpp:174-201): Liu over the union of both parent-edge sets, pst summed.
+  void merge(const JNodeTable &lhs, const JNodeTable &rhs) {
+    const jnid_t n = lhs.size();
+    if (rhs.size() != n) throw std::invalid_argument("merge: trees of different sizes");
+    DeviceArray<sheep_jnode> out(n);
+    check(sheep_merge_trees(ctx(), lhs.device(), rhs.device(), n, out.get()));
+    assign_from_device(out, n, std::max<jnid_t>(max_id(), n));
+  }
+
+  Facts getFacts() const {
+    Facts x;
+    check(sheep_facts(ctx(), device(), end_id_, &x.f));
+    return x;
+  }
+
+ private:
+  std::vector<sheep_jnode> nodes_;
+  jnid_t end_id_ = 0;
+  mutable std::unique_ptr<DeviceArray<sheep_jnode>> dev_;
+  mutable sheep_kids *kids_ = nullptr;
+};
+
+// JTree(graph, seq) (jtree.h:111-122 + jtree.cpp:66-145): the map step.
+class JTree {
+ public:
+  JNodeTable jnodes;
+  JTree(const GraphWrapper &graph, const DeviceSequence &seq) {
+    DeviceArray<sheep_jnode> t(seq.n);
+    check(sheep_build_tree(ctx(), graph.records(), graph.numRecords(), seq.pos.get(), seq.pos_size, seq.n, t.get()));
+    jnodes.assign_from_device(t, (jnid_t)seq.n, (jnid_t)seq.n);
+  }
+  jnid_t size() const { return jnodes.size(); }
+};
+
+inline void print_ratio_line(const char *label, uint64_t v, double denom) {
+  printf("%s%zu (%f%%)\n", label, (size_t)v, (double)v / denom);
+}
+
+// Partition(seq, jnodes, k, balance, vtx, pst, pre) (partition.cpp:50-67).
+class Partition {
+ public:
+  Partition(const DeviceSequence &seq, const JNodeTable &jnodes, part_t np, double balance_factor = 1.03,
+            bool vtx_weight = false, bool pst_weight = true, bool pre_weight = false)
+      : num_parts_(np) {
+    if (pre_weight) throw std::invalid_argument("pre_weight (-u) is outside this build's scope");
+    parts_ = DeviceArray<int16_t>(seq.pos_size);
+    check(sheep_partition(ctx(), jnodes.device(), jnodes.size(), seq.seq.get(), seq.pos_size, jnodes.kids(), np,
+                          balance_factor, vtx_weight, pst_weight, parts_.get(), &info_));
+  }
+  const sheep_partition_info &info() const { return info_; }
+  const int16_t *device() const { return parts_.get(); }
+  std::vector<part_t> parts() const {
+    std::vector<part_t> h(parts_.size());
+    if (!h.empty()) parts_.download(h.data(), h.size());
+    return h;
+  }
+
+  void print() const {   // partition.h:135-143
+    printf("Actually created %d partitions.\n", (int)info_.created);
+    printf("First two partition sizes: %zu and %zu\n", (size_t)info_.first_size, (size_t)info_.second_size);
+  }
+
+  // evaluate(graph) (partition.cpp:428-473) then evaluate(graph, seq) (:475-521).
+  void evaluate(const GraphWrapper &graph, const DeviceSequence &seq) const {
+    sheep_eval e;
+    check(sheep_evaluate(ctx(), graph.records(), graph.numRecords(), seq.pos.get(), seq.pos_size, parts_.get(), 0,
+                         &e));
+    const double E = (double)e.edges;
+    const double Nk = (double)(e.nodes / (uint64_t)num_parts_), Ek = (double)(e.edges / (uint64_t)num_parts_);
+    print_ratio_line("edges cut: ", e.edges_cut, E);
+    print_ratio_line("Vcom. vol: ", e.vcom_vol, E);
+    print_ratio_line("  balance: ", e.max_vertex_bal, Nk);
+    print_ratio_line("ECV(hash): ", e.ecv_hash, E);
+    print_ratio_line("  balance: ", e.max_hash_bal, Ek);
+    print_ratio_line("ECV(down): ", e.ecv_down, E);
+    print_ratio_line("  balance: ", e.max_down_bal, Ek);
+    print_ratio_line("ECV(up)  : ", e.ecv_up, E);
+    print_ratio_line("  balance: ", e.max_up_bal, Ek);
+  }
+
+ private:
+  DeviceArray<int16_t> parts_;
+  part_t num_parts_;
+  sheep_partition_info info_{};
+};
+
+}  // namespace sheep
