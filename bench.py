@@ -29,7 +29,8 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level table)
 # Leaf regions (one kernel or one fused kernel family per launch); aggregates such as
 # "etree" / "partition" / "sequence" are reported in phases but not rooflined.
-LEAF = ("degree", "relabel", "etree_union", "etree_cross", "etree_apply", "evaluate")
+LEAF = ("degree", "degree_heads", "relabel", "pst", "etree_split", "etree_union", "etree_cross", "etree_apply",
+        "etree_compact", "evaluate")
 
 
 def parse():
@@ -43,6 +44,12 @@ def parse():
     ap.add_argument("--seed", type=int, default=None, help="RMAT seed (default: the scale, SURVEY §8d)")
     ap.add_argument("--cpu-scale", type=int, default=22, help="RMAT scale of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="gloo stages the exchanges through host memory (rehearsal)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on cuda:0 (rehearse N ranks on a 1-GPU box; needs gloo)")
+    ap.add_argument("--verify", action="store_true",
+                    help="rank 0 also builds the whole-graph tree and checks the merged one against it")
     return ap.parse_args()
 
 
@@ -51,46 +58,43 @@ def main():
     import torch
     import torch.distributed as dist
     import sheep_amd
+    from sheep_amd import dist as sdist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
+    if a.same_device:
+        if a.dist_backend != "gloo":
+            raise SystemExit("--same-device needs --dist-backend gloo (RCCL wants one rank per GPU)")
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     seed = a.scale if a.seed is None else a.seed
 
     ctx = sheep_amd.Context(local)
     rec = sheep_amd.rmat(a.scale, a.ef, seed, ctx=ctx)          # whole graph, identical on every rank
     R = rec.shape[0]
-    beg, end = rank * R // world, (rank + 1) * R // world      # contiguous edge shard (graph2tree -l)
+    beg, end = sdist.shard_bounds(R, rank, world)               # contiguous edge shard (graph2tree -l)
     shard = rec[beg:end]
     vs_cap = 1 << a.scale
     deg = torch.zeros(vs_cap, dtype=torch.int32, device="cuda")
-    mx = torch.zeros(1, dtype=torch.int64, device="cuda")
 
     def step():
         deg.zero_()
         _, max_slot = sheep_amd.degree_count(shard, mode="llama", deg=deg, ctx=ctx)
         vs = max_slot
         if world > 1:                                           # sequence.h:72,78 MPI_Allreduce
-            mx.fill_(max_slot)
-            dist.all_reduce(deg, op=dist.ReduceOp.SUM)
-            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-            vs = int(mx.item())
+            vs = sdist.allreduce_degrees(deg, max_slot)
         s = sheep_amd.sequence_from_degrees(deg, vs, ctx=ctx)
         tree = sheep_amd.build_tree(shard, s, ctx=ctx)
-        r = 1
-        while r < world:                                        # binomial reduce to rank 0 (jnode.cpp:241)
-            if rank % (2 * r) == r:
-                dist.send(tree, rank - r)
-            elif rank % (2 * r) == 0 and rank + r < world:
-                other = torch.empty_like(tree)
-                dist.recv(other, rank + r)
-                tree = sheep_amd.merge_trees(tree, other, ctx=ctx)
-            r *= 2
+        if world > 1:                                           # binomial reduce to rank 0 (jnode.cpp:241)
+            tree = sdist.reduce_trees(tree, lambda x, y: sheep_amd.merge_trees(x, y, ctx=ctx), rank, world)
         res = None
         if rank == 0:
             kids = sheep_amd.KidTable(tree, ctx)
@@ -115,7 +119,7 @@ def main():
     barrier()
     t = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([t], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([t], dtype=torch.float64, device="cuda" if a.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
 
@@ -137,6 +141,14 @@ def main():
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "alg_bytes_per_launch": int(b_launch), "ms_per_launch": round(ms_launch, 4)}
 
+    verified = None
+    if a.verify and rank == 0:                                  # merged tree == whole-graph tree
+        whole = sheep_amd.build_tree(rec, s, ctx=ctx)
+        verified = bool(torch.equal(whole, tree))
+        del whole
+        if not verified:
+            print("bench: merged tree differs from the whole-graph tree", file=sys.stderr, flush=True)
+
     out = None
     if rank == 0:
         n = s.n
@@ -157,12 +169,16 @@ def main():
             "data": "synthetic (Graph500 RMAT, seeded, self-loops/duplicates removed)",
             "config": {"workload": f"RMAT-{a.scale} ef{a.ef}, k={a.k}", "records": R, "vertex_slots": s.pos_size,
                        "tree_nodes": n, "k": a.k, "created": res.created, "seed": seed,
-                       "parallelism": f"edge-shards x{world}"},
+                       "parallelism": f"edge-shards x{world}"
+                       + ("" if a.dist_backend == "nccl" else f" ({a.dist_backend}"
+                          + (", one device" if a.same_device else "") + ")")},
             "path_roofline": {"alg_bytes": b_alg, "achieved_GBs": round(b_alg * a.steps / t / 1e9, 2),
                               "frac": round(b_alg * a.steps / t / 1e9 / (HBM_PEAK_GBS * world), 4)},
             "roofline": roof,
             "phases": phases,
         }
+        if verified is not None:
+            out["verified_vs_whole_graph"] = verified
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a, ctx)
     del rec, shard

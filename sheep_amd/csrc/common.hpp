@@ -72,6 +72,8 @@ struct Ctx {
     return (T *)get(name, count * sizeof(T));
   }
   void sync() { HIP_CHECK(hipStreamSynchronize(stream)); }
+  // algorithmic bytes learned only after the launches (device-side counts)
+  void add_bytes(const char *name, uint64_t bytes) { if (timing) timers[name].bytes += bytes; }
 
   hipEvent_t ev() {
     if (!event_pool.empty()) { hipEvent_t e = event_pool.back(); event_pool.pop_back(); return e; }
@@ -224,10 +226,12 @@ void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uin
 void histogram_edge_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t K, uint32_t *cnt);
 // etree.hip
 void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent);
-// append.hip — sharded appends: counters (NSHARD * SHARD_STRIDE u64, zeroed), the pack
-// step returns the total and leaves the items contiguous in dst.
+// append.hip — sharded appends: counters (NSHARD * SHARD_STRIDE u64, zeroed).  The pack
+// step moves the shard regions of a producer that streamed *n_in items together in dst
+// and writes the total to *total_out (device; must not alias n_in).  With cond, it runs
+// only if *cond != 0, and then also zeroes the counter set zero_after.  No host sync.
 unsigned long long *shard_counters(Ctx &c, const char *tag);
 template <typename T>
-uint64_t pack_shards(Ctx &c, const T *src, T *dst, uint64_t ntiles, uint32_t per_item,
-                     const unsigned long long *counters);
+void pack_shards(Ctx &c, const T *src, T *dst, const uint64_t *n_in, const unsigned long long *counters,
+                 uint64_t *total_out, const uint64_t *cond = nullptr, unsigned long long *zero_after = nullptr);
 }  // namespace sheep

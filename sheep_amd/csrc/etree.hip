@@ -116,22 +116,42 @@ __global__ __launch_bounds__(BLOCK) void k_relabel(const sheep_xs1 *__restrict__
 }
 
 // ---- one D&C level ---------------------------------------------------------------
+// Every count a level needs stays in device memory (the per-level stats row, below):
+// kernels read their list lengths there and size their loops from them, the host only
+// sizes grids from an upper bound.  A level is a chain of launches with no host round
+// trip; kernels whose list is empty return at once.
+//
+// stats row of level l (u64): [0] live edges entering the level (holes included),
+// [1] light edges, [2] cross edges, [3] dead edges at the compaction check, [4] 1 if the
+// level compacted, [5..7] unresolved light edges after hooking round 0..2.
+constexpr int ST_ROW = 8, ST_LIVE = 0, ST_NL = 1, ST_NX = 2, ST_DEAD = 3, ST_COMPACT = 4, ST_HOOK = 5;
+constexpr int HOOK_ROUNDS = 3;
+// counter sets zeroed at every level: light, cross, hook rounds, compaction
+constexpr int CSET_LIGHT = 0, CSET_CROSS = 1, CSET_HOOK = 2, CSET_COMPACT = CSET_HOOK + HOOK_ROUNDS, NCSET = CSET_COMPACT + 1;
+constexpr uint64_t CSET_WORDS = (uint64_t)NSHARD * SHARD_STRIDE;
+
 __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t *__restrict__ uf, uint32_t *__restrict__ mt,
-                                                 uint32_t *__restrict__ top, uint32_t *__restrict__ claim, uint64_t n) {
+                                                 uint32_t *__restrict__ top, uint32_t *__restrict__ claim, uint64_t n,
+                                                 unsigned long long *__restrict__ csets) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
+  const uint64_t t0 = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (uint64_t i = t0; i < n; i += stride) {
     uf[i] = (uint32_t)i;
     mt[i] = INVALID;
     top[i] = (uint32_t)i;
     claim[i] = INVALID;
   }
+  for (uint64_t i = t0; i < NCSET * CSET_WORDS; i += stride) csets[i] = 0;
 }
+
+__global__ void k_set_u64(uint64_t *p, uint64_t v) { *p = v; }
 
 // top[root] = the component's largest id.  Every vertex of a non-singleton light
 // component is an endpoint of a light edge and its maximum is the hi end of one, so a
 // max over the light edges' hi ends suffices (singletons keep top = self).
-__global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict__ lbuf, uint64_t nl, uint32_t *uf,
-                                                     uint32_t *__restrict__ top) {
+__global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict__ lbuf, const uint64_t *__restrict__ n_l,
+                                                     uint32_t *uf, uint32_t *__restrict__ top) {
+  const uint64_t nl = *n_l;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   const uint64_t iters = (nl + stride - 1) / stride;
   uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -157,13 +177,17 @@ __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict_
 }
 
 // One streaming pass classifies the live edges of a level: light (both ends in the
-// left half of their subproblem) -> the edge value into lbuf; cross -> its index into
-// xidx.  Edges inside a right half are left alone.  The dense lists keep every lane of
-// the union / find kernels busy (no divergence around dependent pointer chases).
-__global__ __launch_bounds__(BLOCK) void k_split(const uint64_t *__restrict__ edges, uint64_t m, int s, uint32_t clo,
+// left half of their subproblem) -> the edge value to the light shards; cross -> its
+// index to the cross shards.  Edges inside a right half are left alone.  The dense
+// lists keep every lane of the union / find kernels busy (no divergence around
+// dependent pointer chases).
+__global__ __launch_bounds__(BLOCK) void k_split(const uint64_t *__restrict__ edges, const uint64_t *__restrict__ n_live,
+                                                 uint64_t *__restrict__ st, int s, uint32_t clo,
                                                  uint64_t *__restrict__ lbuf, uint32_t *__restrict__ xidx,
                                                  unsigned long long *__restrict__ lcnt,
                                                  unsigned long long *__restrict__ xcnt) {
+  const uint64_t m = *n_live;
+  if (blockIdx.x == 0 && threadIdx.x == 0) st[ST_LIVE] = m;
   const uint64_t ntiles = (m + TILE - 1) / TILE;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     uint64_t ev[TILE_ITEMS];
@@ -197,9 +221,10 @@ __global__ __launch_bounds__(BLOCK) void k_split(const uint64_t *__restrict__ ed
 // not retried here: the edge goes to `out` for the next round.  Retrying in place made
 // thousands of threads fight over a forming giant component's root (each failure =
 // another round trip); rounds instead resolve such a pile-up in a few passes.
-__global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict__ in, uint64_t nin, uint32_t *uf,
-                                                      uint64_t *__restrict__ out,
+__global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict__ in, const uint64_t *__restrict__ n_in,
+                                                      uint32_t *uf, uint64_t *__restrict__ out,
                                                       unsigned long long *__restrict__ counter) {
+  const uint64_t nin = *n_in;
   const uint64_t ntiles = (nin + TILE - 1) / TILE;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     uint64_t ev[TILE_ITEMS];
@@ -225,6 +250,25 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
   }
 }
 
+// The edges still unresolved after HOOK_ROUNDS rounds (few: the pile-ups are gone) are
+// hooked in place, retrying until each one's roots agree.  Lock-free: a failed CAS
+// means another hook made progress.
+__global__ __launch_bounds__(BLOCK) void k_hook_finish(const uint64_t *__restrict__ in, const uint64_t *__restrict__ n_in,
+                                                       uint32_t *uf) {
+  const uint64_t nin = *n_in;
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nin; i += stride) {
+    const uint64_t e = in[i];
+    uint32_t a = (uint32_t)e, b = (uint32_t)(e >> 32);
+    for (;;) {
+      find2(uf, a, b);
+      if (a == b) break;
+      const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+      if (atomicCAS(&uf[hi], hi, lo) == hi) break;
+    }
+  }
+}
+
 // parent(top of every component with a cross edge) = m_r (jnode.h:158-162 adopt).
 __global__ __launch_bounds__(BLOCK) void k_assign_parents(const uint32_t *__restrict__ uf, const uint32_t *__restrict__ mt,
                                                           const uint32_t *__restrict__ top, uint64_t n,
@@ -238,8 +282,9 @@ __global__ __launch_bounds__(BLOCK) void k_assign_parents(const uint32_t *__rest
 
 // For every cross edge (a,b): r = root of a's light component; m_r = min b (atomicMin).
 __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict__ edges,
-                                                      const uint32_t *__restrict__ xidx, uint64_t nx, uint32_t *uf,
-                                                      uint32_t *__restrict__ mt, uint32_t *__restrict__ xtop) {
+                                                      const uint32_t *__restrict__ xidx, const uint64_t *__restrict__ n_x,
+                                                      uint32_t *uf, uint32_t *__restrict__ mt, uint32_t *__restrict__ xtop) {
+  const uint64_t nx = *n_x;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   const uint64_t iters = (nx + stride - 1) / stride;
   uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -276,9 +321,11 @@ __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict
 // edges into one hub, all carry the same m.)  claim is n x u32, L3-resident, unlike a
 // global hash table of the pairs.
 __global__ __launch_bounds__(BLOCK) void k_cross_apply(uint64_t *__restrict__ edges, const uint32_t *__restrict__ xidx,
-                                                       const uint32_t *__restrict__ xtop, uint64_t nx,
+                                                       const uint32_t *__restrict__ xtop, const uint64_t *__restrict__ n_x,
                                                        const uint32_t *__restrict__ mt, uint32_t *__restrict__ claim,
                                                        unsigned long long *__restrict__ dead) {
+  const uint64_t nx = *n_x;
+  if ((uint64_t)blockIdx.x * BLOCK >= nx) return;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   uint32_t ndead = 0;
   for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < nx; j += stride) {
@@ -307,8 +354,23 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(uint64_t *__restrict__ ed
   }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_compact_edges(const uint64_t *__restrict__ in, uint64_t m,
+// Compaction, decided on the device: once a quarter of the list is dead (counted since
+// the last compaction) the live edges are appended to `out` (pack_shards then moves them
+// back and updates the live count); otherwise every workgroup returns at once.
+__global__ __launch_bounds__(BLOCK) void k_compact_edges(const uint64_t *__restrict__ in, uint64_t *__restrict__ st,
+                                                         const unsigned long long *__restrict__ dead,
                                                          uint64_t *__restrict__ out, unsigned long long *__restrict__ counter) {
+  const uint64_t m = st[ST_LIVE];
+  __shared__ uint64_t s_dead;
+  if (threadIdx.x < WAVE) {
+    const uint64_t d = wave_sum((uint64_t)(threadIdx.x < NSHARD ? dead[(uint64_t)threadIdx.x * SHARD_STRIDE] : 0));
+    if (threadIdx.x == 0) s_dead = d;
+  }
+  __syncthreads();
+  const uint64_t nd = s_dead;
+  const bool go = nd && nd * 4 >= m;
+  if (blockIdx.x == 0 && threadIdx.x == 0) { st[ST_DEAD] = nd; st[ST_COMPACT] = go; }
+  if (!go) return;
   const uint64_t ntiles = (m + TILE - 1) / TILE;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     uint64_t ev[TILE_ITEMS];
@@ -366,6 +428,8 @@ void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
 static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
 
 // Elimination tree of `m` edges ((hi<<32)|lo, lo < hi < n).  `edges` is consumed.
+// One pass of launches per level, no host synchronisation inside the loop (see the
+// stats row above); the stats come back once at the end for the timers / debug log.
 void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent) {
   fill_u32(c, parent, n, INVALID);
   if (n < 2 || m == 0) return;
@@ -381,84 +445,96 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
   uint32_t *mt = c.get_as<uint32_t>("et_mt", n);
   uint32_t *top = c.get_as<uint32_t>("et_top", n);
   uint32_t *claim = c.get_as<uint32_t>("et_claim", n);
-  // scratch regions of sharded appends need whole tiles: m rounded up
+  // every list is bounded by m; scratch regions of sharded appends need whole tiles
   const uint64_t mcap = (m + TILE - 1) / TILE * TILE;
-  uint32_t *xidx = c.get_as<uint32_t>("et_xidx", m);
+  uint32_t *xidx = c.get_as<uint32_t>("et_xidx", mcap);
   uint32_t *xtop = c.get_as<uint32_t>("et_xtop", mcap);   // also the cross list's shard scratch
   uint64_t *alt = c.get_as<uint64_t>("et_alt", mcap);     // shard scratch: light list, compaction
-  unsigned long long *lcnt = shard_counters(c, "light"), *xcnt = shard_counters(c, "cross");
-  unsigned long long *hcnt = shard_counters(c, "hook"), *ccnt = shard_counters(c, "compact");
+  uint64_t *lbuf = c.get_as<uint64_t>("et_light", mcap);  // must outlive the hook rounds (k_light_top)
+  uint64_t *hk[2] = {c.get_as<uint64_t>("et_lwa", mcap), c.get_as<uint64_t>("et_lwb", mcap)};
+  unsigned long long *csets = c.get_as<unsigned long long>("et_csets", NCSET * CSET_WORDS);
   unsigned long long *dcnt = shard_counters(c, "dead");
-  std::vector<uint64_t> h_dcnt(NSHARD * SHARD_STRIDE);
-  unsigned long long *d = (unsigned long long *)c.d_scalars;
-  uint64_t live = m, dead = 0;
-  for (int lvl = 0; lvl < L && live > 0; ++lvl) {
+  uint64_t *stats = c.get_as<uint64_t>("et_stats", (uint64_t)(L + 1) * ST_ROW);
+  uint64_t *d_live = stats + (uint64_t)L * ST_ROW;
+  HIP_CHECK(hipMemsetAsync(stats, 0, (uint64_t)L * ST_ROW * sizeof(uint64_t), c.stream));
+  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, c.stream, d_live, m);
+  LAUNCH_CHECK();
+  auto cset = [&](int k) { return csets + (uint64_t)k * CSET_WORDS; };
+  const unsigned gt = grid_tiles(m), gf = grid_for(m), gn = grid_for(n);
+  for (int lvl = 0; lvl < L; ++lvl) {
     const int s = L - 1 - lvl;
-    const uint64_t ntl = (live + TILE - 1) / TILE;
-    hipLaunchKernelGGL(k_reset, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, uf, mt, top, claim, n);
+    uint64_t *st = stats + (uint64_t)lvl * ST_ROW;
+    hipLaunchKernelGGL(k_reset, dim3(gn), dim3(BLOCK), 0, c.stream, uf, mt, top, claim, n, csets);
     LAUNCH_CHECK();
-    HIP_CHECK(hipMemsetAsync(lcnt, 0, NSHARD * SHARD_STRIDE * sizeof(uint64_t), c.stream));
-    HIP_CHECK(hipMemsetAsync(xcnt, 0, NSHARD * SHARD_STRIDE * sizeof(uint64_t), c.stream));
-    uint64_t nl = 0, nx = 0;
-    uint64_t *lbuf = nullptr;
     {
-      TimedRegion tr(c, "etree_split", 8 * live);
-      hipLaunchKernelGGL(k_split, dim3(grid_tiles(live)), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges, live, s,
-                         clo, alt, xtop, lcnt, xcnt);
+      TimedRegion tr(c, "etree_split");
+      hipLaunchKernelGGL(k_split, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges, (const uint64_t *)d_live,
+                         st, s, clo, alt, xtop, cset(CSET_LIGHT), cset(CSET_CROSS));
       LAUNCH_CHECK();
-      // the dense light list must outlive the hook rounds (k_light_top reads it)
-      lbuf = c.get_as<uint64_t>("et_light", live);
-      nl = pack_shards<uint64_t>(c, alt, lbuf, ntl, 1, lcnt);
-      nx = pack_shards<uint32_t>(c, xtop, xidx, ntl, 1, xcnt);
+      pack_shards<uint64_t>(c, alt, lbuf, st + ST_LIVE, cset(CSET_LIGHT), st + ST_NL);
+      pack_shards<uint32_t>(c, xtop, xidx, st + ST_LIVE, cset(CSET_CROSS), st + ST_NX);
     }
-    if (nl) {
-      TimedRegion tr(c, "etree_union", 8 * nl);
-      const uint64_t lcap = (nl + TILE - 1) / TILE * TILE;
-      uint64_t *scr = c.get_as<uint64_t>("et_lwa", lcap), *dst = c.get_as<uint64_t>("et_lwb", lcap);
-      const uint64_t *in = lbuf;
-      uint64_t nin = nl;
-      for (int round = 0; nin; ++round) {
-        if (round > 4096) throw Error(SHEEP_ERR_HIP, "etree: union rounds do not converge");
-        HIP_CHECK(hipMemsetAsync(hcnt, 0, NSHARD * SHARD_STRIDE * sizeof(uint64_t), c.stream));
-        hipLaunchKernelGGL(k_hook_round, dim3(grid_tiles(nin)), dim3(BLOCK), 0, c.stream, in, nin, uf, scr, hcnt);
+    {
+      TimedRegion tr(c, "etree_union");
+      const uint64_t *in = lbuf, *n_in = st + ST_NL;
+      for (int round = 0; round < HOOK_ROUNDS; ++round) {
+        uint64_t *dst = hk[round & 1];
+        hipLaunchKernelGGL(k_hook_round, dim3(gt), dim3(BLOCK), 0, c.stream, in, n_in, uf, alt, cset(CSET_HOOK + round));
         LAUNCH_CHECK();
-        nin = pack_shards<uint64_t>(c, scr, dst, (nin + TILE - 1) / TILE, 1, hcnt);
+        pack_shards<uint64_t>(c, alt, dst, n_in, cset(CSET_HOOK + round), st + ST_HOOK + round);
         in = dst;
+        n_in = st + ST_HOOK + round;
       }
-      hipLaunchKernelGGL(k_light_top, dim3(grid_for(nl)), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf, nl, uf, top);
+      hipLaunchKernelGGL(k_hook_finish, dim3(gf), dim3(BLOCK), 0, c.stream, in, n_in, uf);
+      LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_light_top, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
+                         (const uint64_t *)(st + ST_NL), uf, top);
       LAUNCH_CHECK();
     }
-    if (nx) {
-      {
-        TimedRegion tr(c, "etree_cross", 16 * nx);
-        hipLaunchKernelGGL(k_cross_find, dim3(grid_for(nx)), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges,
-                           (const uint32_t *)xidx, nx, uf, mt, xtop);
-        LAUNCH_CHECK();
-      }
-      TimedRegion tr(c, "etree_apply", 20 * nx);
-      hipLaunchKernelGGL(k_assign_parents, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)uf,
+    {
+      TimedRegion tr(c, "etree_cross");
+      hipLaunchKernelGGL(k_cross_find, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges,
+                         (const uint32_t *)xidx, (const uint64_t *)(st + ST_NX), uf, mt, xtop);
+      LAUNCH_CHECK();
+    }
+    {
+      TimedRegion tr(c, "etree_apply");
+      hipLaunchKernelGGL(k_assign_parents, dim3(gn), dim3(BLOCK), 0, c.stream, (const uint32_t *)uf,
                          (const uint32_t *)mt, (const uint32_t *)top, n, parent);
       LAUNCH_CHECK();
-      HIP_CHECK(hipMemsetAsync(dcnt, 0, NSHARD * SHARD_STRIDE * sizeof(uint64_t), c.stream));
-      hipLaunchKernelGGL(k_cross_apply, dim3(grid_for(nx)), dim3(BLOCK), 0, c.stream, edges, xidx, xtop, nx, mt, claim,
-                         dcnt);
+      hipLaunchKernelGGL(k_cross_apply, dim3(gf), dim3(BLOCK), 0, c.stream, edges, xidx, xtop,
+                         (const uint64_t *)(st + ST_NX), mt, claim, dcnt);
       LAUNCH_CHECK();
-      HIP_CHECK(hipMemcpyAsync(h_dcnt.data(), dcnt, h_dcnt.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-      c.sync();
-      for (int k = 0; k < NSHARD; ++k) dead += h_dcnt[(uint64_t)k * SHARD_STRIDE];
     }
+    {
+      TimedRegion tr(c, "etree_compact");
+      hipLaunchKernelGGL(k_compact_edges, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges, st,
+                         (const unsigned long long *)dcnt, alt, cset(CSET_COMPACT));
+      LAUNCH_CHECK();
+      pack_shards<uint64_t>(c, alt, edges, st + ST_LIVE, cset(CSET_COMPACT), d_live, st + ST_COMPACT, dcnt);
+    }
+  }
+  if (!c.timing && !g_debug_etree) return;
+  std::vector<uint64_t> h((uint64_t)(L + 1) * ST_ROW);
+  HIP_CHECK(hipMemcpyAsync(h.data(), stats, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  for (int lvl = 0; lvl < L; ++lvl) {
+    const uint64_t *r = &h[(uint64_t)lvl * ST_ROW];
+    uint64_t hooked = r[ST_NL];
+    for (int k = 0; k < HOOK_ROUNDS - 1; ++k) hooked += r[ST_HOOK + k];
+    // algorithmic bytes: split reads every live edge; hooking reads each
+    // light edge once per round it takes part in; the cross pass gathers the edge and
+    // writes its top; apply reads index, top, edge and writes the edge back
+    c.add_bytes("etree_split", 8 * r[ST_LIVE]);
+    c.add_bytes("etree_union", 8 * hooked + 8 * r[ST_NL]);
+    c.add_bytes("etree_cross", 16 * r[ST_NX]);
+    c.add_bytes("etree_apply", 24 * r[ST_NX]);
+    c.add_bytes("etree_compact", r[ST_COMPACT] ? 16 * r[ST_LIVE] : 0);
     if (g_debug_etree)
-      fprintf(stderr, "etree lvl %d s %d live %lu light %lu cross %lu dead %lu\n", lvl, s, (unsigned long)live,
-              (unsigned long)nl, (unsigned long)nx, (unsigned long)dead);
-    if (dead * 4 >= live && dead) {   // compact once a quarter of the list is dead
-      TimedRegion tr(c, "etree_compact", 16 * live);
-      HIP_CHECK(hipMemsetAsync(ccnt, 0, NSHARD * SHARD_STRIDE * sizeof(uint64_t), c.stream));
-      hipLaunchKernelGGL(k_compact_edges, dim3(grid_tiles(live)), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges,
-                         live, alt, ccnt);
-      LAUNCH_CHECK();
-      live = pack_shards<uint64_t>(c, alt, edges, ntl, 1, ccnt);
-      dead = 0;
-    }
+      fprintf(stderr, "etree lvl %d s %d live %lu light %lu cross %lu dead %lu compact %lu hook-left %lu %lu %lu\n", lvl,
+              L - 1 - lvl, (unsigned long)r[ST_LIVE], (unsigned long)r[ST_NL], (unsigned long)r[ST_NX],
+              (unsigned long)r[ST_DEAD], (unsigned long)r[ST_COMPACT], (unsigned long)r[ST_HOOK],
+              (unsigned long)r[ST_HOOK + 1], (unsigned long)r[ST_HOOK + 2]);
   }
 }
 

@@ -1,0 +1,75 @@
+"""Edge-shard schedule over N ranks: the MI355X replacement of graph2tree's MPI `-ir`
+path (graph2tree.cpp:161-216).
+
+  * shard_bounds      — contiguous record shards, like `-l part/num_parts`;
+  * allreduce_degrees — one all-reduce of the per-shard degree histograms plus a max of
+                        max_slot (sequence.h:70-78 `mpiSequence`'s MPI_Allreduce);
+  * reduce_trees      — binomial reduction of the partial trees to rank 0 (the shape of
+                        MPI_Reduce with mpi_merge_reduction, jnode.cpp:203-250): at hop r,
+                        rank i with i % 2r == r sends to i - r, which merges.  Merging is
+                        associative and commutative (the elimination tree of the union of
+                        the parent edges), so the tree at rank 0 equals the serial one.
+
+One process per GPU.  With the "nccl" backend (RCCL over xGMI) device tensors are sent
+as they are.  With "gloo" they are staged through host memory, which lets the schedule
+run on CPUs (tests/test_dist.py) and lets several ranks share one GPU for a rehearsal.
+The compute is injected (`merge`), so the same schedule drives the HIP kernels in
+bench.py and the CPU oracle in the tests.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(nrec: int, rank: int, world: int) -> tuple[int, int]:
+    return rank * nrec // world, (rank + 1) * nrec // world
+
+
+def _host_staged() -> bool:
+    return dist.get_backend() == "gloo"
+
+
+def _send(t: torch.Tensor, dst: int) -> None:
+    dist.send(t.cpu() if _host_staged() and t.is_cuda else t, dst)
+
+
+def _recv_like(like: torch.Tensor, src: int) -> torch.Tensor:
+    if _host_staged() and like.is_cuda:
+        buf = torch.empty(like.shape, dtype=like.dtype, device="cpu")
+        dist.recv(buf, src)
+        return buf.to(like.device)
+    buf = torch.empty_like(like)
+    dist.recv(buf, src)
+    return buf
+
+
+def _all_reduce(t: torch.Tensor, op) -> None:
+    if _host_staged() and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op)
+
+
+def allreduce_degrees(deg: torch.Tensor, max_slot: int) -> int:
+    """Sum the shards' degree histograms in place; returns the global max_slot."""
+    mx = torch.tensor([max_slot], dtype=torch.int64, device=deg.device)
+    _all_reduce(deg, dist.ReduceOp.SUM)
+    _all_reduce(mx, dist.ReduceOp.MAX)
+    return int(mx.item())
+
+
+def reduce_trees(tree: torch.Tensor, merge, rank: int, world: int):
+    """Binomial reduction to rank 0.  Returns the merged tree on rank 0, None elsewhere
+    (a rank is done once it has sent)."""
+    r = 1
+    while r < world:
+        if rank % (2 * r) == r:
+            _send(tree, rank - r)
+            return None
+        if rank + r < world:
+            tree = merge(tree, _recv_like(tree, rank + r))
+        r *= 2
+    return tree
