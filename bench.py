@@ -168,7 +168,8 @@ def main():
             "dtype": "u32",
             "data": "synthetic (Graph500 RMAT, seeded, self-loops/duplicates removed)",
             "config": {"workload": f"RMAT-{a.scale} ef{a.ef}, k={a.k}", "records": R, "vertex_slots": s.pos_size,
-                       "tree_nodes": n, "k": a.k, "created": res.created, "seed": seed,
+                       "tree_nodes": n, "k": a.k, "created": res.created, "packing_nodes": res.packing_nodes,
+                       "heavy_nodes": res.heavy_nodes, "seed": seed,
                        "parallelism": f"edge-shards x{world}"
                        + ("" if a.dist_backend == "nccl" else f" ({a.dist_backend}"
                           + (", one device" if a.same_device else "") + ")")},

@@ -76,6 +76,7 @@ int sheep_ctx_destroy(sheep_ctx *ctx) {
   HIP_CHECK(hipSetDevice(c.device));
   HIP_CHECK(hipStreamSynchronize(c.stream));
   for (auto &kv : c.ws) if (kv.second.p) hipFree(kv.second.p);
+  for (auto &kv : c.pinned) if (kv.second.p) hipHostFree(kv.second.p);
   for (auto &kv : c.timers) for (auto &p : kv.second.pending) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
   for (hipEvent_t e : c.event_pool) hipEventDestroy(e);
   if (c.h_scalars) hipHostFree(c.h_scalars);

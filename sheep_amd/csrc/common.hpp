@@ -47,6 +47,7 @@ struct Ctx {
 
   struct Buf { void *p = nullptr; size_t bytes = 0; };
   std::map<std::string, Buf> ws;
+  std::map<std::string, Buf> pinned;   // host memory the kernels write directly (mapped)
 
   uint64_t *h_scalars = nullptr;   // pinned host mirror
   uint64_t *d_scalars = nullptr;   // device scalars (counters / flags)
@@ -70,6 +71,18 @@ struct Ctx {
   }
   template <typename T> T *get_as(const std::string &name, size_t count) {
     return (T *)get(name, count * sizeof(T));
+  }
+  // Host buffer a kernel can store into: results small enough to stage arrive with the
+  // one stream sync that has to happen anyway, instead of a copy per array.
+  void *get_pinned(const std::string &name, size_t bytes) {
+    Buf &b = pinned[name];
+    if (b.bytes < bytes) {
+      if (b.p) HIP_CHECK(hipHostFree(b.p));
+      b.p = nullptr;
+      HIP_CHECK(hipHostMalloc(&b.p, bytes, hipHostMallocMapped));
+      b.bytes = bytes;
+    }
+    return b.p;
   }
   void sync() { HIP_CHECK(hipStreamSynchronize(stream)); }
   // algorithmic bytes learned only after the launches (device-side counts)
@@ -225,7 +238,7 @@ void radix_sort_keys_u64(Ctx &c, uint64_t *keys, uint64_t n, int end_bit, uint64
 void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt);
 void histogram_edge_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t K, uint32_t *cnt);
 // etree.hip
-void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent);
+void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, bool by_lo);
 // append.hip — sharded appends: counters (NSHARD * SHARD_STRIDE u64, zeroed).  The pack
 // step moves the shard regions of a producer that streamed *n_in items together in dst
 // and writes the total to *total_out (device; must not alias n_in).  With cond, it runs

@@ -70,6 +70,29 @@ __device__ __forceinline__ uint32_t find_plain(uint32_t *uf, uint32_t x) {
 }
 
 
+// K independent chains in lockstep: each round issues one load per unfinished chain,
+// so a thread keeps K pointer chases in flight instead of one.
+template <int K> __device__ __forceinline__ void find_many(uint32_t *uf, uint32_t (&x)[K], const bool (&v)[K]) {
+  uint32_t p[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k] = v[k] ? uf[x[k]] : x[k];
+  for (;;) {
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < K; ++k) any |= p[k] != x[k];
+    if (!any) break;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (p[k] != x[k]) {
+        const uint32_t g = uf[p[k]];
+        if (g != p[k]) uf[x[k]] = g;
+        x[k] = p[k];
+        p[k] = g;
+      }
+    }
+  }
+}
+
 // ---- relabel + pst (jtree.cpp:72-91) -------------------------------------------------
 // One record = one undirected pair.  Both endpoints sequenced: pst[lo]++ and a tree
 // edge (lo,hi).  One endpoint sequenced, the other a slot < pos_size but absent from
@@ -121,18 +144,84 @@ __global__ __launch_bounds__(BLOCK) void k_relabel(const sheep_xs1 *__restrict__
 // sizes grids from an upper bound.  A level is a chain of launches with no host round
 // trip; kernels whose list is empty return at once.
 //
-// stats row of level l (u64): [0] live edges entering the level (holes included),
-// [1] light edges, [2] cross edges, [3] dead edges at the compaction check, [4] 1 if the
-// level compacted, [5..7] unresolved light edges after hooking round 0..2.
-constexpr int ST_ROW = 8, ST_LIVE = 0, ST_NL = 1, ST_NX = 2, ST_DEAD = 3, ST_COMPACT = 4, ST_HOOK = 5;
+// stats row of level l (u64): [0] length of the edge list entering the level (holes
+// and stale entries included), [1] light edges, [2] cross edges, [3] dead entries at the
+// compaction check, [4] 1 if the level compacted, [5..7] unresolved light edges after
+// hooking round 0..2, [8] list length after the level's appends, [9] which of the two
+// list buffers holds the list during the level (flips after every compaction), [10]
+// edges activated from the level's bucket, [11] of those, light ones (appended to the
+// list), [12] TILE x the split's tile count (sizes its shard regions).
+constexpr int ST_ROW = 16, ST_LIVE = 0, ST_NL = 1, ST_NX = 2, ST_DEAD = 3, ST_COMPACT = 4, ST_HOOK = 5, ST_GROWN = 8,
+              ST_SEL = 9, ST_R0 = 10, ST_NR0L = 11, ST_VT = 12;
 constexpr int HOOK_ROUNDS = 3;
 // counter sets zeroed at every level: light, cross, hook rounds, compaction
 constexpr int CSET_LIGHT = 0, CSET_CROSS = 1, CSET_HOOK = 2, CSET_COMPACT = CSET_HOOK + HOOK_ROUNDS, NCSET = CSET_COMPACT + 1;
 constexpr uint64_t CSET_WORDS = (uint64_t)NSHARD * SHARD_STRIDE;
 
+// ---- first-activity buckets ---------------------------------------------------------
+// An edge (lo, hi) takes part in level s only if bit s of ya = spread(lo) is 0 (light
+// or cross); while ya's bits above stay 1 it sits in right halves and every level would
+// just re-read it.  So the input is bucketed once by its first active level
+// f = the highest zero bit of ya, and level s activates bucket s: the list the levels
+// stream holds only edges that have been active (and their contractions).
+constexpr int NBUCKET = 32;
+
+__device__ __forceinline__ int first_level(uint64_t e, uint32_t clo, uint32_t mask) {
+  const uint32_t inv = ~spread((uint32_t)e, clo) & mask;   // nonzero: lo < hi <= n-1 keeps ya < 2^L - 1
+  return 31 - __clz(inv);
+}
+
+// cnt[f * gridDim.x + block] = edges of bucket f among the block's tiles
+__global__ __launch_bounds__(BLOCK) void k_bucket_count(const uint64_t *__restrict__ edges, uint64_t m, uint32_t clo,
+                                                        uint32_t mask, uint32_t *__restrict__ cnt) {
+  __shared__ uint32_t h[NBUCKET];
+  if (threadIdx.x < NBUCKET) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t ntiles = (m + TILE - 1) / TILE;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
+      const uint64_t e = i < m ? edges[i] : DEAD;
+      if (e != DEAD) atomicAdd(&h[first_level(e, clo, mask)], 1u);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < NBUCKET) cnt[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
+}
+
+// Same tiles per block as k_bucket_count; off = exclusive scan of its counts.
+__global__ __launch_bounds__(BLOCK) void k_bucket_scatter(const uint64_t *__restrict__ edges, uint64_t m, uint32_t clo,
+                                                          uint32_t mask, const uint32_t *__restrict__ off,
+                                                          uint64_t *__restrict__ r0) {
+  __shared__ uint32_t cur[NBUCKET];
+  if (threadIdx.x < NBUCKET) cur[threadIdx.x] = off[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
+  __syncthreads();
+  const uint64_t ntiles = (m + TILE - 1) / TILE;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
+      const uint64_t e = i < m ? edges[i] : DEAD;
+      if (e != DEAD) r0[atomicAdd(&cur[first_level(e, clo, mask)], 1u)] = e;
+    }
+  }
+}
+
+// seg[s] = first entry of bucket s, seg[L + s] = one past its last
+__global__ void k_bucket_bounds(const uint32_t *__restrict__ off, uint32_t g, int L, uint64_t *__restrict__ seg) {
+  const int s = threadIdx.x;
+  if (s < L) {
+    seg[s] = off[(uint64_t)s * g];
+    seg[L + s] = off[(uint64_t)(s + 1) * g];
+  }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t *__restrict__ uf, uint32_t *__restrict__ mt,
                                                  uint32_t *__restrict__ top, uint32_t *__restrict__ claim, uint64_t n,
-                                                 unsigned long long *__restrict__ csets) {
+                                                 unsigned long long *__restrict__ csets, uint64_t *__restrict__ status,
+                                                 uint64_t nstatus, const uint64_t *__restrict__ prev, uint64_t *__restrict__ st,
+                                                 unsigned long long *__restrict__ dead) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   const uint64_t t0 = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
   for (uint64_t i = t0; i < n; i += stride) {
@@ -142,6 +231,10 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t *__restrict__ uf, uint
     claim[i] = INVALID;
   }
   for (uint64_t i = t0; i < NCSET * CSET_WORDS; i += stride) csets[i] = 0;
+  for (uint64_t i = t0; i < nstatus; i += stride) status[i] = 0;
+  const bool compacted = prev && prev[ST_COMPACT];
+  if (t0 == 0) st[ST_SEL] = prev ? prev[ST_SEL] ^ (uint64_t)compacted : 0;
+  if (compacted && t0 < NSHARD) dead[t0 * SHARD_STRIDE] = 0;   // dead entries are counted since the last compaction
 }
 
 __global__ void k_set_u64(uint64_t *p, uint64_t v) { *p = v; }
@@ -149,53 +242,74 @@ __global__ void k_set_u64(uint64_t *p, uint64_t v) { *p = v; }
 // top[root] = the component's largest id.  Every vertex of a non-singleton light
 // component is an endpoint of a light edge and its maximum is the hi end of one, so a
 // max over the light edges' hi ends suffices (singletons keep top = self).
+constexpr int XK = 4;   // items per thread in the gather kernels (independent chains in flight)
+
 __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict__ lbuf, const uint64_t *__restrict__ n_l,
                                                      uint32_t *uf, uint32_t *__restrict__ top) {
   const uint64_t nl = *n_l;
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK * XK;
   const uint64_t iters = (nl + stride - 1) / stride;
-  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  for (uint64_t it = 0; it < iters; ++it, i += stride) {   // wave-uniform trip count (ballots)
-    uint32_t r = 0, b = 0;
-    const bool live = i < nl;
-    if (live) {
-      const uint64_t e = lbuf[i];
-      b = (uint32_t)(e >> 32);
-      r = find_plain(uf, (uint32_t)e);
+  uint64_t base = (uint64_t)blockIdx.x * BLOCK * XK + threadIdx.x;
+  for (uint64_t it = 0; it < iters; ++it, base += stride) {   // wave-uniform trip count (ballots)
+    uint32_t r[XK], b[XK];
+    bool live[XK];
+#pragma unroll
+    for (int k = 0; k < XK; ++k) {
+      const uint64_t i = base + (uint64_t)k * BLOCK;
+      live[k] = i < nl;
+      const uint64_t e = live[k] ? lbuf[i] : 0;
+      r[k] = (uint32_t)e;
+      b[k] = (uint32_t)(e >> 32);
     }
+    find_many<XK>(uf, r, live);
     // top only grows: combine lanes sharing the first lane's root, skip useless atomics
-    const uint64_t lm = __ballot(live);
-    if (lm) {
+#pragma unroll
+    for (int k = 0; k < XK; ++k) {
+      const uint64_t lm = __ballot(live[k]);
+      if (!lm) continue;
       const int first = __ffsll((unsigned long long)lm) - 1;
-      const uint32_t r0 = __shfl(r, first, 64);
-      const bool same = live && r == r0;
-      const uint32_t v = wave_max(same ? b : 0u);
+      const uint32_t r0 = __shfl(r[k], first, 64);
+      const bool same = live[k] && r[k] == r0;
+      const uint32_t v = wave_max(same ? b[k] : 0u);
       if ((int)__lane_id() == first && v > top[r0]) atomicMax(&top[r0], v);
-      if (live && !same && b > top[r]) atomicMax(&top[r], b);
+      if (live[k] && !same && b[k] > top[r[k]]) atomicMax(&top[r[k]], b[k]);
     }
   }
 }
 
-// One streaming pass classifies the live edges of a level: light (both ends in the
-// left half of their subproblem) -> the edge value to the light shards; cross -> its
-// index to the cross shards.  Edges inside a right half are left alone.  The dense
-// lists keep every lane of the union / find kernels busy (no divergence around
-// dependent pointer chases).
-__global__ __launch_bounds__(BLOCK) void k_split(const uint64_t *__restrict__ edges, const uint64_t *__restrict__ n_live,
-                                                 uint64_t *__restrict__ st, int s, uint32_t clo,
-                                                 uint64_t *__restrict__ lbuf, uint32_t *__restrict__ xidx,
+// One streaming pass classifies the edge list of a level plus the bucket of edges it
+// activates: light (both ends in the left half of their subproblem) -> the light
+// shards; cross -> the cross shards.  Edges inside a right half are left alone; stale
+// entries (cross edges of an earlier level, whose ends now lie in different
+// subproblems: (ya ^ yb) >> s >= 2) are skipped.  Light edges of the bucket join the
+// list (staged in r0l, appended by k_cross_apply).  The dense lists keep every lane of
+// the union / find kernels busy and are read sequentially.
+__global__ __launch_bounds__(BLOCK) void k_split(const uint64_t *__restrict__ buf0, const uint64_t *__restrict__ buf1,
+                                                 const uint64_t *__restrict__ n_live, uint64_t *__restrict__ st, int s,
+                                                 uint32_t clo, const uint64_t *__restrict__ r0,
+                                                 const uint64_t *__restrict__ seg, int L,
+                                                 uint64_t *__restrict__ lbuf, uint64_t *__restrict__ xbuf,
                                                  unsigned long long *__restrict__ lcnt,
-                                                 unsigned long long *__restrict__ xcnt) {
-  const uint64_t m = *n_live;
-  if (blockIdx.x == 0 && threadIdx.x == 0) st[ST_LIVE] = m;
-  const uint64_t ntiles = (m + TILE - 1) / TILE;
+                                                 unsigned long long *__restrict__ xcnt, uint64_t *__restrict__ r0l) {
+  const uint64_t len = *n_live;
+  const uint64_t *list = st[ST_SEL] ? buf1 : buf0;
+  const uint64_t rb = seg[s], rn = seg[L + s] - rb;
+  const uint64_t td = (len + TILE - 1) / TILE, ntiles = td + (rn + TILE - 1) / TILE;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st[ST_LIVE] = len;
+    st[ST_R0] = rn;
+    st[ST_VT] = ntiles * TILE;
+  }
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const bool act = tile >= td;   // a tile of the activated bucket (uniform per workgroup)
+    const uint64_t *src = act ? r0 + rb + (tile - td) * TILE : list + tile * TILE;
+    const uint64_t lim = act ? rn - (tile - td) * TILE : len - tile * TILE;
     uint64_t ev[TILE_ITEMS];
     uint32_t fl = 0, fx = 0;
 #pragma unroll
     for (int j = 0; j < TILE_ITEMS; ++j) {
-      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
-      ev[j] = i < m ? edges[i] : DEAD;
+      const uint64_t i = (uint64_t)j * BLOCK + threadIdx.x;
+      ev[j] = i < lim ? src[i] : DEAD;
     }
 #pragma unroll
     for (int j = 0; j < TILE_ITEMS; ++j) {
@@ -207,10 +321,14 @@ __global__ __launch_bounds__(BLOCK) void k_split(const uint64_t *__restrict__ ed
     }
     uint64_t sl = shard_reserve((uint32_t)__popc(fl), lcnt, tile, ntiles, 1);
     uint64_t sx = shard_reserve((uint32_t)__popc(fx), xcnt, tile, ntiles, 1);
+    uint64_t sr = act ? block_reserve((uint32_t)__popc(fl), (unsigned long long *)(st + ST_NR0L)) : 0;
 #pragma unroll
     for (int j = 0; j < TILE_ITEMS; ++j) {
-      if (fl & (1u << j)) lbuf[sl++] = ev[j];
-      if (fx & (1u << j)) xidx[sx++] = (uint32_t)(tile * TILE + (uint64_t)j * BLOCK + threadIdx.x);
+      if (fl & (1u << j)) {
+        lbuf[sl++] = ev[j];
+        if (act) r0l[sr++] = ev[j];
+      }
+      if (fx & (1u << j)) xbuf[sx++] = ev[j];
     }
   }
 }
@@ -281,34 +399,40 @@ __global__ __launch_bounds__(BLOCK) void k_assign_parents(const uint32_t *__rest
 }
 
 // For every cross edge (a,b): r = root of a's light component; m_r = min b (atomicMin).
-__global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict__ edges,
-                                                      const uint32_t *__restrict__ xidx, const uint64_t *__restrict__ n_x,
+__global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict__ xbuf, const uint64_t *__restrict__ n_x,
                                                       uint32_t *uf, uint32_t *__restrict__ mt, uint32_t *__restrict__ xtop) {
   const uint64_t nx = *n_x;
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK * XK;
   const uint64_t iters = (nx + stride - 1) / stride;
-  uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  for (uint64_t it = 0; it < iters; ++it, j += stride) {   // wave-uniform trip count (ballots)
-    const bool cross = j < nx;
-    uint32_t t = 0, b = 0;
-    if (cross) {
-      const uint64_t e = edges[xidx[j]];
-      b = (uint32_t)(e >> 32);
-      t = find_plain(uf, (uint32_t)e);
-      xtop[j] = t;
+  uint64_t base = (uint64_t)blockIdx.x * BLOCK * XK + threadIdx.x;
+  for (uint64_t it = 0; it < iters; ++it, base += stride) {   // wave-uniform trip count (ballots)
+    uint32_t t[XK], b[XK];
+    bool cross[XK];
+#pragma unroll
+    for (int k = 0; k < XK; ++k) {
+      cross[k] = base + (uint64_t)k * BLOCK < nx;
+      const uint64_t e = cross[k] ? xbuf[base + (uint64_t)k * BLOCK] : 0;
+      t[k] = (uint32_t)e;
+      b[k] = (uint32_t)(e >> 32);
     }
+    find_many<XK>(uf, t, cross);
+#pragma unroll
+    for (int k = 0; k < XK; ++k)
+      if (cross[k]) xtop[base + (uint64_t)k * BLOCK] = t[k];
     // Power-law graphs send most cross edges of a level to one giant component's top:
     // combine in the wave first (lanes sharing the first lane's top) and skip atomics a
     // plain read already shows useless (mt only decreases; a stale read is >= the true
     // value, so skipping stays exact).
-    const uint64_t cm = __ballot(cross);
-    if (cm) {
+#pragma unroll
+    for (int k = 0; k < XK; ++k) {
+      const uint64_t cm = __ballot(cross[k]);
+      if (!cm) continue;
       const int first = __ffsll((unsigned long long)cm) - 1;
-      const uint32_t t0 = __shfl(t, first, 64);
-      const bool same = cross && t == t0;
-      const uint32_t v = wave_min(same ? b : INVALID);
+      const uint32_t t0 = __shfl(t[k], first, 64);
+      const bool same = cross[k] && t[k] == t0;
+      const uint32_t v = wave_min(same ? b[k] : INVALID);
       if ((int)__lane_id() == first && v < mt[t0]) atomicMin(&mt[t0], v);
-      if (cross && !same && b < mt[t]) atomicMin(&mt[t], b);
+      if (cross[k] && !same && b[k] < mt[t[k]]) atomicMin(&mt[t[k]], b[k]);
     }
   }
 }
@@ -320,27 +444,39 @@ __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict
 // the same b is kept without a check — the common duplicates, a giant component's many
 // edges into one hub, all carry the same m.)  claim is n x u32, L3-resident, unlike a
 // global hash table of the pairs.
-__global__ __launch_bounds__(BLOCK) void k_cross_apply(uint64_t *__restrict__ edges, const uint32_t *__restrict__ xidx,
-                                                       const uint32_t *__restrict__ xtop, const uint64_t *__restrict__ n_x,
-                                                       const uint32_t *__restrict__ mt, uint32_t *__restrict__ claim,
-                                                       unsigned long long *__restrict__ dead) {
-  const uint64_t nx = *n_x;
-  if ((uint64_t)blockIdx.x * BLOCK >= nx) return;
+//
+// The contracted edges are APPENDED: cross edge j goes to edges[len + j] (DEAD if it
+// died), a sequential write; its old entry is left as it is — stale from the next level
+// on (see k_split) — instead of being rewritten in place, which cost a scattered
+// partial-line write per cross edge.  Every processed edge leaves one dead entry behind
+// (two if it died), counted for the compaction check.
+__global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restrict__ xbuf, const uint32_t *__restrict__ xtop,
+                                                       const uint64_t *__restrict__ st, const uint32_t *__restrict__ mt,
+                                                       uint32_t *__restrict__ claim, uint64_t *__restrict__ buf0,
+                                                       uint64_t *__restrict__ buf1, const uint64_t *__restrict__ r0l,
+                                                       uint64_t cap, unsigned long long *__restrict__ dead,
+                                                       unsigned long long *__restrict__ err) {
+  const uint64_t nx = st[ST_NX], len = st[ST_LIVE], nr = st[ST_NR0L];
+  if (len + nx + nr > cap) {   // cannot happen (the list stays below 7/3 m); fail loudly
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(err, 1ull);
+    return;
+  }
+  uint64_t *out = (st[ST_SEL] ? buf1 : buf0) + len;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < nr; j += stride) out[nx + j] = r0l[j];
+  if ((uint64_t)blockIdx.x * BLOCK >= nx) return;
   uint32_t ndead = 0;
   for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < nx; j += stride) {
-    const uint32_t idx = xidx[j], r = xtop[j];
-    const uint32_t m = mt[r];
-    const uint64_t e = edges[idx];
-    const uint32_t b = (uint32_t)(e >> 32);
+    const uint32_t m = mt[xtop[j]];
+    const uint32_t b = (uint32_t)(xbuf[j] >> 32);
     bool kill = b == m;
     if (!kill) {
       uint32_t c = claim[b];
       if (c == INVALID) c = atomicCAS(&claim[b], INVALID, m);
       kill = c == m;   // someone else's (m, b) is kept (our own successful CAS returned INVALID)
     }
-    if (kill) { edges[idx] = DEAD; ++ndead; }
-    else edges[idx] = ((uint64_t)b << 32) | m;
+    out[j] = kill ? DEAD : ((uint64_t)b << 32) | m;
+    ndead += 1 + kill;
   }
   // one add per workgroup, spread over the shard counters (a single hot counter
   // serialises ~1e5 adds per millisecond)
@@ -355,13 +491,57 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(uint64_t *__restrict__ ed
 }
 
 // Compaction, decided on the device: once a quarter of the list is dead (counted since
-// the last compaction) the live edges are appended to `out` (pack_shards then moves them
-// back and updates the live count); otherwise every workgroup returns at once.
-__global__ __launch_bounds__(BLOCK) void k_compact_edges(const uint64_t *__restrict__ in, uint64_t *__restrict__ st,
-                                                         const unsigned long long *__restrict__ dead,
-                                                         uint64_t *__restrict__ out, unsigned long long *__restrict__ counter) {
-  const uint64_t m = st[ST_LIVE];
-  __shared__ uint64_t s_dead;
+// the last compaction) the entries still alive at the next level — not DEAD, both ends
+// in one half: (ya ^ yb) >> s == 0 — are copied, in order, into the other list buffer
+// (the next level reads from there); otherwise the list just keeps its appended tail.
+//
+// One pass, 16 B per entry: workgroups take 16K-entry chunks in ticket order, count the
+// kept entries (values stay in registers), and get the chunk's output offset by
+// decoupled look-back over the chunk status words (aggregate / inclusive prefix).  Ticket
+// order means every predecessor chunk is owned by a running workgroup, so the wait ends.
+constexpr int C_ROWS = 64;                                    // 64-entry rows per wave
+constexpr uint64_t C_CHUNK = (uint64_t)WAVE * C_ROWS * (BLOCK / WAVE);   // 16384 entries
+constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 1ull << 63, LB_VAL = LB_AGG - 1;
+
+__device__ __forceinline__ bool entry_kept(uint64_t e, int s, uint32_t clo) {
+  return e != DEAD && ((spread((uint32_t)e, clo) ^ spread((uint32_t)(e >> 32), clo)) >> s) == 0;
+}
+
+// Called by one whole wave: publishes the chunk's aggregate, then sums predecessors 64
+// status words per step (one round trip per 64 chunks, not per chunk) back to the first
+// inclusive prefix; returns the exclusive prefix and publishes the inclusive one.
+__device__ uint64_t chunk_lookback(uint64_t *status, uint64_t chunk, uint64_t total) {
+  const int lane = threadIdx.x & 63;
+  if (chunk == 0) {
+    if (lane == 0) __hip_atomic_store(&status[0], LB_INC | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0) __hip_atomic_store(&status[chunk], LB_AGG | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t acc = 0;
+  int64_t base = (int64_t)chunk - 1;
+  for (;;) {
+    const int64_t j = base - lane;
+    const uint64_t v = j >= 0 ? __hip_atomic_load(&status[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : LB_INC;
+    const uint64_t incm = __ballot((v & LB_INC) != 0);
+    const int first = incm ? __ffsll((unsigned long long)incm) - 1 : 63;
+    const uint64_t need = first == 63 ? ~0ull : ((2ull << first) - 1);
+    if ((__ballot((v & ~LB_VAL) != 0) & need) != need) continue;   // a predecessor has not counted yet
+    acc += wave_sum(lane <= first ? (v & LB_VAL) : 0ull);
+    if (incm) break;
+    base -= WAVE;
+  }
+  if (lane == 0) __hip_atomic_store(&status[chunk], LB_INC | (acc + total), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  return acc;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_compact_edges(uint64_t *__restrict__ buf0, uint64_t *__restrict__ buf1,
+                                                         uint64_t *__restrict__ st, uint64_t *__restrict__ d_len, int s,
+                                                         uint32_t clo, const unsigned long long *__restrict__ dead,
+                                                         uint64_t *__restrict__ status,
+                                                         unsigned long long *__restrict__ ticket) {
+  const uint64_t m = st[ST_LIVE] + st[ST_NX] + st[ST_NR0L];
+  __shared__ uint64_t s_dead, s_chunk, s_base;
+  __shared__ uint32_t s_w[BLOCK / WAVE];
   if (threadIdx.x < WAVE) {
     const uint64_t d = wave_sum((uint64_t)(threadIdx.x < NSHARD ? dead[(uint64_t)threadIdx.x * SHARD_STRIDE] : 0));
     if (threadIdx.x == 0) s_dead = d;
@@ -369,22 +549,53 @@ __global__ __launch_bounds__(BLOCK) void k_compact_edges(const uint64_t *__restr
   __syncthreads();
   const uint64_t nd = s_dead;
   const bool go = nd && nd * 4 >= m;
-  if (blockIdx.x == 0 && threadIdx.x == 0) { st[ST_DEAD] = nd; st[ST_COMPACT] = go; }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st[ST_DEAD] = nd;
+    st[ST_COMPACT] = go;
+    st[ST_GROWN] = m;
+    if (!go) *d_len = m;
+  }
   if (!go) return;
-  const uint64_t ntiles = (m + TILE - 1) / TILE;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    uint64_t ev[TILE_ITEMS];
-    uint32_t flags = 0;
+  const uint64_t *in = st[ST_SEL] ? buf1 : buf0;
+  uint64_t *out = st[ST_SEL] ? buf0 : buf1;
+  const uint64_t nchunks = (m + C_CHUNK - 1) / C_CHUNK;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (;;) {
+    if (threadIdx.x == 0) s_chunk = atomicAdd(ticket, 1ull);
+    __syncthreads();
+    const uint64_t chunk = s_chunk;
+    if (chunk >= nchunks) break;
+    const uint64_t wbase = chunk * C_CHUNK + (uint64_t)wave * WAVE * C_ROWS + lane;
+    uint64_t v[C_ROWS];
+    uint32_t cnt = 0;
 #pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) {
-      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
-      ev[j] = i < m ? in[i] : DEAD;
-      if (ev[j] != DEAD) flags |= 1u << j;
+    for (int r = 0; r < C_ROWS; ++r) {
+      const uint64_t i = wbase + (uint64_t)r * WAVE;
+      v[r] = i < m ? in[i] : DEAD;
     }
-    uint64_t slot = shard_reserve((uint32_t)__popc(flags), counter, tile, ntiles, 1);
 #pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j)
-      if (flags & (1u << j)) out[slot++] = ev[j];
+    for (int r = 0; r < C_ROWS; ++r) cnt += (uint32_t)__popcll(__ballot(entry_kept(v[r], s, clo)));
+    if (lane == 0) s_w[wave] = cnt;
+    __syncthreads();
+    if (wave == 0) {
+      const uint64_t total = (uint64_t)s_w[0] + s_w[1] + s_w[2] + s_w[3];
+      const uint64_t excl = chunk_lookback(status, chunk, total);
+      if (lane == 0) {
+        s_base = excl;
+        if (chunk == nchunks - 1) *d_len = excl + total;
+      }
+    }
+    __syncthreads();
+    uint64_t pos = s_base;
+    for (int w = 0; w < wave; ++w) pos += s_w[w];
+#pragma unroll
+    for (int r = 0; r < C_ROWS; ++r) {
+      const bool k = entry_kept(v[r], s, clo);
+      const uint64_t mask = __ballot(k);
+      if (k) out[pos + __popcll(mask & lanemask_lt())] = v[r];
+      pos += __popcll(mask);
+    }
+    __syncthreads();   // s_chunk / s_w / s_base are rewritten for the next chunk
   }
 }
 
@@ -427,10 +638,18 @@ void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
 
 static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
 
-// Elimination tree of `m` edges ((hi<<32)|lo, lo < hi < n).  `edges` is consumed.
+// The edge list grows by its cross edges each level and is compacted once a quarter is
+// dead; between compactions it stays below 4/3 of the surviving edges (<= m), plus one
+// level's appends (<= m): 7/3 m.
+static uint64_t edge_capacity(uint64_t m) { return m * 7 / 3 + 2 * TILE; }
+
+// Elimination tree of `m` edges ((hi<<32)|lo, lo < hi < n, DEAD holes allowed).  `edges`
+// is consumed.  by_lo: the edges are ordered by lo (a merge's parent edges), so the
+// first-activity buckets are ranges of it; otherwise they are bucketed by one counting
+// pass and `edges` (which must then hold edge_capacity(m) entries) becomes a list buffer.
 // One pass of launches per level, no host synchronisation inside the loop (see the
 // stats row above); the stats come back once at the end for the timers / debug log.
-void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent) {
+void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, bool by_lo) {
   fill_u32(c, parent, n, INVALID);
   if (n < 2 || m == 0) return;
   if (m >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "too many edges for one shard");
@@ -447,32 +666,81 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
   uint32_t *claim = c.get_as<uint32_t>("et_claim", n);
   // every list is bounded by m; scratch regions of sharded appends need whole tiles
   const uint64_t mcap = (m + TILE - 1) / TILE * TILE;
-  uint32_t *xidx = c.get_as<uint32_t>("et_xidx", mcap);
-  uint32_t *xtop = c.get_as<uint32_t>("et_xtop", mcap);   // also the cross list's shard scratch
-  uint64_t *alt = c.get_as<uint64_t>("et_alt", mcap);     // shard scratch: light list, compaction
+  const uint64_t ecap = edge_capacity(m);
+  uint32_t *xtop = c.get_as<uint32_t>("et_xtop", mcap);
+  uint64_t *xbuf = c.get_as<uint64_t>("et_cross", mcap);
+  // the two list buffers (compaction flips between them) and the bucketed input r0
+  uint64_t *list0 = by_lo ? c.get_as<uint64_t>("et_list1", ecap) : edges;
+  uint64_t *other = c.get_as<uint64_t>("et_list2", ecap);
+  uint64_t *r0 = by_lo ? edges : c.get_as<uint64_t>("et_r0", m);
+  uint64_t *seg = c.get_as<uint64_t>("et_seg", 2 * (uint64_t)L);
+  const uint32_t mask = (uint32_t)((1ull << L) - 1);
+  if (by_lo) {
+    // bucket s = lo with ya in [2^L - 2^(s+1), 2^L - 2^s): a range of lo, entries 2 lo, 2 lo + 1
+    auto first_lo = [&](uint64_t y) {   // min lo with spread(lo) >= y
+      uint64_t a = 0, b = n;
+      while (a < b) {
+        const uint64_t x = (a + b) / 2;
+        if (x + ((x * (uint64_t)clo) >> 32) >= y) b = x; else a = x + 1;
+      }
+      return a;
+    };
+    uint64_t *h = (uint64_t *)c.get_pinned("et_seg_host", 2 * (size_t)L * sizeof(uint64_t));
+    for (int b = 0; b < L; ++b) {
+      h[b] = 2 * first_lo((1ull << L) - (2ull << b));
+      h[L + b] = 2 * first_lo((1ull << L) - (1ull << b));
+      if (h[L + b] > m) h[L + b] = m;
+      if (h[b] > h[L + b]) h[b] = h[L + b];
+    }
+    HIP_CHECK(hipMemcpyAsync(seg, h, 2 * (size_t)L * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+  } else {
+    TimedRegion tr(c, "etree_bucket", 24 * m);
+    const unsigned g = grid_tiles(m);
+    uint32_t *bc = c.get_as<uint32_t>("et_bcnt", (uint64_t)(NBUCKET + 1) * g);
+    HIP_CHECK(hipMemsetAsync(bc, 0, (uint64_t)(NBUCKET + 1) * g * sizeof(uint32_t), c.stream));
+    hipLaunchKernelGGL(k_bucket_count, dim3(g), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges, m, clo, mask, bc);
+    LAUNCH_CHECK();
+    scan_exclusive_u32(c, bc, bc, (uint64_t)(NBUCKET + 1) * g, nullptr);
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(g), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges, m, clo, mask,
+                       (const uint32_t *)bc, r0);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_bucket_bounds, dim3(1), dim3(64), 0, c.stream, (const uint32_t *)bc, g, L, seg);
+    LAUNCH_CHECK();
+  }
+  uint64_t *r0l = c.get_as<uint64_t>("et_r0l", mcap);   // light edges of a level's bucket, staged
+  // split's shard regions follow ITS tiles: the list (up to ecap) plus a bucket (up to m)
+  const uint64_t lcap = (ecap + m + 2 * TILE) / TILE * TILE;
+  uint64_t *alt = c.get_as<uint64_t>("et_alt", lcap);     // shard scratch: light list, hooking
+  uint64_t *xscr = c.get_as<uint64_t>("et_xscr", lcap);   // shard scratch: cross list, then a hook list
+  const uint64_t nstatus = (ecap + C_CHUNK - 1) / C_CHUNK + 1;
+  uint64_t *status = c.get_as<uint64_t>("et_lookback", nstatus);
   uint64_t *lbuf = c.get_as<uint64_t>("et_light", mcap);  // must outlive the hook rounds (k_light_top)
-  uint64_t *hk[2] = {c.get_as<uint64_t>("et_lwa", mcap), c.get_as<uint64_t>("et_lwb", mcap)};
+  uint64_t *hk[2] = {xscr, c.get_as<uint64_t>("et_lwb", mcap)};
+  unsigned long long *err = (unsigned long long *)c.d_scalars + 14;
+  HIP_CHECK(hipMemsetAsync(err, 0, sizeof(uint64_t), c.stream));
   unsigned long long *csets = c.get_as<unsigned long long>("et_csets", NCSET * CSET_WORDS);
   unsigned long long *dcnt = shard_counters(c, "dead");
   uint64_t *stats = c.get_as<uint64_t>("et_stats", (uint64_t)(L + 1) * ST_ROW);
   uint64_t *d_live = stats + (uint64_t)L * ST_ROW;
   HIP_CHECK(hipMemsetAsync(stats, 0, (uint64_t)L * ST_ROW * sizeof(uint64_t), c.stream));
-  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, c.stream, d_live, m);
+  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, c.stream, d_live, 0);   // the list starts empty
   LAUNCH_CHECK();
   auto cset = [&](int k) { return csets + (uint64_t)k * CSET_WORDS; };
-  const unsigned gt = grid_tiles(m), gf = grid_for(m), gn = grid_for(n);
+  const unsigned gt = grid_tiles(ecap + m), gf = grid_for(m, BLOCK * XK), gn = grid_for(n);
   for (int lvl = 0; lvl < L; ++lvl) {
     const int s = L - 1 - lvl;
     uint64_t *st = stats + (uint64_t)lvl * ST_ROW;
-    hipLaunchKernelGGL(k_reset, dim3(gn), dim3(BLOCK), 0, c.stream, uf, mt, top, claim, n, csets);
+    hipLaunchKernelGGL(k_reset, dim3(gn), dim3(BLOCK), 0, c.stream, uf, mt, top, claim, n, csets, status, nstatus,
+                       (const uint64_t *)(lvl ? st - ST_ROW : nullptr), st, dcnt);
     LAUNCH_CHECK();
     {
       TimedRegion tr(c, "etree_split");
-      hipLaunchKernelGGL(k_split, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges, (const uint64_t *)d_live,
-                         st, s, clo, alt, xtop, cset(CSET_LIGHT), cset(CSET_CROSS));
+      hipLaunchKernelGGL(k_split, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)list0, (const uint64_t *)other,
+                         (const uint64_t *)d_live, st, s, clo, (const uint64_t *)r0, (const uint64_t *)seg, L, alt, xscr,
+                         cset(CSET_LIGHT), cset(CSET_CROSS), r0l);
       LAUNCH_CHECK();
-      pack_shards<uint64_t>(c, alt, lbuf, st + ST_LIVE, cset(CSET_LIGHT), st + ST_NL);
-      pack_shards<uint32_t>(c, xtop, xidx, st + ST_LIVE, cset(CSET_CROSS), st + ST_NX);
+      pack_shards<uint64_t>(c, alt, lbuf, st + ST_VT, cset(CSET_LIGHT), st + ST_NL);
+      pack_shards<uint64_t>(c, xscr, xbuf, st + ST_VT, cset(CSET_CROSS), st + ST_NX);
     }
     {
       TimedRegion tr(c, "etree_union");
@@ -493,8 +761,8 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
     }
     {
       TimedRegion tr(c, "etree_cross");
-      hipLaunchKernelGGL(k_cross_find, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges,
-                         (const uint32_t *)xidx, (const uint64_t *)(st + ST_NX), uf, mt, xtop);
+      hipLaunchKernelGGL(k_cross_find, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)xbuf,
+                         (const uint64_t *)(st + ST_NX), uf, mt, xtop);
       LAUNCH_CHECK();
     }
     {
@@ -502,18 +770,21 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
       hipLaunchKernelGGL(k_assign_parents, dim3(gn), dim3(BLOCK), 0, c.stream, (const uint32_t *)uf,
                          (const uint32_t *)mt, (const uint32_t *)top, n, parent);
       LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_cross_apply, dim3(gf), dim3(BLOCK), 0, c.stream, edges, xidx, xtop,
-                         (const uint64_t *)(st + ST_NX), mt, claim, dcnt);
+      hipLaunchKernelGGL(k_cross_apply, dim3(grid_for(m)), dim3(BLOCK), 0, c.stream, (const uint64_t *)xbuf,
+                         (const uint32_t *)xtop, (const uint64_t *)st, (const uint32_t *)mt, claim, list0, other,
+                         (const uint64_t *)r0l, ecap, dcnt, err);
       LAUNCH_CHECK();
     }
     {
       TimedRegion tr(c, "etree_compact");
-      hipLaunchKernelGGL(k_compact_edges, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges, st,
-                         (const unsigned long long *)dcnt, alt, cset(CSET_COMPACT));
+      hipLaunchKernelGGL(k_compact_edges, dim3(grid_for(ecap, (unsigned)C_CHUNK, 256 * 4)), dim3(BLOCK), 0, c.stream,
+                         list0, other, st, d_live, s, clo, (const unsigned long long *)dcnt, status, cset(CSET_COMPACT));
       LAUNCH_CHECK();
-      pack_shards<uint64_t>(c, alt, edges, st + ST_LIVE, cset(CSET_COMPACT), d_live, st + ST_COMPACT, dcnt);
     }
   }
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 14, err, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  if (c.h_scalars[14]) throw Error(SHEEP_ERR_HIP, "etree: edge list capacity exceeded");
   if (!c.timing && !g_debug_etree) return;
   std::vector<uint64_t> h((uint64_t)(L + 1) * ST_ROW);
   HIP_CHECK(hipMemcpyAsync(h.data(), stats, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
@@ -522,17 +793,18 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
     const uint64_t *r = &h[(uint64_t)lvl * ST_ROW];
     uint64_t hooked = r[ST_NL];
     for (int k = 0; k < HOOK_ROUNDS - 1; ++k) hooked += r[ST_HOOK + k];
-    // algorithmic bytes: split reads every live edge; hooking reads each
-    // light edge once per round it takes part in; the cross pass gathers the edge and
-    // writes its top; apply reads index, top, edge and writes the edge back
-    c.add_bytes("etree_split", 8 * r[ST_LIVE]);
+    // algorithmic bytes: split reads every list entry; hooking reads each
+    // light edge once per round it takes part in; the cross pass reads the edge and
+    // writes its top; apply reads edge, top, m and claim and appends the contraction
+    c.add_bytes("etree_split", 8 * (r[ST_LIVE] + r[ST_R0]));
     c.add_bytes("etree_union", 8 * hooked + 8 * r[ST_NL]);
-    c.add_bytes("etree_cross", 16 * r[ST_NX]);
-    c.add_bytes("etree_apply", 24 * r[ST_NX]);
-    c.add_bytes("etree_compact", r[ST_COMPACT] ? 16 * r[ST_LIVE] : 0);
+    c.add_bytes("etree_cross", 12 * r[ST_NX]);
+    c.add_bytes("etree_apply", 20 * r[ST_NX]);
+    c.add_bytes("etree_compact", r[ST_COMPACT] ? 8 * r[ST_GROWN] + 8 * (r[ST_GROWN] - r[ST_DEAD]) : 0);
     if (g_debug_etree)
-      fprintf(stderr, "etree lvl %d s %d live %lu light %lu cross %lu dead %lu compact %lu hook-left %lu %lu %lu\n", lvl,
-              L - 1 - lvl, (unsigned long)r[ST_LIVE], (unsigned long)r[ST_NL], (unsigned long)r[ST_NX],
+      fprintf(stderr, "etree lvl %d s %d list %lu bucket %lu light %lu cross %lu dead %lu compact %lu hook-left %lu %lu %lu\n",
+              lvl, L - 1 - lvl, (unsigned long)r[ST_LIVE], (unsigned long)r[ST_R0], (unsigned long)r[ST_NL],
+              (unsigned long)r[ST_NX],
               (unsigned long)r[ST_DEAD], (unsigned long)r[ST_COMPACT], (unsigned long)r[ST_HOOK],
               (unsigned long)r[ST_HOOK + 1], (unsigned long)r[ST_HOOK + 2]);
   }
@@ -543,7 +815,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   uint32_t *pst = c.get_as<uint32_t>("bt_pst", n ? n : 1);
   uint32_t *parent = c.get_as<uint32_t>("bt_parent", n ? n : 1);
   HIP_CHECK(hipMemsetAsync(pst, 0, n * sizeof(uint32_t), c.stream));
-  uint64_t *edges = c.get_as<uint64_t>("bt_edges", nrec ? nrec : 1);
+  uint64_t *edges = c.get_as<uint64_t>("bt_edges", edge_capacity(nrec ? nrec : 1));
   unsigned long long *d = (unsigned long long *)c.d_scalars + 8;
   HIP_CHECK(hipMemsetAsync(d + 1, 0, sizeof(uint64_t), c.stream));
   if (nrec) {
@@ -562,7 +834,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   }
   {
     TimedRegion tr(c, "etree", 8 * m);
-    etree_from_edges(c, edges, m, n, parent);
+    etree_from_edges(c, edges, m, n, parent, false);
   }
   if (n) {
     hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, tree);
@@ -584,7 +856,7 @@ void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n,
   if (c.h_scalars[11]) throw Error(SHEEP_ERR_ARG, "merge: a parent is not a later node of the tree");
   {
     TimedRegion tr(c, "merge", 16 * n);
-    etree_from_edges(c, edges, 2 * n, n, parent);
+    etree_from_edges(c, edges, 2 * n, n, parent, true);
   }
   hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);
   LAUNCH_CHECK();

@@ -217,14 +217,44 @@ __global__ __launch_bounds__(BLOCK) void k_pack_event(const uint32_t *__restrict
   if ((threadIdx.x & 63) == 0 && best != INVALID) atomicMin(next, best);
 }
 
-__global__ void k_event_info(uint32_t *__restrict__ ev, const uint32_t *__restrict__ koff,
-                             const uint32_t *__restrict__ parent, const uint32_t *__restrict__ tD) {
-  if (threadIdx.x != 0) return;
+// Everything the host needs for one packing event, stored straight into mapped host
+// memory: hdr = {v, koff[v], #kids, tD(v) (INVALID for a root), R[v] lo, R[v] hi}, then
+// the node's kids in their current order and their R (the first `cap` of them).
+constexpr uint32_t EV_STAGE = 1u << 16;
+__global__ __launch_bounds__(BLOCK) void k_event_stage(const uint32_t *__restrict__ ev, const uint32_t *__restrict__ koff,
+                                                       const uint32_t *__restrict__ parent, const uint32_t *__restrict__ tD,
+                                                       const uint32_t *__restrict__ kids, const uint64_t *__restrict__ R,
+                                                       uint32_t *__restrict__ hdr, uint32_t *__restrict__ kid_out,
+                                                       uint64_t *__restrict__ r_out, uint32_t cap) {
   const uint32_t v = ev[0];
-  if (v == INVALID) return;
-  ev[1] = koff[v];
-  ev[2] = koff[v + 1];
-  ev[3] = parent[v] == INVALID ? INVALID : tD[v];
+  if (v == INVALID) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = INVALID;
+    return;
+  }
+  const uint32_t beg = koff[v], cnt = koff[v + 1] - beg;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint64_t r = R[v];
+    hdr[0] = v;
+    hdr[1] = beg;
+    hdr[2] = cnt;
+    hdr[3] = parent[v] == INVALID ? INVALID : tD[v];
+    hdr[4] = (uint32_t)r;
+    hdr[5] = (uint32_t)(r >> 32);
+  }
+  const uint32_t lim = cnt < cap ? cnt : cap;
+  for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < lim; j += gridDim.x * BLOCK) {
+    const uint32_t kid = kids[beg + j];
+    kid_out[j] = kid;
+    r_out[j] = R[kid];
+  }
+}
+
+// Kid orders re-sorted during the events, written back in one batch at the end
+// (a node packs at most once per call, so no event reads an order another one wrote).
+__global__ void k_scatter_u32(const uint32_t *__restrict__ pos, const uint32_t *__restrict__ val, uint64_t m,
+                              uint32_t *__restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) out[pos[i]] = val[i];
 }
 
 __global__ void k_kid_r(const uint32_t *__restrict__ kids, uint32_t beg, uint32_t cnt, const uint64_t *__restrict__ R,
@@ -402,82 +432,103 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
                        (const uint32_t *)rst, (const uint32_t *)ren, t.tD, t.tU, hst, hen);
     LAUNCH_CHECK();
   }
-  // ev[0] = next packing node (INVALID: none), ev[1..3] = koff[v], koff[v+1], tD(v)
+  // ev[0] = next packing node (INVALID: none); one stream sync per event
   uint32_t *ev = (uint32_t *)(c.d_scalars + 44);
-  uint32_t *h_ev = (uint32_t *)(c.h_scalars + 44);
+  uint8_t *stage = (uint8_t *)c.get_pinned("pt_event", 64 + (size_t)EV_STAGE * 12);
+  uint32_t *hdr = (uint32_t *)stage, *st_kids = (uint32_t *)(stage + 64);
+  uint64_t *st_r = (uint64_t *)(stage + 64 + (size_t)EV_STAGE * 4);
+  uint32_t *d_hdr, *d_kids;
+  uint64_t *d_r;
+  HIP_CHECK(hipHostGetDevicePointer((void **)&d_hdr, hdr, 0));
+  HIP_CHECK(hipHostGetDevicePointer((void **)&d_kids, st_kids, 0));
+  HIP_CHECK(hipHostGetDevicePointer((void **)&d_r, st_r, 0));
   std::vector<uint64_t> part_size;
   std::vector<uint32_t> asg_ids;
   std::vector<int16_t> asg_part;
-  std::vector<uint32_t> seg, order, sorted;
+  std::vector<uint32_t> seg, order, sorted, upl_pos, upl_ids;
   std::vector<uint64_t> segR, scb;
   std::vector<char> done;
   uint32_t v = INVALID, vpos = INVALID;
   uint64_t delta = 0;
-  for (;;) {
-    HIP_CHECK(hipMemsetAsync(ev, 0xFF, sizeof(uint32_t), c.stream));
-    if (nh) {
-      hipLaunchKernelGGL(k_pack_event, dim3(grid_for(nh)), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh,
-                         (const uint32_t *)hst, (const uint32_t *)hen, R, v, vpos, delta, max_component, ev);
+  {
+    TimedRegion tr(c, "partition_events");
+    for (;;) {
+      HIP_CHECK(hipMemsetAsync(ev, 0xFF, sizeof(uint32_t), c.stream));
+      if (nh) {
+        hipLaunchKernelGGL(k_pack_event, dim3(grid_for(nh)), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh,
+                           (const uint32_t *)hst, (const uint32_t *)hen, R, v, vpos, delta, max_component, ev);
+        LAUNCH_CHECK();
+      }
+      hipLaunchKernelGGL(k_event_stage, dim3(64), dim3(BLOCK), 0, c.stream, (const uint32_t *)ev, k->koff, k->parent,
+                         t.tD, (const uint32_t *)k->kids, (const uint64_t *)R, d_hdr, d_kids, d_r, EV_STAGE);
       LAUNCH_CHECK();
-    }
-    hipLaunchKernelGGL(k_event_info, dim3(1), dim3(WAVE), 0, c.stream, ev, k->koff, k->parent, t.tD);
-    LAUNCH_CHECK();
-    d2h(c, h_ev, (const uint32_t *)ev, 4);
-    c.sync();
-    v = h_ev[0];
-    if (v == INVALID) break;
-    info->packing_nodes++;
-    const uint32_t beg = h_ev[1], cnt = h_ev[2] - h_ev[1];
-    vpos = h_ev[3];
-    seg.resize(cnt); segR.resize(cnt);
-    if (cnt) {
-      uint64_t *kR = c.get_as<uint64_t>("pt_kR", cnt);
-      hipLaunchKernelGGL(k_kid_r, dim3(grid_for(cnt)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->kids, beg, cnt,
-                         (const uint64_t *)R, kR);
-      LAUNCH_CHECK();
-      d2h(c, seg.data(), (const uint32_t *)k->kids + beg, cnt);
-      d2h(c, segR.data(), (const uint64_t *)kR, cnt);
-    }
-    uint64_t cb = 0;
-    d2h(c, &cb, (const uint64_t *)R + v, 1);
-    c.sync();
-    const uint64_t cb0 = cb;
-    // std::sort on the current kid order with the reference comparator (:104-106);
-    // sorting positions with a comparator on their keys is the same sort.
-    order.resize(cnt);
-    for (uint32_t j = 0; j < cnt; ++j) order[j] = j;
-    std::sort(order.begin(), order.end(), [&segR](uint32_t a, uint32_t b) { return segR[a] > segR[b]; });
-    sorted.resize(cnt); scb.resize(cnt);
-    for (uint32_t j = 0; j < cnt; ++j) { sorted[j] = seg[order[j]]; scb[j] = segR[order[j]]; }
-    if (cnt) {
-      h2d(c, k->kids + beg, sorted.data(), cnt);
-      c.sync();   // `sorted` is a pageable host buffer reused by the next event
-    }
-    done.assign(cnt, 0);
-    do {
-      for (uint32_t j = 0; cb > max_component && j < cnt; ++j) {
-        if (scb[j] > max_component) throw Error(SHEEP_ERR_PACK, "forwardPartition: kid exceeds max_component");
-        if (done[j]) continue;
-        for (size_t p = 0; p != part_size.size(); ++p) {
-          if (part_size[p] + scb[j] <= max_component) {
-            cb -= scb[j];
-            part_size[p] += scb[j];
-            done[j] = 1;
-            asg_ids.push_back(sorted[j]);
-            asg_part.push_back((int16_t)p);
-            break;
+      c.sync();
+      v = hdr[0];
+      if (v == INVALID) break;
+      info->packing_nodes++;
+      const uint32_t beg = hdr[1], cnt = hdr[2];
+      vpos = hdr[3];
+      uint64_t cb = (uint64_t)hdr[4] | ((uint64_t)hdr[5] << 32);
+      seg.assign(st_kids, st_kids + std::min(cnt, EV_STAGE));
+      segR.assign(st_r, st_r + std::min(cnt, EV_STAGE));
+      if (cnt > EV_STAGE) {   // a node with more kids than the staging area: fetch the rest
+        seg.resize(cnt); segR.resize(cnt);
+        uint64_t *kR = c.get_as<uint64_t>("pt_kR", cnt);
+        hipLaunchKernelGGL(k_kid_r, dim3(grid_for(cnt)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->kids, beg, cnt,
+                           (const uint64_t *)R, kR);
+        LAUNCH_CHECK();
+        d2h(c, seg.data() + EV_STAGE, (const uint32_t *)k->kids + beg + EV_STAGE, cnt - EV_STAGE);
+        d2h(c, segR.data() + EV_STAGE, (const uint64_t *)kR + EV_STAGE, cnt - EV_STAGE);
+        c.sync();
+      }
+      const uint64_t cb0 = cb;
+      // std::sort on the current kid order with the reference comparator (:104-106);
+      // sorting positions with a comparator on their keys is the same sort.
+      order.resize(cnt);
+      for (uint32_t j = 0; j < cnt; ++j) order[j] = j;
+      std::sort(order.begin(), order.end(), [&segR](uint32_t a, uint32_t b) { return segR[a] > segR[b]; });
+      sorted.resize(cnt); scb.resize(cnt);
+      for (uint32_t j = 0; j < cnt; ++j) {
+        sorted[j] = seg[order[j]];
+        scb[j] = segR[order[j]];
+        if (j != order[j]) { upl_pos.push_back(beg + j); upl_ids.push_back(sorted[j]); }
+      }
+      done.assign(cnt, 0);
+      do {
+        for (uint32_t j = 0; cb > max_component && j < cnt; ++j) {
+          if (scb[j] > max_component) throw Error(SHEEP_ERR_PACK, "forwardPartition: kid exceeds max_component");
+          if (done[j]) continue;
+          for (size_t p = 0; p != part_size.size(); ++p) {
+            if (part_size[p] + scb[j] <= max_component) {
+              cb -= scb[j];
+              part_size[p] += scb[j];
+              done[j] = 1;
+              asg_ids.push_back(sorted[j]);
+              asg_part.push_back((int16_t)p);
+              break;
+            }
           }
         }
-      }
-      if (cb > max_component) {
-        bool any = false;
-        for (uint32_t j = 0; j < cnt; ++j) any |= !done[j];
-        if (!any || part_size.size() >= 32767)
-          throw Error(SHEEP_ERR_PACK, "forwardPartition: node weight exceeds max_component (reference loops forever)");
-        part_size.push_back(0);
-      }
-    } while (cb > max_component);
-    delta = cb0 - cb;
+        if (cb > max_component) {
+          bool any = false;
+          for (uint32_t j = 0; j < cnt; ++j) any |= !done[j];
+          if (!any || part_size.size() >= 32767)
+            throw Error(SHEEP_ERR_PACK, "forwardPartition: node weight exceeds max_component (reference loops forever)");
+          part_size.push_back(0);
+        }
+      } while (cb > max_component);
+      delta = cb0 - cb;
+    }
+  }
+  if (!upl_pos.empty()) {   // persist the sorted kid orders (forwardPartition mutates kids, :104-106)
+    const uint64_t mu = upl_pos.size();
+    uint32_t *dp = c.get_as<uint32_t>("pt_uplpos", mu), *dv = c.get_as<uint32_t>("pt_uplids", mu);
+    h2d(c, dp, upl_pos.data(), mu);
+    h2d(c, dv, upl_ids.data(), mu);
+    hipLaunchKernelGGL(k_scatter_u32, dim3(grid_for(mu)), dim3(BLOCK), 0, c.stream, (const uint32_t *)dp,
+                       (const uint32_t *)dv, mu, k->kids);
+    LAUNCH_CHECK();
+    c.sync();   // the host vectors die with this call
   }
   // roots (ascending) with their final cb
   uint32_t *rids = c.get_as<uint32_t>("pt_roots", n);
