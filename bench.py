@@ -29,8 +29,14 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level table)
 # Leaf regions (one kernel or one fused kernel family per launch); aggregates such as
 # "etree" / "partition" / "sequence" are reported in phases but not rooflined.
-LEAF = ("degree", "degree_heads", "relabel", "pst", "etree_split", "etree_union", "etree_cross", "etree_apply",
-        "etree_compact", "evaluate")
+LEAF = ("degree", "degree_heads", "relabel", "pst", "etree_bucket", "etree_split", "etree_union", "etree_cross",
+        "etree_apply", "etree_compact", "evaluate")
+# kernels of a region, for roofline.traffic from the committed PMC passes (tools/pmc_traffic.py);
+# regions whose kernels are shared with other regions (histograms, packs) get traffic null
+REGION_KERNELS = {"relabel": ["k_relabel"], "degree": ["k_degree"], "etree_split": ["k_split"],
+                  "etree_cross": ["k_cross_find"], "etree_apply": ["k_assign_parents", "k_cross_apply"],
+                  "etree_compact": ["k_compact_edges"], "etree_bucket": ["k_bucket_count", "k_bucket_scatter"]}
+PMC_FILE = os.path.join(ROOT, "profiles", "r1", "pmc_traffic_rmat{scale}.json")
 
 
 def parse():
@@ -140,6 +146,7 @@ def main():
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "alg_bytes_per_launch": int(b_launch), "ms_per_launch": round(ms_launch, 4)}
+        roof.update(pmc_traffic(a, dom, p["launches"] / a.steps))
 
     verified = None
     if a.verify and rank == 0:                                  # merged tree == whole-graph tree
@@ -188,6 +195,23 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def pmc_traffic(a, region, launches_per_step):
+    """roofline.traffic: HBM bytes per launch of the region's kernels from the committed
+    rocprofv3 PMC passes for this workload (FETCH_SIZE and WRITE_SIZE, separate passes);
+    null when there is no profile for it or the kernels are shared between regions."""
+    path = PMC_FILE.format(scale=a.scale)
+    ks = REGION_KERNELS.get(region)
+    if not ks or not os.path.exists(path):
+        return {}
+    prof = json.load(open(path))
+    if prof.get("workload") != f"RMAT-{a.scale} ef{a.ef}, k={a.k}" or any(k not in prof["kernels"] for k in ks):
+        return {}
+    raw = sum(prof["kernels"][k]["traffic_raw"] for k in ks) / launches_per_step
+    cor = sum(prof["kernels"][k]["traffic_stream_corrected"] for k in ks) / launches_per_step
+    return {"traffic": int(raw), "traffic_stream_corrected": int(cor),
+            "traffic_source": os.path.relpath(path, ROOT) + " (FETCH_SIZE + WRITE_SIZE; Infinity-Cache hits included)"}
 
 
 def cpu_baseline(a, ctx):
