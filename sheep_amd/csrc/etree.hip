@@ -144,18 +144,21 @@ __global__ __launch_bounds__(BLOCK) void k_relabel(const sheep_xs1 *__restrict__
 // sizes grids from an upper bound.  A level is a chain of launches with no host round
 // trip; kernels whose list is empty return at once.
 //
-// stats row of level l (u64): [0] length of the edge list entering the level (holes
-// and stale entries included), [1] light edges, [2] cross edges, [3] dead entries at the
-// compaction check, [4] 1 if the level compacted, [5..7] unresolved light edges after
-// hooking round 0..2, [8] list length after the level's appends, [9] which of the two
-// list buffers holds the list during the level (flips after every compaction), [10]
-// edges activated from the level's bucket, [11] of those, light ones (appended to the
-// list), [12] TILE x the split's tile count (sizes its shard regions).
-constexpr int ST_ROW = 16, ST_LIVE = 0, ST_NL = 1, ST_NX = 2, ST_DEAD = 3, ST_COMPACT = 4, ST_HOOK = 5, ST_GROWN = 8,
-              ST_SEL = 9, ST_R0 = 10, ST_NR0L = 11, ST_VT = 12;
+// The level's input is the list (edges active at an earlier level: light ones and
+// contractions) plus the bucket of edges whose first active level this is.  k_split
+// streams both once and writes, in order, three dense lists: the entries that stay
+// (light and right-half edges) into the NEXT list buffer, the light edges, and the cross
+// edges; k_cross_apply appends the contractions after the entries that stayed.  Cross
+// edges are thereby dropped from the list as they are taken, so the list never holds
+// stale or dead entries for long and needs no separate compaction.
+//
+// stats row of level l (u64): [0] list length entering the level, [1] light edges,
+// [2] cross edges, [3] entries that stayed, [5..7] unresolved light edges after hooking
+// round 0..2, [10] edges activated from the level's bucket.
+constexpr int ST_ROW = 16, ST_LIVE = 0, ST_NL = 1, ST_NX = 2, ST_KEPT = 3, ST_HOOK = 5, ST_R0 = 10;
 constexpr int HOOK_ROUNDS = 3;
-// counter sets zeroed at every level: light, cross, hook rounds, compaction
-constexpr int CSET_LIGHT = 0, CSET_CROSS = 1, CSET_HOOK = 2, CSET_COMPACT = CSET_HOOK + HOOK_ROUNDS, NCSET = CSET_COMPACT + 1;
+// counter sets zeroed at every level: hook rounds (sharded appends)
+constexpr int CSET_HOOK = 0, NCSET = CSET_HOOK + HOOK_ROUNDS;
 constexpr uint64_t CSET_WORDS = (uint64_t)NSHARD * SHARD_STRIDE;
 
 // ---- first-activity buckets ---------------------------------------------------------
@@ -219,9 +222,7 @@ __global__ void k_bucket_bounds(const uint32_t *__restrict__ off, uint32_t g, in
 
 __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t *__restrict__ uf, uint32_t *__restrict__ mt,
                                                  uint32_t *__restrict__ top, uint32_t *__restrict__ claim, uint64_t n,
-                                                 unsigned long long *__restrict__ csets, uint64_t *__restrict__ status,
-                                                 uint64_t nstatus, const uint64_t *__restrict__ prev, uint64_t *__restrict__ st,
-                                                 unsigned long long *__restrict__ dead) {
+                                                 unsigned long long *__restrict__ csets) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   const uint64_t t0 = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
   for (uint64_t i = t0; i < n; i += stride) {
@@ -231,13 +232,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t *__restrict__ uf, uint
     claim[i] = INVALID;
   }
   for (uint64_t i = t0; i < NCSET * CSET_WORDS; i += stride) csets[i] = 0;
-  for (uint64_t i = t0; i < nstatus; i += stride) status[i] = 0;
-  const bool compacted = prev && prev[ST_COMPACT];
-  if (t0 == 0) st[ST_SEL] = prev ? prev[ST_SEL] ^ (uint64_t)compacted : 0;
-  if (compacted && t0 < NSHARD) dead[t0 * SHARD_STRIDE] = 0;   // dead entries are counted since the last compaction
 }
-
-__global__ void k_set_u64(uint64_t *p, uint64_t v) { *p = v; }
 
 // top[root] = the component's largest id.  Every vertex of a non-singleton light
 // component is an endpoint of a light edge and its maximum is the hi end of one, so a
@@ -273,62 +268,6 @@ __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict_
       const uint32_t v = wave_max(same ? b[k] : 0u);
       if ((int)__lane_id() == first && v > top[r0]) atomicMax(&top[r0], v);
       if (live[k] && !same && b[k] > top[r[k]]) atomicMax(&top[r[k]], b[k]);
-    }
-  }
-}
-
-// One streaming pass classifies the edge list of a level plus the bucket of edges it
-// activates: light (both ends in the left half of their subproblem) -> the light
-// shards; cross -> the cross shards.  Edges inside a right half are left alone; stale
-// entries (cross edges of an earlier level, whose ends now lie in different
-// subproblems: (ya ^ yb) >> s >= 2) are skipped.  Light edges of the bucket join the
-// list (staged in r0l, appended by k_cross_apply).  The dense lists keep every lane of
-// the union / find kernels busy and are read sequentially.
-__global__ __launch_bounds__(BLOCK) void k_split(const uint64_t *__restrict__ buf0, const uint64_t *__restrict__ buf1,
-                                                 const uint64_t *__restrict__ n_live, uint64_t *__restrict__ st, int s,
-                                                 uint32_t clo, const uint64_t *__restrict__ r0,
-                                                 const uint64_t *__restrict__ seg, int L,
-                                                 uint64_t *__restrict__ lbuf, uint64_t *__restrict__ xbuf,
-                                                 unsigned long long *__restrict__ lcnt,
-                                                 unsigned long long *__restrict__ xcnt, uint64_t *__restrict__ r0l) {
-  const uint64_t len = *n_live;
-  const uint64_t *list = st[ST_SEL] ? buf1 : buf0;
-  const uint64_t rb = seg[s], rn = seg[L + s] - rb;
-  const uint64_t td = (len + TILE - 1) / TILE, ntiles = td + (rn + TILE - 1) / TILE;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st[ST_LIVE] = len;
-    st[ST_R0] = rn;
-    st[ST_VT] = ntiles * TILE;
-  }
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const bool act = tile >= td;   // a tile of the activated bucket (uniform per workgroup)
-    const uint64_t *src = act ? r0 + rb + (tile - td) * TILE : list + tile * TILE;
-    const uint64_t lim = act ? rn - (tile - td) * TILE : len - tile * TILE;
-    uint64_t ev[TILE_ITEMS];
-    uint32_t fl = 0, fx = 0;
-#pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) {
-      const uint64_t i = (uint64_t)j * BLOCK + threadIdx.x;
-      ev[j] = i < lim ? src[i] : DEAD;
-    }
-#pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) {
-      if (ev[j] == DEAD) continue;
-      const uint32_t ya = spread((uint32_t)ev[j], clo), yb = spread((uint32_t)(ev[j] >> 32), clo);
-      const uint32_t d = (ya ^ yb) >> s;
-      if (d == 0 && ((yb >> s) & 1) == 0) fl |= 1u << j;
-      else if (d == 1) fx |= 1u << j;
-    }
-    uint64_t sl = shard_reserve((uint32_t)__popc(fl), lcnt, tile, ntiles, 1);
-    uint64_t sx = shard_reserve((uint32_t)__popc(fx), xcnt, tile, ntiles, 1);
-    uint64_t sr = act ? block_reserve((uint32_t)__popc(fl), (unsigned long long *)(st + ST_NR0L)) : 0;
-#pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) {
-      if (fl & (1u << j)) {
-        lbuf[sl++] = ev[j];
-        if (act) r0l[sr++] = ev[j];
-      }
-      if (fx & (1u << j)) xbuf[sx++] = ev[j];
     }
   }
 }
@@ -445,27 +384,14 @@ __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict
 // edges into one hub, all carry the same m.)  claim is n x u32, L3-resident, unlike a
 // global hash table of the pairs.
 //
-// The contracted edges are APPENDED: cross edge j goes to edges[len + j] (DEAD if it
-// died), a sequential write; its old entry is left as it is — stale from the next level
-// on (see k_split) — instead of being rewritten in place, which cost a scattered
-// partial-line write per cross edge.  Every processed edge leaves one dead entry behind
-// (two if it died), counted for the compaction check.
+// The contracted edges are APPENDED to the next list, after the entries k_split kept:
+// cross edge j goes to next[kept + j] (DEAD if it died) — a sequential write.
 __global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restrict__ xbuf, const uint32_t *__restrict__ xtop,
                                                        const uint64_t *__restrict__ st, const uint32_t *__restrict__ mt,
-                                                       uint32_t *__restrict__ claim, uint64_t *__restrict__ buf0,
-                                                       uint64_t *__restrict__ buf1, const uint64_t *__restrict__ r0l,
-                                                       uint64_t cap, unsigned long long *__restrict__ dead,
-                                                       unsigned long long *__restrict__ err) {
-  const uint64_t nx = st[ST_NX], len = st[ST_LIVE], nr = st[ST_NR0L];
-  if (len + nx + nr > cap) {   // cannot happen (the list stays below 7/3 m); fail loudly
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(err, 1ull);
-    return;
-  }
-  uint64_t *out = (st[ST_SEL] ? buf1 : buf0) + len;
+                                                       uint32_t *__restrict__ claim, uint64_t *__restrict__ next) {
+  const uint64_t nx = st[ST_NX];
+  uint64_t *out = next + st[ST_KEPT];
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < nr; j += stride) out[nx + j] = r0l[j];
-  if ((uint64_t)blockIdx.x * BLOCK >= nx) return;
-  uint32_t ndead = 0;
   for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < nx; j += stride) {
     const uint32_t m = mt[xtop[j]];
     const uint32_t b = (uint32_t)(xbuf[j] >> 32);
@@ -476,126 +402,161 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restric
       kill = c == m;   // someone else's (m, b) is kept (our own successful CAS returned INVALID)
     }
     out[j] = kill ? DEAD : ((uint64_t)b << 32) | m;
-    ndead += 1 + kill;
-  }
-  // one add per workgroup, spread over the shard counters (a single hot counter
-  // serialises ~1e5 adds per millisecond)
-  __shared__ uint32_t s_dead[BLOCK / WAVE];
-  ndead = wave_sum(ndead);
-  if ((threadIdx.x & 63) == 0) s_dead[threadIdx.x >> 6] = ndead;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t t = s_dead[0] + s_dead[1] + s_dead[2] + s_dead[3];
-    if (t) atomicAdd(dead + (uint64_t)(blockIdx.x % NSHARD) * SHARD_STRIDE, (unsigned long long)t);
   }
 }
 
-// Compaction, decided on the device: once a quarter of the list is dead (counted since
-// the last compaction) the entries still alive at the next level — not DEAD, both ends
-// in one half: (ya ^ yb) >> s == 0 — are copied, in order, into the other list buffer
-// (the next level reads from there); otherwise the list just keeps its appended tail.
-//
-// One pass, 16 B per entry: workgroups take 16K-entry chunks in ticket order, count the
-// kept entries (values stay in registers), and get the chunk's output offset by
-// decoupled look-back over the chunk status words (aggregate / inclusive prefix).  Ticket
-// order means every predecessor chunk is owned by a running workgroup, so the wait ends.
-constexpr int C_ROWS = 64;                                    // 64-entry rows per wave
-constexpr uint64_t C_CHUNK = (uint64_t)WAVE * C_ROWS * (BLOCK / WAVE);   // 16384 entries
-constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 1ull << 63, LB_VAL = LB_AGG - 1;
+// ---- the level's split: three dense outputs --------------------------------------
+// Count pass (per 2048-entry tile: entries that stay, light, cross), one-workgroup scan
+// of the tile counts, write pass (each tile re-read and written at its offsets).  Two
+// reads per entry, but every pass streams at full occupancy; an ordered single pass
+// (decoupled look-back) serialised on the chunk chain.
 
-__device__ __forceinline__ bool entry_kept(uint64_t e, int s, uint32_t clo) {
-  return e != DEAD && ((spread((uint32_t)e, clo) ^ spread((uint32_t)(e >> 32), clo)) >> s) == 0;
+// Classes of an entry at level s (ya, yb = spread positions of lo, hi):
+//   cross  (ya ^ yb) >> s == 1          -> the cross list (contracted by k_cross_apply)
+//   light  same half, bit s of yb == 0  -> the light list, and it stays in the list
+//   right  same half, bit s of yb == 1  -> stays in the list
+// DEAD entries (contractions that died) are dropped.
+__device__ __forceinline__ uint32_t classify(uint64_t e, int s, uint32_t clo) {
+  if (e == DEAD) return 0;
+  const uint32_t ya = spread((uint32_t)e, clo), yb = spread((uint32_t)(e >> 32), clo);
+  const uint32_t d = (ya ^ yb) >> s;
+  if (d == 1) return 4;                          // cross
+  return ((yb >> s) & 1) == 0 ? 3 : 1;           // light (bit 1: light, bit 0: stays) / right
 }
 
-// Called by one whole wave: publishes the chunk's aggregate, then sums predecessors 64
-// status words per step (one round trip per 64 chunks, not per chunk) back to the first
-// inclusive prefix; returns the exclusive prefix and publishes the inclusive one.
-__device__ uint64_t chunk_lookback(uint64_t *status, uint64_t chunk, uint64_t total) {
-  const int lane = threadIdx.x & 63;
-  if (chunk == 0) {
-    if (lane == 0) __hip_atomic_store(&status[0], LB_INC | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    return 0;
+// The level's virtual input: the list (prev level's kept entries + contraction slots),
+// then the bucket of edges first active at this level.
+struct SplitIn {
+  const uint64_t *list, *r0;
+  uint64_t len, rb, m;
+  __device__ SplitIn(const uint64_t *l, const uint64_t *prev, const uint64_t *r, const uint64_t *seg, int s, int L)
+      : list(l), r0(r) {
+    len = prev ? prev[ST_KEPT] + prev[ST_NX] : 0;
+    rb = seg[s];
+    m = len + (seg[L + s] - rb);
   }
-  if (lane == 0) __hip_atomic_store(&status[chunk], LB_AGG | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  uint64_t acc = 0;
-  int64_t base = (int64_t)chunk - 1;
-  for (;;) {
-    const int64_t j = base - lane;
-    const uint64_t v = j >= 0 ? __hip_atomic_load(&status[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : LB_INC;
-    const uint64_t incm = __ballot((v & LB_INC) != 0);
-    const int first = incm ? __ffsll((unsigned long long)incm) - 1 : 63;
-    const uint64_t need = first == 63 ? ~0ull : ((2ull << first) - 1);
-    if ((__ballot((v & ~LB_VAL) != 0) & need) != need) continue;   // a predecessor has not counted yet
-    acc += wave_sum(lane <= first ? (v & LB_VAL) : 0ull);
-    if (incm) break;
-    base -= WAVE;
+  __device__ __forceinline__ uint64_t operator[](uint64_t i) const {
+    return i < len ? list[i] : i < m ? r0[rb + (i - len)] : DEAD;
   }
-  if (lane == 0) __hip_atomic_store(&status[chunk], LB_INC | (acc + total), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  return acc;
+};
+
+// the three class bits as three 16-bit counters
+__device__ __forceinline__ uint64_t pack3(uint32_t c) {
+  return (uint64_t)(c & 1) | ((uint64_t)((c >> 1) & 1) << 16) | ((uint64_t)(c >> 2) << 32);
 }
 
-__global__ __launch_bounds__(BLOCK) void k_compact_edges(uint64_t *__restrict__ buf0, uint64_t *__restrict__ buf1,
-                                                         uint64_t *__restrict__ st, uint64_t *__restrict__ d_len, int s,
-                                                         uint32_t clo, const unsigned long long *__restrict__ dead,
-                                                         uint64_t *__restrict__ status,
-                                                         unsigned long long *__restrict__ ticket) {
-  const uint64_t m = st[ST_LIVE] + st[ST_NX] + st[ST_NR0L];
-  __shared__ uint64_t s_dead, s_chunk, s_base;
-  __shared__ uint32_t s_w[BLOCK / WAVE];
-  if (threadIdx.x < WAVE) {
-    const uint64_t d = wave_sum((uint64_t)(threadIdx.x < NSHARD ? dead[(uint64_t)threadIdx.x * SHARD_STRIDE] : 0));
-    if (threadIdx.x == 0) s_dead = d;
-  }
-  __syncthreads();
-  const uint64_t nd = s_dead;
-  const bool go = nd && nd * 4 >= m;
+__global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
+                                                       uint64_t *__restrict__ st, int s, uint32_t clo,
+                                                       const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
+                                                       int L, uint32_t *__restrict__ cnt, uint64_t cstride) {
+  const SplitIn in(list, prev, r0, seg, s, L);
+  const uint64_t ntiles = (in.m + TILE - 1) / TILE;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st[ST_DEAD] = nd;
-    st[ST_COMPACT] = go;
-    st[ST_GROWN] = m;
-    if (!go) *d_len = m;
+    st[ST_LIVE] = in.len;
+    st[ST_R0] = in.m - in.len;
   }
-  if (!go) return;
-  const uint64_t *in = st[ST_SEL] ? buf1 : buf0;
-  uint64_t *out = st[ST_SEL] ? buf0 : buf1;
-  const uint64_t nchunks = (m + C_CHUNK - 1) / C_CHUNK;
+  __shared__ uint64_t s_w[BLOCK / WAVE];
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    uint64_t ev[TILE_ITEMS];
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) ev[j] = in[tile * TILE + (uint64_t)j * BLOCK + threadIdx.x];
+    uint64_t c3 = 0;
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) c3 += pack3(classify(ev[j], s, clo));
+    c3 = wave_sum(c3);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c3;
+    __syncthreads();
+    if (threadIdx.x < 3) {
+      uint64_t t = 0;
+      for (int w = 0; w < BLOCK / WAVE; ++w) t += s_w[w];
+      cnt[threadIdx.x * cstride + tile] = (uint32_t)((t >> (16 * threadIdx.x)) & 0xFFFF);
+    }
+    __syncthreads();
+  }
+}
+
+// One workgroup: exclusive scans of the three tile-count rows in place; totals -> st.
+constexpr int SCAN_B = 1024;
+__global__ __launch_bounds__(SCAN_B) void k_split_scan(const uint64_t *__restrict__ prev, const uint64_t *__restrict__ seg,
+                                                       int s, int L, uint64_t *__restrict__ st, uint32_t *__restrict__ cnt,
+                                                       uint64_t cstride) {
+  const uint64_t len = prev ? prev[ST_KEPT] + prev[ST_NX] : 0;
+  const uint64_t ntiles = (len + seg[L + s] - seg[s] + TILE - 1) / TILE;
+  __shared__ uint32_t s_w[SCAN_B / WAVE];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (;;) {
-    if (threadIdx.x == 0) s_chunk = atomicAdd(ticket, 1ull);
-    __syncthreads();
-    const uint64_t chunk = s_chunk;
-    if (chunk >= nchunks) break;
-    const uint64_t wbase = chunk * C_CHUNK + (uint64_t)wave * WAVE * C_ROWS + lane;
-    uint64_t v[C_ROWS];
-    uint32_t cnt = 0;
+  const uint64_t per = (ntiles + SCAN_B - 1) / SCAN_B, b0 = threadIdx.x * per;
+  for (int row = 0; row < 3; ++row) {
+    uint32_t *a = cnt + row * cstride;
+    uint32_t sum = 0;
+    for (uint64_t i = b0; i < b0 + per && i < ntiles; ++i) sum += a[i];
+    uint32_t inc = sum;
 #pragma unroll
-    for (int r = 0; r < C_ROWS; ++r) {
-      const uint64_t i = wbase + (uint64_t)r * WAVE;
-      v[r] = i < m ? in[i] : DEAD;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
     }
-#pragma unroll
-    for (int r = 0; r < C_ROWS; ++r) cnt += (uint32_t)__popcll(__ballot(entry_kept(v[r], s, clo)));
-    if (lane == 0) s_w[wave] = cnt;
+    if (lane == 63) s_w[wave] = inc;
     __syncthreads();
-    if (wave == 0) {
-      const uint64_t total = (uint64_t)s_w[0] + s_w[1] + s_w[2] + s_w[3];
-      const uint64_t excl = chunk_lookback(status, chunk, total);
-      if (lane == 0) {
-        s_base = excl;
-        if (chunk == nchunks - 1) *d_len = excl + total;
-      }
+    uint32_t off = 0, tot = 0;
+    for (int w = 0; w < SCAN_B / WAVE; ++w) {
+      const uint32_t x = s_w[w];
+      if (w < wave) off += x;
+      tot += x;
     }
+    uint32_t run = off + inc - sum;
+    for (uint64_t i = b0; i < b0 + per && i < ntiles; ++i) {
+      const uint32_t x = a[i];
+      a[i] = run;
+      run += x;
+    }
+    if (threadIdx.x == 0) st[row == 0 ? ST_KEPT : row == 1 ? ST_NL : ST_NX] = tot;
     __syncthreads();
-    uint64_t pos = s_base;
-    for (int w = 0; w < wave; ++w) pos += s_w[w];
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
+                                                       int s, uint32_t clo, const uint64_t *__restrict__ r0,
+                                                       const uint64_t *__restrict__ seg, int L,
+                                                       const uint32_t *__restrict__ cnt, uint64_t cstride,
+                                                       uint64_t *__restrict__ next, uint64_t *__restrict__ lbuf,
+                                                       uint64_t *__restrict__ xbuf) {
+  const SplitIn in(list, prev, r0, seg, s, L);
+  const uint64_t ntiles = (in.m + TILE - 1) / TILE;
+  __shared__ uint64_t s_w[BLOCK / WAVE];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    uint64_t ev[TILE_ITEMS];
+    uint32_t cl[TILE_ITEMS];
+    uint64_t c3 = 0;
 #pragma unroll
-    for (int r = 0; r < C_ROWS; ++r) {
-      const bool k = entry_kept(v[r], s, clo);
-      const uint64_t mask = __ballot(k);
-      if (k) out[pos + __popcll(mask & lanemask_lt())] = v[r];
-      pos += __popcll(mask);
+    for (int j = 0; j < TILE_ITEMS; ++j) ev[j] = in[tile * TILE + (uint64_t)j * BLOCK + threadIdx.x];
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      cl[j] = classify(ev[j], s, clo);
+      c3 += pack3(cl[j]);
     }
-    __syncthreads();   // s_chunk / s_w / s_base are rewritten for the next chunk
+    // thread-major ranks inside the tile: exclusive scan of the packed counters
+    uint64_t inc = c3;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    uint64_t off = 0;
+    for (int w = 0; w < wave; ++w) off += s_w[w];
+    const uint64_t ex = off + inc - c3;
+    uint64_t pk = cnt[tile] + (ex & 0xFFFF);
+    uint64_t pl = cnt[cstride + tile] + ((ex >> 16) & 0xFFFF);
+    uint64_t px = cnt[2 * cstride + tile] + (ex >> 32);
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      if (cl[j] & 1) next[pk++] = ev[j];
+      if (cl[j] & 2) lbuf[pl++] = ev[j];
+      if (cl[j] & 4) xbuf[px++] = ev[j];
+    }
+    __syncthreads();   // s_w is rewritten by the next tile
   }
 }
 
@@ -638,15 +599,14 @@ void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
 
 static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
 
-// The edge list grows by its cross edges each level and is compacted once a quarter is
-// dead; between compactions it stays below 4/3 of the surviving edges (<= m), plus one
-// level's appends (<= m): 7/3 m.
-static uint64_t edge_capacity(uint64_t m) { return m * 7 / 3 + 2 * TILE; }
+// A level's next list holds the entries that stayed (alive, <= m) plus one contraction
+// slot per cross edge (<= m).
+static uint64_t list_capacity(uint64_t m) { return 2 * m + TILE; }
 
 // Elimination tree of `m` edges ((hi<<32)|lo, lo < hi < n, DEAD holes allowed).  `edges`
 // is consumed.  by_lo: the edges are ordered by lo (a merge's parent edges), so the
 // first-activity buckets are ranges of it; otherwise they are bucketed by one counting
-// pass and `edges` (which must then hold edge_capacity(m) entries) becomes a list buffer.
+// pass.
 // One pass of launches per level, no host synchronisation inside the loop (see the
 // stats row above); the stats come back once at the end for the timers / debug log.
 void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, bool by_lo) {
@@ -666,12 +626,11 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
   uint32_t *claim = c.get_as<uint32_t>("et_claim", n);
   // every list is bounded by m; scratch regions of sharded appends need whole tiles
   const uint64_t mcap = (m + TILE - 1) / TILE * TILE;
-  const uint64_t ecap = edge_capacity(m);
+  const uint64_t lcap = list_capacity(m);
   uint32_t *xtop = c.get_as<uint32_t>("et_xtop", mcap);
   uint64_t *xbuf = c.get_as<uint64_t>("et_cross", mcap);
-  // the two list buffers (compaction flips between them) and the bucketed input r0
-  uint64_t *list0 = by_lo ? c.get_as<uint64_t>("et_list1", ecap) : edges;
-  uint64_t *other = c.get_as<uint64_t>("et_list2", ecap);
+  // the two list buffers (level l reads one and writes the other) and the bucketed input r0
+  uint64_t *lists[2] = {c.get_as<uint64_t>("et_list1", lcap), c.get_as<uint64_t>("et_list2", lcap)};
   uint64_t *r0 = by_lo ? edges : c.get_as<uint64_t>("et_r0", m);
   uint64_t *seg = c.get_as<uint64_t>("et_seg", 2 * (uint64_t)L);
   const uint32_t mask = (uint32_t)((1ull << L) - 1);
@@ -707,40 +666,36 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
     hipLaunchKernelGGL(k_bucket_bounds, dim3(1), dim3(64), 0, c.stream, (const uint32_t *)bc, g, L, seg);
     LAUNCH_CHECK();
   }
-  uint64_t *r0l = c.get_as<uint64_t>("et_r0l", mcap);   // light edges of a level's bucket, staged
-  // split's shard regions follow ITS tiles: the list (up to ecap) plus a bucket (up to m)
-  const uint64_t lcap = (ecap + m + 2 * TILE) / TILE * TILE;
-  uint64_t *alt = c.get_as<uint64_t>("et_alt", lcap);     // shard scratch: light list, hooking
-  uint64_t *xscr = c.get_as<uint64_t>("et_xscr", lcap);   // shard scratch: cross list, then a hook list
-  const uint64_t nstatus = (ecap + C_CHUNK - 1) / C_CHUNK + 1;
-  uint64_t *status = c.get_as<uint64_t>("et_lookback", nstatus);
+  // a split reads at most the list plus a bucket: (lcap + m) entries, in TILE tiles
+  const uint64_t cstride = (lcap + m + TILE - 1) / TILE + 1;
+  uint32_t *tcnt = c.get_as<uint32_t>("et_tilecnt", 3 * cstride);
   uint64_t *lbuf = c.get_as<uint64_t>("et_light", mcap);  // must outlive the hook rounds (k_light_top)
-  uint64_t *hk[2] = {xscr, c.get_as<uint64_t>("et_lwb", mcap)};
-  unsigned long long *err = (unsigned long long *)c.d_scalars + 14;
-  HIP_CHECK(hipMemsetAsync(err, 0, sizeof(uint64_t), c.stream));
+  uint64_t *alt = c.get_as<uint64_t>("et_alt", mcap);     // shard scratch of the hook rounds
+  uint64_t *hk[2] = {c.get_as<uint64_t>("et_lwa", mcap), c.get_as<uint64_t>("et_lwb", mcap)};
   unsigned long long *csets = c.get_as<unsigned long long>("et_csets", NCSET * CSET_WORDS);
-  unsigned long long *dcnt = shard_counters(c, "dead");
-  uint64_t *stats = c.get_as<uint64_t>("et_stats", (uint64_t)(L + 1) * ST_ROW);
-  uint64_t *d_live = stats + (uint64_t)L * ST_ROW;
+  uint64_t *stats = c.get_as<uint64_t>("et_stats", (uint64_t)L * ST_ROW);
   HIP_CHECK(hipMemsetAsync(stats, 0, (uint64_t)L * ST_ROW * sizeof(uint64_t), c.stream));
-  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, c.stream, d_live, 0);   // the list starts empty
-  LAUNCH_CHECK();
   auto cset = [&](int k) { return csets + (uint64_t)k * CSET_WORDS; };
-  const unsigned gt = grid_tiles(ecap + m), gf = grid_for(m, BLOCK * XK), gn = grid_for(n);
+  const unsigned gt = grid_tiles(m), gt2 = grid_tiles(lcap + m), gf = grid_for(m, BLOCK * XK), gn = grid_for(n);
   for (int lvl = 0; lvl < L; ++lvl) {
     const int s = L - 1 - lvl;
     uint64_t *st = stats + (uint64_t)lvl * ST_ROW;
-    hipLaunchKernelGGL(k_reset, dim3(gn), dim3(BLOCK), 0, c.stream, uf, mt, top, claim, n, csets, status, nstatus,
-                       (const uint64_t *)(lvl ? st - ST_ROW : nullptr), st, dcnt);
+    const uint64_t *prev = lvl ? st - ST_ROW : nullptr;
+    uint64_t *cur = lists[lvl & 1], *next = lists[(lvl + 1) & 1];
+    hipLaunchKernelGGL(k_reset, dim3(gn), dim3(BLOCK), 0, c.stream, uf, mt, top, claim, n, csets);
     LAUNCH_CHECK();
     {
       TimedRegion tr(c, "etree_split");
-      hipLaunchKernelGGL(k_split, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)list0, (const uint64_t *)other,
-                         (const uint64_t *)d_live, st, s, clo, (const uint64_t *)r0, (const uint64_t *)seg, L, alt, xscr,
-                         cset(CSET_LIGHT), cset(CSET_CROSS), r0l);
+      hipLaunchKernelGGL(k_split_count, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo,
+                         (const uint64_t *)r0, (const uint64_t *)seg, L, tcnt, cstride);
       LAUNCH_CHECK();
-      pack_shards<uint64_t>(c, alt, lbuf, st + ST_VT, cset(CSET_LIGHT), st + ST_NL);
-      pack_shards<uint64_t>(c, xscr, xbuf, st + ST_VT, cset(CSET_CROSS), st + ST_NX);
+      hipLaunchKernelGGL(k_split_scan, dim3(1), dim3(SCAN_B), 0, c.stream, prev, (const uint64_t *)seg, s, L, st, tcnt,
+                         cstride);
+      LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_split_write, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, s, clo,
+                         (const uint64_t *)r0, (const uint64_t *)seg, L, (const uint32_t *)tcnt, cstride, next, lbuf,
+                         xbuf);
+      LAUNCH_CHECK();
     }
     {
       TimedRegion tr(c, "etree_union");
@@ -771,41 +726,30 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
                          (const uint32_t *)mt, (const uint32_t *)top, n, parent);
       LAUNCH_CHECK();
       hipLaunchKernelGGL(k_cross_apply, dim3(grid_for(m)), dim3(BLOCK), 0, c.stream, (const uint64_t *)xbuf,
-                         (const uint32_t *)xtop, (const uint64_t *)st, (const uint32_t *)mt, claim, list0, other,
-                         (const uint64_t *)r0l, ecap, dcnt, err);
-      LAUNCH_CHECK();
-    }
-    {
-      TimedRegion tr(c, "etree_compact");
-      hipLaunchKernelGGL(k_compact_edges, dim3(grid_for(ecap, (unsigned)C_CHUNK, 256 * 4)), dim3(BLOCK), 0, c.stream,
-                         list0, other, st, d_live, s, clo, (const unsigned long long *)dcnt, status, cset(CSET_COMPACT));
+                         (const uint32_t *)xtop, (const uint64_t *)st, (const uint32_t *)mt, claim, next);
       LAUNCH_CHECK();
     }
   }
-  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 14, err, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-  c.sync();
-  if (c.h_scalars[14]) throw Error(SHEEP_ERR_HIP, "etree: edge list capacity exceeded");
   if (!c.timing && !g_debug_etree) return;
-  std::vector<uint64_t> h((uint64_t)(L + 1) * ST_ROW);
+  std::vector<uint64_t> h((uint64_t)L * ST_ROW);
   HIP_CHECK(hipMemcpyAsync(h.data(), stats, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
   for (int lvl = 0; lvl < L; ++lvl) {
     const uint64_t *r = &h[(uint64_t)lvl * ST_ROW];
     uint64_t hooked = r[ST_NL];
     for (int k = 0; k < HOOK_ROUNDS - 1; ++k) hooked += r[ST_HOOK + k];
-    // algorithmic bytes: split reads every list entry; hooking reads each
-    // light edge once per round it takes part in; the cross pass reads the edge and
-    // writes its top; apply reads edge, top, m and claim and appends the contraction
-    c.add_bytes("etree_split", 8 * (r[ST_LIVE] + r[ST_R0]));
+    // algorithmic bytes: split reads the list and the bucket and writes the
+    // three lists; hooking reads each light edge once per round it takes part in; the
+    // cross pass reads the edge and writes its top; apply reads edge, top, m and claim
+    // and appends the contraction
+    c.add_bytes("etree_split", 8 * (r[ST_LIVE] + r[ST_R0]) + 8 * (r[ST_KEPT] + r[ST_NL] + r[ST_NX]));
     c.add_bytes("etree_union", 8 * hooked + 8 * r[ST_NL]);
     c.add_bytes("etree_cross", 12 * r[ST_NX]);
     c.add_bytes("etree_apply", 20 * r[ST_NX]);
-    c.add_bytes("etree_compact", r[ST_COMPACT] ? 8 * r[ST_GROWN] + 8 * (r[ST_GROWN] - r[ST_DEAD]) : 0);
     if (g_debug_etree)
-      fprintf(stderr, "etree lvl %d s %d list %lu bucket %lu light %lu cross %lu dead %lu compact %lu hook-left %lu %lu %lu\n",
-              lvl, L - 1 - lvl, (unsigned long)r[ST_LIVE], (unsigned long)r[ST_R0], (unsigned long)r[ST_NL],
-              (unsigned long)r[ST_NX],
-              (unsigned long)r[ST_DEAD], (unsigned long)r[ST_COMPACT], (unsigned long)r[ST_HOOK],
+      fprintf(stderr, "etree lvl %d s %d list %lu bucket %lu kept %lu light %lu cross %lu hook-left %lu %lu %lu\n", lvl,
+              L - 1 - lvl, (unsigned long)r[ST_LIVE], (unsigned long)r[ST_R0], (unsigned long)r[ST_KEPT],
+              (unsigned long)r[ST_NL], (unsigned long)r[ST_NX], (unsigned long)r[ST_HOOK],
               (unsigned long)r[ST_HOOK + 1], (unsigned long)r[ST_HOOK + 2]);
   }
 }
@@ -815,7 +759,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   uint32_t *pst = c.get_as<uint32_t>("bt_pst", n ? n : 1);
   uint32_t *parent = c.get_as<uint32_t>("bt_parent", n ? n : 1);
   HIP_CHECK(hipMemsetAsync(pst, 0, n * sizeof(uint32_t), c.stream));
-  uint64_t *edges = c.get_as<uint64_t>("bt_edges", edge_capacity(nrec ? nrec : 1));
+  uint64_t *edges = c.get_as<uint64_t>("bt_edges", nrec ? nrec : 1);
   unsigned long long *d = (unsigned long long *)c.d_scalars + 8;
   HIP_CHECK(hipMemsetAsync(d + 1, 0, sizeof(uint64_t), c.stream));
   if (nrec) {

@@ -197,40 +197,45 @@ __global__ void k_parts_to_vid(const uint32_t *__restrict__ seq, uint64_t n, con
 __global__ __launch_bounds__(BLOCK) void k_pack_event(const uint32_t *__restrict__ hids, uint64_t nh,
                                                       const uint32_t *__restrict__ hst, const uint32_t *__restrict__ hen,
                                                       uint64_t *__restrict__ R, uint32_t v, uint32_t vpos,
-                                                      uint64_t delta, uint64_t maxc, uint32_t *__restrict__ next) {
+                                                      uint64_t delta, uint64_t maxc, const uint64_t *__restrict__ prev,
+                                                      unsigned long long *__restrict__ next) {
+  // hids ascends and nodes below the last packing node v are final: start at v's index
+  const uint64_t start = *prev == ~0ull ? 0 : (uint32_t)*prev;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  const uint64_t iters = (nh + stride - 1) / stride;
-  uint64_t h = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  uint32_t best = INVALID;
-  for (uint64_t it = 0; it < iters; ++it, h += stride) {
-    if (h >= nh) continue;
+  uint64_t best = ~0ull;   // (id << 32) | index of the next packing node
+  for (uint64_t h = start + (uint64_t)blockIdx.x * BLOCK + threadIdx.x; h < nh; h += stride) {
     const uint32_t a = hids[h];
-    if (v != INVALID && a < v) continue;      // final: below the last packing node
     uint64_t r = R[a];
     if (delta && (a == v || (vpos != INVALID && hst[h] <= vpos && vpos <= hen[h]))) {
       r -= delta;
       R[a] = r;
     }
-    if (r > maxc && (v == INVALID || a > v) && a < best) best = a;
+    if (r > maxc && (v == INVALID || a > v)) {
+      const uint64_t key = ((uint64_t)a << 32) | h;
+      best = key < best ? key : best;
+    }
   }
   best = wave_min(best);
-  if ((threadIdx.x & 63) == 0 && best != INVALID) atomicMin(next, best);
+  if ((threadIdx.x & 63) == 0 && best != ~0ull) atomicMin(next, (unsigned long long)best);
 }
 
 // Everything the host needs for one packing event, stored straight into mapped host
 // memory: hdr = {v, koff[v], #kids, tD(v) (INVALID for a root), R[v] lo, R[v] hi}, then
 // the node's kids in their current order and their R (the first `cap` of them).
 constexpr uint32_t EV_STAGE = 1u << 16;
-__global__ __launch_bounds__(BLOCK) void k_event_stage(const uint32_t *__restrict__ ev, const uint32_t *__restrict__ koff,
+__global__ __launch_bounds__(BLOCK) void k_event_stage(const uint64_t *__restrict__ ev, uint64_t *__restrict__ prev,
+                                                       const uint32_t *__restrict__ koff,
                                                        const uint32_t *__restrict__ parent, const uint32_t *__restrict__ tD,
                                                        const uint32_t *__restrict__ kids, const uint64_t *__restrict__ R,
                                                        uint32_t *__restrict__ hdr, uint32_t *__restrict__ kid_out,
                                                        uint64_t *__restrict__ r_out, uint32_t cap) {
-  const uint32_t v = ev[0];
+  const uint64_t e = *ev;
+  const uint32_t v = e == ~0ull ? INVALID : (uint32_t)(e >> 32);
   if (v == INVALID) {
     if (blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = INVALID;
     return;
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *prev = e;
   const uint32_t beg = koff[v], cnt = koff[v + 1] - beg;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     const uint64_t r = R[v];
@@ -432,8 +437,11 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
                        (const uint32_t *)rst, (const uint32_t *)ren, t.tD, t.tU, hst, hen);
     LAUNCH_CHECK();
   }
-  // ev[0] = next packing node (INVALID: none); one stream sync per event
-  uint32_t *ev = (uint32_t *)(c.d_scalars + 44);
+  // ev = (next packing node << 32) | its index in hids (~0: none); evprev = the last one.
+  // One stream sync per event.
+  unsigned long long *ev = (unsigned long long *)(c.d_scalars + 44);
+  uint64_t *evprev = c.d_scalars + 46;
+  HIP_CHECK(hipMemsetAsync(evprev, 0xFF, sizeof(uint64_t), c.stream));
   uint8_t *stage = (uint8_t *)c.get_pinned("pt_event", 64 + (size_t)EV_STAGE * 12);
   uint32_t *hdr = (uint32_t *)stage, *st_kids = (uint32_t *)(stage + 64);
   uint64_t *st_r = (uint64_t *)(stage + 64 + (size_t)EV_STAGE * 4);
@@ -453,13 +461,15 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   {
     TimedRegion tr(c, "partition_events");
     for (;;) {
-      HIP_CHECK(hipMemsetAsync(ev, 0xFF, sizeof(uint32_t), c.stream));
+      HIP_CHECK(hipMemsetAsync(ev, 0xFF, sizeof(uint64_t), c.stream));
       if (nh) {
         hipLaunchKernelGGL(k_pack_event, dim3(grid_for(nh)), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh,
-                           (const uint32_t *)hst, (const uint32_t *)hen, R, v, vpos, delta, max_component, ev);
+                           (const uint32_t *)hst, (const uint32_t *)hen, R, v, vpos, delta, max_component,
+                           (const uint64_t *)evprev, ev);
         LAUNCH_CHECK();
       }
-      hipLaunchKernelGGL(k_event_stage, dim3(64), dim3(BLOCK), 0, c.stream, (const uint32_t *)ev, k->koff, k->parent,
+      hipLaunchKernelGGL(k_event_stage, dim3(64), dim3(BLOCK), 0, c.stream, (const uint64_t *)ev, evprev, k->koff,
+                         k->parent,
                          t.tD, (const uint32_t *)k->kids, (const uint64_t *)R, d_hdr, d_kids, d_r, EV_STAGE);
       LAUNCH_CHECK();
       c.sync();
