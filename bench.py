@@ -29,7 +29,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level table)
 # Leaf regions (one kernel or one fused kernel family per launch); aggregates such as
 # "etree" / "partition" / "sequence" are reported in phases but not rooflined.
-LEAF = ("degree", "degree_heads", "relabel", "pst", "etree_bucket", "etree_split", "etree_union", "etree_cross",
+LEAF = ("degree", "degree_heads", "relabel", "pst_group", "etree_split", "etree_union", "etree_cross",
         "etree_apply", "etree_compact", "evaluate")
 # kernels of a region, for roofline.traffic from the committed PMC passes (tools/pmc_traffic.py);
 # regions whose kernels are shared with other regions (histograms, packs) get traffic null

@@ -237,8 +237,11 @@ void radix_sort_keys_u64(Ctx &c, uint64_t *keys, uint64_t n, int end_bit, uint64
 // hist.hip — cnt[key] += occurrences, keys bucketed through LDS (no scattered atomics)
 void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt);
 void histogram_edge_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t K, uint32_t *cnt);
+void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, int L, uint32_t clo, uint32_t *pst,
+                       uint64_t *r0, uint64_t *seg);
 // etree.hip
-void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, bool by_lo);
+void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg);
+void spread_params(uint64_t n, int *L, uint32_t *clo);
 // append.hip — sharded appends: counters (NSHARD * SHARD_STRIDE u64, zeroed).  The pack
 // step moves the shard regions of a producer that streamed *n_in items together in dst
 // and writes the total to *total_out (device; must not alias n_in).  With cond, it runs

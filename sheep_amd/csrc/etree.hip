@@ -164,61 +164,11 @@ constexpr uint64_t CSET_WORDS = (uint64_t)NSHARD * SHARD_STRIDE;
 // ---- first-activity buckets ---------------------------------------------------------
 // An edge (lo, hi) takes part in level s only if bit s of ya = spread(lo) is 0 (light
 // or cross); while ya's bits above stay 1 it sits in right halves and every level would
-// just re-read it.  So the input is bucketed once by its first active level
-// f = the highest zero bit of ya, and level s activates bucket s: the list the levels
-// stream holds only edges that have been active (and their contractions).
-constexpr int NBUCKET = 32;
-
-__device__ __forceinline__ int first_level(uint64_t e, uint32_t clo, uint32_t mask) {
-  const uint32_t inv = ~spread((uint32_t)e, clo) & mask;   // nonzero: lo < hi <= n-1 keeps ya < 2^L - 1
-  return 31 - __clz(inv);
-}
-
-// cnt[f * gridDim.x + block] = edges of bucket f among the block's tiles
-__global__ __launch_bounds__(BLOCK) void k_bucket_count(const uint64_t *__restrict__ edges, uint64_t m, uint32_t clo,
-                                                        uint32_t mask, uint32_t *__restrict__ cnt) {
-  __shared__ uint32_t h[NBUCKET];
-  if (threadIdx.x < NBUCKET) h[threadIdx.x] = 0;
-  __syncthreads();
-  const uint64_t ntiles = (m + TILE - 1) / TILE;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-#pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) {
-      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
-      const uint64_t e = i < m ? edges[i] : DEAD;
-      if (e != DEAD) atomicAdd(&h[first_level(e, clo, mask)], 1u);
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < NBUCKET) cnt[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
-}
-
-// Same tiles per block as k_bucket_count; off = exclusive scan of its counts.
-__global__ __launch_bounds__(BLOCK) void k_bucket_scatter(const uint64_t *__restrict__ edges, uint64_t m, uint32_t clo,
-                                                          uint32_t mask, const uint32_t *__restrict__ off,
-                                                          uint64_t *__restrict__ r0) {
-  __shared__ uint32_t cur[NBUCKET];
-  if (threadIdx.x < NBUCKET) cur[threadIdx.x] = off[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
-  __syncthreads();
-  const uint64_t ntiles = (m + TILE - 1) / TILE;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-#pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) {
-      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
-      const uint64_t e = i < m ? edges[i] : DEAD;
-      if (e != DEAD) r0[atomicAdd(&cur[first_level(e, clo, mask)], 1u)] = e;
-    }
-  }
-}
-
-// seg[s] = first entry of bucket s, seg[L + s] = one past its last
-__global__ void k_bucket_bounds(const uint32_t *__restrict__ off, uint32_t g, int L, uint64_t *__restrict__ seg) {
-  const int s = threadIdx.x;
-  if (s < L) {
-    seg[s] = off[(uint64_t)s * g];
-    seg[L + s] = off[(uint64_t)(s + 1) * g];
-  }
-}
+// just re-read it.  So the input comes grouped by its first active level f = the
+// highest zero bit of ya — a range of lo (hist.hip group_edges_by_lo for a map; a
+// merge's parent edges are already in lo order) — and level s activates group s: the
+// list the levels stream holds only edges that have been active (and their
+// contractions).
 
 __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t *__restrict__ uf, uint32_t *__restrict__ mt,
                                                  uint32_t *__restrict__ top, uint32_t *__restrict__ claim, uint64_t n,
@@ -599,26 +549,33 @@ void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
 
 static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
 
+// spread(x) = floor(x * c / 2^32), c = floor(2^(32+L) / n) in [2^32, 2^33), L = ceil(log2 n):
+// monotone, injective on [0,n), image in [0, 2^L).  clo = c - 2^32.
+void spread_params(uint64_t n, int *L_out, uint32_t *clo_out) {
+  int L = 0;
+  while ((1ull << L) < n) ++L;
+  const unsigned __int128 cfull = (((unsigned __int128)1) << (32 + L)) / n;
+  *L_out = L;
+  *clo_out = (uint32_t)(cfull - (((unsigned __int128)1) << 32));
+}
+
 // A level's next list holds the entries that stayed (alive, <= m) plus one contraction
 // slot per cross edge (<= m).
 static uint64_t list_capacity(uint64_t m) { return 2 * m + TILE; }
 
-// Elimination tree of `m` edges ((hi<<32)|lo, lo < hi < n, DEAD holes allowed).  `edges`
-// is consumed.  by_lo: the edges are ordered by lo (a merge's parent edges), so the
-// first-activity buckets are ranges of it; otherwise they are bucketed by one counting
-// pass.
+// Elimination tree of `m` edges ((hi<<32)|lo, lo < hi < n, DEAD holes allowed), grouped
+// by first active level: seg[s] / seg[L + s] (device) delimit group s.  seg == nullptr:
+// the edges are a merge's parent edges (entries 2 lo, 2 lo + 1), whose groups are
+// computed here.  The edges are read only.
 // One pass of launches per level, no host synchronisation inside the loop (see the
 // stats row above); the stats come back once at the end for the timers / debug log.
-void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, bool by_lo) {
+void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg_in) {
   fill_u32(c, parent, n, INVALID);
   if (n < 2 || m == 0) return;
   if (m >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "too many edges for one shard");
-  int L = 0;
-  while ((1ull << L) < n) ++L;
-  // spread(x) = floor(x * c / 2^32), c = floor(2^(32+L) / n) in [2^32, 2^33): monotone,
-  // injective on [0,n), image in [0, 2^L).
-  unsigned __int128 cfull = (((unsigned __int128)1) << (32 + L)) / n;
-  uint32_t clo = (uint32_t)(cfull - (((unsigned __int128)1) << 32));
+  int L;
+  uint32_t clo;
+  spread_params(n, &L, &clo);
 
   uint32_t *uf = c.get_as<uint32_t>("et_uf", n);
   uint32_t *mt = c.get_as<uint32_t>("et_mt", n);
@@ -631,10 +588,11 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
   uint64_t *xbuf = c.get_as<uint64_t>("et_cross", mcap);
   // the two list buffers (level l reads one and writes the other) and the bucketed input r0
   uint64_t *lists[2] = {c.get_as<uint64_t>("et_list1", lcap), c.get_as<uint64_t>("et_list2", lcap)};
-  uint64_t *r0 = by_lo ? edges : c.get_as<uint64_t>("et_r0", m);
-  uint64_t *seg = c.get_as<uint64_t>("et_seg", 2 * (uint64_t)L);
-  const uint32_t mask = (uint32_t)((1ull << L) - 1);
-  if (by_lo) {
+  const uint64_t *r0 = edges;
+  const uint64_t *seg = seg_in;
+  if (!seg) {
+    uint64_t *dseg = c.get_as<uint64_t>("et_seg", 2 * (uint64_t)L);
+    seg = dseg;
     // bucket s = lo with ya in [2^L - 2^(s+1), 2^L - 2^s): a range of lo, entries 2 lo, 2 lo + 1
     auto first_lo = [&](uint64_t y) {   // min lo with spread(lo) >= y
       uint64_t a = 0, b = n;
@@ -651,20 +609,7 @@ void etree_from_edges(Ctx &c, uint64_t *edges, uint64_t m, uint64_t n, uint32_t 
       if (h[L + b] > m) h[L + b] = m;
       if (h[b] > h[L + b]) h[b] = h[L + b];
     }
-    HIP_CHECK(hipMemcpyAsync(seg, h, 2 * (size_t)L * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
-  } else {
-    TimedRegion tr(c, "etree_bucket", 24 * m);
-    const unsigned g = grid_tiles(m);
-    uint32_t *bc = c.get_as<uint32_t>("et_bcnt", (uint64_t)(NBUCKET + 1) * g);
-    HIP_CHECK(hipMemsetAsync(bc, 0, (uint64_t)(NBUCKET + 1) * g * sizeof(uint32_t), c.stream));
-    hipLaunchKernelGGL(k_bucket_count, dim3(g), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges, m, clo, mask, bc);
-    LAUNCH_CHECK();
-    scan_exclusive_u32(c, bc, bc, (uint64_t)(NBUCKET + 1) * g, nullptr);
-    hipLaunchKernelGGL(k_bucket_scatter, dim3(g), dim3(BLOCK), 0, c.stream, (const uint64_t *)edges, m, clo, mask,
-                       (const uint32_t *)bc, r0);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_bucket_bounds, dim3(1), dim3(64), 0, c.stream, (const uint32_t *)bc, g, L, seg);
-    LAUNCH_CHECK();
+    HIP_CHECK(hipMemcpyAsync(dseg, h, 2 * (size_t)L * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
   }
   // a split reads at most the list plus a bucket: (lcap + m) entries, in TILE tiles
   const uint64_t cstride = (lcap + m + TILE - 1) / TILE + 1;
@@ -772,13 +717,21 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   c.sync();
   if (c.h_scalars[9]) throw Error(SHEEP_ERR_RANGE, "vector::_M_range_check: neighbour vid beyond the sequence's index (jtree.cpp:75)");
   const uint64_t m = nrec;   // edges[i] per record, DEAD holes included
-  if (nrec) {
-    TimedRegion tr(c, "pst", 8 * nrec);
-    histogram_edge_lo(c, edges, m, n, pst);
-  }
-  {
+  if (n >= 2 && nrec) {
+    int L;
+    uint32_t clo;
+    spread_params(n, &L, &clo);
+    uint64_t *r0 = c.get_as<uint64_t>("bt_grouped", m);
+    uint64_t *seg = c.get_as<uint64_t>("bt_seg", 2 * (uint64_t)L);
+    {
+      // pst = histogram of the edges' lo; the same passes group the edges by lo
+      TimedRegion tr(c, "pst_group", 20 * m);
+      group_edges_by_lo(c, edges, m, n, L, clo, pst, r0, seg);
+    }
     TimedRegion tr(c, "etree", 8 * m);
-    etree_from_edges(c, edges, m, n, parent, false);
+    etree_from_edges(c, r0, m, n, parent, seg);
+  } else {
+    fill_u32(c, parent, n, INVALID);
   }
   if (n) {
     hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, tree);
@@ -800,7 +753,7 @@ void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n,
   if (c.h_scalars[11]) throw Error(SHEEP_ERR_ARG, "merge: a parent is not a later node of the tree");
   {
     TimedRegion tr(c, "merge", 16 * n);
-    etree_from_edges(c, edges, 2 * n, n, parent, true);
+    etree_from_edges(c, edges, 2 * n, n, parent, nullptr);
   }
   hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);
   LAUNCH_CHECK();

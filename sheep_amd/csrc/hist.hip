@@ -16,6 +16,7 @@
 //
 // Traffic per key: two reads of the source + 2 B written + 2 B read back, all of it
 // coalesced (runs of ~T/NB u16), against one scattered RMW per key.
+#include <type_traits>
 #include <vector>
 
 #include "common.hpp"
@@ -45,6 +46,23 @@ struct EdgeLoKeys {
   __device__ __forceinline__ uint32_t operator()(uint64_t i) const {
     const uint64_t e = edges[i];
     return e == ~0ull ? NO_KEY : (uint32_t)e;
+  }
+};
+
+// lo of a tree edge, shifted so that every first-activity range of the elimination tree
+// (etree.hip: lo with ya = spread(lo) having its highest zero bit at s) starts on a
+// bucket boundary: key = lo + padoff[f(lo)].  Grouping edges by key then yields, per
+// range, a run of whole buckets.
+struct EdgeLoPadded {
+  const uint64_t *edges;
+  const uint32_t *padoff;
+  uint32_t clo, mask;
+  __device__ __forceinline__ uint32_t operator()(uint64_t i) const { return key(edges[i]); }
+  __device__ __forceinline__ uint32_t key(uint64_t e) const {
+    if (e == ~0ull) return NO_KEY;
+    const uint32_t lo = (uint32_t)e;
+    const uint32_t inv = ~(lo + __umulhi(lo, clo)) & mask;
+    return lo + padoff[31 - __clz(inv)];
   }
 };
 
@@ -150,6 +168,51 @@ __global__ __launch_bounds__(HB) void k_hist_scatter(Src src, uint64_t n, uint32
   }
 }
 
+// k_hist_scatter for tree edges grouped by padded lo: besides the u16 key runs it moves
+// each edge to the same position of `grouped` (the thread still holds it), so the
+// elimination tree's input comes out in lo-bucket order at no extra read.
+__global__ __launch_bounds__(HB) void k_lo_scatter(EdgeLoPadded src, uint64_t n, uint32_t nb,
+                                                   const uint32_t *__restrict__ offsets, uint64_t ntiles,
+                                                   uint16_t *__restrict__ out, uint64_t *__restrict__ grouped) {
+  extern __shared__ uint32_t lds[];
+  uint32_t *cur = lds;
+  uint32_t *start = lds + nb;
+  uint32_t *wsum = lds + 2 * nb;
+  uint32_t *stage = lds + 2 * nb + HB / WAVE;
+  for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x << TLOG;
+  uint64_t e[KPT];
+  uint32_t k[KPT];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const uint64_t i = base + (uint64_t)j * HB + threadIdx.x;
+    e[j] = i < n ? src.edges[i] : ~0ull;
+  }
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    k[j] = src.key(e[j]);
+    if (k[j] != NO_KEY) atomicAdd(&cur[k[j] >> WBITS], 1u);
+  }
+  __syncthreads();
+  const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
+  for (uint32_t b = threadIdx.x; b < nb; b += HB) start[b] = cur[b];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < KPT; ++j)
+    if (k[j] != NO_KEY) {
+      const uint32_t b = k[j] >> WBITS;
+      const uint32_t p = atomicAdd(&cur[b], 1u);
+      stage[p] = (b << 16) | (k[j] & (W - 1));
+      grouped[offsets[(uint64_t)b * ntiles + blockIdx.x] + (p - start[b])] = e[j];
+    }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < total; j += HB) {
+    const uint32_t x = stage[j], b = x >> 16;
+    out[offsets[(uint64_t)b * ntiles + blockIdx.x] + (j - start[b])] = (uint16_t)(x & 0xFFFF);
+  }
+}
+
 // One workgroup per chunk = (bucket, slice of its keys).  A bucket's keys can be very
 // skewed (pst: a few thousand positions own most lower endpoints; one bucket took
 // 21 ms alone on RMAT-26), so buckets are cut into slices of <= CHUNK keys; a bucket
@@ -162,7 +225,8 @@ struct Chunk {
 constexpr uint64_t CHUNK = 1u << 20;
 
 __global__ __launch_bounds__(HB) void k_hist_final(const uint16_t *__restrict__ keys, const Chunk *__restrict__ chunks,
-                                                   uint64_t K, uint32_t *__restrict__ cnt) {
+                                                   uint64_t K, const uint32_t *__restrict__ kbase,
+                                                   uint32_t *__restrict__ cnt) {
   extern __shared__ uint32_t lds[];
   const Chunk ch = chunks[blockIdx.x];
   for (uint32_t i = threadIdx.x; i < W; i += HB) lds[i] = 0;
@@ -179,7 +243,8 @@ __global__ __launch_bounds__(HB) void k_hist_final(const uint16_t *__restrict__ 
       if (k[j] != NO_KEY) atomicAdd(&lds[k[j]], 1u);
   }
   __syncthreads();
-  const uint64_t k0 = (uint64_t)ch.bucket << WBITS;
+  // counter index of the bucket's first key (padded keys: the range's own lo offset)
+  const uint64_t k0 = kbase ? kbase[ch.bucket] : (uint64_t)ch.bucket << WBITS;
   for (uint32_t i = threadIdx.x; i < W; i += HB) {
     const uint32_t v = lds[i];
     if (!v || k0 + i >= K) continue;
@@ -188,8 +253,13 @@ __global__ __launch_bounds__(HB) void k_hist_final(const uint16_t *__restrict__ 
   }
 }
 
+// Adds the histogram of src's keys over [0, K) into cnt.  With `grouped`, src is
+// EdgeLoPadded, K its padded key range, kbase the counter index of each bucket's first
+// key, and the edges are also written to `grouped` in bucket order; bstart_out (nb + 1
+// entries, device) receives each bucket's first position there.
 template <typename Src>
-void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt) {
+void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint64_t *grouped = nullptr,
+                   const uint32_t *kbase = nullptr, uint32_t *bstart_out = nullptr) {
   if (n == 0 || K == 0) return;
   const uint32_t nb = (uint32_t)((K + W - 1) >> WBITS);
   const uint64_t ntiles = (n + TKEYS - 1) >> TLOG;
@@ -201,6 +271,7 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt) {
     HIP_CHECK(hipFuncSetAttribute((const void *)k_hist_scatter<HeadKeys>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIP_CHECK(hipFuncSetAttribute((const void *)k_hist_scatter<EdgeLoKeys>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIP_CHECK(hipFuncSetAttribute((const void *)k_hist_final, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_CHECK(hipFuncSetAttribute((const void *)k_lo_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
   uint32_t *tile_hist = c.get_as<uint32_t>("hist_tiles", ntiles * nb + 1);
@@ -210,8 +281,13 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt) {
   LAUNCH_CHECK();
   uint32_t *total = c.get_as<uint32_t>("hist_total", 1);
   scan_exclusive_u32(c, tile_hist, tile_hist, ntiles * nb, total);
-  hipLaunchKernelGGL(k_hist_scatter<Src>, dim3((unsigned)ntiles), dim3(HB), lds_scatter, c.stream, src, n, nb,
-                     (const uint32_t *)tile_hist, ntiles, keys);
+  if constexpr (std::is_same<Src, EdgeLoPadded>::value) {
+    hipLaunchKernelGGL(k_lo_scatter, dim3((unsigned)ntiles), dim3(HB), lds_scatter, c.stream, src, n, nb,
+                       (const uint32_t *)tile_hist, ntiles, keys, grouped);
+  } else {
+    hipLaunchKernelGGL(k_hist_scatter<Src>, dim3((unsigned)ntiles), dim3(HB), lds_scatter, c.stream, src, n, nb,
+                       (const uint32_t *)tile_hist, ntiles, keys);
+  }
   LAUNCH_CHECK();
   // bucket starts (column 0 of the bucket-major offsets) -> chunk list
   std::vector<uint32_t> bstart(nb + 1);
@@ -219,6 +295,7 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt) {
                              nb, hipMemcpyDeviceToHost, c.stream));
   HIP_CHECK(hipMemcpyAsync(&bstart[nb], total, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
+  if (bstart_out) HIP_CHECK(hipMemcpyAsync(bstart_out, bstart.data(), (nb + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
   std::vector<Chunk> chunks;
   for (uint32_t b = 0; b < nb; ++b) {
     const uint64_t beg = bstart[b], end = bstart[b + 1];
@@ -226,13 +303,22 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt) {
     const uint32_t shared = end - beg > CHUNK;
     for (uint64_t x = beg; x < end; x += CHUNK) chunks.push_back({x, x + CHUNK < end ? x + CHUNK : end, b, shared});
   }
-  if (chunks.empty()) return;
+  if (chunks.empty()) {
+    c.sync();   // bstart is a pageable host buffer
+    return;
+  }
   Chunk *dch = c.get_as<Chunk>("hist_chunks", chunks.size());
   HIP_CHECK(hipMemcpyAsync(dch, chunks.data(), chunks.size() * sizeof(Chunk), hipMemcpyHostToDevice, c.stream));
   hipLaunchKernelGGL(k_hist_final, dim3((unsigned)chunks.size()), dim3(HB), W * 4, c.stream, (const uint16_t *)keys,
-                     (const Chunk *)dch, K, cnt);
+                     (const Chunk *)dch, K, kbase, cnt);
   LAUNCH_CHECK();
   c.sync();   // `chunks` is a pageable host buffer
+}
+
+// seg[i] = position of bucket sb[i] in the grouped array (sb: bucket indices)
+__global__ void k_seg_from_buckets(const uint32_t *__restrict__ bstart, const uint64_t *__restrict__ sb, int L,
+                                   uint64_t *__restrict__ seg) {
+  for (int i = threadIdx.x; i < 2 * L; i += blockDim.x) seg[i] = bstart[sb[i]];
 }
 
 }  // namespace
@@ -242,6 +328,55 @@ void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uin
 }
 void histogram_edge_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t K, uint32_t *cnt) {
   histogram_add(c, EdgeLoKeys{edges}, m, K, cnt);
+}
+
+// pst[lo] += edges with that lo, and the edges grouped for the elimination tree: r0 holds
+// them in padded-lo bucket order and seg[s] / seg[L + s] delimit the edges whose first
+// active level is s ("first-activity buckets").
+void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, int L, uint32_t clo, uint32_t *pst,
+                       uint64_t *r0, uint64_t *seg) {
+  // lo range of level s: ya = spread(lo) in [2^L - 2^(s+1), 2^L - 2^s)
+  auto first_lo = [&](uint64_t y) {
+    uint64_t a = 0, b = n;
+    while (a < b) {
+      const uint64_t x = (a + b) / 2;
+      if (x + ((x * (uint64_t)clo) >> 32) >= y) b = x; else a = x + 1;
+    }
+    return a;
+  };
+  std::vector<uint32_t> padoff(32, 0);
+  std::vector<uint64_t> pstart(L), plen(L);
+  uint64_t run = 0;
+  for (int s = L - 1; s >= 0; --s) {   // ranges in increasing lo
+    const uint64_t beg = first_lo((1ull << L) - (2ull << s)), end = first_lo((1ull << L) - (1ull << s));
+    const uint64_t len = end > beg ? end - beg : 0;
+    pstart[s] = run;
+    plen[s] = (len + W - 1) / W * W;
+    padoff[s] = (uint32_t)(run - beg);
+    run += plen[s];
+  }
+  const uint64_t K = run ? run : W;
+  if (K >= (1ull << 32)) throw Error(SHEEP_ERR_ARG, "group_edges_by_lo: key range too large");
+  const uint32_t nb = (uint32_t)(K / W);
+  std::vector<uint32_t> kbase(nb);
+  for (int s = 0; s < L; ++s)
+    for (uint64_t b = pstart[s] / W; b < (pstart[s] + plen[s]) / W; ++b) kbase[b] = (uint32_t)(b * W - padoff[s]);
+  uint32_t *d_pad = c.get_as<uint32_t>("grp_padoff", 32);
+  uint32_t *d_kbase = c.get_as<uint32_t>("grp_kbase", nb);
+  uint32_t *d_bstart = c.get_as<uint32_t>("grp_bstart", nb + 1);
+  HIP_CHECK(hipMemcpyAsync(d_pad, padoff.data(), 32 * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
+  HIP_CHECK(hipMemcpyAsync(d_kbase, kbase.data(), nb * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
+  HIP_CHECK(hipMemsetAsync(d_bstart, 0, (nb + 1) * sizeof(uint32_t), c.stream));
+  const uint32_t mask = (uint32_t)((1ull << L) - 1);
+  histogram_add(c, EdgeLoPadded{edges, d_pad, clo, mask}, m, K, pst, r0, d_kbase, d_bstart);
+  std::vector<uint64_t> hseg(2 * (size_t)L);
+  for (int s = 0; s < L; ++s) { hseg[s] = pstart[s] / W; hseg[L + s] = (pstart[s] + plen[s]) / W; }
+  uint64_t *d_sb = c.get_as<uint64_t>("grp_segb", 2 * (size_t)L);
+  HIP_CHECK(hipMemcpyAsync(d_sb, hseg.data(), 2 * (size_t)L * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+  hipLaunchKernelGGL(k_seg_from_buckets, dim3(1), dim3(64), 0, c.stream, (const uint32_t *)d_bstart,
+                     (const uint64_t *)d_sb, L, seg);
+  LAUNCH_CHECK();
+  c.sync();   // the host vectors above are pageable
 }
 
 }  // namespace sheep
