@@ -356,8 +356,8 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restric
 }
 
 // ---- the level's split: three dense outputs --------------------------------------
-// Count pass (per 2048-entry tile: entries that stay, light, cross), one-workgroup scan
-// of the tile counts, write pass (each tile re-read and written at its offsets).  Two
+// Count pass (per 2048-entry tile: entries that stay, light, cross), one scan of the
+// three count rows, write pass (each tile re-read and written at its offsets).  Two
 // reads per entry, but every pass streams at full occupancy; an ordered single pass
 // (decoupled look-back) serialised on the chunk chain.
 
@@ -398,7 +398,7 @@ __device__ __forceinline__ uint64_t pack3(uint32_t c) {
 __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
                                                        uint64_t *__restrict__ st, int s, uint32_t clo,
                                                        const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
-                                                       int L, uint32_t *__restrict__ cnt, uint64_t cstride) {
+                                                       int L, uint64_t *__restrict__ cnt, uint64_t cstride) {
   const SplitIn in(list, prev, r0, seg, s, L);
   const uint64_t ntiles = (in.m + TILE - 1) / TILE;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -419,59 +419,28 @@ __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restric
     if (threadIdx.x < 3) {
       uint64_t t = 0;
       for (int w = 0; w < BLOCK / WAVE; ++w) t += s_w[w];
-      cnt[threadIdx.x * cstride + tile] = (uint32_t)((t >> (16 * threadIdx.x)) & 0xFFFF);
+      cnt[threadIdx.x * cstride + tile] = (t >> (16 * threadIdx.x)) & 0xFFFF;
     }
     __syncthreads();
   }
 }
 
-// One workgroup: exclusive scans of the three tile-count rows in place; totals -> st.
-constexpr int SCAN_B = 1024;
-__global__ __launch_bounds__(SCAN_B) void k_split_scan(const uint64_t *__restrict__ prev, const uint64_t *__restrict__ seg,
-                                                       int s, int L, uint64_t *__restrict__ st, uint32_t *__restrict__ cnt,
-                                                       uint64_t cstride) {
-  const uint64_t len = prev ? prev[ST_KEPT] + prev[ST_NX] : 0;
-  const uint64_t ntiles = (len + seg[L + s] - seg[s] + TILE - 1) / TILE;
-  __shared__ uint32_t s_w[SCAN_B / WAVE];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t per = (ntiles + SCAN_B - 1) / SCAN_B, b0 = threadIdx.x * per;
-  for (int row = 0; row < 3; ++row) {
-    uint32_t *a = cnt + row * cstride;
-    uint32_t sum = 0;
-    for (uint64_t i = b0; i < b0 + per && i < ntiles; ++i) sum += a[i];
-    uint32_t inc = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += u;
-    }
-    if (lane == 63) s_w[wave] = inc;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-    for (int w = 0; w < SCAN_B / WAVE; ++w) {
-      const uint32_t x = s_w[w];
-      if (w < wave) off += x;
-      tot += x;
-    }
-    uint32_t run = off + inc - sum;
-    for (uint64_t i = b0; i < b0 + per && i < ntiles; ++i) {
-      const uint32_t x = a[i];
-      a[i] = run;
-      run += x;
-    }
-    if (threadIdx.x == 0) st[row == 0 ? ST_KEPT : row == 1 ? ST_NL : ST_NX] = tot;
-    __syncthreads();
-  }
-}
-
+// cnt: the three rows (stride cstride, zero-padded) scanned as ONE exclusive scan, so a
+// row's offsets are relative to its first entry; the row totals go to st.
 __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
-                                                       int s, uint32_t clo, const uint64_t *__restrict__ r0,
-                                                       const uint64_t *__restrict__ seg, int L,
-                                                       const uint32_t *__restrict__ cnt, uint64_t cstride,
+                                                       uint64_t *__restrict__ st, int s, uint32_t clo,
+                                                       const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
+                                                       int L, const uint64_t *__restrict__ cnt, uint64_t cstride,
                                                        uint64_t *__restrict__ next, uint64_t *__restrict__ lbuf,
                                                        uint64_t *__restrict__ xbuf) {
   const SplitIn in(list, prev, r0, seg, s, L);
   const uint64_t ntiles = (in.m + TILE - 1) / TILE;
+  const uint64_t b0 = cnt[0], b1 = cnt[cstride], b2 = cnt[2 * cstride], b3 = cnt[3 * cstride];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st[ST_KEPT] = b1 - b0;
+    st[ST_NL] = b2 - b1;
+    st[ST_NX] = b3 - b2;
+  }
   __shared__ uint64_t s_w[BLOCK / WAVE];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -497,9 +466,9 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
     uint64_t off = 0;
     for (int w = 0; w < wave; ++w) off += s_w[w];
     const uint64_t ex = off + inc - c3;
-    uint64_t pk = cnt[tile] + (ex & 0xFFFF);
-    uint64_t pl = cnt[cstride + tile] + ((ex >> 16) & 0xFFFF);
-    uint64_t px = cnt[2 * cstride + tile] + (ex >> 32);
+    uint64_t pk = cnt[tile] - b0 + (ex & 0xFFFF);
+    uint64_t pl = cnt[cstride + tile] - b1 + ((ex >> 16) & 0xFFFF);
+    uint64_t px = cnt[2 * cstride + tile] - b2 + (ex >> 32);
 #pragma unroll
     for (int j = 0; j < TILE_ITEMS; ++j) {
       if (cl[j] & 1) next[pk++] = ev[j];
@@ -613,7 +582,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   }
   // a split reads at most the list plus a bucket: (lcap + m) entries, in TILE tiles
   const uint64_t cstride = (lcap + m + TILE - 1) / TILE + 1;
-  uint32_t *tcnt = c.get_as<uint32_t>("et_tilecnt", 3 * cstride);
+  uint64_t *tcnt = c.get_as<uint64_t>("et_tilecnt", 3 * cstride + 1);
   uint64_t *lbuf = c.get_as<uint64_t>("et_light", mcap);  // must outlive the hook rounds (k_light_top)
   uint64_t *alt = c.get_as<uint64_t>("et_alt", mcap);     // shard scratch of the hook rounds
   uint64_t *hk[2] = {c.get_as<uint64_t>("et_lwa", mcap), c.get_as<uint64_t>("et_lwb", mcap)};
@@ -631,14 +600,13 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     LAUNCH_CHECK();
     {
       TimedRegion tr(c, "etree_split");
+      HIP_CHECK(hipMemsetAsync(tcnt, 0, (3 * cstride + 1) * sizeof(uint64_t), c.stream));
       hipLaunchKernelGGL(k_split_count, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo,
                          (const uint64_t *)r0, (const uint64_t *)seg, L, tcnt, cstride);
       LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_split_scan, dim3(1), dim3(SCAN_B), 0, c.stream, prev, (const uint64_t *)seg, s, L, st, tcnt,
-                         cstride);
-      LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_split_write, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, s, clo,
-                         (const uint64_t *)r0, (const uint64_t *)seg, L, (const uint32_t *)tcnt, cstride, next, lbuf,
+      scan_exclusive_u64(c, tcnt, tcnt, 3 * cstride + 1, nullptr);
+      hipLaunchKernelGGL(k_split_write, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo,
+                         (const uint64_t *)r0, (const uint64_t *)seg, L, (const uint64_t *)tcnt, cstride, next, lbuf,
                          xbuf);
       LAUNCH_CHECK();
     }
