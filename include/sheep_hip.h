@@ -173,6 +173,14 @@ int sheep_evaluate(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec,
                    const uint32_t *pos_dev, uint64_t pos_size, const int16_t *parts_vid_dev,
                    int what, sheep_eval *out);
 
+/* ---- partition files ----------------------------------------------------------------
+ * edge_part_dev[i] = the part record i is written to by writePartitionedGraph
+ * (partition.cpp:588-670): the part of its earlier-positioned endpoint.  An endpoint
+ * without a position or a part -> SHEEP_ERR_RANGE (the reference's pos.at() / assert).
+ * The host writes the per-part text files (sheep.hpp Partition::writePartitionedGraph). */
+int sheep_edge_parts(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec, const uint32_t *pos_dev,
+                     uint64_t pos_size, const int16_t *parts_vid_dev, int16_t *edge_part_dev);
+
 /* ---- tree facts (TREEFAQS) -------------------------------------------------------- */
 int sheep_facts(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n, sheep_facts_t *out);
 

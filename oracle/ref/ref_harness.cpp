@@ -99,7 +99,8 @@ static int usage() {
           "ref_harness seq G OUT_SEQ                      degreeSequence (LLAMA degrees)\n"
           "ref_harness tree G SEQ|- OUT_TRE [p/k]         JTree (+ partial load), TREEFAQS\n"
           "ref_harness part G SEQ|- TREE PARTS_PREFIX k.. partition_tree -f -g flow + parts dumps\n"
-          "ref_harness write G SEQ|- TREE k PREFIX        Partition + graph-based writePartitionedGraph\n");
+          "ref_harness write G SEQ|- TREE k PREFIX        Partition + graph-based writePartitionedGraph\n"
+          "ref_harness writefile G SEQ|- TREE k PREFIX    Partition + file-based writePartitionedGraph\n");
   return 1;
 }
 
@@ -143,6 +144,16 @@ int main(int argc, char **argv) {
     Partition part(seq, jnodes, (short)atoi(argv[5]), 1.03, false, true, false);
     part.print();
     part.writePartitionedGraph(g, seq, argv[6]);
+    return 0;
+  }
+  if (cmd == "writefile" && argc == 7) {   // partition_tree -g G -o PREFIX SEQ TREE k
+    HarnessGraph g(argv[2]);
+    std::vector<vid_t> seq = strcmp(argv[3], "-") == 0 ? degreeSequence(g) : readSequence(argv[3]);
+    JNodeTable jnodes(argv[4]);
+    Partition part(seq, jnodes, (short)atoi(argv[5]), 1.03, false, true, false);
+    part.print();
+    char const *const input = argv[2];
+    part.writePartitionedGraph(input, seq, argv[6]);
     return 0;
   }
   return usage();

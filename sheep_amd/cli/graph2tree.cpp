@@ -111,8 +111,7 @@ int main(int argc, char *argv[]) {
     if (partitions != 0) {
       Partition p(seq, tree.jnodes, (part_t)partitions);
       if (out_name != "") {
-        printf("Partitioned-graph output (-p with -o) is not supported by this build yet.\n");
-        return 1;
+        p.writePartitionedGraph(graph, seq, out_name.c_str(), false);   // graph2tree.cpp:212-213
       } else if (is_leader) {
         p.print();
       }

@@ -4,7 +4,8 @@
 //   partition_tree [-v -f -b BAL -x -d -u -g GRAPH -o PREFIX] SEQ TREE K [K ...]
 //
 // Modes (partition_tree.cpp:114-163): simple (no -g: print per k), partition + evaluate
-// (-g: both evaluators per k, SEQ "-" = degree sequence), partition + files (-g -o).
+// (-g: both evaluators per k, SEQ "-" = degree sequence), partition + files (-g -o:
+// one k, SEQ "-" = file sequence, one SNAP file per part in input-record order).
 // One kid table serves every k, so the FFD sort order persists across k exactly like
 // the reference's in-place std::sort (partition.cpp:104-106).
 #include <unistd.h>
@@ -91,8 +92,16 @@ int main(int argc, char *argv[]) {
         part.evaluate(graph, seq);
       }
     } else {
-      printf("Partitioned-graph output (-o) is not supported by this build yet.\n");
-      return 1;
+      /* PARTITIONING AND I/O (partition_tree.cpp:146-163): one k, files in input order */
+      GraphWrapper graph(graph_filename);
+      DeviceSequence seq = uploadSequence(strcmp(argv[optind], "-") == 0 ? fileSequence(graph_filename)
+                                                                         : readSequence(argv[optind]));
+      const short num_parts = atoi(argv[optind + 2]);
+      auto partition_start = std::chrono::steady_clock::now();
+      Partition part(seq, jnodes, num_parts, balance_factor, vtx_weight, pst_weight, pre_weight);
+      if (verbose) printf("Partitioning took: %f seconds\n", seconds_since(partition_start));
+      part.print();
+      part.writePartitionedGraph(graph, seq, output_filename, true);
     }
     if (verbose) printf("Finished in: %f seconds\n", seconds_since(start_point));
   } catch (const std::out_of_range &e) {

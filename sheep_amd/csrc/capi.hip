@@ -27,6 +27,8 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
 void evaluate(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
               const int16_t *parts, int what, sheep_eval *out);
 void tree_facts(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_facts_t *out);
+void edge_parts(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
+                const int16_t *parts_vid, int16_t *out);
 uint64_t rmat_generate(Ctx &c, int scale, int ef, uint64_t seed, sheep_xs1 *out, uint64_t cap);
 uint64_t rmat_generate_host(int scale, int ef, uint64_t seed, sheep_xs1 *out, uint64_t cap);
 }  // namespace sheep
@@ -246,6 +248,14 @@ int sheep_evaluate(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, const ui
   API_BEGIN
   NEED(ctx && out && (rec || !nrec) && ((pos && parts_vid) || !pos_size), "null argument");
   sheep::evaluate(ctx->c, rec, nrec, pos, pos_size, parts_vid, what, out);
+  API_END
+}
+
+int sheep_edge_parts(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
+                     const int16_t *parts_vid, int16_t *edge_part) {
+  API_BEGIN
+  NEED(ctx && ((rec && pos && parts_vid && edge_part) || !nrec), "null argument");
+  sheep::edge_parts(ctx->c, rec, nrec, pos, pos_size, parts_vid, edge_part);
   API_END
 }
 

@@ -197,3 +197,47 @@ void evaluate(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, 
 }
 
 }  // namespace sheep
+
+// ---- partition files (partition.cpp:588-670 writePartitionedGraph) -----------------------
+namespace sheep {
+namespace {
+
+// The part an edge is written to: the part of its earlier-positioned endpoint
+// (X_pos < Y_pos ? X_part : Y_part; a self-loop takes its vertex's part).  An endpoint
+// outside the sequence or without a part is the reference's pos.at() throw / assert.
+__global__ __launch_bounds__(BLOCK) void k_edge_parts(const sheep_xs1 *__restrict__ rec, uint64_t nrec,
+                                                      const uint32_t *__restrict__ pos, uint64_t pos_size,
+                                                      const int16_t *__restrict__ parts, int16_t *__restrict__ out,
+                                                      unsigned long long *__restrict__ err) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  bool bad = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nrec; i += stride) {
+    const sheep_xs1 r = rec[i];
+    int16_t p = SHEEP_INVALID_PART;
+    if (r.tail < pos_size && r.head < pos_size) {
+      const uint32_t xp = pos[r.tail], yp = pos[r.head];
+      const int16_t xq = parts[r.tail], yq = parts[r.head];
+      if (xp != INVALID && yp != INVALID && xq != SHEEP_INVALID_PART && yq != SHEEP_INVALID_PART) p = xp < yp ? xq : yq;
+    }
+    bad |= p == SHEEP_INVALID_PART;
+    out[i] = p;
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(err, 1ull);
+}
+
+}  // namespace
+
+void edge_parts(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
+                const int16_t *parts_vid, int16_t *out) {
+  if (!nrec) return;
+  unsigned long long *err = (unsigned long long *)c.d_scalars + 58;
+  HIP_CHECK(hipMemsetAsync(err, 0, sizeof(uint64_t), c.stream));
+  hipLaunchKernelGGL(k_edge_parts, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos, pos_size, parts_vid,
+                     out, err);
+  LAUNCH_CHECK();
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 58, err, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  if (c.h_scalars[58]) throw Error(SHEEP_ERR_RANGE, "vector::_M_range_check: an edge endpoint has no position or part (partition.cpp:657-664)");
+}
+
+}  // namespace sheep

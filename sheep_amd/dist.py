@@ -4,6 +4,8 @@ path (graph2tree.cpp:161-216).
   * shard_bounds      — contiguous record shards, like `-l part/num_parts`;
   * allreduce_degrees — one all-reduce of the per-shard degree histograms plus a max of
                         max_slot (sequence.h:70-78 `mpiSequence`'s MPI_Allreduce);
+  * sync_parts        — rank 0's part array to every rank (Partition::mpi_sync,
+                        partition.cpp:69-79), so each rank can write its shard's files;
   * reduce_trees      — binomial reduction of the partial trees to rank 0 (the shape of
                         MPI_Reduce with mpi_merge_reduction, jnode.cpp:203-250): at hop r,
                         rank i with i % 2r == r sends to i - r, which merges.  Merging is
@@ -73,3 +75,18 @@ def reduce_trees(tree: torch.Tensor, merge, rank: int, world: int):
             tree = merge(tree, _recv_like(tree, rank + r))
         r *= 2
     return tree
+
+
+def sync_parts(parts: torch.Tensor | None, pos_size: int, device) -> torch.Tensor:
+    """Partition::mpi_sync: broadcast rank 0's vid-indexed int16 parts (created on the
+    other ranks with the size rank 0 has)."""
+    if dist.get_rank() != 0:
+        parts = torch.empty(pos_size, dtype=torch.int16, device=device)
+    raw = parts.view(torch.uint8)   # gloo has no int16 collectives
+    if _host_staged() and raw.is_cuda:
+        h = raw.cpu()
+        dist.broadcast(h, 0)
+        raw.copy_(h)
+    else:
+        dist.broadcast(raw, 0)
+    return parts

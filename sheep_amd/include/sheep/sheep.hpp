@@ -149,16 +149,24 @@ class GraphWrapper {
       loops += all[i].tail == all[i].head;
     }
     edges_ = (2 * nrec_ - loops) / 2;   // max_edges / 2 (graph_wrapper.h:79-81)
+    dat_ = is_dat(filename);
   }
   size_t getMaxVid() const { return max_nodes_; }
   size_t getEdges() const { return edges_; }
   size_t getNodes() const;   // slots with degree != 0 (counted on the GPU)
   const sheep_xs1 *records() const { return rec_.get(); }
   uint64_t numRecords() const { return nrec_; }
+  bool isDat() const { return dat_; }
+  std::vector<sheep_xs1> hostRecords() const {
+    std::vector<sheep_xs1> h(nrec_);
+    if (nrec_) rec_.download(h.data(), nrec_);
+    return h;
+  }
 
  private:
   DeviceArray<sheep_xs1> rec_;
   uint64_t nrec_ = 0, max_nodes_ = 0, edges_ = 0;
+  bool dat_ = false;
   mutable int64_t nodes_ = -1;
 };
 
@@ -393,6 +401,67 @@ class Partition {
     print_ratio_line("  balance: ", e.max_down_bal, Ek);
     print_ratio_line("ECV(up)  : ", e.ecv_up, E);
     print_ratio_line("  balance: ", e.max_up_bal, Ek);
+  }
+
+  // writePartitionedGraph (partition.cpp:588-670): one SNAP text file per part,
+  // PREFIX%04d, lines "X Y".  An edge goes to the part of its earlier-positioned endpoint
+  // (computed on the GPU, sheep_edge_parts).
+  //   file_order = true  — partition_tree -o (:632-670): the records as the input file
+  //                        is read; an XS1 file repeats its last record (XS1Reader tests
+  //                        eof before the read that fails, readerwriter.h:50-57).
+  //   file_order = false — graph2tree -p -o (:588-630): the graph's node order, X
+  //                        ascending, its adjacency in load (record) order, only X < Y.
+  void writePartitionedGraph(const GraphWrapper &g, const DeviceSequence &seq, const char *prefix,
+                             bool file_order) const {
+    const uint64_t R = g.numRecords();
+    DeviceArray<int16_t> dpart(R);
+    check(sheep_edge_parts(ctx(), g.records(), R, seq.pos.get(), seq.pos_size, parts_.get(), dpart.get()));
+    std::vector<int16_t> ep(R);
+    if (R) dpart.download(ep.data(), R);
+    const std::vector<sheep_xs1> rec = g.hostRecords();
+    const std::vector<part_t> pv = parts();
+    part_t max_part = -1;
+    for (part_t x : pv) max_part = std::max(max_part, x);
+    if (max_part >= 10000) throw std::runtime_error("writePartitionedGraph: more than 9999 parts (partition.cpp:599)");
+    std::vector<FILE *> files;
+    std::vector<std::string> bufs(max_part + 1);
+    for (part_t p = 0; p <= max_part; ++p) {
+      char name[4096];
+      snprintf(name, sizeof name, "%s%04d", prefix, (int)p);
+      FILE *f = fopen(name, "w");
+      if (!f) {
+        for (FILE *o : files) fclose(o);
+        throw std::runtime_error(std::string("cannot create ") + name);
+      }
+      files.push_back(f);
+    }
+    auto put = [&](part_t p, uint32_t x, uint32_t y) {
+      std::string &b = bufs.at(p);
+      char line[32];
+      const int len = snprintf(line, sizeof line, "%u %u\n", x, y);
+      b.append(line, len);
+      if (b.size() > (1u << 20)) { fwrite(b.data(), 1, b.size(), files[p]); b.clear(); }
+    };
+    if (file_order) {
+      for (uint64_t i = 0; i < R; ++i) put(ep[i], rec[i].tail, rec[i].head);
+      if (g.isDat() && R) put(ep[R - 1], rec[R - 1].tail, rec[R - 1].head);
+    } else {
+      // counting sort of the non-loop records by their smaller vid, stable in record order
+      const uint64_t vmax = g.getMaxVid();
+      std::vector<uint64_t> start(vmax + 1, 0);
+      for (uint64_t i = 0; i < R; ++i)
+        if (rec[i].tail != rec[i].head) ++start[std::min(rec[i].tail, rec[i].head) + 1];
+      for (uint64_t v = 0; v < vmax; ++v) start[v + 1] += start[v];
+      std::vector<uint64_t> order(start[vmax]);
+      for (uint64_t i = 0; i < R; ++i)
+        if (rec[i].tail != rec[i].head) order[start[std::min(rec[i].tail, rec[i].head)]++] = i;
+      for (uint64_t i : order)
+        put(ep[i], std::min(rec[i].tail, rec[i].head), std::max(rec[i].tail, rec[i].head));
+    }
+    for (part_t p = 0; p <= max_part; ++p) {
+      fwrite(bufs[p].data(), 1, bufs[p].size(), files[p]);
+      fclose(files[p]);
+    }
   }
 
  private:

@@ -21,6 +21,8 @@ Outputs per graph G (see MANIFEST.json for md5s):
   G.merge.tre      merge_trees CLI over the two halves
   G.part.txt       partition_tree -f -g flow (TREEFAQS, per-k print + both evaluators)
   G.k<K>.parts     vid-indexed int16 parts per k (same run, so kid order persists)
+  G.k<K>.g%04d     writePartitionedGraph(graph, seq, prefix) files (graph2tree -p K -o)
+  G.k<K>.f%04d     writePartitionedGraph(filename, seq, prefix) files (partition_tree -o)
 """
 import hashlib
 import json
@@ -37,6 +39,9 @@ REF = os.path.join(ROOT, "oracle", "_ref")
 sys.path.insert(0, ROOT)
 
 KS = {"hep": [2, 3, 4, 16, 64], "rmat10": [2, 16], "rmat12": [4, 16, 64], "rmat14": [16, 64], "edge": [1, 2, 3]}
+# partition files (writePartitionedGraph): graph order (graph2tree -p -o) -> G.k<K>.g%04d,
+# input-file order (partition_tree -g G -o) -> G.k<K>.f%04d
+WRITE_K = {"hep": 4, "rmat10": 16, "edge": 2}
 
 
 def run(*args, **kw):
@@ -95,6 +100,11 @@ def main():
         out = run(H, "part", dat, os.path.join(HERE, f"{name}.seq"), a, os.path.join(HERE, f"{name}."),
                   *KS[name])
         open(os.path.join(HERE, f"{name}.part.txt"), "w").write(out)
+        if name in WRITE_K:
+            k = WRITE_K[name]
+            for cmd, tag in (("write", "g"), ("writefile", "f")):
+                shutil.copyfile(os.path.join(HERE, f"{name}.tre"), a)
+                run(H, cmd, dat, os.path.join(HERE, f"{name}.seq"), a, k, os.path.join(HERE, f"{name}.k{k}.{tag}"))
     shutil.rmtree(tmp)
     for f in sorted(os.listdir(HERE)):
         if f.endswith((".py", ".json")) or f.startswith("_"):
@@ -105,6 +115,7 @@ def main():
     for big in ("rmat12.dat", "rmat14.dat"):
         os.remove(os.path.join(HERE, big))
     manifest["_ks"] = KS
+    manifest["_write_k"] = WRITE_K
     manifest["_rmat"] = {"rmat10": [10, 16, 10], "rmat12": [12, 16, 12], "rmat14": [14, 16, 14]}
     json.dump(manifest, open(os.path.join(HERE, "MANIFEST.json"), "w"), indent=1, sort_keys=True)
     print(f"wrote {len(manifest)} entries")

@@ -52,6 +52,15 @@ def _rank_main(rank, world, port, name, out_path):
 
         tree = sdist.reduce_trees(tree, merge, rank, world)
         assert (tree is None) == (rank != 0)
+        # Partition::mpi_sync: rank 0 partitions, every rank gets the parts
+        parts = None
+        if rank == 0:
+            t0 = tree.numpy().view(np.uint32)
+            parts = torch.from_numpy(oracle.partition(t0[:, 0], t0[:, 1], seq, 4)[0])
+        n_slots = int(seq.max()) + 1
+        parts = sdist.sync_parts(parts, n_slots, "cpu")
+        gp, gw = golden_tree(name)
+        assert np.array_equal(parts.numpy(), oracle.partition(gp, gw, seq, 4)[0])
         if rank == 0:
             t = tree.numpy().view(np.uint32)
             json.dump({"seq": seq.tolist(), "parent": t[:, 0].tolist(), "pst": t[:, 1].tolist()}, open(out_path, "w"))
