@@ -98,6 +98,7 @@ def lib() -> ctypes.CDLL:
         "sheep_partition": ([P, P, U64, P, U64, P, I16, D, I32, I32, P, ctypes.POINTER(_PartInfo)], I32),
         "sheep_evaluate": ([P, P, U64, P, U64, P, I32, ctypes.POINTER(_Eval)], I32),
         "sheep_facts": ([P, P, U64, ctypes.POINTER(_Facts)], I32),
+        "sheep_edge_parts": ([P, P, U64, P, U64, P, P], I32),
         "sheep_rmat_generate": ([P, I32, I32, U64, P, U64, ctypes.POINTER(U64)], I32),
         "sheep_rmat_generate_host": ([I32, I32, U64, P, U64, ctypes.POINTER(U64)], I32),
     }
@@ -407,6 +408,18 @@ def evaluate(records, seq: Sequence, parts, what: int = 0, nrec: int | None = No
     _check(lib().sheep_evaluate(ctx.handle, _ptr(records), nrec, _ptr(seq.pos), seq.pos_size, _ptr(parts), what,
                                 ctypes.byref(out)))
     return EvalResult(*[getattr(out, f) for f, _ in _Eval._fields_])
+
+
+def edge_parts(records, seq: Sequence, parts, nrec: int | None = None, ctx: Context | None = None):
+    """Part each record is written to by writePartitionedGraph (partition.cpp:588-670):
+    the part of its earlier-positioned endpoint (device int16 per record)."""
+    ctx = ctx or default_context()
+    nrec = records.shape[0] if nrec is None else nrec
+    t = _torch()
+    out = t.empty(max(int(nrec), 1), dtype=t.int16, device="cuda")
+    _check(lib().sheep_edge_parts(ctx.handle, _ptr(records), nrec, _ptr(seq.pos), seq.pos_size, _ptr(parts),
+                                  _ptr(out)))
+    return out[:nrec]
 
 
 @dataclass
