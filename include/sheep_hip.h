@@ -150,6 +150,12 @@ int sheep_build_tree(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec,
 /* ---- reduce: merge two trees over the same n ------------------------------------ */
 int sheep_merge_trees(sheep_ctx *ctx, const sheep_jnode *a_dev, const sheep_jnode *b_dev,
                       uint64_t n, sheep_jnode *out_dev);
+/* k trees over the same n, stored one after another (trees_dev[j * n + i]): the whole
+ * reduction mpi_merge performs over k ranks (jnode.cpp:203-250, MPI_Reduce with
+ * mpi_merge_reduction) in one pass — the elimination tree of the union of all k
+ * parent-edge sets, pst summed.  Equal to any order of k - 1 sheep_merge_trees calls. */
+int sheep_merge_trees_many(sheep_ctx *ctx, const sheep_jnode *trees_dev, uint32_t k,
+                           uint64_t n, sheep_jnode *out_dev);
 
 /* ---- partition ------------------------------------------------------------------ */
 int sheep_kids_create(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n,

@@ -93,6 +93,7 @@ def lib() -> ctypes.CDLL:
         "sheep_positions": ([P, P, U64, P, U64], I32),
         "sheep_build_tree": ([P, P, U64, P, U64, U64, P], I32),
         "sheep_merge_trees": ([P, P, P, U64, P], I32),
+        "sheep_merge_trees_many": ([P, P, ctypes.c_uint32, U64, P], I32),
         "sheep_kids_create": ([P, P, U64, ctypes.POINTER(P)], I32),
         "sheep_kids_destroy": ([P], I32),
         "sheep_partition": ([P, P, U64, P, U64, P, I16, D, I32, I32, P, ctypes.POINTER(_PartInfo)], I32),
@@ -288,6 +289,18 @@ def merge_trees(a, b, ctx: Context | None = None):
         raise ValueError("trees of different sizes")
     out = t.empty((max(n, 1), 2), dtype=t.int32, device="cuda")
     _check(lib().sheep_merge_trees(ctx.handle, _ptr(a), _ptr(b), n, _ptr(out)))
+    return out[:n]
+
+
+def merge_trees_many(trees, ctx: Context | None = None):
+    """The whole mpi_merge reduction (jnode.cpp:203-250) in one pass: `trees` is a
+    (k, n, 2) int32 tensor of k partial trees; returns their merged tree."""
+    ctx = ctx or default_context()
+    t = _torch()
+    k, n = trees.shape[0], trees.shape[1]
+    trees = trees.contiguous()
+    out = t.empty((max(n, 1), 2), dtype=t.int32, device="cuda")
+    _check(lib().sheep_merge_trees_many(ctx.handle, _ptr(trees), k, n, _ptr(out)))
     return out[:n]
 
 

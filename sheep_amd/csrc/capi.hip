@@ -21,6 +21,7 @@ void positions(Ctx &c, const uint32_t *seq, uint64_t n, uint32_t *pos, uint64_t 
 void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size, uint64_t n,
                       sheep_jnode *tree);
 void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n, sheep_jnode *out);
+void merge_trees_many(Ctx &c, const sheep_jnode *trees, uint32_t k, uint64_t n, sheep_jnode *out);
 void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t *seq, uint64_t pos_size,
                     sheep_kids *k, int16_t np, double balance, int vtx, int pstw, int16_t *parts_vid,
                     sheep_partition_info *info);
@@ -205,6 +206,14 @@ int sheep_merge_trees(sheep_ctx *ctx, const sheep_jnode *a, const sheep_jnode *b
   API_BEGIN
   NEED(ctx && ((a && b && out) || !n), "null argument");
   sheep::merge_trees(ctx->c, a, b, n, out);
+  API_END
+}
+
+int sheep_merge_trees_many(sheep_ctx *ctx, const sheep_jnode *trees, uint32_t k, uint64_t n, sheep_jnode *out) {
+  API_BEGIN
+  NEED(ctx && ((trees && out) || !n), "null argument");
+  NEED(k >= 1, "merge: no trees");
+  sheep::merge_trees_many(ctx->c, trees, k, n, out);
   API_END
 }
 

@@ -240,7 +240,8 @@ void histogram_edge_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t K, ui
 void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, int L, uint32_t clo, uint32_t *pst,
                        uint64_t *r0, uint64_t *seg);
 // etree.hip
-void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg);
+void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
+                      int fin_bits, uint32_t per_lo);
 void spread_params(uint64_t n, int *L, uint32_t *clo);
 // append.hip — sharded appends: counters (NSHARD * SHARD_STRIDE u64, zeroed).  The pack
 // step moves the shard regions of a producer that streamed *n_in items together in dst

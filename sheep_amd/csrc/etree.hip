@@ -21,6 +21,7 @@
 // component with a cross edge; vertices never assigned are roots.  The result is the
 // unique elimination tree of (edge multiset, order) — identical to Liu's.  Level
 // ranges are dyadic in a monotone spread of [0,n) onto [0,2^L) so halves are balanced.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -39,6 +40,7 @@ __device__ __forceinline__ uint32_t spread(uint32_t x, uint32_t clo) { return x 
 // of x.  Plain loads/stores are therefore safe while other threads hook: a stale root
 // only makes its CAS fail, and the edge is simply kept for the next round.  The
 // component's top (its largest id, which the etree needs) is tracked separately.
+// (Linking under the larger root instead, so root = top, measured 2x slower hooking.)
 
 // Path splitting on two chains in lockstep (both loads in flight at once).
 __device__ __forceinline__ void find2(uint32_t *uf, uint32_t &x, uint32_t &y) {
@@ -184,11 +186,57 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t *__restrict__ uf, uint
   for (uint64_t i = t0; i < NCSET * CSET_WORDS; i += stride) csets[i] = 0;
 }
 
+// End of a level: back to the reset state for the next one.  Only light endpoints (uf,
+// top), cross roots (mt) and cross hi ends (claim) were written, so when those lists are
+// short against n they are undone entry by entry (k_cross_apply then also stored the
+// parents); otherwise a dense pass assigns parent(top of every component with a cross
+// edge) = m_r (jnode.h:158-162 adopt) and rewrites the arrays whole.  The choice is made
+// on the device from the level's counts (no host round trip).
+__device__ __forceinline__ bool level_sparse(uint64_t nl, uint64_t nx, uint64_t n) {
+  return (nl + nx) * 8 < n;   // a scattered 4-B store costs about a line; a dense pass 16 B per vertex
+}
+
+__global__ __launch_bounds__(BLOCK) void k_level_clean(const uint64_t *__restrict__ lbuf, const uint64_t *__restrict__ xbuf,
+                                                       const uint32_t *__restrict__ xtop,
+                                                       const uint64_t *__restrict__ st, uint32_t *__restrict__ uf,
+                                                       uint32_t *__restrict__ mt, uint32_t *__restrict__ top,
+                                                       uint32_t *__restrict__ claim, uint64_t n,
+                                                       uint32_t *__restrict__ parent,
+                                                       unsigned long long *__restrict__ csets) {
+  const uint64_t nl = st[ST_NL], nx = st[ST_NX];
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const uint64_t t0 = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (uint64_t i = t0; i < NCSET * CSET_WORDS; i += stride) csets[i] = 0;
+  if (!level_sparse(nl, nx, n)) {
+    for (uint64_t i = t0; i < n; i += stride) {
+      const uint32_t m = mt[i];
+      if (m != INVALID && uf[i] == i) parent[top[i]] = m;
+      uf[i] = (uint32_t)i;
+      mt[i] = INVALID;
+      top[i] = (uint32_t)i;
+      claim[i] = INVALID;
+    }
+    return;
+  }
+  for (uint64_t i = t0; i < nl; i += stride) {
+    const uint64_t e = lbuf[i];
+    const uint32_t a = (uint32_t)e, b = (uint32_t)(e >> 32);
+    uf[a] = a;
+    uf[b] = b;
+    top[a] = a;
+    top[b] = b;
+  }
+  for (uint64_t i = t0; i < nx; i += stride) {
+    mt[xtop[i]] = INVALID;
+    claim[(uint32_t)(xbuf[i] >> 32)] = INVALID;
+  }
+}
+
+constexpr int XK = 4;   // items per thread in the gather kernels (independent chains in flight)
+
 // top[root] = the component's largest id.  Every vertex of a non-singleton light
 // component is an endpoint of a light edge and its maximum is the hi end of one, so a
 // max over the light edges' hi ends suffices (singletons keep top = self).
-constexpr int XK = 4;   // items per thread in the gather kernels (independent chains in flight)
-
 __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict__ lbuf, const uint64_t *__restrict__ n_l,
                                                      uint32_t *uf, uint32_t *__restrict__ top) {
   const uint64_t nl = *n_l;
@@ -276,17 +324,6 @@ __global__ __launch_bounds__(BLOCK) void k_hook_finish(const uint64_t *__restric
   }
 }
 
-// parent(top of every component with a cross edge) = m_r (jnode.h:158-162 adopt).
-__global__ __launch_bounds__(BLOCK) void k_assign_parents(const uint32_t *__restrict__ uf, const uint32_t *__restrict__ mt,
-                                                          const uint32_t *__restrict__ top, uint64_t n,
-                                                          uint32_t *__restrict__ parent) {
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride) {
-    const uint32_t m = mt[v];
-    if (m != INVALID && uf[v] == v) parent[top[v]] = m;
-  }
-}
-
 // For every cross edge (a,b): r = root of a's light component; m_r = min b (atomicMin).
 __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict__ xbuf, const uint64_t *__restrict__ n_x,
                                                       uint32_t *uf, uint32_t *__restrict__ mt, uint32_t *__restrict__ xtop) {
@@ -338,12 +375,16 @@ __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict
 // cross edge j goes to next[kept + j] (DEAD if it died) — a sequential write.
 __global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restrict__ xbuf, const uint32_t *__restrict__ xtop,
                                                        const uint64_t *__restrict__ st, const uint32_t *__restrict__ mt,
-                                                       uint32_t *__restrict__ claim, uint64_t *__restrict__ next) {
+                                                       const uint32_t *__restrict__ top, uint32_t *__restrict__ claim,
+                                                       uint64_t *__restrict__ next, uint32_t *__restrict__ parent,
+                                                       uint64_t n) {
   const uint64_t nx = st[ST_NX];
+  const bool sparse = level_sparse(st[ST_NL], nx, n);
   uint64_t *out = next + st[ST_KEPT];
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < nx; j += stride) {
-    const uint32_t m = mt[xtop[j]];
+    const uint32_t r = xtop[j], m = mt[r];
+    if (sparse) parent[top[r]] = m;   // jnode.h:158-162 adopt (all cross edges of r store the same m)
     const uint32_t b = (uint32_t)(xbuf[j] >> 32);
     bool kill = b == m;
     if (!kill) {
@@ -479,6 +520,178 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
   }
 }
 
+// ---- the last levels: Liu's algorithm per block -------------------------------------
+// Below level B the subproblems are blocks of 2^B spread positions (at most as many
+// vertices), independent of each other: every live edge has both ends in one block, and
+// a vertex whose parent an earlier level assigned is a root of its block's elimination
+// tree (it was the top of its light component, so every later neighbour it had lay in
+// the other half and its edges there were contracted away).  So each block runs the
+// reference's own sequential algorithm — Liu's, jtree.cpp:66-110 — on its edges sorted
+// by hi: for each edge (a, v), r = find(a); if r != v, parent[r] = v and r links under v.
+// ONE LANE per block, its union-find in LDS (one byte per vertex, lane l's entry x at
+// x * 64 + l), so B levels of a dozen launches each become one launch.
+// A block with more than FIN_HEAVY edges (a hub's block) is handed to a whole wave
+// instead, which takes the edges of one hi 64 at a time.  Used for merges, whose edges
+// (two parent edges per node plus contractions) spread evenly over the blocks.
+constexpr int FIN_BITS_MAX = 8;     // 2^8 one-byte entries x 64 lanes = 16 KB of LDS per wave
+constexpr uint64_t FIN_HEAVY = 256;
+
+__global__ void k_fin_gather(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
+                             const uint64_t *__restrict__ r0, uint64_t rb, uint64_t re, uint64_t *__restrict__ out,
+                             uint64_t *__restrict__ n_out) {
+  // out = list ++ r0[rb, re), halves swapped (lo << 32 | hi) so a sort on the low bits sorts by hi
+  const uint64_t len = prev ? prev[ST_KEPT] + prev[ST_NX] : 0, m = len + (re - rb);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *n_out = m;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    const uint64_t e = i < len ? list[i] : r0[rb + (i - len)];
+    out[i] = e == DEAD ? DEAD : (e << 32) | (e >> 32);
+  }
+}
+
+// Block bounds and classes.  eb[b] = first sorted entry of block b (an entry's block is
+// spread(hi) >> B; eb[nb] = first DEAD entry), found by binary search — live edges crowd
+// into a fraction of the blocks, so boundary detection would leave single threads to
+// fill long runs of empty ones.  vb[b] = first vertex of block b (vb[nb] = n), by
+// boundary detection over the vertices (every block holds at least one).  Non-empty
+// blocks go to the light list (one lane each) or, above FIN_HEAVY edges, the heavy list.
+__global__ __launch_bounds__(BLOCK) void k_fin_bounds(const uint64_t *__restrict__ fin, const uint64_t *__restrict__ n_fin,
+                                                      uint32_t clo, int B, uint64_t nb, uint64_t n,
+                                                      uint64_t *__restrict__ eb, uint32_t *__restrict__ vb,
+                                                      uint32_t *__restrict__ light, uint32_t *__restrict__ heavy,
+                                                      unsigned long long *__restrict__ n_lh) {
+  const uint64_t nf = *n_fin;
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const uint64_t t0 = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  auto lower = [&](uint64_t b) {   // first entry whose block is >= b (DEAD: block nb)
+    uint64_t a = 0, z = nf;
+    while (a < z) {
+      const uint64_t x = (a + z) / 2;
+      const uint64_t e = fin[x];
+      const uint64_t eb_x = e == DEAD ? nb : spread((uint32_t)e, clo) >> B;
+      if (eb_x < b) a = x + 1; else z = x;
+    }
+    return a;
+  };
+  const uint64_t iters = (nb + stride - 1) / stride;   // wave-uniform (appends below)
+  for (uint64_t it = 0; it < iters; ++it) {
+    const uint64_t b = t0 + it * stride;
+    uint64_t e0 = 0, e1 = 0;
+    if (b < nb) {
+      e0 = lower(b);
+      e1 = lower(b + 1);
+      eb[b] = e0;
+      if (b + 1 == nb) eb[nb] = e1;
+    }
+    const bool big = e1 - e0 > FIN_HEAVY, small = e1 > e0 && !big;
+    const uint64_t sl = wave_append(small, n_lh), sh = wave_append(big, n_lh + 1);
+    if (small) light[sl] = (uint32_t)b;
+    if (big) heavy[sh] = (uint32_t)b;
+  }
+  auto vblk = [&](uint64_t x) -> uint64_t { return x >= n ? nb : spread((uint32_t)x, clo) >> B; };
+  for (uint64_t x = t0; x <= n; x += stride) {
+    const uint64_t lo = x ? vblk(x - 1) + 1 : 0, hi = vblk(x);
+    for (uint64_t b = lo; b <= hi; ++b) vb[b] = (uint32_t)x;
+  }
+}
+
+template <int B>
+__global__ __launch_bounds__(WAVE) void k_fin_lanes(const uint64_t *__restrict__ fin, const uint64_t *__restrict__ eb,
+                                                    const uint32_t *__restrict__ vb, const uint32_t *__restrict__ light,
+                                                    const unsigned long long *__restrict__ n_light,
+                                                    uint32_t *__restrict__ parent) {
+  static_assert(B <= 8, "one-byte union-find entries");
+  __shared__ uint8_t uf[(1 << B) * WAVE];
+  const int l = threadIdx.x;
+  const uint64_t j = (uint64_t)blockIdx.x * WAVE + l;
+  if (j >= *n_light) return;
+  const uint32_t b = light[j];
+  const uint64_t e0 = eb[b], e1 = eb[b + 1];
+  const uint32_t v0 = vb[b], cnt = vb[b + 1] - v0;
+  for (uint32_t x = 0; x < cnt; ++x) uf[x * WAVE + l] = (uint8_t)x;
+  // eight loads in flight per lane: the lanes walk distinct ranges, so each load is a miss
+  for (uint64_t p = e0; p < e1; p += 8) {
+    uint64_t ev[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ev[k] = p + k < e1 ? fin[p + k] : DEAD;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (ev[k] == DEAD) break;
+      const uint32_t v = (uint32_t)ev[k] - v0;
+      uint32_t x = (uint32_t)(ev[k] >> 32) - v0;
+      if (x >= cnt || v >= cnt) continue;   // both ends lie in the block (the D&C invariant)
+      uint32_t px = uf[x * WAVE + l];
+      while (px != x) {   // path halving
+        const uint32_t g = uf[px * WAVE + l];
+        uf[x * WAVE + l] = (uint8_t)g;
+        x = g;
+        px = uf[x * WAVE + l];
+      }
+      if (x != v) {
+        parent[v0 + x] = v0 + v;
+        uf[x * WAVE + l] = (uint8_t)v;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t fin_find(uint8_t *uf, uint32_t x) {
+  uint32_t p = uf[x];
+  while (p != x) {   // path halving (pointers only move up: safe with other lanes)
+    const uint32_t g = uf[p];
+    uf[x] = (uint8_t)g;
+    x = g;
+    p = uf[x];
+  }
+  return x;
+}
+
+// A heavy block: one wave, its edges staged through LDS FIN_STAGE at a time (coalesced),
+// then taken one hi at a time, 64 edges per step.  Lanes with the same root store the
+// same link; distinct roots link under v side by side, as Liu's loop over v's
+// neighbours would.
+constexpr int FIN_STAGE = 2048;
+template <int B>
+__global__ __launch_bounds__(WAVE) void k_fin_heavy(const uint64_t *__restrict__ fin, const uint64_t *__restrict__ eb,
+                                                    const uint32_t *__restrict__ vb, const uint32_t *__restrict__ heavy,
+                                                    const unsigned long long *__restrict__ n_heavy,
+                                                    uint32_t *__restrict__ parent) {
+  __shared__ uint8_t uf[1 << B];
+  __shared__ uint64_t stage[FIN_STAGE];
+  const int lane = threadIdx.x;
+  const unsigned long long nh = *n_heavy;
+  for (uint64_t h = blockIdx.x; h < nh; h += gridDim.x) {
+    const uint32_t b = heavy[h];
+    const uint32_t v0 = vb[b], cnt = vb[b + 1] - v0;
+    const uint64_t e0 = eb[b], e1 = eb[b + 1];
+    __syncthreads();   // the previous block is done with uf and stage
+    for (uint32_t i = lane; i < cnt; i += WAVE) uf[i] = (uint8_t)i;
+    for (uint64_t base = e0; base < e1; base += FIN_STAGE) {
+      const uint32_t len = (uint32_t)(e1 - base < FIN_STAGE ? e1 - base : FIN_STAGE);
+      __syncthreads();
+      for (uint32_t i = lane; i < len; i += WAVE) stage[i] = fin[base + i];
+      __syncthreads();
+      for (uint32_t p = 0; p < len;) {
+        const uint32_t v = (uint32_t)stage[p];
+        const uint32_t idx = p + lane;
+        const uint64_t e = idx < len ? stage[idx] : DEAD;
+        const bool mine = e != DEAD && (uint32_t)e == v;
+        const uint64_t mask = __ballot(mine);
+        const uint32_t x = (uint32_t)(e >> 32) - v0, vv = v - v0;
+        if (mine && x < cnt && vv < cnt) {
+          const uint32_t r = fin_find(uf, x);
+          if (r != vv) {
+            parent[v0 + r] = v;
+            uf[r] = (uint8_t)vv;
+          }
+        }
+        __syncthreads();   // this v's links before the next v's finds
+        p += __popcll(mask);   // v's entries are a prefix of the window (sorted by hi)
+      }
+    }
+  }
+}
+
 // Parent edges of both trees, in place: edges[2i] from a, edges[2i+1] from b (DEAD when
 // absent or equal to a's).
 __global__ __launch_bounds__(BLOCK) void k_tree_edges(const sheep_jnode *__restrict__ a, const sheep_jnode *__restrict__ b,
@@ -501,6 +714,33 @@ __global__ __launch_bounds__(BLOCK) void k_tree_edges(const sheep_jnode *__restr
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(err, 1ull);
 }
 
+// K trees stored one after another (trees[k * n + i]): edges[K i + k] = node i's parent
+// edge in tree k, DEAD when absent or equal to an earlier tree's; pst = the sum.
+__global__ __launch_bounds__(BLOCK) void k_tree_edges_many(const sheep_jnode *__restrict__ trees, uint32_t K,
+                                                           uint64_t n, uint64_t *__restrict__ edges,
+                                                           uint32_t *__restrict__ pst_out,
+                                                           unsigned long long *__restrict__ err) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  bool bad = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
+    uint32_t w = 0;
+    for (uint32_t k = 0; k < K; ++k) {
+      const sheep_jnode x = trees[(uint64_t)k * n + i];
+      w += x.pst_weight;
+      uint32_t p = x.parent;
+      if (p != INVALID && (p <= i || p >= n)) {
+        bad = true;
+        p = INVALID;
+      }
+      for (uint32_t j = 0; j < k && p != INVALID; ++j)
+        if ((uint32_t)(edges[K * i + j] >> 32) == p) p = INVALID;
+      edges[K * i + k] = p != INVALID ? ((uint64_t)p << 32) | (uint32_t)i : DEAD;
+    }
+    pst_out[i] = w;
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(err, 1ull);
+}
+
 __global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t *__restrict__ pst, uint64_t n,
                             sheep_jnode *__restrict__ out) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
@@ -517,6 +757,15 @@ __global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t 
 void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
 
 static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
+static int env_int(const char *name, int def) {
+  const char *v = getenv(name);
+  return v && *v ? atoi(v) : def;
+}
+// Finishing block size (log2 positions) of the per-block Liu pass: merges use it; a
+// map's hub blocks would pile onto single lanes, so maps run every level globally.
+// SHEEP_FIN_MERGE / SHEEP_FIN_MAP override (0 = off) for experiments.
+static const int g_fin_merge = env_int("SHEEP_FIN_MERGE", 8);
+static const int g_fin_map = env_int("SHEEP_FIN_MAP", 0);
 
 // spread(x) = floor(x * c / 2^32), c = floor(2^(32+L) / n) in [2^32, 2^33), L = ceil(log2 n):
 // monotone, injective on [0,n), image in [0, 2^L).  clo = c - 2^32.
@@ -534,11 +783,12 @@ static uint64_t list_capacity(uint64_t m) { return 2 * m + TILE; }
 
 // Elimination tree of `m` edges ((hi<<32)|lo, lo < hi < n, DEAD holes allowed), grouped
 // by first active level: seg[s] / seg[L + s] (device) delimit group s.  seg == nullptr:
-// the edges are a merge's parent edges (entries 2 lo, 2 lo + 1), whose groups are
+// the edges are a merge's parent edges (entries per_lo * lo + k), whose groups are
 // computed here.  The edges are read only.
 // One pass of launches per level, no host synchronisation inside the loop (see the
 // stats row above); the stats come back once at the end for the timers / debug log.
-void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg_in) {
+void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg_in,
+                      int fin_bits, uint32_t per_lo) {
   fill_u32(c, parent, n, INVALID);
   if (n < 2 || m == 0) return;
   if (m >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "too many edges for one shard");
@@ -562,7 +812,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   if (!seg) {
     uint64_t *dseg = c.get_as<uint64_t>("et_seg", 2 * (uint64_t)L);
     seg = dseg;
-    // bucket s = lo with ya in [2^L - 2^(s+1), 2^L - 2^s): a range of lo, entries 2 lo, 2 lo + 1
+    // bucket s = lo with ya in [2^L - 2^(s+1), 2^L - 2^s): a range of lo, entries per_lo * lo + k
     auto first_lo = [&](uint64_t y) {   // min lo with spread(lo) >= y
       uint64_t a = 0, b = n;
       while (a < b) {
@@ -573,8 +823,8 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     };
     uint64_t *h = (uint64_t *)c.get_pinned("et_seg_host", 2 * (size_t)L * sizeof(uint64_t));
     for (int b = 0; b < L; ++b) {
-      h[b] = 2 * first_lo((1ull << L) - (2ull << b));
-      h[L + b] = 2 * first_lo((1ull << L) - (1ull << b));
+      h[b] = per_lo * first_lo((1ull << L) - (2ull << b));
+      h[L + b] = per_lo * first_lo((1ull << L) - (1ull << b));
       if (h[L + b] > m) h[L + b] = m;
       if (h[b] > h[L + b]) h[b] = h[L + b];
     }
@@ -583,21 +833,24 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   // a split reads at most the list plus a bucket: (lcap + m) entries, in TILE tiles
   const uint64_t cstride = (lcap + m + TILE - 1) / TILE + 1;
   uint64_t *tcnt = c.get_as<uint64_t>("et_tilecnt", 3 * cstride + 1);
-  uint64_t *lbuf = c.get_as<uint64_t>("et_light", mcap);  // must outlive the hook rounds (k_light_top)
+  uint64_t *lbuf = c.get_as<uint64_t>("et_light", mcap);  // must outlive the hook rounds (k_level_clean)
   uint64_t *alt = c.get_as<uint64_t>("et_alt", mcap);     // shard scratch of the hook rounds
   uint64_t *hk[2] = {c.get_as<uint64_t>("et_lwa", mcap), c.get_as<uint64_t>("et_lwb", mcap)};
   unsigned long long *csets = c.get_as<unsigned long long>("et_csets", NCSET * CSET_WORDS);
-  uint64_t *stats = c.get_as<uint64_t>("et_stats", (uint64_t)L * ST_ROW);
-  HIP_CHECK(hipMemsetAsync(stats, 0, (uint64_t)L * ST_ROW * sizeof(uint64_t), c.stream));
+  uint64_t *stats = c.get_as<uint64_t>("et_stats", (uint64_t)(L + 1) * ST_ROW);
+  HIP_CHECK(hipMemsetAsync(stats, 0, (uint64_t)(L + 1) * ST_ROW * sizeof(uint64_t), c.stream));
   auto cset = [&](int k) { return csets + (uint64_t)k * CSET_WORDS; };
   const unsigned gt = grid_tiles(m), gt2 = grid_tiles(lcap + m), gf = grid_for(m, BLOCK * XK), gn = grid_for(n);
-  for (int lvl = 0; lvl < L; ++lvl) {
+  const int FINB = fin_bits < 0 ? 0 : fin_bits > FIN_BITS_MAX ? FIN_BITS_MAX : fin_bits;   // levels s < FINB: Liu per block (0: none)
+  const int nglobal = L > FINB ? L - FINB : 0;
+  // the union-find state starts clean; each level restores it at its end (k_level_clean)
+  hipLaunchKernelGGL(k_reset, dim3(gn), dim3(BLOCK), 0, c.stream, uf, mt, top, claim, n, csets);
+  LAUNCH_CHECK();
+  for (int lvl = 0; lvl < nglobal; ++lvl) {
     const int s = L - 1 - lvl;
     uint64_t *st = stats + (uint64_t)lvl * ST_ROW;
     const uint64_t *prev = lvl ? st - ST_ROW : nullptr;
     uint64_t *cur = lists[lvl & 1], *next = lists[(lvl + 1) & 1];
-    hipLaunchKernelGGL(k_reset, dim3(gn), dim3(BLOCK), 0, c.stream, uf, mt, top, claim, n, csets);
-    LAUNCH_CHECK();
     {
       TimedRegion tr(c, "etree_split");
       HIP_CHECK(hipMemsetAsync(tcnt, 0, (3 * cstride + 1) * sizeof(uint64_t), c.stream));
@@ -635,19 +888,83 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     }
     {
       TimedRegion tr(c, "etree_apply");
-      hipLaunchKernelGGL(k_assign_parents, dim3(gn), dim3(BLOCK), 0, c.stream, (const uint32_t *)uf,
-                         (const uint32_t *)mt, (const uint32_t *)top, n, parent);
-      LAUNCH_CHECK();
       hipLaunchKernelGGL(k_cross_apply, dim3(grid_for(m)), dim3(BLOCK), 0, c.stream, (const uint64_t *)xbuf,
-                         (const uint32_t *)xtop, (const uint64_t *)st, (const uint32_t *)mt, claim, next);
+                         (const uint32_t *)xtop, (const uint64_t *)st, (const uint32_t *)mt, (const uint32_t *)top, claim, next, parent, n);
       LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_level_clean, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
+                         (const uint64_t *)xbuf, (const uint32_t *)xtop, (const uint64_t *)st, uf, mt, top, claim, n,
+                         parent, csets);
+      LAUNCH_CHECK();
+    }
+  }
+  if (FINB) {
+    // the last min(L, B) levels: the list plus the groups s < B, sorted by hi, then
+    // Liu's algorithm per 2^B-position block
+    TimedRegion tr(c, "etree_finish");
+    const int sg = (L < FINB ? L : FINB) - 1;   // highest group left
+    uint64_t hseg[2];
+    HIP_CHECK(hipMemcpyAsync(&hseg[0], seg + sg, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipMemcpyAsync(&hseg[1], seg + L, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+    const uint64_t *prev = nglobal ? stats + (uint64_t)(nglobal - 1) * ST_ROW : nullptr;
+    const uint64_t cap = lcap + (hseg[1] - hseg[0]);
+    uint64_t *fin = c.get_as<uint64_t>("et_fin", cap), *fin_alt = c.get_as<uint64_t>("et_fin_alt", cap);
+    uint64_t *n_fin = stats + (uint64_t)L * ST_ROW;
+    hipLaunchKernelGGL(k_fin_gather, dim3(grid_for(cap)), dim3(BLOCK), 0, c.stream, (const uint64_t *)lists[nglobal & 1],
+                       prev, r0, hseg[0], hseg[1], fin, n_fin);
+    LAUNCH_CHECK();
+    HIP_CHECK(hipMemcpyAsync(c.h_scalars + 15, n_fin, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+    const uint64_t nf = c.h_scalars[15];
+    if (nf) {
+      // L + 1 bits: hi < 2^L, and DEAD (all ones) sorts after every edge
+      radix_sort_keys_u64(c, fin, nf, L + 1, fin_alt);
+      const uint64_t nb = L > FINB ? 1ull << (L - FINB) : 1;
+      uint64_t *eb = c.get_as<uint64_t>("et_fin_eb", nb + 1);
+      uint32_t *vb = c.get_as<uint32_t>("et_fin_vb", nb + 1);
+      uint32_t *light = c.get_as<uint32_t>("et_fin_light", nb), *heavy = c.get_as<uint32_t>("et_fin_heavy", nb);
+      unsigned long long *n_lh = (unsigned long long *)(n_fin + 1);   // light, heavy counts (zeroed with stats)
+      hipLaunchKernelGGL(k_fin_bounds, dim3(grid_for(nb > n ? nb + 1 : n + 1)), dim3(BLOCK), 0, c.stream,
+                         (const uint64_t *)fin, (const uint64_t *)n_fin, clo, FINB, nb, n, eb, vb, light, heavy, n_lh);
+      LAUNCH_CHECK();
+      const unsigned gl = (unsigned)((nb + WAVE - 1) / WAVE), gh = (unsigned)(nb < 4096 ? nb : 4096);
+      switch (FINB) {
+#define SHEEP_FIN_CASE(B)                                                                                        \
+  case B:                                                                                                        \
+    hipLaunchKernelGGL(k_fin_lanes<B>, dim3(gl), dim3(WAVE), 0, c.stream, (const uint64_t *)fin, (const uint64_t *)eb, \
+                       (const uint32_t *)vb, (const uint32_t *)light, (const unsigned long long *)n_lh, parent);  \
+    LAUNCH_CHECK();                                                                                              \
+    hipLaunchKernelGGL(k_fin_heavy<B>, dim3(gh), dim3(WAVE), 0, c.stream, (const uint64_t *)fin, (const uint64_t *)eb, \
+                       (const uint32_t *)vb, (const uint32_t *)heavy, (const unsigned long long *)(n_lh + 1), parent); \
+    LAUNCH_CHECK();                                                                                              \
+    break;
+        SHEEP_FIN_CASE(1) SHEEP_FIN_CASE(2) SHEEP_FIN_CASE(3) SHEEP_FIN_CASE(4)
+        SHEEP_FIN_CASE(5) SHEEP_FIN_CASE(6) SHEEP_FIN_CASE(7) SHEEP_FIN_CASE(8)
+#undef SHEEP_FIN_CASE
+        default: throw Error(SHEEP_ERR_ARG, "etree: bad finishing block size");
+      }
+      if (g_debug_etree) {
+        std::vector<uint64_t> h(nb + 1);
+        uint64_t nh = 0;
+        HIP_CHECK(hipMemcpyAsync(h.data(), eb, (nb + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipMemcpyAsync(&nh, n_lh + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+        c.sync();
+        uint64_t mx = 0, nonempty = 0;
+        for (uint64_t b = 0; b < nb; ++b) {
+          mx = std::max(mx, h[b + 1] - h[b]);
+          nonempty += h[b + 1] > h[b];
+        }
+        fprintf(stderr, "etree finish B %d nf %lu live %lu blocks %lu nonempty %lu heavy %lu max-edges %lu\n", FINB,
+                (unsigned long)nf, (unsigned long)h[nb], (unsigned long)nb, (unsigned long)nonempty, (unsigned long)nh,
+                (unsigned long)mx);
+      }
     }
   }
   if (!c.timing && !g_debug_etree) return;
   std::vector<uint64_t> h((uint64_t)L * ST_ROW);
   HIP_CHECK(hipMemcpyAsync(h.data(), stats, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
-  for (int lvl = 0; lvl < L; ++lvl) {
+  for (int lvl = 0; lvl < nglobal; ++lvl) {
     const uint64_t *r = &h[(uint64_t)lvl * ST_ROW];
     uint64_t hooked = r[ST_NL];
     for (int k = 0; k < HOOK_ROUNDS - 1; ++k) hooked += r[ST_HOOK + k];
@@ -697,7 +1014,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
       group_edges_by_lo(c, edges, m, n, L, clo, pst, r0, seg);
     }
     TimedRegion tr(c, "etree", 8 * m);
-    etree_from_edges(c, r0, m, n, parent, seg);
+    etree_from_edges(c, r0, m, n, parent, seg, g_fin_map, 0);
   } else {
     fill_u32(c, parent, n, INVALID);
   }
@@ -721,7 +1038,32 @@ void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n,
   if (c.h_scalars[11]) throw Error(SHEEP_ERR_ARG, "merge: a parent is not a later node of the tree");
   {
     TimedRegion tr(c, "merge", 16 * n);
-    etree_from_edges(c, edges, 2 * n, n, parent, nullptr);
+    etree_from_edges(c, edges, 2 * n, n, parent, nullptr, g_fin_merge, 2);
+  }
+  hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);
+  LAUNCH_CHECK();
+}
+
+// K trees at once: the elimination tree of the union of all K parent-edge sets, the same
+// tree as K - 1 pairwise merges in any order (merge is associative and commutative) —
+// the whole of mpi_merge's reduction (jnode.cpp:203-250) in one pass.
+void merge_trees_many(Ctx &c, const sheep_jnode *trees, uint32_t K, uint64_t n, sheep_jnode *out) {
+  if (n == 0) return;
+  if (K == 0) throw Error(SHEEP_ERR_ARG, "merge: no trees");
+  if ((uint64_t)K * n >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "merge: too many parent edges for one pass");
+  uint32_t *pst = c.get_as<uint32_t>("mg_pst", n);
+  uint32_t *parent = c.get_as<uint32_t>("mg_parent", n);
+  uint64_t *edges = c.get_as<uint64_t>("mg_edges", (uint64_t)K * n);
+  unsigned long long *d = (unsigned long long *)c.d_scalars + 10;
+  HIP_CHECK(hipMemsetAsync(d + 1, 0, sizeof(uint64_t), c.stream));
+  hipLaunchKernelGGL(k_tree_edges_many, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, trees, K, n, edges, pst, d + 1);
+  LAUNCH_CHECK();
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 11, d + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  if (c.h_scalars[11]) throw Error(SHEEP_ERR_ARG, "merge: a parent is not a later node of the tree");
+  {
+    TimedRegion tr(c, "merge", 8 * (uint64_t)K * n);
+    etree_from_edges(c, edges, (uint64_t)K * n, n, parent, nullptr, g_fin_merge, K);
   }
   hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);
   LAUNCH_CHECK();

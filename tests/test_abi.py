@@ -29,7 +29,7 @@ def lib():
 def test_header_declares_the_path():
     names = declared()
     for must in ("sheep_degree_count", "sheep_sequence_from_degrees", "sheep_positions", "sheep_build_tree",
-                 "sheep_merge_trees", "sheep_kids_create", "sheep_partition", "sheep_evaluate", "sheep_facts"):
+                 "sheep_merge_trees", "sheep_merge_trees_many", "sheep_kids_create", "sheep_partition", "sheep_evaluate", "sheep_facts"):
         assert must in names
 
 

@@ -132,6 +132,45 @@ def test_shards_merge_to_whole_tree(gpu_ctx):
     assert np.array_equal(p, whole[0]) and np.array_equal(w, whole[1])
 
 
+@pytest.mark.parametrize("name", GRAPHS)
+def test_merge_many_golden_halves(gpu_ctx, name):
+    """sheep_merge_trees_many over the two golden half-shard trees == the golden merge."""
+    import sheep_amd
+    import torch
+    h = [sheep_amd.tree_to_device(*golden_tree(name, w)) for w in ("h1.tre", "h2.tre")]
+    p, w = _tree_np(sheep_amd.merge_trees_many(torch.stack(h)))
+    gp, gw = golden_tree(name, "merge.tre")
+    assert np.array_equal(p, gp) and np.array_equal(w, gw)
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 8])
+def test_merge_many_shards_to_whole_tree(gpu_ctx, k):
+    """k contiguous shards merged in ONE pass == the whole tree == pairwise merges."""
+    import sheep_amd
+    import torch
+    d = sheep_amd.rmat(17, 16, 7)
+    s = sheep_amd.degree_sequence(d)
+    whole = _tree_np(sheep_amd.build_tree(d, s))
+    R = d.shape[0]
+    parts = [sheep_amd.build_tree(d[i * R // k:(i + 1) * R // k], s) for i in range(k)]
+    p, w = _tree_np(sheep_amd.merge_trees_many(torch.stack(parts)))
+    assert np.array_equal(p, whole[0]) and np.array_equal(w, whole[1])
+    acc = parts[0]
+    for t in parts[1:]:
+        acc = sheep_amd.merge_trees(acc, t)
+    p2, w2 = _tree_np(acc)
+    assert np.array_equal(p2, whole[0]) and np.array_equal(w2, whole[1])
+
+
+def test_merge_many_rejects_bad_parent(gpu_ctx):
+    import sheep_amd
+    import torch
+    a = sheep_amd.tree_to_device(np.array([1, 2, 0xFFFFFFFF], np.uint32), np.zeros(3, np.uint32))
+    b = sheep_amd.tree_to_device(np.array([2, 0, 0xFFFFFFFF], np.uint32), np.zeros(3, np.uint32))   # 1 -> 0: not later
+    with pytest.raises(ValueError, match="not a later node"):   # SHEEP_ERR_ARG
+        sheep_amd.merge_trees_many(torch.stack([a, b]))
+
+
 def test_unsequenced_and_out_of_range(gpu_ctx):
     """A neighbour missing from the sequence counts as POSTORDER forever (jtree.cpp:84-90);
     a neighbour beyond max(seq) makes index.at() throw (jtree.cpp:75)."""

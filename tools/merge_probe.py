@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
-"""Time the reduce step alone: two half-shard trees of RMAT-<scale> merged on one GPU.
+"""Time the reduce step alone on one GPU: K shard trees of RMAT-<scale> reduced to one.
 
-    python tools/merge_probe.py [scale] [reps]
+    python tools/merge_probe.py [scale] [reps] [K]
 
-Prints the merge's wall time per call and the per-region device times (HIP events), and
-checks the merged tree against the whole-graph tree."""
+Two schedules are timed: the binomial pairwise schedule's critical path (the
+ceil(log2 K) merges rank 0 performs; the other ranks' merges are precomputed,
+untimed, as they would run on their own GPUs) and one K-way merge
+(sheep_merge_trees_many).  Both results are checked against the whole-graph tree.
+Prints wall time per reduction and the per-region device times (HIP events)."""
 import os
 import sys
 import time
@@ -17,27 +20,51 @@ def main():
     import sheep_amd
     scale = int(sys.argv[1]) if len(sys.argv) > 1 else 24
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    K = int(sys.argv[3]) if len(sys.argv) > 3 else 2
     ctx = sheep_amd.Context(0)
     rec = sheep_amd.rmat(scale, 16, scale, ctx=ctx)
     s = sheep_amd.degree_sequence(rec, ctx=ctx)
     R = rec.shape[0]
-    a = sheep_amd.build_tree(rec[: R // 2], s, ctx=ctx)
-    b = sheep_amd.build_tree(rec[R // 2:], s, ctx=ctx)
+    parts = [sheep_amd.build_tree(rec[i * R // K:(i + 1) * R // K], s, ctx=ctx) for i in range(K)]
     whole = sheep_amd.build_tree(rec, s, ctx=ctx)
-    m = sheep_amd.merge_trees(a, b, ctx=ctx)
-    assert torch.equal(m, whole), "merged tree differs from the whole-graph tree"
-    torch.cuda.synchronize()
-    ctx.timing(True)
-    ctx.timer_reset()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        m = sheep_amd.merge_trees(a, b, ctx=ctx)
-    torch.cuda.synchronize()
-    t = (time.perf_counter() - t0) / reps
-    print(f"RMAT-{scale}: n={s.n} merge {1e3 * t:.2f} ms/call")
-    for name in ctx.timer_names():
-        ms, launches, nbytes = ctx.timer(name)
-        print(f"  {name:16s} {ms / reps:8.3f} ms/call  launches {launches // reps}")
+    del rec
+    # binomial schedule: at hop r, rank i (i % 2r == 0) merges rank i + r's tree
+    inputs = []   # rank 0's (left, right) pair per hop
+    cur = list(parts)
+    r = 1
+    while r < K:
+        nxt = list(cur)
+        for i in range(0, K, 2 * r):
+            if i + r < K:
+                if i == 0:
+                    inputs.append(cur[i + r])
+                nxt[i] = sheep_amd.merge_trees(cur[i], cur[i + r], ctx=ctx)
+        cur = nxt
+        r *= 2
+    assert torch.equal(cur[0], whole), "pairwise merge differs from the whole-graph tree"
+    stacked = torch.stack(parts)
+    m = sheep_amd.merge_trees_many(stacked, ctx=ctx)
+    assert torch.equal(m, whole), "K-way merge differs from the whole-graph tree"
+    print(f"RMAT-{scale}: n={s.n} K={K} hops={len(inputs)}")
+    for label, fn in (("pairwise critical path", None), ("one K-way merge", None)):
+        torch.cuda.synchronize()
+        ctx.timing(True)
+        ctx.timer_reset()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            if label.startswith("pairwise"):
+                acc = parts[0]
+                for other in inputs:
+                    acc = sheep_amd.merge_trees(acc, other, ctx=ctx)
+            else:
+                sheep_amd.merge_trees_many(stacked, ctx=ctx)
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / reps
+        ctx.timing(False)
+        print(f"{label}: {1e3 * t:.2f} ms per reduction")
+        for name in ctx.timer_names():
+            ms, launches, nbytes = ctx.timer(name)
+            print(f"  {name:16s} {ms / reps:8.3f} ms  launches {launches / reps:g}")
 
 
 if __name__ == "__main__":
