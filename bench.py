@@ -4,7 +4,7 @@
 One step = the whole hot path over one synthetic graph already resident in HBM:
 
   degree count (per edge shard) -> [RCCL all-reduce of degrees] -> degree sequence
-  -> per-shard elimination tree (map) -> [log2(N) send/recv rounds + tree merge]
+  -> per-shard elimination tree (map) -> [gather to rank 0 + one K-way tree merge]
   -> makeKids + partition_tree forwardPartition (k parts) on rank 0
 
 (reference: graph2tree.cpp:161-216 `-ir` + partition_tree.cpp:130-143).
@@ -34,7 +34,7 @@ LEAF = ("degree", "degree_heads", "relabel", "pst_group", "etree_split", "etree_
 # kernels of a region, for roofline.traffic from the committed PMC passes (tools/pmc_traffic.py);
 # regions whose kernels are shared with other regions (histograms, packs) get traffic null
 REGION_KERNELS = {"relabel": ["k_relabel"], "degree": ["k_degree"], "etree_split": ["k_split"],
-                  "etree_cross": ["k_cross_find"], "etree_apply": ["k_assign_parents", "k_cross_apply"],
+                  "etree_cross": ["k_cross_find"], "etree_apply": ["k_cross_apply", "k_level_clean"],
                   "etree_compact": ["k_compact_edges"], "etree_bucket": ["k_bucket_count", "k_bucket_scatter"]}
 PMC_FILE = os.path.join(ROOT, "profiles", "r1", "pmc_traffic_rmat{scale}.json")
 
@@ -54,6 +54,9 @@ def parse():
                     help="gloo stages the exchanges through host memory (rehearsal)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on cuda:0 (rehearse N ranks on a 1-GPU box; needs gloo)")
+    ap.add_argument("--reduce", default="kway", choices=("kway", "binomial"),
+                    help="kway: gather the partial trees to rank 0 and merge them in one pass; "
+                         "binomial: ceil(log2 N) send/recv hops with a pairwise merge each")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 also builds the whole-graph tree and checks the merged one against it")
     return ap.parse_args()
@@ -99,7 +102,9 @@ def main():
             vs = sdist.allreduce_degrees(deg, max_slot)
         s = sheep_amd.sequence_from_degrees(deg, vs, ctx=ctx)
         tree = sheep_amd.build_tree(shard, s, ctx=ctx)
-        if world > 1:                                           # binomial reduce to rank 0 (jnode.cpp:241)
+        if world > 1 and a.reduce == "kway":                    # reduce to rank 0 (jnode.cpp:241) in one pass
+            tree = sdist.reduce_trees_kway(tree, lambda t: sheep_amd.merge_trees_many(t, ctx=ctx), rank, world)
+        elif world > 1:                                         # binomial reduce to rank 0 (jnode.cpp:241)
             tree = sdist.reduce_trees(tree, lambda x, y: sheep_amd.merge_trees(x, y, ctx=ctx), rank, world)
         res = None
         if rank == 0:
@@ -177,7 +182,7 @@ def main():
             "config": {"workload": f"RMAT-{a.scale} ef{a.ef}, k={a.k}", "records": R, "vertex_slots": s.pos_size,
                        "tree_nodes": n, "k": a.k, "created": res.created, "packing_nodes": res.packing_nodes,
                        "heavy_nodes": res.heavy_nodes, "seed": seed,
-                       "parallelism": f"edge-shards x{world}"
+                       "parallelism": f"edge-shards x{world}" + (f", {a.reduce} reduce" if world > 1 else "")
                        + ("" if a.dist_backend == "nccl" else f" ({a.dist_backend}"
                           + (", one device" if a.same_device else "") + ")")},
             "path_roofline": {"alg_bytes": b_alg, "achieved_GBs": round(b_alg * a.steps / t / 1e9, 2),

@@ -11,6 +11,11 @@ path (graph2tree.cpp:161-216).
                         rank i with i % 2r == r sends to i - r, which merges.  Merging is
                         associative and commutative (the elimination tree of the union of
                         the parent edges), so the tree at rank 0 equals the serial one.
+  * reduce_trees_kway — the same reduction as ONE gather + ONE K-way merge on rank 0
+                        (sheep_merge_trees_many): every rank sends its tree straight to
+                        rank 0 (each over its own xGMI link, all at once), and the merge
+                        runs once over all K parent-edge sets instead of ceil(log2 K)
+                        merges in sequence on rank 0's critical path.
 
 One process per GPU.  With the "nccl" backend (RCCL over xGMI) device tensors are sent
 as they are.  With "gloo" they are staged through host memory, which lets the schedule
@@ -75,6 +80,37 @@ def reduce_trees(tree: torch.Tensor, merge, rank: int, world: int):
             tree = merge(tree, _recv_like(tree, rank + r))
         r *= 2
     return tree
+
+
+def gather_trees(tree: torch.Tensor, rank: int, world: int):
+    """Every rank's (n, 2) tree stacked on rank 0 as (world, n, 2); None elsewhere."""
+    if rank != 0:
+        if _host_staged():
+            _send(tree, 0)
+        else:   # the same batched P2P API on both sides (RCCL groups the transfers)
+            for q in dist.batch_isend_irecv([dist.P2POp(dist.isend, tree, 0)]):
+                q.wait()
+        return None
+    out = torch.empty((world,) + tuple(tree.shape), dtype=tree.dtype, device=tree.device)
+    out[0].copy_(tree)
+    if _host_staged() and tree.is_cuda:
+        host = torch.empty((world,) + tuple(tree.shape), dtype=tree.dtype, device="cpu")
+        reqs = [dist.irecv(host[r], r) for r in range(1, world)]
+        for q in reqs:
+            q.wait()
+        out[1:].copy_(host[1:])
+    else:
+        ops = [dist.P2POp(dist.irecv, out[r], r) for r in range(1, world)]
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+    return out
+
+
+def reduce_trees_kway(tree: torch.Tensor, merge_many, rank: int, world: int):
+    """Gather to rank 0, then one K-way merge there.  Returns the merged tree on rank 0,
+    None elsewhere."""
+    stacked = gather_trees(tree, rank, world)
+    return None if stacked is None else merge_many(stacked)
 
 
 def sync_parts(parts: torch.Tensor | None, pos_size: int, device) -> torch.Tensor:

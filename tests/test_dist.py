@@ -22,7 +22,22 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, name, out_path):
+def _oracle_merge(x, y):
+    import oracle
+    xa, ya = x.numpy().view(np.uint32), y.numpy().view(np.uint32)
+    po, wo = oracle.merge(xa[:, 0], xa[:, 1], ya[:, 0], ya[:, 1])
+    return torch.from_numpy(np.stack([po, wo], axis=1).view(np.int32))
+
+
+def _oracle_merge_many(stacked):
+    """K-way merge = any fold of pairwise merges (the oracle has the pairwise one)."""
+    acc = stacked[0]
+    for t in stacked[1:]:
+        acc = _oracle_merge(acc, t)
+    return acc
+
+
+def _rank_main(rank, world, port, name, out_path, reduce="binomial"):
     import oracle
     from sheep_amd import dist as sdist
 
@@ -45,12 +60,14 @@ def _rank_main(rank, world, port, name, out_path):
         p, w = oracle.build_tree(tail, head, seq)
         tree = torch.from_numpy(np.stack([p, w], axis=1).view(np.int32))
 
-        def merge(x, y):
-            xa, ya = x.numpy().view(np.uint32), y.numpy().view(np.uint32)
-            po, wo = oracle.merge(xa[:, 0], xa[:, 1], ya[:, 0], ya[:, 1])
-            return torch.from_numpy(np.stack([po, wo], axis=1).view(np.int32))
-
-        tree = sdist.reduce_trees(tree, merge, rank, world)
+        if reduce == "kway":
+            stacked = sdist.gather_trees(tree, rank, world)
+            if rank == 0:   # the gather itself is exact: row r is rank r's own tree
+                assert stacked.shape == (world,) + tuple(tree.shape)
+                assert torch.equal(stacked[0], tree)
+            tree = None if stacked is None else _oracle_merge_many(stacked)
+        else:
+            tree = sdist.reduce_trees(tree, _oracle_merge, rank, world)
         assert (tree is None) == (rank != 0)
         # Partition::mpi_sync: rank 0 partitions, every rank gets the parts
         parts = None
@@ -77,6 +94,17 @@ def test_sharded_schedule_matches_serial(tmp_path, name, world):
     got = json.load(open(out))
     assert np.array_equal(np.array(got["seq"], np.uint32), golden_seq(name))
     parent, pst = golden_tree(name)
+    assert np.array_equal(np.array(got["parent"], np.uint32), parent)
+    assert np.array_equal(np.array(got["pst"], np.uint32), pst)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_kway_schedule_matches_serial(tmp_path, world):
+    """Gather to rank 0 + one K-way reduction (bench.py's default --reduce kway)."""
+    out = str(tmp_path / "rank0.json")
+    mp.spawn(_rank_main, args=(world, _free_port(), "rmat10", out, "kway"), nprocs=world, join=True)
+    got = json.load(open(out))
+    parent, pst = golden_tree("rmat10")
     assert np.array_equal(np.array(got["parent"], np.uint32), parent)
     assert np.array_equal(np.array(got["pst"], np.uint32), pst)
 
