@@ -33,7 +33,7 @@ LEAF = ("degree", "degree_heads", "relabel", "pst_group", "etree_split", "etree_
         "etree_apply", "etree_compact", "evaluate")
 # kernels of a region, for roofline.traffic from the committed PMC passes (tools/pmc_traffic.py);
 # regions whose kernels are shared with other regions (histograms, packs) get traffic null
-REGION_KERNELS = {"relabel": ["k_relabel"], "degree": ["k_degree"], "etree_split": ["k_split"],
+REGION_KERNELS = {"relabel": ["k_relabel_scatter", "k_relabel_gather"], "degree": ["k_degree"], "etree_split": ["k_split_count", "k_split_write"],
                   "etree_cross": ["k_cross_find"], "etree_apply": ["k_cross_apply", "k_level_clean"],
                   "etree_compact": ["k_compact_edges"], "etree_bucket": ["k_bucket_count", "k_bucket_scatter"]}
 PMC_FILE = os.path.join(ROOT, "profiles", "r1", "pmc_traffic_rmat{scale}.json")
@@ -220,9 +220,16 @@ def pmc_traffic(a, region, launches_per_step):
 
 
 def cpu_baseline(a, ctx):
-    """The oracle (CPU restatement of the reference, oracle/sheep_oracle.cpp) on a
-    bounded sample: RMAT-<cpu-scale> from the same generator, seq + tree + partition,
-    one core.  Test infrastructure timed as a baseline; never the measured path."""
+    """CPU baseline on a bounded sample: RMAT-<cpu-scale> from the same generator,
+    seq + tree + partition(k), one core, graph already in memory.
+
+    kind "reference": the reference's own lib/ code (degreeSequence, JTree + makeKids,
+    Partition -- the graph2tree.cpp:185-208 flow) compiled from /root/reference into
+    oracle/_ref/ref_harness (`time` mode).  The oracle restatement (oracle/sheep_oracle.cpp)
+    is timed beside it as `port`.  Test infrastructure timed as a baseline; never the
+    measured path."""
+    import subprocess
+    import tempfile
     import numpy as np
     import sheep_amd
     import oracle
@@ -231,14 +238,31 @@ def cpu_baseline(a, ctx):
     h = sheep_amd.to_numpy_u32(d).reshape(-1, 3)
     del d
     tail, head = np.ascontiguousarray(h[:, 0]), np.ascontiguousarray(h[:, 1])
+    R = len(tail)
+    sample = f"RMAT-{sc} ef{a.ef} seed {sc} ({R} records), seq+tree+partition k={a.k}, single-threaded"
     t0 = time.perf_counter()
     seq = oracle.sequence(tail, head)
     p, w = oracle.build_tree(tail, head, seq)
     oracle.partition(p, w, seq, a.k)
-    t = time.perf_counter() - t0
-    return {"value": round(len(tail) / t, 1), "unit": "edges/s", "cores": 1, "kind": "port",
-            "sample": f"RMAT-{sc} ef{a.ef} seed {sc} ({len(tail)} records), seq+tree+partition k={a.k}, "
-                      f"oracle/sheep_oracle.cpp single-threaded, {t:.2f} s"}
+    tp = time.perf_counter() - t0
+    port = {"value": round(R / tp, 1), "unit": "edges/s", "cores": 1, "kind": "port",
+            "sample": f"{sample}, oracle/sheep_oracle.cpp, {tp:.2f} s"}
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return port
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, f"rmat{sc}.dat")
+        h.tofile(path)
+        del h
+        r = subprocess.run([harness, "time", path, str(a.k)], capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        port["reference_error"] = r.stderr.strip()[-300:]
+        return port
+    tr = json.loads(r.stdout.strip().splitlines()[-1])["seconds"]
+    return {"value": round(R / tr, 1), "unit": "edges/s", "cores": 1, "kind": "reference",
+            "sample": f"{sample}, reference lib/ (degreeSequence + JTree + makeKids + Partition, "
+                      f"graph2tree.cpp:185-208) built by oracle/ref/Makefile, {tr:.2f} s",
+            "port": port}
 
 
 if __name__ == "__main__":

@@ -1,4 +1,6 @@
+# relabel sub-tile size sweep
+set -o pipefail
 mkdir -p gpurun_out && export HSA_ENABLE_IPC_MODE_LEGACY=0 && export TMPDIR=/tmp
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 4 --steps 2 --warmup 1 --scale 24 --k 64 --dist-backend gloo --same-device --verify > gpurun_out/dist4k.log 2>&1 || exit 1
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 8 --steps 2 --warmup 1 --scale 22 --k 16 --dist-backend gloo --same-device --verify > gpurun_out/dist8k.log 2>&1 || exit 1
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 3 --steps 2 --warmup 1 --scale 22 --k 16 --dist-backend gloo --same-device --verify --reduce binomial > gpurun_out/dist3b.log 2>&1 || exit 1
+for p in 16 8 4; do
+SHEEP_RL_PER=$p timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/b26_per$p.log 2>&1 || exit 1
+done

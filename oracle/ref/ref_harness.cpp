@@ -26,6 +26,7 @@
 #include "partition.h"
 #include "sequence.h"
 
+#include <chrono>
 #include <cstdio>
 #include <fstream>
 #include <string>
@@ -100,7 +101,8 @@ static int usage() {
           "ref_harness tree G SEQ|- OUT_TRE [p/k]         JTree (+ partial load), TREEFAQS\n"
           "ref_harness part G SEQ|- TREE PARTS_PREFIX k.. partition_tree -f -g flow + parts dumps\n"
           "ref_harness write G SEQ|- TREE k PREFIX        Partition + graph-based writePartitionedGraph\n"
-          "ref_harness writefile G SEQ|- TREE k PREFIX    Partition + file-based writePartitionedGraph\n");
+          "ref_harness writefile G SEQ|- TREE k PREFIX    Partition + file-based writePartitionedGraph\n"
+          "ref_harness time G k                           seconds for degreeSequence + JTree + Partition(k)\n");
   return 1;
 }
 
@@ -154,6 +156,18 @@ int main(int argc, char **argv) {
     part.print();
     char const *const input = argv[2];
     part.writePartitionedGraph(input, seq, argv[6]);
+    return 0;
+  }
+  if (cmd == "time" && argc == 4) {   // bench.py cpu_baseline: graph load untimed (inputs resident)
+    HarnessGraph g(argv[2]);
+    auto const t0 = std::chrono::steady_clock::now();
+    std::vector<vid_t> seq = degreeSequence(g);
+    JTree tree(g, seq);
+    tree.jnodes.makeKids();   // graph2tree.cpp:204-206 (Partition requires kids)
+    Partition part(seq, tree.jnodes, (short)atoi(argv[3]), 1.03, false, true, false);
+    double const s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    printf("{\"seconds\": %.6f, \"records\": %zu, \"nodes\": %zu, \"parts\": %zu}\n", s,
+           (size_t)g.getEdges(), seq.size(), part.parts.size());
     return 0;
   }
   return usage();

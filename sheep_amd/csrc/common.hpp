@@ -53,6 +53,12 @@ struct Ctx {
   uint64_t *d_scalars = nullptr;   // device scalars (counters / flags)
   static constexpr int NSCALARS = 64;
 
+  // Bucket layout of the last degree_count's head histogram (LLAMA mode): the scanned
+  // (bucket, tile) offsets live in ws["head_offsets"]; relabel_bucketed reuses them when
+  // it sees the same records and key range (and verifies every region's count in-kernel).
+  struct HeadLayout { const void *rec = nullptr; uint64_t nrec = 0, K = 0; std::vector<uint32_t> bstart; bool valid = false; };
+  HeadLayout head_layout;
+
   bool timing = false;
   struct Timer { std::vector<std::pair<hipEvent_t, hipEvent_t>> pending; double ms = 0; uint64_t launches = 0; uint64_t bytes = 0; };
   std::map<std::string, Timer> timers;
@@ -236,6 +242,10 @@ void radix_sort_pairs_u32(Ctx &c, uint32_t *keys, uint32_t *vals, uint64_t n, in
 void radix_sort_keys_u64(Ctx &c, uint64_t *keys, uint64_t n, int end_bit, uint64_t *keys_alt);
 // hist.hip — cnt[key] += occurrences, keys bucketed through LDS (no scattered atomics)
 void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt);
+// relabel (jtree.cpp:72-91) in head-bucket order; returns the number of edges written, or
+// UINT64_MAX when the key range / record count does not fit the bucket layout.
+uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
+                          uint32_t *pst, uint64_t *edges, unsigned long long *err);
 void histogram_edge_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t K, uint32_t *cnt);
 void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, int L, uint32_t clo, uint32_t *pst,
                        uint64_t *r0, uint64_t *seg);

@@ -757,6 +757,7 @@ __global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t 
 void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
 
 static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
+static const bool g_plain_relabel = getenv("SHEEP_PLAIN_RELABEL") != nullptr;   // A/B: k_relabel only
 static int env_int(const char *name, int def) {
   const char *v = getenv(name);
   return v && *v ? atoi(v) : def;
@@ -992,17 +993,22 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   uint64_t *edges = c.get_as<uint64_t>("bt_edges", nrec ? nrec : 1);
   unsigned long long *d = (unsigned long long *)c.d_scalars + 8;
   HIP_CHECK(hipMemsetAsync(d + 1, 0, sizeof(uint64_t), c.stream));
+  uint64_t m = nrec;   // edges[i] per record, DEAD holes included (k_relabel)
   if (nrec) {
     TimedRegion tr(c, "relabel", 20 * nrec);   // record + 2 pos gathers
-    hipLaunchKernelGGL(k_relabel, dim3(grid_tiles(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos, pos_size, pst,
-                       edges, d + 1);
-    LAUNCH_CHECK();
+    // head-bucketed relabel (hist.hip) when the key range fits its LDS buckets
+    m = g_plain_relabel ? UINT64_MAX : relabel_bucketed(c, rec, nrec, pos, pos_size, pst, edges, d + 1);
+    if (m == UINT64_MAX) {
+      m = nrec;
+      hipLaunchKernelGGL(k_relabel, dim3(grid_tiles(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos, pos_size, pst,
+                         edges, d + 1);
+      LAUNCH_CHECK();
+    }
   }
   HIP_CHECK(hipMemcpyAsync(c.h_scalars + 9, d + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
   if (c.h_scalars[9]) throw Error(SHEEP_ERR_RANGE, "vector::_M_range_check: neighbour vid beyond the sequence's index (jtree.cpp:75)");
-  const uint64_t m = nrec;   // edges[i] per record, DEAD holes included
-  if (n >= 2 && nrec) {
+  if (n >= 2 && m) {
     int L;
     uint32_t clo;
     spread_params(n, &L, &clo);

@@ -16,6 +16,7 @@
 //
 // Traffic per key: two reads of the source + 2 B written + 2 B read back, all of it
 // coalesced (runs of ~T/NB u16), against one scattered RMW per key.
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -259,7 +260,8 @@ __global__ __launch_bounds__(HB) void k_hist_final(const uint16_t *__restrict__ 
 // entries, device) receives each bucket's first position there.
 template <typename Src>
 void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint64_t *grouped = nullptr,
-                   const uint32_t *kbase = nullptr, uint32_t *bstart_out = nullptr) {
+                   const uint32_t *kbase = nullptr, uint32_t *bstart_out = nullptr,
+                   uint32_t *save_offsets = nullptr, std::vector<uint32_t> *save_bstart = nullptr) {
   if (n == 0 || K == 0) return;
   const uint32_t nb = (uint32_t)((K + W - 1) >> WBITS);
   const uint64_t ntiles = (n + TKEYS - 1) >> TLOG;
@@ -281,6 +283,10 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
   LAUNCH_CHECK();
   uint32_t *total = c.get_as<uint32_t>("hist_total", 1);
   scan_exclusive_u32(c, tile_hist, tile_hist, ntiles * nb, total);
+  if (save_offsets) {   // the relabel's bucket layout (relabel_bucketed, below)
+    HIP_CHECK(hipMemcpyAsync(save_offsets, tile_hist, ntiles * nb * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
+    HIP_CHECK(hipMemcpyAsync(save_offsets + ntiles * nb, total, sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
+  }
   if constexpr (std::is_same<Src, EdgeLoPadded>::value) {
     hipLaunchKernelGGL(k_lo_scatter, dim3((unsigned)ntiles), dim3(HB), lds_scatter, c.stream, src, n, nb,
                        (const uint32_t *)tile_hist, ntiles, keys, grouped);
@@ -295,6 +301,7 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
                              nb, hipMemcpyDeviceToHost, c.stream));
   HIP_CHECK(hipMemcpyAsync(&bstart[nb], total, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
+  if (save_bstart) *save_bstart = bstart;
   if (bstart_out) HIP_CHECK(hipMemcpyAsync(bstart_out, bstart.data(), (nb + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
   std::vector<Chunk> chunks;
   for (uint32_t b = 0; b < nb; ++b) {
@@ -315,6 +322,144 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
   c.sync();   // `chunks` is a pageable host buffer
 }
 
+
+// ---- head-bucketed relabel (jtree.cpp:72-91) -----------------------------------------
+// k_relabel's pos[head] gather is random over the whole 4-B-per-slot index (268 MB at
+// RMAT-26): each 4-B load moves a full line.  Here the records are first scattered into
+// the heads' 2^15-slot buckets -- carrying pos[tail], a near-sequential gather since
+// records come tail-sorted -- with the same tiles and bucket-major offsets as the degree
+// pass's head histogram (whose scanned offsets are reused), and then one workgroup per
+// bucket slice holds the bucket's 128 KiB of pos in LDS and relabels from there.
+//   pass A k_relabel_scatter: 12 B record + pos[tail] in, 8 B (ptail << 32 | head) out
+//   pass B k_relabel_gather:  8 B in, 8 B tree edge out, pos read once per slice
+// Edges come out in head-bucket order; every later stage is order-independent (the pst
+// histogram groups them by lo, the elimination tree is unique for the edge multiset).
+constexpr uint32_t PT_OOR = 0xFFFFFFFEu;   // tail >= pos_size (only an error if the head is sequenced)
+constexpr uint64_t NO_PAIR = ~0ull;
+
+// the relabel's keys: heads < pos_size of non-self-loop records (LLAMA HeadKeys when
+// pos_size equals the degree pass's key range)
+struct RelabelKeys {
+  const sheep_xs1 *rec;
+  uint64_t pos_size;
+  __device__ __forceinline__ uint32_t operator()(uint64_t i) const {
+    const sheep_xs1 r = rec[i];
+    return (r.tail == r.head || r.head >= pos_size) ? NO_KEY : r.head;
+  }
+};
+
+// One tile of TKEYS records per workgroup, staged SUB = PER * HB at a time (u64 payloads:
+// a whole tile does not fit LDS).  gb[b] walks the tile's region of bucket b; every write
+// is bounded by the region's end and a region not filled exactly raises flags[1] (stale
+// offsets) so the host recounts.  flags[0]: a sequenced endpoint's neighbour >= pos_size.
+template <int PER>
+__global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restrict__ rec, uint64_t n,
+                                                        const uint32_t *__restrict__ pos, uint64_t pos_size, uint32_t nb,
+                                                        const uint32_t *__restrict__ offsets, uint64_t ntiles,
+                                                        uint64_t *__restrict__ out, unsigned long long *__restrict__ flags) {
+  constexpr uint32_t SUB = PER * HB;
+  extern __shared__ uint32_t lds[];
+  uint32_t *cur = lds, *gb = lds + nb, *end = lds + 2 * nb, *wsum = lds + 3 * nb;
+  uint64_t *stage = (uint64_t *)(lds + ((3 * nb + HB / WAVE + 1) & ~1u));
+  const uint64_t tile = blockIdx.x;
+  for (uint32_t b = threadIdx.x; b < nb; b += HB) {
+    const uint64_t o = (uint64_t)b * ntiles + tile;
+    gb[b] = offsets[o];
+    end[b] = offsets[o + 1];
+  }
+  bool bad = false, lost = false;
+  const uint64_t base = tile << TLOG;
+  for (uint32_t s0 = 0; s0 < TKEYS; s0 += SUB) {
+    for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
+    __syncthreads();
+    uint64_t x[PER];
+    uint32_t pt[PER], hd[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {   // all record loads, then all pos[tail] loads in flight
+      const uint64_t i = base + s0 + (uint64_t)j * HB + threadIdx.x;
+      hd[j] = INVALID;
+      pt[j] = INVALID;
+      if (i < n) {
+        const sheep_xs1 r = rec[i];
+        if (r.tail != r.head) { hd[j] = r.head; pt[j] = r.tail; }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      x[j] = NO_PAIR;
+      if (hd[j] == INVALID && pt[j] == INVALID) continue;
+      const uint32_t t = pt[j], h = hd[j];
+      const uint32_t ptm = t < pos_size ? pos[t] : PT_OOR;
+      if (h >= pos_size) {
+        if (ptm < PT_OOR) bad = true;   // index.at(head) throws (jtree.cpp:75)
+        continue;
+      }
+      x[j] = ((uint64_t)ptm << 32) | h;
+      atomicAdd(&cur[h >> WBITS], 1u);
+    }
+    __syncthreads();
+    const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
+    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] -= cur[b];   // region cursor - local start
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      if (x[j] != NO_PAIR) stage[atomicAdd(&cur[(uint32_t)x[j] >> WBITS], 1u)] = x[j];
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < total; j += HB) {
+      const uint64_t v = stage[j];
+      const uint32_t b = (uint32_t)v >> WBITS, dst = gb[b] + j;
+      if (dst < end[b]) out[dst] = v;
+      else lost = true;
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += cur[b];   // past this sub-tile's run
+    __syncthreads();
+  }
+  for (uint32_t b = threadIdx.x; b < nb; b += HB)
+    if (gb[b] != end[b]) lost = true;
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(&flags[0], 1ull);
+  if (__any(lost) && (threadIdx.x & 63) == 0) atomicAdd(&flags[1], 1ull);
+}
+
+// One workgroup per (bucket, slice of <= CHUNK pairs): the bucket's pos slice in LDS.
+// Same outcomes as k_relabel: both endpoints sequenced -> tree edge (hi << 32 | lo);
+// one sequenced, the other an unsequenced slot -> POSTORDER pst for the sequenced one.
+__global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restrict__ pairs, const Chunk *__restrict__ chunks,
+                                                       const uint32_t *__restrict__ pos, uint64_t pos_size,
+                                                       uint32_t *__restrict__ pst, uint64_t *__restrict__ edges,
+                                                       unsigned long long *__restrict__ flags) {
+  extern __shared__ uint32_t lds[];
+  const Chunk ch = chunks[blockIdx.x];
+  const uint64_t v0 = (uint64_t)ch.bucket << WBITS;
+  for (uint32_t i = threadIdx.x; i < W; i += HB) lds[i] = v0 + i < pos_size ? pos[v0 + i] : INVALID;
+  __syncthreads();
+  bool bad = false;
+  for (uint64_t i0 = ch.beg; i0 < ch.end; i0 += 8 * HB) {
+    uint64_t x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
+      x[j] = i < ch.end ? pairs[i] : NO_PAIR;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
+      if (i >= ch.end) continue;
+      const uint32_t ptm = (uint32_t)(x[j] >> 32), ph = lds[(uint32_t)x[j] & (W - 1)];
+      uint64_t e = ~0ull;   // DEAD
+      if (ph != INVALID) {
+        if (ptm == PT_OOR) bad = true;                       // index.at(tail) throws
+        else if (ptm != INVALID) e = ptm < ph ? ((uint64_t)ph << 32) | ptm : ((uint64_t)ptm << 32) | ph;
+        else atomicAdd(&pst[ph], 1u);
+      } else if (ptm < PT_OOR) {
+        atomicAdd(&pst[ptm], 1u);
+      }
+      edges[i] = e;
+    }
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(&flags[0], 1ull);
+}
+
 // seg[i] = position of bucket sb[i] in the grouped array (sb: bucket indices)
 __global__ void k_seg_from_buckets(const uint32_t *__restrict__ bstart, const uint64_t *__restrict__ sb, int L,
                                    uint64_t *__restrict__ seg) {
@@ -324,8 +469,105 @@ __global__ void k_seg_from_buckets(const uint32_t *__restrict__ bstart, const ui
 }  // namespace
 
 void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt) {
-  histogram_add(c, HeadKeys{rec, llama}, nrec, K, cnt);
+  Ctx::HeadLayout &hl = c.head_layout;
+  hl.valid = false;
+  const uint64_t nb = (K + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
+  if (!llama || nb == 0 || nb > 4096 || ntiles * nb + 1 >= (1ull << 32)) {
+    histogram_add(c, HeadKeys{rec, llama}, nrec, K, cnt);
+    return;
+  }
+  uint32_t *save = c.get_as<uint32_t>("head_offsets", ntiles * nb + 1);
+  histogram_add(c, HeadKeys{rec, llama}, nrec, K, cnt, nullptr, nullptr, nullptr, save, &hl.bstart);
+  hl.rec = rec;
+  hl.nrec = nrec;
+  hl.K = K;
+  hl.valid = hl.bstart.size() == nb + 1;
 }
+
+uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
+                          uint32_t *pst, uint64_t *edges, unsigned long long *err) {
+  const uint64_t nb = (pos_size + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
+  if (nrec == 0 || nb == 0 || nb > 4096 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return UINT64_MAX;
+  static bool attr_set = false;
+  if (!attr_set) {
+    for (const void *f : {(const void *)k_relabel_scatter<16>, (const void *)k_relabel_scatter<8>,
+                          (const void *)k_relabel_scatter<4>, (const void *)k_relabel_gather})
+      HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  Ctx::HeadLayout &hl = c.head_layout;
+  unsigned long long *flags = c.get_as<unsigned long long>("rl_flags", 2);
+  auto recount = [&]() -> uint32_t * {   // the relabel's own (bucket, tile) offsets
+    uint32_t *off = c.get_as<uint32_t>("head_offsets", ntiles * nb + 1);
+    hipLaunchKernelGGL(k_hist_count<RelabelKeys>, dim3((unsigned)ntiles), dim3(CB), nb * 4, c.stream,
+                       RelabelKeys{rec, pos_size}, nrec, (uint32_t)nb, off, ntiles);
+    LAUNCH_CHECK();
+    scan_exclusive_u32(c, off, off, ntiles * nb, off + ntiles * nb);
+    hl.bstart.assign(nb + 1, 0);
+    HIP_CHECK(hipMemcpy2DAsync(hl.bstart.data(), sizeof(uint32_t), off, ntiles * sizeof(uint32_t), sizeof(uint32_t), nb,
+                               hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipMemcpyAsync(&hl.bstart[nb], off + ntiles * nb, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+    hl.rec = rec;
+    hl.nrec = nrec;
+    hl.K = pos_size;
+    hl.valid = true;
+    return off;
+  };
+  const bool cached = hl.valid && hl.rec == rec && hl.nrec == nrec && hl.K == pos_size && hl.bstart.size() == nb + 1;
+  uint32_t *off = cached ? c.get_as<uint32_t>("head_offsets", ntiles * nb + 1) : recount();
+  const uint64_t total = hl.bstart[nb];
+  uint64_t *pairs = c.get_as<uint64_t>("rl_pairs", total ? total : 1);
+  const size_t fixed = ((3 * nb + HB / WAVE + 1) & ~1ull) * 4;
+  auto scatter = [&]() {
+    HIP_CHECK(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c.stream));
+    static const int per_max = getenv("SHEEP_RL_PER") ? atoi(getenv("SHEEP_RL_PER")) : 8;   // experiments
+    if (per_max >= 16 && fixed + 16 * HB * 8 <= 160 * 1024)
+      hipLaunchKernelGGL(k_relabel_scatter<16>, dim3((unsigned)ntiles), dim3(HB), fixed + 16 * HB * 8, c.stream, rec, nrec,
+                         pos, pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
+    else if (per_max >= 8 && fixed + 8 * HB * 8 <= 160 * 1024)
+      hipLaunchKernelGGL(k_relabel_scatter<8>, dim3((unsigned)ntiles), dim3(HB), fixed + 8 * HB * 8, c.stream, rec, nrec,
+                         pos, pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
+    else
+      hipLaunchKernelGGL(k_relabel_scatter<4>, dim3((unsigned)ntiles), dim3(HB), fixed + 4 * HB * 8, c.stream, rec, nrec,
+                         pos, pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
+    LAUNCH_CHECK();
+    HIP_CHECK(hipMemcpyAsync(c.h_scalars + 12, flags, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  };
+  // chunk list of pass B from the bucket starts (host), built while pass A runs
+  std::vector<Chunk> chunks;
+  auto make_chunks = [&]() {
+    chunks.clear();
+    for (uint32_t b = 0; b < nb; ++b) {
+      const uint64_t beg = hl.bstart[b], end = hl.bstart[b + 1];
+      for (uint64_t x = beg; x < end; x += CHUNK) chunks.push_back({x, x + CHUNK < end ? x + CHUNK : end, b, 0});
+    }
+  };
+  scatter();
+  make_chunks();
+  c.sync();
+  if (c.h_scalars[13]) {   // offsets did not match these records: recount, scatter again
+    if (!cached) throw Error(SHEEP_ERR_HIP, "relabel: bucket layout inconsistent with its own count");
+    off = recount();
+    if (hl.bstart[nb] > total) pairs = c.get_as<uint64_t>("rl_pairs", hl.bstart[nb]);
+    scatter();
+    make_chunks();
+    c.sync();
+    if (c.h_scalars[13]) throw Error(SHEEP_ERR_HIP, "relabel: bucket layout inconsistent with its own count");
+  }
+  const uint64_t m = hl.bstart[nb];
+  if (c.h_scalars[12]) HIP_CHECK(hipMemsetAsync(err, 0xFF, 1, c.stream));   // range error (reported by the caller)
+  if (!chunks.empty()) {
+    Chunk *dch = c.get_as<Chunk>("rl_chunks", chunks.size());
+    HIP_CHECK(hipMemcpyAsync(dch, chunks.data(), chunks.size() * sizeof(Chunk), hipMemcpyHostToDevice, c.stream));
+    hipLaunchKernelGGL(k_relabel_gather, dim3((unsigned)chunks.size()), dim3(HB), W * 4, c.stream, (const uint64_t *)pairs,
+                       (const Chunk *)dch, pos, pos_size, pst, edges, err);
+    LAUNCH_CHECK();
+    c.sync();   // `chunks` is a pageable host buffer
+  }
+  return m;
+}
+
 void histogram_edge_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t K, uint32_t *cnt) {
   histogram_add(c, EdgeLoKeys{edges}, m, K, cnt);
 }

@@ -119,6 +119,29 @@ def test_rmat_vs_oracle(gpu_ctx, scale, seed, k):
     assert ev.__dict__ == oev
 
 
+def test_relabel_layout_reuse_and_stale(gpu_ctx):
+    """The bucketed relabel reuses the degree pass's head-bucket offsets; records changed
+    in place after degree_sequence (same pointer and count, other head buckets) must be
+    detected in-kernel and recounted.  Swapping tail/head keeps the undirected graph, so
+    the tree is the oracle's tree of the original records."""
+    import sheep_amd
+    d = sheep_amd.rmat(16, 16, 21)
+    h = sheep_amd.to_numpy_u32(d).reshape(-1, 3)
+    t_, h_ = h[:, 0].copy(), h[:, 1].copy()
+    s = sheep_amd.degree_sequence(d)
+    seq = oracle.sequence(t_, h_)
+    op, ow = oracle.build_tree(t_, h_, seq)
+    p, w = _tree_np(sheep_amd.build_tree(d, s))          # cached layout
+    assert np.array_equal(p, op) and np.array_equal(w, ow)
+    sw = d[::3, 0].clone()
+    d[::3, 0] = d[::3, 1]
+    d[::3, 1] = sw                                      # stale layout: same ptr, same nrec
+    p, w = _tree_np(sheep_amd.build_tree(d, s))
+    assert np.array_equal(p, op) and np.array_equal(w, ow)
+    p, w = _tree_np(sheep_amd.build_tree(d, s))          # the recounted layout, reused
+    assert np.array_equal(p, op) and np.array_equal(w, ow)
+
+
 def test_shards_merge_to_whole_tree(gpu_ctx):
     """Shard independence: 4 contiguous shards, pairwise merges == the whole tree."""
     import sheep_amd
