@@ -1,6 +1,7 @@
-# relabel sub-tile size sweep
+# A/B: LDS-staged pst grouping scatter vs direct stores; GPU tests first
 set -o pipefail
 mkdir -p gpurun_out && export HSA_ENABLE_IPC_MODE_LEGACY=0 && export TMPDIR=/tmp
-for p in 16 8 4; do
-SHEEP_RL_PER=$p timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/b26_per$p.log 2>&1 || exit 1
-done
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gt2.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --verify > gpurun_out/b26s.log 2>&1 || exit 1
+SHEEP_LO_DIRECT=1 timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/b26d.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --scale 22 --k 16 > gpurun_out/b22s.log 2>&1 || exit 1

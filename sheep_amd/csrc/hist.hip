@@ -214,6 +214,56 @@ __global__ __launch_bounds__(HB) void k_lo_scatter(EdgeLoPadded src, uint64_t n,
   }
 }
 
+// k_lo_scatter with LDS-staged edges: SUB = PER * HB edges at a time are counting-sorted
+// by bucket in LDS and each bucket's run is written with consecutive lanes (the u16 key
+// beside it), instead of one scattered 8-B store per lane.  Same offsets, same result
+// (within a (bucket, tile) run the order is the counting sort's, as in k_lo_scatter).
+template <int PER>
+__global__ __launch_bounds__(HB) void k_lo_scatter_staged(EdgeLoPadded src, uint64_t n, uint32_t nb,
+                                                          const uint32_t *__restrict__ offsets, uint64_t ntiles,
+                                                          uint16_t *__restrict__ out, uint64_t *__restrict__ grouped) {
+  constexpr uint32_t SUB = PER * HB;
+  extern __shared__ uint32_t lds[];
+  uint32_t *cur = lds, *gb = lds + nb, *wsum = lds + 2 * nb;
+  uint64_t *stage = (uint64_t *)(lds + ((2 * nb + HB / WAVE + 1) & ~1u));
+  const uint64_t tile = blockIdx.x;
+  for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] = offsets[(uint64_t)b * ntiles + tile];
+  const uint64_t base = tile << TLOG;
+  for (uint32_t s0 = 0; s0 < TKEYS; s0 += SUB) {
+    for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
+    __syncthreads();
+    uint64_t e[PER];
+    uint32_t k[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint64_t i = base + s0 + (uint64_t)j * HB + threadIdx.x;
+      e[j] = i < n ? src.edges[i] : ~0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      k[j] = src.key(e[j]);
+      if (k[j] != NO_KEY) atomicAdd(&cur[k[j] >> WBITS], 1u);
+    }
+    __syncthreads();
+    const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
+    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] -= cur[b];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      if (k[j] != NO_KEY) stage[atomicAdd(&cur[k[j] >> WBITS], 1u)] = e[j];
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < total; j += HB) {
+      const uint64_t v = stage[j];
+      const uint32_t key = src.key(v), dst = gb[key >> WBITS] + j;
+      grouped[dst] = v;
+      out[dst] = (uint16_t)(key & (W - 1));
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += cur[b];
+    __syncthreads();
+  }
+}
+
 // One workgroup per chunk = (bucket, slice of its keys).  A bucket's keys can be very
 // skewed (pst: a few thousand positions own most lower endpoints; one bucket took
 // 21 ms alone on RMAT-26), so buckets are cut into slices of <= CHUNK keys; a bucket
@@ -288,8 +338,20 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
     HIP_CHECK(hipMemcpyAsync(save_offsets + ntiles * nb, total, sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
   }
   if constexpr (std::is_same<Src, EdgeLoPadded>::value) {
-    hipLaunchKernelGGL(k_lo_scatter, dim3((unsigned)ntiles), dim3(HB), lds_scatter, c.stream, src, n, nb,
-                       (const uint32_t *)tile_hist, ntiles, keys, grouped);
+    static const bool direct = getenv("SHEEP_LO_DIRECT") != nullptr;   // A/B: one scattered store per lane
+    const size_t lds_staged = ((2 * (size_t)nb + HB / WAVE + 1) & ~(size_t)1) * 4 + 16 * HB * 8;
+    if (!direct && lds_staged <= 160 * 1024) {
+      static bool staged_attr = false;
+      if (!staged_attr) {
+        HIP_CHECK(hipFuncSetAttribute((const void *)k_lo_scatter_staged<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        staged_attr = true;
+      }
+      hipLaunchKernelGGL(k_lo_scatter_staged<16>, dim3((unsigned)ntiles), dim3(HB), lds_staged, c.stream, src, n, nb,
+                         (const uint32_t *)tile_hist, ntiles, keys, grouped);
+    } else {
+      hipLaunchKernelGGL(k_lo_scatter, dim3((unsigned)ntiles), dim3(HB), lds_scatter, c.stream, src, n, nb,
+                         (const uint32_t *)tile_hist, ntiles, keys, grouped);
+    }
   } else {
     hipLaunchKernelGGL(k_hist_scatter<Src>, dim3((unsigned)ntiles), dim3(HB), lds_scatter, c.stream, src, n, nb,
                        (const uint32_t *)tile_hist, ntiles, keys);
