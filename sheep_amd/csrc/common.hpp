@@ -141,6 +141,26 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 
+// Adds w into cnt[key] for every lane whose key != INVALID, with one atomic per run of
+// equal keys in consecutive lanes (records sorted by tail, as generated and as many
+// edge lists are stored, make tail runs long; a hub's endpoints collapse too).
+__device__ __forceinline__ void run_add(uint32_t *cnt, uint32_t key, uint32_t w) {
+  const int lane = (int)__lane_id();
+  const uint32_t prev = __shfl_up(key, 1, 64);
+  const bool start = key != INVALID && (lane == 0 || prev != key);
+  const uint64_t starts = __ballot(start);
+  const uint32_t rid = (uint32_t)__popcll(starts & ((lane == 63) ? ~0ull : ((2ull << lane) - 1)));
+  uint32_t v = key != INVALID ? w : 0;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_down(v, o, 64);
+    const uint32_t ro = __shfl_down(rid, o, 64);
+    const uint32_t ko = __shfl_down(key, o, 64);
+    if (lane + o < 64 && ro == rid && ko == key) v += u;
+  }
+  if (start && v) atomicAdd(&cnt[key], v);
+}
+
 template <typename T> __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -241,7 +261,12 @@ void radix_sort_pairs_u32(Ctx &c, uint32_t *keys, uint32_t *vals, uint64_t n, in
                           uint32_t *keys_alt, uint32_t *vals_alt);
 void radix_sort_keys_u64(Ctx &c, uint64_t *keys, uint64_t n, int end_bit, uint64_t *keys_alt);
 // hist.hip — cnt[key] += occurrences, keys bucketed through LDS (no scattered atomics)
-void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt);
+void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt,
+                     bool counted = false);
+// the degree pass fused with the heads' bucket counts; false (nothing launched) when the
+// capacity does not fit the bucket layout
+bool degree_fused(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap,
+                  unsigned long long *d_max, unsigned long long *d_err);
 // relabel (jtree.cpp:72-91) in head-bucket order; returns the number of edges written, or
 // UINT64_MAX when the key range / record count does not fit the bucket layout.
 uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,

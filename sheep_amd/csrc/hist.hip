@@ -311,7 +311,8 @@ __global__ __launch_bounds__(HB) void k_hist_final(const uint16_t *__restrict__ 
 template <typename Src>
 void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint64_t *grouped = nullptr,
                    const uint32_t *kbase = nullptr, uint32_t *bstart_out = nullptr,
-                   uint32_t *save_offsets = nullptr, std::vector<uint32_t> *save_bstart = nullptr) {
+                   uint32_t *save_offsets = nullptr, std::vector<uint32_t> *save_bstart = nullptr,
+                   bool counted = false) {
   if (n == 0 || K == 0) return;
   const uint32_t nb = (uint32_t)((K + W - 1) >> WBITS);
   const uint64_t ntiles = (n + TKEYS - 1) >> TLOG;
@@ -328,9 +329,11 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
   }
   uint32_t *tile_hist = c.get_as<uint32_t>("hist_tiles", ntiles * nb + 1);
   uint16_t *keys = c.get_as<uint16_t>("hist_keys", n);
-  hipLaunchKernelGGL(k_hist_count<Src>, dim3((unsigned)ntiles), dim3(CB), nb * 4, c.stream, src, n, nb, tile_hist,
-                     ntiles);
-  LAUNCH_CHECK();
+  if (!counted) {   // (counted: degree_fused already wrote tile_hist, >= nb bucket rows)
+    hipLaunchKernelGGL(k_hist_count<Src>, dim3((unsigned)ntiles), dim3(CB), nb * 4, c.stream, src, n, nb, tile_hist,
+                       ntiles);
+    LAUNCH_CHECK();
+  }
   uint32_t *total = c.get_as<uint32_t>("hist_total", 1);
   scan_exclusive_u32(c, tile_hist, tile_hist, ntiles * nb, total);
   if (save_offsets) {   // the relabel's bucket layout (relabel_bucketed, below)
@@ -384,6 +387,58 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
   c.sync();   // `chunks` is a pageable host buffer
 }
 
+
+
+// ---- degree pass fused with the heads' bucket counts (sequence.h:65-107) --------------
+// k_degree's work (tails with run-combined atomics, the FILE_DAT last record's extra head,
+// max slot, range check) and k_hist_count's per-tile head bucket counts in one read of the
+// records.  Buckets are laid out for the capacity (nb_cap rows); the rows beyond the max
+// slot's stay zero, so the same offsets serve the true key range.
+__global__ __launch_bounds__(CB) void k_degree_fused(const sheep_xs1 *__restrict__ rec, uint64_t n, int mode,
+                                                     uint32_t *__restrict__ deg, uint64_t cap, uint32_t nb,
+                                                     uint32_t *__restrict__ tile_hist, uint64_t ntiles,
+                                                     unsigned long long *__restrict__ d_max,
+                                                     unsigned long long *__restrict__ d_err) {
+  extern __shared__ uint32_t lds[];
+  for (uint32_t b = threadIdx.x; b < nb; b += CB) lds[b] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x << TLOG;
+  uint32_t lmax = 0;
+  bool bad = false;
+  for (uint32_t step = 0; step < TKEYS; step += CB * CPT) {
+    sheep_xs1 r[CPT];
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {   // all loads in flight first
+      const uint64_t i = base + step + (uint64_t)j * CB + threadIdx.x;
+      if (i < n) r[j] = rec[i];
+    }
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const uint64_t i = base + step + (uint64_t)j * CB + threadIdx.x;
+      uint32_t kt = INVALID, kh = INVALID, inc = 1;
+      if (i < n) {
+        const uint32_t t = r[j].tail, h = r[j].head;
+        if (t >= cap || h >= cap) {
+          bad = true;
+        } else {
+          inc = (mode == SHEEP_DEGREE_FILE_DAT && i == n - 1) ? 2u : 1u;
+          kt = t;
+          kh = (mode == SHEEP_DEGREE_LLAMA && t == h) ? INVALID : h;   // LLAMA: self-loop stored once
+          const uint32_t m = (t > h ? t : h) + 1;
+          lmax = m > lmax ? m : lmax;
+        }
+      }
+      run_add(deg, kt, inc);   // every lane of the wave takes part (uniform loop)
+      if (inc == 2 && kh != INVALID) atomicAdd(&deg[kh], 1u);
+      if (kh != INVALID) atomicAdd(&lds[kh >> WBITS], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += CB) tile_hist[(uint64_t)b * ntiles + blockIdx.x] = lds[b];
+  lmax = wave_max(lmax);
+  if ((threadIdx.x & 63) == 0 && lmax) atomicMax(d_max, (unsigned long long)lmax);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(d_err, 1ull);
+}
 
 // ---- head-bucketed relabel (jtree.cpp:72-91) -----------------------------------------
 // k_relabel's pos[head] gather is random over the whole 4-B-per-slot index (268 MB at
@@ -530,16 +585,27 @@ __global__ void k_seg_from_buckets(const uint32_t *__restrict__ bstart, const ui
 
 }  // namespace
 
-void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt) {
+bool degree_fused(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap,
+                  unsigned long long *d_max, unsigned long long *d_err) {
+  const uint64_t nb = (cap + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
+  if (nrec == 0 || nb == 0 || nb > 4096 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return false;
+  uint32_t *tile_hist = c.get_as<uint32_t>("hist_tiles", ntiles * nb + 1);
+  hipLaunchKernelGGL(k_degree_fused, dim3((unsigned)ntiles), dim3(CB), nb * 4, c.stream, rec, nrec, mode, deg, cap,
+                     (uint32_t)nb, tile_hist, ntiles, d_max, d_err);
+  LAUNCH_CHECK();
+  return true;
+}
+
+void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt, bool counted) {
   Ctx::HeadLayout &hl = c.head_layout;
   hl.valid = false;
   const uint64_t nb = (K + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
   if (!llama || nb == 0 || nb > 4096 || ntiles * nb + 1 >= (1ull << 32)) {
-    histogram_add(c, HeadKeys{rec, llama}, nrec, K, cnt);
+    histogram_add(c, HeadKeys{rec, llama}, nrec, K, cnt, nullptr, nullptr, nullptr, nullptr, nullptr, counted);
     return;
   }
   uint32_t *save = c.get_as<uint32_t>("head_offsets", ntiles * nb + 1);
-  histogram_add(c, HeadKeys{rec, llama}, nrec, K, cnt, nullptr, nullptr, nullptr, save, &hl.bstart);
+  histogram_add(c, HeadKeys{rec, llama}, nrec, K, cnt, nullptr, nullptr, nullptr, save, &hl.bstart, counted);
   hl.rec = rec;
   hl.nrec = nrec;
   hl.K = K;

@@ -9,30 +9,12 @@
 //
 // Layout in HBM: records are the 12-byte XS1 AoS exactly as on disk; degree/pos are
 // dense u32 arrays over vertex slots; seq is a dense u32 array over jnids.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace sheep {
 namespace {
-
-// Adds w into cnt[key] for every lane whose key != INVALID, with one atomic per run of
-// equal keys in consecutive lanes (records sorted by tail, as generated and as many
-// edge lists are stored, make tail runs long; a hub's endpoints collapse too).
-__device__ __forceinline__ void run_add(uint32_t *cnt, uint32_t key, uint32_t w) {
-  const int lane = (int)__lane_id();
-  const uint32_t prev = __shfl_up(key, 1, 64);
-  const bool start = key != INVALID && (lane == 0 || prev != key);
-  const uint64_t starts = __ballot(start);
-  const uint32_t rid = (uint32_t)__popcll(starts & ((lane == 63) ? ~0ull : ((2ull << lane) - 1)));
-  uint32_t v = key != INVALID ? w : 0;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t u = __shfl_down(v, o, 64);
-    const uint32_t ro = __shfl_down(rid, o, 64);
-    const uint32_t ko = __shfl_down(key, o, 64);
-    if (lane + o < 64 && ro == rid && ko == key) v += u;
-  }
-  if (start && v) atomicAdd(&cnt[key], v);
-}
 
 __global__ __launch_bounds__(BLOCK) void k_degree(const sheep_xs1 *__restrict__ rec, uint64_t nrec, int mode,
                                                   uint32_t *__restrict__ deg, uint64_t cap,
@@ -143,15 +125,21 @@ void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v) {
   LAUNCH_CHECK();
 }
 
+static const bool g_split_degree = getenv("SHEEP_SPLIT_DEGREE") != nullptr;   // A/B: k_degree + separate head count
+
 void degree_count(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap,
                   uint64_t *max_slot) {
   if (mode < 0 || mode > 2) throw Error(SHEEP_ERR_ARG, "bad degree mode");
   unsigned long long *d = (unsigned long long *)c.d_scalars;
   HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
+  bool counted = false;   // heads' (bucket, tile) counts made by the same pass (hist.hip)
   if (nrec) {
     TimedRegion tr(c, "degree", 12 * nrec);   // one read of the 12-B records
-    hipLaunchKernelGGL(k_degree, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, mode, deg, cap, d, d + 1);
-    LAUNCH_CHECK();
+    counted = !g_split_degree && degree_fused(c, rec, nrec, mode, deg, cap, d, d + 1);
+    if (!counted) {
+      hipLaunchKernelGGL(k_degree, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, mode, deg, cap, d, d + 1);
+      LAUNCH_CHECK();
+    }
   }
   HIP_CHECK(hipMemcpyAsync(c.h_scalars, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
@@ -159,7 +147,7 @@ void degree_count(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_
   *max_slot = c.h_scalars[0];
   if (nrec) {
     TimedRegion tr(c, "degree_heads", 12 * nrec);
-    histogram_heads(c, rec, nrec, mode == SHEEP_DEGREE_LLAMA, *max_slot, deg);
+    histogram_heads(c, rec, nrec, mode == SHEEP_DEGREE_LLAMA, *max_slot, deg, counted);
   }
 }
 
