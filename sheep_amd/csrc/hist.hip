@@ -304,6 +304,15 @@ __global__ __launch_bounds__(HB) void k_hist_final(const uint16_t *__restrict__ 
   }
 }
 
+template <typename Src>
+__global__ __launch_bounds__(BLOCK) void k_count_atomic(Src src, uint64_t n, uint32_t *__restrict__ cnt) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
+    const uint32_t k = src(i);
+    if (k != NO_KEY) atomicAdd(&cnt[k], 1u);
+  }
+}
+
 // Adds the histogram of src's keys over [0, K) into cnt.  With `grouped`, src is
 // EdgeLoPadded, K its padded key range, kbase the counter index of each bucket's first
 // key, and the edges are also written to `grouped` in bucket order; bstart_out (nb + 1
@@ -316,9 +325,16 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
   if (n == 0 || K == 0) return;
   const uint32_t nb = (uint32_t)((K + W - 1) >> WBITS);
   const uint64_t ntiles = (n + TKEYS - 1) >> TLOG;
-  if (ntiles * nb >= (1ull << 32) || n >= (1ull << 32)) throw Error(SHEEP_ERR_ARG, "histogram: too many keys");
-  const size_t lds_scatter = (2 * (size_t)nb + HB / WAVE + TKEYS) * 4;   // <= 160 KiB for nb <= 4096
-  if (lds_scatter > 160 * 1024) throw Error(SHEEP_ERR_ARG, "histogram: key range above 2^27");
+  const size_t lds_scatter = (2 * (size_t)nb + HB / WAVE + TKEYS) * 4;   // <= 160 KiB for nb <= 4087
+  if (lds_scatter > 160 * 1024 || ntiles * nb >= (1ull << 32) || n >= (1ull << 32)) {
+    if constexpr (std::is_same<Src, EdgeLoPadded>::value) {
+      throw Error(SHEEP_ERR_ARG, "group_edges_by_lo: key range above 2^27 or 2^32 edges");
+    } else {   // key ranges beyond the LDS buckets: one scattered atomic per key
+      hipLaunchKernelGGL(k_count_atomic<Src>, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, src, n, cnt);
+      LAUNCH_CHECK();
+      return;
+    }
+  }
   static bool attr_set = false;   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
   if (!attr_set) {
     HIP_CHECK(hipFuncSetAttribute((const void *)k_hist_scatter<HeadKeys>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -599,6 +615,7 @@ bool degree_fused(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_
 void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt, bool counted) {
   Ctx::HeadLayout &hl = c.head_layout;
   hl.valid = false;
+  hl.bstart.clear();
   const uint64_t nb = (K + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
   if (!llama || nb == 0 || nb > 4096 || ntiles * nb + 1 >= (1ull << 32)) {
     histogram_add(c, HeadKeys{rec, llama}, nrec, K, cnt, nullptr, nullptr, nullptr, nullptr, nullptr, counted);

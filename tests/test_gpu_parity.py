@@ -209,6 +209,30 @@ def test_unsequenced_and_out_of_range(gpu_ctx):
     s2 = sheep_amd.sequence_from_host(short)
     with pytest.raises(IndexError):
         sheep_amd.build_tree(_dev_records(rec), s2)
+    swapped = rec.copy()                    # the same record as (0, 10): head beyond max(seq)
+    swapped["tail"], swapped["head"] = rec["head"], rec["tail"]
+    with pytest.raises(IndexError):
+        sheep_amd.build_tree(_dev_records(swapped), s2)
+
+
+def test_wide_vertex_ids_fallback_kernels(gpu_ctx):
+    """Vertex ids above 2^27 exceed the LDS bucket layout (4096 buckets of 2^15 slots):
+    the degree pass and the relabel take their unbucketed kernels (k_degree + separate
+    head count, k_relabel).  Same results as the oracle."""
+    import sheep_amd
+    h = sheep_amd.rmat_host(12, 16, 12)
+    t_ = h[:, 0].astype(np.uint64) * 40000 + 7
+    h_ = h[:, 1].astype(np.uint64) * 40000 + 7
+    assert h_.max() >= (1 << 27)
+    t_, h_ = t_.astype(np.uint32), h_.astype(np.uint32)
+    w = np.ones(len(t_), np.float32)
+    d = sheep_amd.records_to_device(t_, h_, w)
+    s = sheep_amd.degree_sequence(d)
+    seq = oracle.sequence(t_, h_)
+    assert np.array_equal(s.numpy(), seq)
+    p, pw = _tree_np(sheep_amd.build_tree(d, s))
+    op, ow = oracle.build_tree(t_, h_, seq)
+    assert np.array_equal(p, op) and np.array_equal(pw, ow)
 
 
 def test_empty_and_tiny(gpu_ctx):
