@@ -326,9 +326,15 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
   const uint32_t nb = (uint32_t)((K + W - 1) >> WBITS);
   const uint64_t ntiles = (n + TKEYS - 1) >> TLOG;
   const size_t lds_scatter = (2 * (size_t)nb + HB / WAVE + TKEYS) * 4;   // <= 160 KiB for nb <= 4087
-  if (lds_scatter > 160 * 1024 || ntiles * nb >= (1ull << 32) || n >= (1ull << 32)) {
+  // the staged grouping scatter holds 2 nb counters + PER * HB staged edges: nb <= 8192
+  // (lds_exclusive_scan's limit) with PER = 8, i.e. padded lo ranges up to 2^28
+  const size_t lds_staged16 = ((2 * (size_t)nb + HB / WAVE + 1) & ~(size_t)1) * 4 + 16 * HB * 8;
+  const size_t lds_staged8 = lds_staged16 - 8 * HB * 8;
+  const bool fits = std::is_same<Src, EdgeLoPadded>::value ? (nb <= 8 * HB && lds_staged8 <= 160 * 1024)
+                                                            : lds_scatter <= 160 * 1024;
+  if (!fits || ntiles * nb >= (1ull << 32) || n >= (1ull << 32)) {
     if constexpr (std::is_same<Src, EdgeLoPadded>::value) {
-      throw Error(SHEEP_ERR_ARG, "group_edges_by_lo: key range above 2^27 or 2^32 edges");
+      throw Error(SHEEP_ERR_ARG, "group_edges_by_lo: padded lo range above 2^28 or 2^32 edges");
     } else {   // key ranges beyond the LDS buckets: one scattered atomic per key
       hipLaunchKernelGGL(k_count_atomic<Src>, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, src, n, cnt);
       LAUNCH_CHECK();
@@ -358,14 +364,17 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
   }
   if constexpr (std::is_same<Src, EdgeLoPadded>::value) {
     static const bool direct = getenv("SHEEP_LO_DIRECT") != nullptr;   // A/B: one scattered store per lane
-    const size_t lds_staged = ((2 * (size_t)nb + HB / WAVE + 1) & ~(size_t)1) * 4 + 16 * HB * 8;
-    if (!direct && lds_staged <= 160 * 1024) {
-      static bool staged_attr = false;
-      if (!staged_attr) {
-        HIP_CHECK(hipFuncSetAttribute((const void *)k_lo_scatter_staged<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        staged_attr = true;
-      }
-      hipLaunchKernelGGL(k_lo_scatter_staged<16>, dim3((unsigned)ntiles), dim3(HB), lds_staged, c.stream, src, n, nb,
+    static bool staged_attr = false;
+    if (!staged_attr) {
+      HIP_CHECK(hipFuncSetAttribute((const void *)k_lo_scatter_staged<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      HIP_CHECK(hipFuncSetAttribute((const void *)k_lo_scatter_staged<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      staged_attr = true;
+    }
+    if (!direct && lds_staged16 <= 160 * 1024) {
+      hipLaunchKernelGGL(k_lo_scatter_staged<16>, dim3((unsigned)ntiles), dim3(HB), lds_staged16, c.stream, src, n, nb,
+                         (const uint32_t *)tile_hist, ntiles, keys, grouped);
+    } else if (!direct || lds_scatter > 160 * 1024) {
+      hipLaunchKernelGGL(k_lo_scatter_staged<8>, dim3((unsigned)ntiles), dim3(HB), lds_staged8, c.stream, src, n, nb,
                          (const uint32_t *)tile_hist, ntiles, keys, grouped);
     } else {
       hipLaunchKernelGGL(k_lo_scatter, dim3((unsigned)ntiles), dim3(HB), lds_scatter, c.stream, src, n, nb,

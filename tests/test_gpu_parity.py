@@ -248,3 +248,21 @@ def test_empty_and_tiny(gpu_ctx):
     assert list(p) == [0xFFFFFFFF] and list(w) == [0]
     res = sheep_amd.partition(s, sheep_amd.tree_to_device(p, w), 2)
     assert res.created == 1
+
+
+def test_tree_above_2e27_nodes(gpu_ctx):
+    """A path of 1.4e8 vertices: 1.4e8 tree nodes, so the pst grouping's padded lo range
+    needs more than 4087 LDS buckets (staged scatter with 8K-edge sub-tiles); vertex ids
+    above 2^27 also take the atomic heads histogram and k_relabel.  Tree vs the oracle."""
+    import sheep_amd
+    N = 140_000_000
+    t_ = np.arange(N, dtype=np.uint32)
+    h_ = t_ + 1
+    d = sheep_amd.records_to_device(t_, h_)
+    s = sheep_amd.degree_sequence(d)
+    seq = oracle.sequence(t_, h_)
+    assert np.array_equal(s.numpy(), seq)
+    p, w = _tree_np(sheep_amd.build_tree(d, s))
+    del d
+    op, ow = oracle.build_tree(t_, h_, seq)
+    assert np.array_equal(p, op) and np.array_equal(w, ow)
