@@ -494,7 +494,7 @@ struct RelabelKeys {
 // a whole tile does not fit LDS).  gb[b] walks the tile's region of bucket b; every write
 // is bounded by the region's end and a region not filled exactly raises flags[1] (stale
 // offsets) so the host recounts.  flags[0]: a sequenced endpoint's neighbour >= pos_size.
-template <int PER>
+template <int PER, bool NT>
 __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restrict__ rec, uint64_t n,
                                                         const uint32_t *__restrict__ pos, uint64_t pos_size, uint32_t nb,
                                                         const uint32_t *__restrict__ offsets, uint64_t ntiles,
@@ -522,8 +522,15 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
       hd[j] = INVALID;
       pt[j] = INVALID;
       if (i < n) {
-        const sheep_xs1 r = rec[i];
-        if (r.tail != r.head) { hd[j] = r.head; pt[j] = r.tail; }
+        uint32_t t, h;
+        if constexpr (NT) {   // records stream through once: keep pos resident in the caches
+          t = __builtin_nontemporal_load(&rec[i].tail);
+          h = __builtin_nontemporal_load(&rec[i].head);
+        } else {
+          t = rec[i].tail;
+          h = rec[i].head;
+        }
+        if (t != h) { hd[j] = h; pt[j] = t; }
       }
     }
 #pragma unroll
@@ -550,8 +557,12 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
     for (uint32_t j = threadIdx.x; j < total; j += HB) {
       const uint64_t v = stage[j];
       const uint32_t b = (uint32_t)v >> WBITS, dst = gb[b] + j;
-      if (dst < end[b]) out[dst] = v;
-      else lost = true;
+      if (dst < end[b]) {
+        if constexpr (NT) __builtin_nontemporal_store(v, &out[dst]);
+        else out[dst] = v;
+      } else {
+        lost = true;
+      }
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += cur[b];   // past this sub-tile's run
@@ -566,6 +577,7 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
 // One workgroup per (bucket, slice of <= CHUNK pairs): the bucket's pos slice in LDS.
 // Same outcomes as k_relabel: both endpoints sequenced -> tree edge (hi << 32 | lo);
 // one sequenced, the other an unsequenced slot -> POSTORDER pst for the sequenced one.
+template <bool NT>
 __global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restrict__ pairs, const Chunk *__restrict__ chunks,
                                                        const uint32_t *__restrict__ pos, uint64_t pos_size,
                                                        uint32_t *__restrict__ pst, uint64_t *__restrict__ edges,
@@ -581,7 +593,7 @@ __global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restric
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
-      x[j] = i < ch.end ? pairs[i] : NO_PAIR;
+      x[j] = i >= ch.end ? NO_PAIR : NT ? __builtin_nontemporal_load(&pairs[i]) : pairs[i];
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -638,14 +650,19 @@ void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uin
   hl.valid = hl.bstart.size() == nb + 1;
 }
 
+// SHEEP_RL_NT=0/1: plain or non-temporal record/pair streams in the relabel passes (A/B)
+static const bool g_rl_nt = getenv("SHEEP_RL_NT") ? atoi(getenv("SHEEP_RL_NT")) != 0 : false;   // NT: 18.4 vs 13.9 ms at RMAT-26
+
 uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
                           uint32_t *pst, uint64_t *edges, unsigned long long *err) {
   const uint64_t nb = (pos_size + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
   if (nrec == 0 || nb == 0 || nb > 4096 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return UINT64_MAX;
   static bool attr_set = false;
   if (!attr_set) {
-    for (const void *f : {(const void *)k_relabel_scatter<16>, (const void *)k_relabel_scatter<8>,
-                          (const void *)k_relabel_scatter<4>, (const void *)k_relabel_gather})
+    for (const void *f : {(const void *)k_relabel_scatter<16, false>, (const void *)k_relabel_scatter<8, false>,
+                          (const void *)k_relabel_scatter<4, false>, (const void *)k_relabel_gather<false>,
+                          (const void *)k_relabel_scatter<16, true>, (const void *)k_relabel_scatter<8, true>,
+                          (const void *)k_relabel_scatter<4, true>, (const void *)k_relabel_gather<true>})
       HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
@@ -676,15 +693,19 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   auto scatter = [&]() {
     HIP_CHECK(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c.stream));
     static const int per_max = getenv("SHEEP_RL_PER") ? atoi(getenv("SHEEP_RL_PER")) : 8;   // experiments
-    if (per_max >= 16 && fixed + 16 * HB * 8 <= 160 * 1024)
-      hipLaunchKernelGGL(k_relabel_scatter<16>, dim3((unsigned)ntiles), dim3(HB), fixed + 16 * HB * 8, c.stream, rec, nrec,
-                         pos, pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
-    else if (per_max >= 8 && fixed + 8 * HB * 8 <= 160 * 1024)
-      hipLaunchKernelGGL(k_relabel_scatter<8>, dim3((unsigned)ntiles), dim3(HB), fixed + 8 * HB * 8, c.stream, rec, nrec,
-                         pos, pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
-    else
-      hipLaunchKernelGGL(k_relabel_scatter<4>, dim3((unsigned)ntiles), dim3(HB), fixed + 4 * HB * 8, c.stream, rec, nrec,
-                         pos, pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
+    const int per = per_max >= 16 && fixed + 16 * HB * 8 <= 160 * 1024 ? 16
+                  : per_max >= 8 && fixed + 8 * HB * 8 <= 160 * 1024 ? 8 : 4;
+    const size_t lds = fixed + (size_t)per * HB * 8;
+    const dim3 g((unsigned)ntiles), b(HB);
+    const uint32_t nb32 = (uint32_t)nb;
+    const uint32_t *o = off;
+#define SHEEP_RL_SCATTER(P, N) hipLaunchKernelGGL((k_relabel_scatter<P, N>), g, b, lds, c.stream, rec, nrec, pos, pos_size, nb32, o, ntiles, pairs, flags)
+    if (g_rl_nt) {
+      if (per == 16) SHEEP_RL_SCATTER(16, true); else if (per == 8) SHEEP_RL_SCATTER(8, true); else SHEEP_RL_SCATTER(4, true);
+    } else {
+      if (per == 16) SHEEP_RL_SCATTER(16, false); else if (per == 8) SHEEP_RL_SCATTER(8, false); else SHEEP_RL_SCATTER(4, false);
+    }
+#undef SHEEP_RL_SCATTER
     LAUNCH_CHECK();
     HIP_CHECK(hipMemcpyAsync(c.h_scalars + 12, flags, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   };
@@ -714,8 +735,12 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   if (!chunks.empty()) {
     Chunk *dch = c.get_as<Chunk>("rl_chunks", chunks.size());
     HIP_CHECK(hipMemcpyAsync(dch, chunks.data(), chunks.size() * sizeof(Chunk), hipMemcpyHostToDevice, c.stream));
-    hipLaunchKernelGGL(k_relabel_gather, dim3((unsigned)chunks.size()), dim3(HB), W * 4, c.stream, (const uint64_t *)pairs,
-                       (const Chunk *)dch, pos, pos_size, pst, edges, err);
+    if (g_rl_nt)
+      hipLaunchKernelGGL(k_relabel_gather<true>, dim3((unsigned)chunks.size()), dim3(HB), W * 4, c.stream,
+                         (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err);
+    else
+      hipLaunchKernelGGL(k_relabel_gather<false>, dim3((unsigned)chunks.size()), dim3(HB), W * 4, c.stream,
+                         (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err);
     LAUNCH_CHECK();
     c.sync();   // `chunks` is a pageable host buffer
   }
