@@ -142,7 +142,10 @@ int sheep_positions(sheep_ctx *ctx, const uint32_t *seq_dev, uint64_t n, uint32_
  * tree_dev[0,n): Liu's elimination tree of this shard's records under the order pos
  * (parent INVALID = root) and pst_weight = #later neighbours.  Records whose endpoint
  * is >= pos_size while the other endpoint is sequenced -> SHEEP_ERR_RANGE
- * (jtree.cpp:75 index.at). */
+ * (jtree.cpp:75 index.at).  When the context's last sheep_degree_count (LLAMA mode) saw
+ * the same rec_dev/nrec with max_slot == pos_size, its head-bucket layout is reused for
+ * the relabel; records changed in place since are detected on the device and recounted,
+ * so reuse never changes the result. */
 int sheep_build_tree(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec,
                      const uint32_t *pos_dev, uint64_t pos_size, uint64_t n,
                      sheep_jnode *tree_dev);
