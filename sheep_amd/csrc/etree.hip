@@ -468,6 +468,9 @@ __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restric
 
 // cnt: the three rows (stride cstride, zero-padded) scanned as ONE exclusive scan, so a
 // row's offsets are relative to its first entry; the row totals go to st.
+// STAGED: each class's run of the tile is first placed in LDS at its thread-major rank,
+// then copied out by consecutive lanes (the same positions, coalesced stores).
+template <bool STAGED>
 __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
                                                        uint64_t *__restrict__ st, int s, uint32_t clo,
                                                        const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
@@ -507,16 +510,35 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
     uint64_t off = 0;
     for (int w = 0; w < wave; ++w) off += s_w[w];
     const uint64_t ex = off + inc - c3;
-    uint64_t pk = cnt[tile] - b0 + (ex & 0xFFFF);
-    uint64_t pl = cnt[cstride + tile] - b1 + ((ex >> 16) & 0xFFFF);
-    uint64_t px = cnt[2 * cstride + tile] - b2 + (ex >> 32);
+    if constexpr (STAGED) {
+      __shared__ uint64_t stg[TILE];
+      uint64_t tot = 0;
+      for (int w = 0; w < BLOCK / WAVE; ++w) tot += s_w[w];
+      uint64_t *const outs[3] = {next, lbuf, xbuf};
 #pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) {
-      if (cl[j] & 1) next[pk++] = ev[j];
-      if (cl[j] & 2) lbuf[pl++] = ev[j];
-      if (cl[j] & 4) xbuf[px++] = ev[j];
+      for (int k = 0; k < 3; ++k) {
+        uint32_t r = (uint32_t)((ex >> (16 * k)) & 0xFFFF);
+#pragma unroll
+        for (int j = 0; j < TILE_ITEMS; ++j)
+          if ((cl[j] >> k) & 1) stg[r++] = ev[j];
+        __syncthreads();
+        const uint32_t n_k = (uint32_t)((tot >> (16 * k)) & 0xFFFF);
+        uint64_t *const o = outs[k] + (cnt[k * cstride + tile] - cnt[k * cstride]);
+        for (uint32_t i = threadIdx.x; i < n_k; i += BLOCK) o[i] = stg[i];
+        __syncthreads();   // stg (and, after the last class, s_w) is rewritten next
+      }
+    } else {
+      uint64_t pk = cnt[tile] - b0 + (ex & 0xFFFF);
+      uint64_t pl = cnt[cstride + tile] - b1 + ((ex >> 16) & 0xFFFF);
+      uint64_t px = cnt[2 * cstride + tile] - b2 + (ex >> 32);
+#pragma unroll
+      for (int j = 0; j < TILE_ITEMS; ++j) {
+        if (cl[j] & 1) next[pk++] = ev[j];
+        if (cl[j] & 2) lbuf[pl++] = ev[j];
+        if (cl[j] & 4) xbuf[px++] = ev[j];
+      }
+      __syncthreads();   // s_w is rewritten by the next tile
     }
-    __syncthreads();   // s_w is rewritten by the next tile
   }
 }
 
@@ -757,6 +779,7 @@ __global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t 
 void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
 
 static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
+static const bool g_split_staged = getenv("SHEEP_SPLIT_STAGED") ? atoi(getenv("SHEEP_SPLIT_STAGED")) != 0 : true;
 static const bool g_plain_relabel = getenv("SHEEP_PLAIN_RELABEL") != nullptr;   // A/B: k_relabel only
 static int env_int(const char *name, int def) {
   const char *v = getenv(name);
@@ -859,9 +882,14 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
                          (const uint64_t *)r0, (const uint64_t *)seg, L, tcnt, cstride);
       LAUNCH_CHECK();
       scan_exclusive_u64(c, tcnt, tcnt, 3 * cstride + 1, nullptr);
-      hipLaunchKernelGGL(k_split_write, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo,
-                         (const uint64_t *)r0, (const uint64_t *)seg, L, (const uint64_t *)tcnt, cstride, next, lbuf,
-                         xbuf);
+      if (g_split_staged)
+        hipLaunchKernelGGL(k_split_write<true>, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s,
+                           clo, (const uint64_t *)r0, (const uint64_t *)seg, L, (const uint64_t *)tcnt, cstride, next,
+                           lbuf, xbuf);
+      else
+        hipLaunchKernelGGL(k_split_write<false>, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s,
+                           clo, (const uint64_t *)r0, (const uint64_t *)seg, L, (const uint64_t *)tcnt, cstride, next,
+                           lbuf, xbuf);
       LAUNCH_CHECK();
     }
     {
