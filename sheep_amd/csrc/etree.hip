@@ -381,18 +381,37 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restric
   const uint64_t nx = st[ST_NX];
   const bool sparse = level_sparse(st[ST_NL], nx, n);
   uint64_t *out = next + st[ST_KEPT];
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < nx; j += stride) {
-    const uint32_t r = xtop[j], m = mt[r];
-    if (sparse) parent[top[r]] = m;   // jnode.h:158-162 adopt (all cross edges of r store the same m)
-    const uint32_t b = (uint32_t)(xbuf[j] >> 32);
-    bool kill = b == m;
-    if (!kill) {
-      uint32_t c = claim[b];
-      if (c == INVALID) c = atomicCAS(&claim[b], INVALID, m);
-      kill = c == m;   // someone else's (m, b) is kept (our own successful CAS returned INVALID)
+  // XK edges per thread with every gather stage issued for all of them before the next
+  // (xtop/xbuf, then mt, then claim): XK independent chains in flight per lane
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK * XK;
+  for (uint64_t j0 = (uint64_t)blockIdx.x * BLOCK * XK + threadIdx.x; j0 < nx; j0 += stride) {
+    uint32_t r[XK], b[XK], m[XK], cl[XK];
+    bool live[XK];
+#pragma unroll
+    for (int k = 0; k < XK; ++k) {
+      const uint64_t j = j0 + (uint64_t)k * BLOCK;
+      live[k] = j < nx;
+      r[k] = live[k] ? xtop[j] : 0;
+      b[k] = live[k] ? (uint32_t)(xbuf[j] >> 32) : 0;
     }
-    out[j] = kill ? DEAD : ((uint64_t)b << 32) | m;
+#pragma unroll
+    for (int k = 0; k < XK; ++k) m[k] = live[k] ? mt[r[k]] : INVALID;
+#pragma unroll
+    for (int k = 0; k < XK; ++k) {
+      if (live[k] && sparse) parent[top[r[k]]] = m[k];   // jnode.h:158-162 adopt (all cross edges of r store the same m)
+      cl[k] = live[k] && b[k] != m[k] ? claim[b[k]] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < XK; ++k) {
+      if (!live[k]) continue;
+      bool kill = b[k] == m[k];
+      if (!kill) {
+        uint32_t c = cl[k];
+        if (c == INVALID) c = atomicCAS(&claim[b[k]], INVALID, m[k]);
+        kill = c == m[k];   // someone else's (m, b) is kept (our own successful CAS returned INVALID)
+      }
+      out[j0 + (uint64_t)k * BLOCK] = kill ? DEAD : ((uint64_t)b[k] << 32) | m[k];
+    }
   }
 }
 
