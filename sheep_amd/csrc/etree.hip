@@ -276,6 +276,11 @@ __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict_
 // not retried here: the edge goes to `out` for the next round.  Retrying in place made
 // thousands of threads fight over a forming giant component's root (each failure =
 // another round trip); rounds instead resolve such a pile-up in a few passes.
+//
+// BATCH: the finds of all the thread's edges run as one set of independent chains in
+// lockstep (find_many) before any hook; a root that a same-thread hook has meanwhile
+// hooked fails its CAS and the edge goes to the next round, as any lost race does.
+template <bool BATCH>
 __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict__ in, const uint64_t *__restrict__ n_in,
                                                       uint32_t *uf, uint64_t *__restrict__ out,
                                                       unsigned long long *__restrict__ counter) {
@@ -289,14 +294,33 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
       const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
       ev[j] = i < nin ? in[i] : DEAD;
     }
+    if constexpr (BATCH) {
+      uint32_t x[2 * TILE_ITEMS];
+      bool v[2 * TILE_ITEMS];
 #pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) {
-      if (ev[j] == DEAD) continue;
-      uint32_t a = (uint32_t)ev[j], b = (uint32_t)(ev[j] >> 32);
-      find2(uf, a, b);
-      if (a == b) continue;
-      const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-      if (atomicCAS(&uf[hi], hi, lo) != hi) keep |= 1u << j;
+      for (int j = 0; j < TILE_ITEMS; ++j) {
+        v[2 * j] = v[2 * j + 1] = ev[j] != DEAD;
+        x[2 * j] = (uint32_t)ev[j];
+        x[2 * j + 1] = (uint32_t)(ev[j] >> 32);
+      }
+      find_many<2 * TILE_ITEMS>(uf, x, v);
+#pragma unroll
+      for (int j = 0; j < TILE_ITEMS; ++j) {
+        const uint32_t a = x[2 * j], b = x[2 * j + 1];
+        if (!v[2 * j] || a == b) continue;
+        const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+        if (atomicCAS(&uf[hi], hi, lo) != hi) keep |= 1u << j;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < TILE_ITEMS; ++j) {
+        if (ev[j] == DEAD) continue;
+        uint32_t a = (uint32_t)ev[j], b = (uint32_t)(ev[j] >> 32);
+        find2(uf, a, b);
+        if (a == b) continue;
+        const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+        if (atomicCAS(&uf[hi], hi, lo) != hi) keep |= 1u << j;
+      }
     }
     uint64_t slot = shard_reserve((uint32_t)__popc(keep), counter, tile, ntiles, 1);
 #pragma unroll
@@ -799,6 +823,8 @@ void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
 
 static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
 static const bool g_split_staged = getenv("SHEEP_SPLIT_STAGED") ? atoi(getenv("SHEEP_SPLIT_STAGED")) != 0 : true;
+// batched finds leave more hooks to later rounds: etree_union 21-22 ms vs 10.8 at RMAT-26
+static const bool g_hook_batch = getenv("SHEEP_HOOK_BATCH") ? atoi(getenv("SHEEP_HOOK_BATCH")) != 0 : false;
 static const bool g_plain_relabel = getenv("SHEEP_PLAIN_RELABEL") != nullptr;   // A/B: k_relabel only
 static int env_int(const char *name, int def) {
   const char *v = getenv(name);
@@ -916,7 +942,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       const uint64_t *in = lbuf, *n_in = st + ST_NL;
       for (int round = 0; round < HOOK_ROUNDS; ++round) {
         uint64_t *dst = hk[round & 1];
-        hipLaunchKernelGGL(k_hook_round, dim3(gt), dim3(BLOCK), 0, c.stream, in, n_in, uf, alt, cset(CSET_HOOK + round));
+        hipLaunchKernelGGL(g_hook_batch ? k_hook_round<true> : k_hook_round<false>, dim3(gt), dim3(BLOCK), 0, c.stream, in, n_in, uf, alt, cset(CSET_HOOK + round));
         LAUNCH_CHECK();
         pack_shards<uint64_t>(c, alt, dst, n_in, cset(CSET_HOOK + round), st + ST_HOOK + round);
         in = dst;
