@@ -40,7 +40,7 @@ oracle: oracle/lib/libsheep_oracle.so
 
 oracle/lib/libsheep_oracle.so: oracle/sheep_oracle.cpp
 	@mkdir -p oracle/lib
-	$(CXX) -std=c++17 -O2 -fPIC -shared -Wall -o $@ $<
+	$(CXX) -std=c++17 -O2 -fopenmp -fPIC -shared -Wall -o $@ $<
 
 ref:
 	@if [ -d /root/reference/lib ]; then $(MAKE) -C oracle/ref; else echo "no /root/reference: skipping oracle/_ref"; fi

@@ -165,9 +165,13 @@ int sheep_kids_create(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n,
                       sheep_kids **out);
 int sheep_kids_destroy(sheep_kids *kids);
 /* parts_vid_dev[0, pos_size) (pos_size = max(seq)+1) receives the vid-indexed parts
- * (SHEEP_INVALID_PART for unsequenced slots).  info is host (synchronises). */
+ * (SHEEP_INVALID_PART for unsequenced slots): parts of jnids 0 .. seq_n-1 go to
+ * seq[0 .. seq_n-1] (partition.cpp:62-66).  seq_n > n fails with SHEEP_ERR_RANGE, the
+ * reference's parts.at(i) throw; a shorter sequence converts only its own entries.
+ * info->created / first_size / second_size are counted over the vid-indexed vector
+ * (partition.h:135-143).  info is host (synchronises). */
 int sheep_partition(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n,
-                    const uint32_t *seq_dev, uint64_t pos_size, sheep_kids *kids, int16_t k,
+                    const uint32_t *seq_dev, uint64_t seq_n, uint64_t pos_size, sheep_kids *kids, int16_t k,
                     double balance, int vtx_weight, int pst_weight, int16_t *parts_vid_dev,
                     sheep_partition_info *info);
 
@@ -181,6 +185,27 @@ int sheep_partition(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n,
 int sheep_evaluate(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec,
                    const uint32_t *pos_dev, uint64_t pos_size, const int16_t *parts_vid_dev,
                    int what, sheep_eval *out);
+/* The same evaluators over edge shards (the records of one graph
+ * split over devices or passes):
+ *   sheep_eval_sizes      u64 words of the bitset and accumulator state for (what,
+ *                         nparts, pos_size); nparts = max part + 1
+ *                         (sheep_eval_num_parts);
+ *   sheep_eval_shard      ORs one shard's owner bits into bits_dev and adds its counts into
+ *                         acc_dev (both zeroed by the caller before the first shard);
+ *   sheep_eval_combine    bits_dev |= bits_src, acc_dev += acc_src (state of another
+ *                         device's shards, copied over: the reduction step);
+ *   sheep_eval_finish     the per-vertex pass over the combined state and the result
+ *                         (host, synchronises).
+ * shard + finish over all records == sheep_evaluate. */
+int sheep_eval_sizes(int what, int32_t nparts, uint64_t pos_size, uint64_t *bits_words, uint64_t *acc_words);
+int sheep_eval_num_parts(sheep_ctx *ctx, const int16_t *parts_vid_dev, uint64_t pos_size, int32_t *nparts_out);
+int sheep_eval_shard(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec, const uint32_t *pos_dev,
+                     uint64_t pos_size, const int16_t *parts_vid_dev, int what, int32_t nparts,
+                     uint64_t *bits_dev, uint64_t *acc_dev);
+int sheep_eval_combine(sheep_ctx *ctx, uint64_t *bits_dev, const uint64_t *bits_src_dev, uint64_t bits_words,
+                       uint64_t *acc_dev, const uint64_t *acc_src_dev, uint64_t acc_words);
+int sheep_eval_finish(sheep_ctx *ctx, const uint64_t *bits_dev, const uint64_t *acc_dev, uint64_t pos_size,
+                      const int16_t *parts_vid_dev, int what, int32_t nparts, sheep_eval *out);
 
 /* ---- partition files ----------------------------------------------------------------
  * edge_part_dev[i] = the part record i is written to by writePartitionedGraph

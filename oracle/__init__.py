@@ -30,8 +30,9 @@ def lib():
         L.or_kids_create.argtypes = [P, U64]
         L.or_kids_create.restype = P
         L.or_kids_free.argtypes = [P]
-        L.or_partition.argtypes = [P, P, U64, P, P, ctypes.c_int16, ctypes.c_double, I32, I32, P, U64,
+        L.or_partition.argtypes = [P, P, U64, P, U64, P, ctypes.c_int16, ctypes.c_double, I32, I32, P, U64,
                                    ctypes.POINTER(U64), P]
+        L.or_set_threads.argtypes = [I32]
         L.or_evaluate.argtypes = [P, P, U64, P, U64, P, U64, P]
         L.or_facts_text.argtypes = [P, P, U64, P, U64]
         L.or_eval_text.argtypes = [P, ctypes.c_int16, P, U64]
@@ -52,13 +53,20 @@ def _p(a):
     return a.ctypes.data
 
 
+def set_threads(n: int):
+    """OpenMP threads of the graph build and evaluators (default 1)."""
+    lib().or_set_threads(int(n))
+
+
 def sequence(tail, head, mode="llama"):
+    """mode 'llama' (degreeSequence over the LLAMA graph), 'records' (the same degrees
+    counted straight from the records, no adjacency build), 'dat' / 'net' (fileSequence)."""
     tail, head = _u32(tail), _u32(head)
     cap = 2 * len(tail) + 2
     out = np.empty(cap, np.uint32)
     n = ctypes.c_uint64()
-    _chk(lib().or_sequence(_p(tail), _p(head), len(tail), {"llama": 0, "dat": 1, "net": 2}[mode], _p(out), cap,
-                           ctypes.byref(n)))
+    _chk(lib().or_sequence(_p(tail), _p(head), len(tail), {"llama": 0, "dat": 1, "net": 2, "records": 3}[mode],
+                           _p(out), cap, ctypes.byref(n)))
     return out[: n.value].copy()
 
 
@@ -115,7 +123,7 @@ def partition(parent, pst, seq, k, balance=1.03, vtx=False, pstw=True, kids=None
     parts = np.empty(cap, np.int16)
     vs = ctypes.c_uint64()
     info = np.zeros(3, np.int64)
-    _chk(lib().or_partition(_p(parent), _p(pst), len(parent), _p(seq), kids.h, int(k), float(balance), int(vtx),
+    _chk(lib().or_partition(_p(parent), _p(pst), len(parent), _p(seq), len(seq), kids.h, int(k), float(balance), int(vtx),
                             int(pstw), _p(parts), cap, ctypes.byref(vs), _p(info)))
     return parts[: vs.value].copy(), {"created": int(info[0]), "max_component": int(info[1]),
                                       "packing_nodes": int(info[2])}

@@ -26,8 +26,9 @@
 #include <numeric>
 #include <stdexcept>
 #include <string>
-#include <unordered_set>
 #include <vector>
+
+#include <omp.h>
 
 namespace oracle {
 
@@ -54,6 +55,9 @@ struct LlamaGraph {
   std::vector<uint32_t> adj;   // neighbours in record order
   uint64_t num_nodes = 0;
 
+  // With more than one OpenMP thread (or_set_threads) the adjacency lists are filled
+  // concurrently, so their order is not record order; nothing the oracle computes from
+  // a graph (degrees, the elimination tree, the evaluators) depends on that order.
   LlamaGraph(const uint32_t *tail, const uint32_t *head, uint64_t R,
              uint64_t part = 0, uint64_t num_parts = 0) {
     uint64_t beg = 0, end = R;
@@ -61,22 +65,38 @@ struct LlamaGraph {
       beg = (part - 1) * R / num_parts;
       end = part * R / num_parts;
     }
-    for (uint64_t i = beg; i < end; ++i)
-      max_nodes = std::max(max_nodes, std::max(tail[i], head[i]) + 1);
+    uint32_t mx = 0;
+#pragma omp parallel for reduction(max : mx) schedule(static)
+    for (uint64_t i = beg; i < end; ++i) mx = std::max(mx, std::max(tail[i], head[i]) + 1);
+    max_nodes = mx;
     off.assign((size_t)max_nodes + 1, 0);
+    uint64_t *o = off.data();
+#pragma omp parallel for schedule(static)
     for (uint64_t i = beg; i < end; ++i) {
-      off[tail[i] + 1]++;
-      if (tail[i] != head[i]) off[head[i] + 1]++;
+      __atomic_fetch_add(&o[tail[i] + 1], 1, __ATOMIC_RELAXED);
+      if (tail[i] != head[i]) __atomic_fetch_add(&o[head[i] + 1], 1, __ATOMIC_RELAXED);
     }
     for (uint32_t v = 0; v < max_nodes; ++v) off[v + 1] += off[v];
     adj.resize(off[max_nodes]);
     std::vector<uint64_t> cur(off.begin(), off.end() - 1);
-    for (uint64_t i = beg; i < end; ++i) {
-      adj[cur[tail[i]]++] = head[i];
-      if (tail[i] != head[i]) adj[cur[head[i]]++] = tail[i];
+    uint64_t *c = cur.data();
+    uint32_t *a = adj.data();
+    if (omp_get_max_threads() == 1) {
+      for (uint64_t i = beg; i < end; ++i) {
+        a[c[tail[i]]++] = head[i];
+        if (tail[i] != head[i]) a[c[head[i]]++] = tail[i];
+      }
+    } else {
+#pragma omp parallel for schedule(static)
+      for (uint64_t i = beg; i < end; ++i) {
+        a[__atomic_fetch_add(&c[tail[i]], 1, __ATOMIC_RELAXED)] = head[i];
+        if (tail[i] != head[i]) a[__atomic_fetch_add(&c[head[i]], 1, __ATOMIC_RELAXED)] = tail[i];
+      }
     }
-    for (uint32_t v = 0; v < max_nodes; ++v)
-      if (deg(v) != 0) ++num_nodes;
+    uint64_t nn = 0;
+#pragma omp parallel for reduction(+ : nn) schedule(static)
+    for (uint32_t v = 0; v < max_nodes; ++v) nn += deg(v) != 0;
+    num_nodes = nn;
   }
   uint64_t deg(uint32_t v) const { return v < max_nodes ? off[v + 1] - off[v] : 0; }
   bool isNode(uint32_t v) const { return v < max_nodes && deg(v) != 0; }   // :83-85
@@ -103,6 +123,23 @@ static std::vector<uint32_t> sort_by_degree(const std::vector<uint64_t> &degree)
 std::vector<uint32_t> degreeSequence(const LlamaGraph &g) {
   std::vector<uint64_t> degree(g.max_nodes);
   for (uint32_t x = 0; x < g.max_nodes; ++x) degree[x] = g.deg(x);
+  return sort_by_degree(degree);
+}
+
+// The same sequence without building the adjacency: LLAMA's getDeg(v) (graph_wrapper.h:
+// 87-89) is the number of adjacency entries of v = records with tail v plus records with
+// head v that are not self-loops.
+std::vector<uint32_t> degreeSequenceFromRecords(const uint32_t *tail, const uint32_t *head, uint64_t R) {
+  uint32_t mx = 0;
+#pragma omp parallel for reduction(max : mx) schedule(static)
+  for (uint64_t i = 0; i < R; ++i) mx = std::max(mx, std::max(tail[i], head[i]) + 1);
+  std::vector<uint64_t> degree(mx, 0);
+  uint64_t *d = degree.data();
+#pragma omp parallel for schedule(static)
+  for (uint64_t i = 0; i < R; ++i) {
+    __atomic_fetch_add(&d[tail[i]], 1, __ATOMIC_RELAXED);
+    if (tail[i] != head[i]) __atomic_fetch_add(&d[head[i]], 1, __ATOMIC_RELAXED);
+  }
   return sort_by_degree(degree);
 }
 
@@ -375,55 +412,108 @@ static inline uint32_t cormen_hash(uint32_t k) {            // partition.cpp:423
   return k * s;
 }
 
+// The reference inserts owners into a std::unordered_set<part_t> per node and takes its
+// size(); PartSet is the same distinct count over a bitset of the part ids.
+struct PartSet {
+  std::vector<uint64_t> w;
+  std::vector<uint32_t> touched;
+  size_t n = 0;
+  explicit PartSet(size_t nparts) : w((nparts + 63) / 64, 0) {}
+  void insert(part_t p) {
+    uint64_t &x = w.at((size_t)(uint16_t)p >> 6);
+    const uint64_t b = 1ull << (p & 63);
+    if (!(x & b)) {
+      if (!x) touched.push_back((uint32_t)((size_t)(uint16_t)p >> 6));
+      x |= b;
+      ++n;
+    }
+  }
+  size_t size() const { return n; }
+  void clear() {
+    for (uint32_t i : touched) w[i] = 0;
+    touched.clear();
+    n = 0;
+  }
+};
+
 EvalResult evaluate(const LlamaGraph &g, const std::vector<part_t> &parts,
                     const std::vector<uint32_t> &seq, bool with_seq) {
   EvalResult r;
   r.edges = g.getEdges();
   r.nodes = g.getNodes();
   part_t max_part = *std::max_element(parts.begin(), parts.end());
-  std::vector<uint64_t> vbal(max_part + 1, 0), hbal(max_part + 1, 0);
-  for (uint32_t X = 0; X < g.max_nodes; ++X) {               // evaluate(graph) :428-473
-    if (!g.isNode(X)) continue;
-    part_t Xp = parts.at(X);
-    if (Xp == INVALID_PART) throw std::runtime_error("unassigned vertex");
-    vbal.at(Xp) += 1;
-    std::unordered_set<part_t> vc = {Xp}, eh;
-    for (uint64_t e = g.off[X]; e < g.off[X + 1]; ++e) {
-      uint32_t Y = g.adj[e];
-      part_t Yp = parts.at(Y);
-      if (X < Y && Xp != Yp) ++r.edges_cut;
-      vc.insert(Yp);
-      part_t hp = cormen_hash(X) < cormen_hash(Y) ? Xp : Yp;
-      eh.insert(hp);
-      if (X < Y) hbal.at(hp) += 1;
+  const size_t np = (size_t)max_part + 1;
+  std::vector<uint64_t> vbal(np, 0), hbal(np, 0);
+  uint64_t cut = 0, vcom = 0, ecvh = 0;
+  bool bad = false;
+#pragma omp parallel reduction(+ : cut, vcom, ecvh) reduction(|| : bad)
+  {
+    std::vector<uint64_t> lv(np, 0), lh(np, 0);
+    PartSet vc(np), eh(np);
+#pragma omp for schedule(dynamic, 4096)
+    for (uint32_t X = 0; X < g.max_nodes; ++X) {             // evaluate(graph) :428-473
+      if (!g.isNode(X)) continue;
+      part_t Xp = parts.at(X);
+      if (Xp == INVALID_PART) { bad = true; continue; }
+      lv.at(Xp) += 1;
+      vc.clear(); eh.clear();
+      vc.insert(Xp);
+      for (uint64_t e = g.off[X]; e < g.off[X + 1]; ++e) {
+        uint32_t Y = g.adj[e];
+        part_t Yp = parts.at(Y);
+        if (Yp == INVALID_PART) { bad = true; continue; }
+        if (X < Y && Xp != Yp) ++cut;
+        vc.insert(Yp);
+        part_t hp = cormen_hash(X) < cormen_hash(Y) ? Xp : Yp;
+        eh.insert(hp);
+        if (X < Y) lh.at(hp) += 1;
+      }
+      vcom += vc.size() - 1;
+      ecvh += eh.size() - 1;
     }
-    r.vcom_vol += vc.size() - 1;
-    r.ecv_hash += eh.size() - 1;
+#pragma omp critical
+    for (size_t p = 0; p < np; ++p) { vbal[p] += lv[p]; hbal[p] += lh[p]; }
   }
+  if (bad) throw std::runtime_error("unassigned vertex");
+  r.edges_cut = cut; r.vcom_vol = vcom; r.ecv_hash = ecvh;
   r.max_vertex_bal = *std::max_element(vbal.begin(), vbal.end());
   r.max_hash_bal = *std::max_element(hbal.begin(), hbal.end());
   if (!with_seq) return r;
 
   std::vector<uint32_t> pos((size_t)*std::max_element(seq.begin(), seq.end()) + 1, INVALID);
   for (uint32_t i = 0; i < seq.size(); ++i) pos[seq[i]] = i;
-  std::vector<uint64_t> dbal(max_part + 1, 0), ubal(max_part + 1, 0);
-  for (uint32_t X = 0; X < g.max_nodes; ++X) {               // evaluate(graph, seq) :475-521
-    if (!g.isNode(X)) continue;
-    uint32_t Xpos = pos.at(X);
-    part_t Xp = parts.at(X);
-    std::unordered_set<part_t> dn, up;
-    for (uint64_t e = g.off[X]; e < g.off[X + 1]; ++e) {
-      uint32_t Y = g.adj[e];
-      uint32_t Ypos = pos.at(Y);
-      part_t Yp = parts.at(Y);
-      dn.insert(Xpos < Ypos ? Xp : Yp);
-      up.insert(Xpos > Ypos ? Xp : Yp);
-      if (Xpos < Ypos) dbal.at(Xp) += 1;
-      if (Xpos > Ypos) ubal.at(Xp) += 1;
+  std::vector<uint64_t> dbal(np, 0), ubal(np, 0);
+  uint64_t down = 0, upc = 0;
+  bool oor = false;
+#pragma omp parallel reduction(+ : down, upc) reduction(|| : oor)
+  {
+    std::vector<uint64_t> ld(np, 0), lu(np, 0);
+    PartSet dn(np), up(np);
+#pragma omp for schedule(dynamic, 4096)
+    for (uint32_t X = 0; X < g.max_nodes; ++X) {             // evaluate(graph, seq) :475-521
+      if (!g.isNode(X)) continue;
+      if (X >= pos.size()) { oor = true; continue; }          // pos.at(X) throws
+      uint32_t Xpos = pos[X];
+      part_t Xp = parts.at(X);
+      dn.clear(); up.clear();
+      for (uint64_t e = g.off[X]; e < g.off[X + 1]; ++e) {
+        uint32_t Y = g.adj[e];
+        if (Y >= pos.size()) { oor = true; continue; }
+        uint32_t Ypos = pos[Y];
+        part_t Yp = parts.at(Y);
+        dn.insert(Xpos < Ypos ? Xp : Yp);
+        up.insert(Xpos > Ypos ? Xp : Yp);
+        if (Xpos < Ypos) ld.at(Xp) += 1;
+        if (Xpos > Ypos) lu.at(Xp) += 1;
+      }
+      down += dn.size() - 1;
+      upc += up.size() - 1;
     }
-    r.ecv_down += dn.size() - 1;
-    r.ecv_up += up.size() - 1;
+#pragma omp critical
+    for (size_t p = 0; p < np; ++p) { dbal[p] += ld[p]; ubal[p] += lu[p]; }
   }
+  if (oor) throw std::out_of_range("vector::_M_range_check: pos.at()");
+  r.ecv_down = down; r.ecv_up = upc;
   r.max_down_bal = *std::max_element(dbal.begin(), dbal.end());
   r.max_up_bal = *std::max_element(ubal.begin(), ubal.end());
   return r;
@@ -462,6 +552,10 @@ static thread_local std::string g_err;
 extern "C" {
 const char *or_last_error() { return g_err.c_str(); }
 
+// OpenMP threads for the graph build and the evaluators (default 1; tests raise it for
+// BASELINE-size parity checks).
+void or_set_threads(int n) { omp_set_num_threads(n < 1 ? 1 : n); }
+
 // mode 0: LLAMA degree sequence (degreeSequence / mpiSequence); mode 1: file sequence
 // over .dat records (last record twice); mode 2: file sequence over .net pairs.
 int or_sequence(const uint32_t *tail, const uint32_t *head, uint64_t R, int mode,
@@ -469,6 +563,7 @@ int or_sequence(const uint32_t *tail, const uint32_t *head, uint64_t R, int mode
   OR_TRY({
     std::vector<uint32_t> s;
     if (mode == 0) s = degreeSequence(LlamaGraph(tail, head, R));
+    else if (mode == 3) s = degreeSequenceFromRecords(tail, head, R);
     else s = fileSequence(tail, head, R, mode == 1);
     if (s.size() > cap) throw std::length_error("seq capacity");
     std::copy(s.begin(), s.end(), seq_out);
@@ -516,13 +611,13 @@ void *or_kids_create(const uint32_t *parent, uint64_t n) {
 void or_kids_free(void *k) { delete (std::vector<std::vector<uint32_t>> *)k; }
 
 // parts_out: vid-indexed, capacity cap (>= max(seq)+1).  info[3] = created (max part+1),
-// max_component, packing nodes.
-int or_partition(const uint32_t *parent, const uint32_t *pst, uint64_t n, const uint32_t *seq,
+// max_component, packing nodes.  seq has seq_n entries (the tree n).
+int or_partition(const uint32_t *parent, const uint32_t *pst, uint64_t n, const uint32_t *seq, uint64_t seq_n,
                  void *kids, int16_t k, double balance, int vtx, int pstw, int16_t *parts_out,
                  uint64_t cap, uint64_t *vs_out, int64_t *info) {
   OR_TRY({
     Tree t{{parent, parent + n}, {pst, pst + n}};
-    std::vector<uint32_t> s(seq, seq + n);
+    std::vector<uint32_t> s(seq, seq + seq_n);
     auto &kt = *(std::vector<std::vector<uint32_t>> *)kids;
     PartitionResult r = partitionTree(s, t, kt, k, balance, vtx != 0, pstw != 0);
     if (r.parts.size() > cap) throw std::length_error("parts capacity");

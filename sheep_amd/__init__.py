@@ -96,9 +96,14 @@ def lib() -> ctypes.CDLL:
         "sheep_merge_trees_many": ([P, P, ctypes.c_uint32, U64, P], I32),
         "sheep_kids_create": ([P, P, U64, ctypes.POINTER(P)], I32),
         "sheep_kids_destroy": ([P], I32),
-        "sheep_partition": ([P, P, U64, P, U64, P, I16, D, I32, I32, P, ctypes.POINTER(_PartInfo)], I32),
+        "sheep_partition": ([P, P, U64, P, U64, U64, P, I16, D, I32, I32, P, ctypes.POINTER(_PartInfo)], I32),
         "sheep_evaluate": ([P, P, U64, P, U64, P, I32, ctypes.POINTER(_Eval)], I32),
         "sheep_facts": ([P, P, U64, ctypes.POINTER(_Facts)], I32),
+        "sheep_eval_sizes": ([I32, I32, U64, ctypes.POINTER(U64), ctypes.POINTER(U64)], I32),
+        "sheep_eval_num_parts": ([P, P, U64, ctypes.POINTER(ctypes.c_int32)], I32),
+        "sheep_eval_shard": ([P, P, U64, P, U64, P, I32, I32, P, P], I32),
+        "sheep_eval_combine": ([P, P, P, U64, P, P, U64], I32),
+        "sheep_eval_finish": ([P, P, P, U64, P, I32, I32, ctypes.POINTER(_Eval)], I32),
         "sheep_edge_parts": ([P, P, U64, P, U64, P, P], I32),
         "sheep_rmat_generate": ([P, I32, I32, U64, P, U64, ctypes.POINTER(U64)], I32),
         "sheep_rmat_generate_host": ([I32, I32, U64, P, U64, ctypes.POINTER(U64)], I32),
@@ -184,9 +189,13 @@ def _torch():
     return torch
 
 
-def _dev_u32(n: int):
+def _dev(ctx: "Context") -> str:
+    return f"cuda:{ctx.device}"
+
+
+def _dev_u32(n: int, ctx: "Context"):
     t = _torch()
-    return t.empty(max(int(n), 1), dtype=t.int32, device="cuda")
+    return t.empty(max(int(n), 1), dtype=t.int32, device=_dev(ctx))
 
 
 def records_to_device(tail: np.ndarray, head: np.ndarray, weight: np.ndarray | None = None):
@@ -225,7 +234,6 @@ def degree_count(records, nrec: int | None = None, mode: str = "llama", deg=None
     t = _torch()
     nrec = records.shape[0] if nrec is None else nrec
     if deg is None:
-        vs_cap = vs_cap or (1 << 32) - 1
         raise ValueError("pass a zeroed degree tensor `deg` of the vertex-slot capacity")
     ms = ctypes.c_uint64()
     _check(lib().sheep_degree_count(ctx.handle, _ptr(records), nrec, DEGREE_MODES[mode], _ptr(deg), deg.numel(),
@@ -235,7 +243,7 @@ def degree_count(records, nrec: int | None = None, mode: str = "llama", deg=None
 
 def sequence_from_degrees(deg, vs: int, ctx: Context | None = None) -> Sequence:
     ctx = ctx or default_context()
-    seq, pos = _dev_u32(vs), _dev_u32(vs)
+    seq, pos = _dev_u32(vs, ctx), _dev_u32(vs, ctx)
     n = ctypes.c_uint64()
     _check(lib().sheep_sequence_from_degrees(ctx.handle, _ptr(deg), vs, _ptr(seq), _ptr(pos), ctypes.byref(n)))
     return Sequence(seq, pos, n.value, vs)
@@ -246,10 +254,9 @@ def degree_sequence(records, mode: str = "llama", vs_cap: int | None = None, ctx
     ctx = ctx or default_context()
     t = _torch()
     nrec = records.shape[0]
-    if vs_cap is None:
-        vs_cap = int(records[:, :2].max().item()) + 1 if nrec else 1
-        vs_cap = vs_cap if vs_cap > 0 else (1 << 32) - 1
-    deg = t.zeros(max(vs_cap, 1), dtype=t.int32, device="cuda")
+    if vs_cap is None:   # 1 + max vid, the ids read as u32 (an int32 tensor holds them)
+        vs_cap = int((records[:, :2].to(t.int64) & 0xFFFFFFFF).max().item()) + 1 if nrec else 1
+    deg = t.zeros(max(vs_cap, 1), dtype=t.int32, device=_dev(ctx))
     _, vs = degree_count(records, nrec, mode, deg, ctx=ctx)
     return sequence_from_degrees(deg, vs, ctx)
 
@@ -261,8 +268,8 @@ def sequence_from_host(seq: np.ndarray, ctx: Context | None = None) -> Sequence:
     seq = np.asarray(seq, dtype=np.uint32)
     n = len(seq)
     pos_size = int(seq.max()) + 1 if n else 0
-    d_seq = t.from_numpy(seq.view(np.int32).copy()).to("cuda") if n else _dev_u32(1)
-    pos = _dev_u32(pos_size)
+    d_seq = t.from_numpy(seq.view(np.int32).copy()).to(_dev(ctx)) if n else _dev_u32(1, ctx)
+    pos = _dev_u32(pos_size, ctx)
     _check(lib().sheep_positions(ctx.handle, _ptr(d_seq), n, _ptr(pos), pos_size))
     return Sequence(d_seq, pos, n, pos_size)
 
@@ -275,7 +282,7 @@ def build_tree(records, seq: Sequence, nrec: int | None = None, ctx: Context | N
     ctx = ctx or default_context()
     t = _torch()
     nrec = records.shape[0] if nrec is None else nrec
-    tree = t.empty((max(seq.n, 1), 2), dtype=t.int32, device="cuda")
+    tree = t.empty((max(seq.n, 1), 2), dtype=t.int32, device=_dev(ctx))
     _check(lib().sheep_build_tree(ctx.handle, _ptr(records), nrec, _ptr(seq.pos), seq.pos_size, seq.n, _ptr(tree)))
     return tree[: seq.n]
 
@@ -287,7 +294,7 @@ def merge_trees(a, b, ctx: Context | None = None):
     n = a.shape[0]
     if b.shape[0] != n:
         raise ValueError("trees of different sizes")
-    out = t.empty((max(n, 1), 2), dtype=t.int32, device="cuda")
+    out = t.empty((max(n, 1), 2), dtype=t.int32, device=_dev(ctx))
     _check(lib().sheep_merge_trees(ctx.handle, _ptr(a), _ptr(b), n, _ptr(out)))
     return out[:n]
 
@@ -299,7 +306,7 @@ def merge_trees_many(trees, ctx: Context | None = None):
     t = _torch()
     k, n = trees.shape[0], trees.shape[1]
     trees = trees.contiguous()
-    out = t.empty((max(n, 1), 2), dtype=t.int32, device="cuda")
+    out = t.empty((max(n, 1), 2), dtype=t.int32, device=_dev(ctx))
     _check(lib().sheep_merge_trees_many(ctx.handle, _ptr(trees), k, n, _ptr(out)))
     return out[:n]
 
@@ -365,9 +372,9 @@ def partition(seq: Sequence, tree, k: int, balance: float = 1.03, vtx_weight: bo
     t = _torch()
     kids = kids or KidTable(tree, ctx)
     pos_size = seq.pos_size
-    parts = t.empty(max(pos_size, 1), dtype=t.int16, device="cuda")
+    parts = t.empty(max(pos_size, 1), dtype=t.int16, device=_dev(ctx))
     info = _PartInfo()
-    _check(lib().sheep_partition(ctx.handle, _ptr(tree), tree.shape[0], _ptr(seq.seq), pos_size, kids.handle,
+    _check(lib().sheep_partition(ctx.handle, _ptr(tree), tree.shape[0], _ptr(seq.seq), seq.n, pos_size, kids.handle,
                                  int(k), float(balance), int(vtx_weight), int(pst_weight), _ptr(parts),
                                  ctypes.byref(info)))
     return PartitionResult(parts[:pos_size], int(k), info.created, info.first_size, info.second_size,
@@ -423,13 +430,51 @@ def evaluate(records, seq: Sequence, parts, what: int = 0, nrec: int | None = No
     return EvalResult(*[getattr(out, f) for f, _ in _Eval._fields_])
 
 
+class ShardedEvaluator:
+    """Partition::evaluate over edge shards (SURVEY §8(e) step 6): each shard's records ORed
+    into per-vertex part bitsets and summed counts, states of other devices combined with
+    :meth:`combine`, one node pass in :meth:`finish`."""
+
+    def __init__(self, seq: Sequence, parts, what: int = 0, nparts: int | None = None,
+                 ctx: Context | None = None):
+        self.ctx = ctx or default_context()
+        t = _torch()
+        self.seq, self.parts, self.what = seq, parts, what
+        if nparts is None:
+            n = ctypes.c_int32()
+            _check(lib().sheep_eval_num_parts(self.ctx.handle, _ptr(parts), seq.pos_size, ctypes.byref(n)))
+            nparts = n.value
+        self.nparts = nparts
+        bw, aw = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().sheep_eval_sizes(what, nparts, seq.pos_size, ctypes.byref(bw), ctypes.byref(aw)))
+        self.bits = t.zeros(max(bw.value, 1), dtype=t.int64, device=f"cuda:{self.ctx.device}")
+        self.acc = t.zeros(aw.value, dtype=t.int64, device=f"cuda:{self.ctx.device}")
+        self.bits_words, self.acc_words = bw.value, aw.value
+
+    def add(self, records, nrec: int | None = None):
+        nrec = records.shape[0] if nrec is None else nrec
+        _check(lib().sheep_eval_shard(self.ctx.handle, _ptr(records), nrec, _ptr(self.seq.pos), self.seq.pos_size,
+                                      _ptr(self.parts), self.what, self.nparts, _ptr(self.bits), _ptr(self.acc)))
+
+    def combine(self, bits, acc):
+        """OR another state's bits (same layout, on this device) and add its counts."""
+        _check(lib().sheep_eval_combine(self.ctx.handle, _ptr(self.bits), _ptr(bits), self.bits_words,
+                                        _ptr(self.acc), _ptr(acc), self.acc_words))
+
+    def finish(self) -> "EvalResult":
+        out = _Eval()
+        _check(lib().sheep_eval_finish(self.ctx.handle, _ptr(self.bits), _ptr(self.acc), self.seq.pos_size,
+                                       _ptr(self.parts), self.what, self.nparts, ctypes.byref(out)))
+        return EvalResult(*[getattr(out, f) for f, _ in _Eval._fields_])
+
+
 def edge_parts(records, seq: Sequence, parts, nrec: int | None = None, ctx: Context | None = None):
     """Part each record is written to by writePartitionedGraph (partition.cpp:588-670):
     the part of its earlier-positioned endpoint (device int16 per record)."""
     ctx = ctx or default_context()
     nrec = records.shape[0] if nrec is None else nrec
     t = _torch()
-    out = t.empty(max(int(nrec), 1), dtype=t.int16, device="cuda")
+    out = t.empty(max(int(nrec), 1), dtype=t.int16, device=_dev(ctx))
     _check(lib().sheep_edge_parts(ctx.handle, _ptr(records), nrec, _ptr(seq.pos), seq.pos_size, _ptr(parts),
                                   _ptr(out)))
     return out[:nrec]
@@ -470,7 +515,7 @@ def rmat(scale: int, edgefactor: int = 16, seed: int = 1, ctx: Context | None = 
     ctx = ctx or default_context()
     t = _torch()
     cap = edgefactor << scale
-    out = t.empty((cap, 3), dtype=t.int32, device="cuda")
+    out = t.empty((cap, 3), dtype=t.int32, device=_dev(ctx))
     n = ctypes.c_uint64()
     _check(lib().sheep_rmat_generate(ctx.handle, scale, edgefactor, seed, _ptr(out), cap, ctypes.byref(n)))
     return out[: n.value]

@@ -22,11 +22,19 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
                       sheep_jnode *tree);
 void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n, sheep_jnode *out);
 void merge_trees_many(Ctx &c, const sheep_jnode *trees, uint32_t k, uint64_t n, sheep_jnode *out);
-void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t *seq, uint64_t pos_size,
+void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t *seq, uint64_t seq_n, uint64_t pos_size,
                     sheep_kids *k, int16_t np, double balance, int vtx, int pstw, int16_t *parts_vid,
                     sheep_partition_info *info);
 void evaluate(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
               const int16_t *parts, int what, sheep_eval *out);
+void eval_sizes(int what, int nparts, uint64_t pos_size, uint64_t *bits_words, uint64_t *acc_words);
+int eval_num_parts(Ctx &c, const int16_t *parts, uint64_t pos_size);
+void eval_shard(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
+                const int16_t *parts, int what, int nparts, uint64_t *bits, uint64_t *acc);
+void eval_combine(Ctx &c, uint64_t *bits, const uint64_t *bits_src, uint64_t words, uint64_t *acc,
+                  const uint64_t *acc_src, uint64_t acc_words);
+void eval_finish(Ctx &c, const uint64_t *bits, const uint64_t *acc, uint64_t pos_size, const int16_t *parts, int what,
+                 int nparts, sheep_eval *out);
 void tree_facts(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_facts_t *out);
 void edge_parts(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
                 const int16_t *parts_vid, int16_t *out);
@@ -35,6 +43,22 @@ uint64_t rmat_generate_host(int scale, int ef, uint64_t seed, sheep_xs1 *out, ui
 }  // namespace sheep
 
 using sheep::Error;
+
+// Every entry point that takes a context runs on that context's device (workspaces are
+// allocated and kernels launched there), whatever device the calling thread has current;
+// the caller's current device is restored on return.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(const sheep_ctx *x) {
+    if (!x) return;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != x->c.device) HIP_CHECK(hipSetDevice(x->c.device));
+    else prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
 
 #define API_BEGIN try {
 #define API_END                                                          \
@@ -74,6 +98,7 @@ int sheep_ctx_create(int device, void *hip_stream, sheep_ctx **out) {
 
 int sheep_ctx_destroy(sheep_ctx *ctx) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   if (!ctx) return SHEEP_OK;
   sheep::Ctx &c = ctx->c;
   HIP_CHECK(hipSetDevice(c.device));
@@ -91,6 +116,7 @@ int sheep_ctx_destroy(sheep_ctx *ctx) {
 
 int sheep_ctx_sync(sheep_ctx *ctx) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx, "null ctx");
   ctx->c.sync();
   API_END
@@ -100,6 +126,7 @@ void *sheep_ctx_stream(sheep_ctx *ctx) { return ctx ? (void *)ctx->c.stream : nu
 
 int sheep_malloc(sheep_ctx *ctx, size_t bytes, void **dev_out) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx && dev_out, "null argument");
   HIP_CHECK(hipSetDevice(ctx->c.device));
   HIP_CHECK(hipMalloc(dev_out, bytes ? bytes : 1));
@@ -108,6 +135,7 @@ int sheep_malloc(sheep_ctx *ctx, size_t bytes, void **dev_out) {
 
 int sheep_free(sheep_ctx *ctx, void *dev) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx, "null ctx");
   if (dev) HIP_CHECK(hipFree(dev));
   API_END
@@ -115,6 +143,7 @@ int sheep_free(sheep_ctx *ctx, void *dev) {
 
 int sheep_memcpy_h2d(sheep_ctx *ctx, void *dst, const void *src, size_t bytes) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx, "null ctx");
   if (bytes) {
     HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->c.stream));
@@ -125,6 +154,7 @@ int sheep_memcpy_h2d(sheep_ctx *ctx, void *dst, const void *src, size_t bytes) {
 
 int sheep_memcpy_d2h(sheep_ctx *ctx, void *dst, const void *src, size_t bytes) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx, "null ctx");
   if (bytes) {
     HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->c.stream));
@@ -135,6 +165,7 @@ int sheep_memcpy_d2h(sheep_ctx *ctx, void *dst, const void *src, size_t bytes) {
 
 int sheep_timer_enable(sheep_ctx *ctx, int on) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx, "null ctx");
   ctx->c.timing = on != 0;
   API_END
@@ -142,6 +173,7 @@ int sheep_timer_enable(sheep_ctx *ctx, int on) {
 
 int sheep_timer_get(sheep_ctx *ctx, const char *name, double *ms, uint64_t *launches, uint64_t *alg_bytes) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx && name && ms && launches, "null argument");
   ctx->c.collect_timers();
   auto it = ctx->c.timers.find(name);
@@ -154,6 +186,7 @@ int sheep_timer_get(sheep_ctx *ctx, const char *name, double *ms, uint64_t *laun
 
 int sheep_timer_names(sheep_ctx *ctx, char *buf, size_t cap) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx && buf && cap, "null argument");
   std::string s;
   for (auto &kv : ctx->c.timers) { if (!s.empty()) s += ','; s += kv.first; }
@@ -164,6 +197,7 @@ int sheep_timer_names(sheep_ctx *ctx, char *buf, size_t cap) {
 
 int sheep_timer_reset(sheep_ctx *ctx) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx, "null ctx");
   ctx->c.collect_timers();
   ctx->c.timers.clear();
@@ -173,6 +207,7 @@ int sheep_timer_reset(sheep_ctx *ctx) {
 int sheep_degree_count(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap,
                        uint64_t *max_slot_out) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx && (rec || !nrec) && deg && max_slot_out, "null argument");
   sheep::degree_count(ctx->c, rec, nrec, mode, deg, cap, max_slot_out);
   API_END
@@ -181,6 +216,7 @@ int sheep_degree_count(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, int 
 int sheep_sequence_from_degrees(sheep_ctx *ctx, const uint32_t *deg, uint64_t vs, uint32_t *seq, uint32_t *pos,
                                 uint64_t *n_out) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx && (deg || !vs) && n_out, "null argument");
   *n_out = sheep::sequence_from_degrees(ctx->c, deg, vs, seq, pos);
   API_END
@@ -188,6 +224,7 @@ int sheep_sequence_from_degrees(sheep_ctx *ctx, const uint32_t *deg, uint64_t vs
 
 int sheep_positions(sheep_ctx *ctx, const uint32_t *seq, uint64_t n, uint32_t *pos, uint64_t pos_size) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx && (seq || !n) && (pos || !pos_size), "null argument");
   sheep::positions(ctx->c, seq, n, pos, pos_size);
   API_END
@@ -196,6 +233,7 @@ int sheep_positions(sheep_ctx *ctx, const uint32_t *seq, uint64_t n, uint32_t *p
 int sheep_build_tree(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
                      uint64_t n, sheep_jnode *tree) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx && (rec || !nrec) && (pos || !pos_size) && (tree || !n), "null argument");
   NEED(n < 0xFFFFFFFFull, "tree too large for 32-bit node ids");
   sheep::relabel_and_tree(ctx->c, rec, nrec, pos, pos_size, n, tree);
@@ -204,6 +242,7 @@ int sheep_build_tree(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, const 
 
 int sheep_merge_trees(sheep_ctx *ctx, const sheep_jnode *a, const sheep_jnode *b, uint64_t n, sheep_jnode *out) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx && ((a && b && out) || !n), "null argument");
   sheep::merge_trees(ctx->c, a, b, n, out);
   API_END
@@ -211,6 +250,7 @@ int sheep_merge_trees(sheep_ctx *ctx, const sheep_jnode *a, const sheep_jnode *b
 
 int sheep_merge_trees_many(sheep_ctx *ctx, const sheep_jnode *trees, uint32_t k, uint64_t n, sheep_jnode *out) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx && ((trees && out) || !n), "null argument");
   NEED(k >= 1, "merge: no trees");
   sheep::merge_trees_many(ctx->c, trees, k, n, out);
@@ -219,6 +259,7 @@ int sheep_merge_trees_many(sheep_ctx *ctx, const sheep_jnode *trees, uint32_t k,
 
 int sheep_kids_create(sheep_ctx *ctx, const sheep_jnode *tree, uint64_t n, sheep_kids **out) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx && out && (tree || !n), "null argument");
   sheep_kids *k = new sheep_kids();
   try {
@@ -235,34 +276,85 @@ int sheep_kids_create(sheep_ctx *ctx, const sheep_jnode *tree, uint64_t n, sheep
 int sheep_kids_destroy(sheep_kids *k) {
   API_BEGIN
   if (!k) return SHEEP_OK;
+  int prev = -1;
+  if (k->ctx && hipGetDevice(&prev) == hipSuccess && prev != k->ctx->device) HIP_CHECK(hipSetDevice(k->ctx->device));
+  else prev = -1;
   if (k->ctx) k->ctx->sync();
   hipFree(k->parent);
   hipFree(k->koff);
   hipFree(k->kids);
   delete k;
+  if (prev >= 0) HIP_CHECK(hipSetDevice(prev));
   API_END
 }
 
-int sheep_partition(sheep_ctx *ctx, const sheep_jnode *tree, uint64_t n, const uint32_t *seq, uint64_t pos_size,
+int sheep_partition(sheep_ctx *ctx, const sheep_jnode *tree, uint64_t n, const uint32_t *seq, uint64_t seq_n, uint64_t pos_size,
                     sheep_kids *kids, int16_t k, double balance, int vtx_weight, int pst_weight, int16_t *parts_vid,
                     sheep_partition_info *info) {
   API_BEGIN
-  NEED(ctx && kids && info && ((tree && seq) || !n) && (parts_vid || !pos_size), "null argument");
-  sheep::partition_tree(ctx->c, tree, n, seq, pos_size, kids, k, balance, vtx_weight, pst_weight, parts_vid, info);
+  DeviceGuard dg(ctx);
+  NEED(ctx && kids && info && (tree || !n) && (seq || !seq_n) && (parts_vid || !pos_size), "null argument");
+  sheep::partition_tree(ctx->c, tree, n, seq, seq_n, pos_size, kids, k, balance, vtx_weight, pst_weight, parts_vid, info);
   API_END
 }
 
 int sheep_evaluate(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
                    const int16_t *parts_vid, int what, sheep_eval *out) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx && out && (rec || !nrec) && ((pos && parts_vid) || !pos_size), "null argument");
   sheep::evaluate(ctx->c, rec, nrec, pos, pos_size, parts_vid, what, out);
+  API_END
+}
+
+int sheep_eval_sizes(int what, int32_t nparts, uint64_t pos_size, uint64_t *bits_words, uint64_t *acc_words) {
+  API_BEGIN
+  NEED(bits_words && acc_words && nparts >= 1, "bad argument");
+  sheep::eval_sizes(what, nparts, pos_size, bits_words, acc_words);
+  API_END
+}
+
+int sheep_eval_num_parts(sheep_ctx *ctx, const int16_t *parts_vid, uint64_t pos_size, int32_t *nparts_out) {
+  API_BEGIN
+  DeviceGuard dg(ctx);
+  NEED(ctx && nparts_out && (parts_vid || !pos_size), "null argument");
+  *nparts_out = sheep::eval_num_parts(ctx->c, parts_vid, pos_size);
+  API_END
+}
+
+int sheep_eval_shard(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
+                     const int16_t *parts_vid, int what, int32_t nparts, uint64_t *bits, uint64_t *acc) {
+  API_BEGIN
+  DeviceGuard dg(ctx);
+  NEED(ctx && bits && acc && (rec || !nrec) && ((pos && parts_vid) || !pos_size), "null argument");
+  NEED(nparts >= 1 && !(what & ~7), "bad argument");
+  sheep::eval_shard(ctx->c, rec, nrec, pos, pos_size, parts_vid, what, nparts, bits, acc);
+  API_END
+}
+
+int sheep_eval_combine(sheep_ctx *ctx, uint64_t *bits, const uint64_t *bits_src, uint64_t words, uint64_t *acc,
+                       const uint64_t *acc_src, uint64_t acc_words) {
+  API_BEGIN
+  DeviceGuard dg(ctx);
+  NEED(ctx && ((bits && bits_src) || !words) && ((acc && acc_src) || !acc_words), "null argument");
+  sheep::eval_combine(ctx->c, bits, bits_src, words, acc, acc_src, acc_words);
+  API_END
+}
+
+int sheep_eval_finish(sheep_ctx *ctx, const uint64_t *bits, const uint64_t *acc, uint64_t pos_size,
+                      const int16_t *parts_vid, int what, int32_t nparts, sheep_eval *out) {
+  API_BEGIN
+  DeviceGuard dg(ctx);
+  NEED(ctx && out && acc && ((bits && parts_vid) || !pos_size), "null argument");
+  NEED(nparts >= 1 && !(what & ~7), "bad argument");
+  sheep::eval_finish(ctx->c, bits, acc, pos_size, parts_vid, what, nparts, out);
   API_END
 }
 
 int sheep_edge_parts(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
                      const int16_t *parts_vid, int16_t *edge_part) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx && ((rec && pos && parts_vid && edge_part) || !nrec), "null argument");
   sheep::edge_parts(ctx->c, rec, nrec, pos, pos_size, parts_vid, edge_part);
   API_END
@@ -270,6 +362,7 @@ int sheep_edge_parts(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, const 
 
 int sheep_facts(sheep_ctx *ctx, const sheep_jnode *tree, uint64_t n, sheep_facts_t *out) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx && out && (tree || !n), "null argument");
   sheep::tree_facts(ctx->c, tree, n, out);
   API_END
@@ -278,6 +371,7 @@ int sheep_facts(sheep_ctx *ctx, const sheep_jnode *tree, uint64_t n, sheep_facts
 int sheep_rmat_generate(sheep_ctx *ctx, int scale, int ef, uint64_t seed, sheep_xs1 *out, uint64_t cap,
                         uint64_t *nrec_out) {
   API_BEGIN
+  DeviceGuard dg(ctx);
   NEED(ctx && out && nrec_out, "null argument");
   *nrec_out = sheep::rmat_generate(ctx->c, scale, ef, seed, out, cap);
   API_END

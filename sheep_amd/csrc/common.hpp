@@ -5,6 +5,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <map>
+#include <mutex>
+#include <set>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -37,6 +39,18 @@ inline unsigned grid_for(uint64_t items, unsigned per_block = BLOCK, unsigned ca
   uint64_t g = (items + per_block - 1) / per_block;
   if (g == 0) g = 1;
   return (unsigned)(g < cap ? g : cap);
+}
+
+// Raises a kernel's dynamic-LDS limit to the gfx950 CU's 160 KiB, once per (kernel,
+// device): the attribute belongs to the device that is current when it is set.
+inline void allow_full_lds(const void *kernel) {
+  static std::mutex m;
+  static std::set<std::pair<const void *, int>> done;
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(m);
+  if (done.insert({kernel, dev}).second)
+    HIP_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 }
 
 // Per-context state: device, stream, grow-only named workspaces, pinned scalars, timers.

@@ -276,11 +276,8 @@ __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict_
 // not retried here: the edge goes to `out` for the next round.  Retrying in place made
 // thousands of threads fight over a forming giant component's root (each failure =
 // another round trip); rounds instead resolve such a pile-up in a few passes.
-//
-// BATCH: the finds of all the thread's edges run as one set of independent chains in
-// lockstep (find_many) before any hook; a root that a same-thread hook has meanwhile
-// hooked fails its CAS and the edge goes to the next round, as any lost race does.
-template <bool BATCH>
+// (Batched finds of all the thread's edges before any hook left more hooks to later
+// rounds: 21-22 ms against 10.8 ms at RMAT-26.)
 __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict__ in, const uint64_t *__restrict__ n_in,
                                                       uint32_t *uf, uint64_t *__restrict__ out,
                                                       unsigned long long *__restrict__ counter) {
@@ -294,33 +291,14 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
       const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
       ev[j] = i < nin ? in[i] : DEAD;
     }
-    if constexpr (BATCH) {
-      uint32_t x[2 * TILE_ITEMS];
-      bool v[2 * TILE_ITEMS];
 #pragma unroll
-      for (int j = 0; j < TILE_ITEMS; ++j) {
-        v[2 * j] = v[2 * j + 1] = ev[j] != DEAD;
-        x[2 * j] = (uint32_t)ev[j];
-        x[2 * j + 1] = (uint32_t)(ev[j] >> 32);
-      }
-      find_many<2 * TILE_ITEMS>(uf, x, v);
-#pragma unroll
-      for (int j = 0; j < TILE_ITEMS; ++j) {
-        const uint32_t a = x[2 * j], b = x[2 * j + 1];
-        if (!v[2 * j] || a == b) continue;
-        const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-        if (atomicCAS(&uf[hi], hi, lo) != hi) keep |= 1u << j;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < TILE_ITEMS; ++j) {
-        if (ev[j] == DEAD) continue;
-        uint32_t a = (uint32_t)ev[j], b = (uint32_t)(ev[j] >> 32);
-        find2(uf, a, b);
-        if (a == b) continue;
-        const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-        if (atomicCAS(&uf[hi], hi, lo) != hi) keep |= 1u << j;
-      }
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      if (ev[j] == DEAD) continue;
+      uint32_t a = (uint32_t)ev[j], b = (uint32_t)(ev[j] >> 32);
+      find2(uf, a, b);
+      if (a == b) continue;
+      const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+      if (atomicCAS(&uf[hi], hi, lo) != hi) keep |= 1u << j;
     }
     uint64_t slot = shard_reserve((uint32_t)__popc(keep), counter, tile, ntiles, 1);
 #pragma unroll
@@ -529,10 +507,9 @@ __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restric
 }
 
 // cnt: the three rows (stride cstride, zero-padded) scanned as ONE exclusive scan, so a
-// row's offsets are relative to its first entry; the row totals go to st.
-// STAGED: each class's run of the tile is first placed in LDS at its thread-major rank,
-// then copied out by consecutive lanes (the same positions, coalesced stores).
-template <bool STAGED>
+// row's offsets are relative to its first entry; the row totals go to st.  Each class's
+// run of the tile is first placed in LDS at its thread-major rank, then copied out by
+// consecutive lanes (per-thread stores to the same positions: 16.6 against 12.2 ms).
 __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
                                                        uint64_t *__restrict__ st, int s, uint32_t clo,
                                                        const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
@@ -572,34 +549,21 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
     uint64_t off = 0;
     for (int w = 0; w < wave; ++w) off += s_w[w];
     const uint64_t ex = off + inc - c3;
-    if constexpr (STAGED) {
-      __shared__ uint64_t stg[TILE];
-      uint64_t tot = 0;
-      for (int w = 0; w < BLOCK / WAVE; ++w) tot += s_w[w];
-      uint64_t *const outs[3] = {next, lbuf, xbuf};
+    __shared__ uint64_t stg[TILE];
+    uint64_t tot = 0;
+    for (int w = 0; w < BLOCK / WAVE; ++w) tot += s_w[w];
+    uint64_t *const outs[3] = {next, lbuf, xbuf};
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        uint32_t r = (uint32_t)((ex >> (16 * k)) & 0xFFFF);
+    for (int k = 0; k < 3; ++k) {
+      uint32_t r = (uint32_t)((ex >> (16 * k)) & 0xFFFF);
 #pragma unroll
-        for (int j = 0; j < TILE_ITEMS; ++j)
-          if ((cl[j] >> k) & 1) stg[r++] = ev[j];
-        __syncthreads();
-        const uint32_t n_k = (uint32_t)((tot >> (16 * k)) & 0xFFFF);
-        uint64_t *const o = outs[k] + (cnt[k * cstride + tile] - cnt[k * cstride]);
-        for (uint32_t i = threadIdx.x; i < n_k; i += BLOCK) o[i] = stg[i];
-        __syncthreads();   // stg (and, after the last class, s_w) is rewritten next
-      }
-    } else {
-      uint64_t pk = cnt[tile] - b0 + (ex & 0xFFFF);
-      uint64_t pl = cnt[cstride + tile] - b1 + ((ex >> 16) & 0xFFFF);
-      uint64_t px = cnt[2 * cstride + tile] - b2 + (ex >> 32);
-#pragma unroll
-      for (int j = 0; j < TILE_ITEMS; ++j) {
-        if (cl[j] & 1) next[pk++] = ev[j];
-        if (cl[j] & 2) lbuf[pl++] = ev[j];
-        if (cl[j] & 4) xbuf[px++] = ev[j];
-      }
-      __syncthreads();   // s_w is rewritten by the next tile
+      for (int j = 0; j < TILE_ITEMS; ++j)
+        if ((cl[j] >> k) & 1) stg[r++] = ev[j];
+      __syncthreads();
+      const uint32_t n_k = (uint32_t)((tot >> (16 * k)) & 0xFFFF);
+      uint64_t *const o = outs[k] + (cnt[k * cstride + tile] - cnt[k * cstride]);
+      for (uint32_t i = threadIdx.x; i < n_k; i += BLOCK) o[i] = stg[i];
+      __syncthreads();   // stg (and, after the last class, s_w) is rewritten next
     }
   }
 }
@@ -841,19 +805,9 @@ __global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t 
 void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
 
 static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
-static const bool g_split_staged = getenv("SHEEP_SPLIT_STAGED") ? atoi(getenv("SHEEP_SPLIT_STAGED")) != 0 : true;
-// batched finds leave more hooks to later rounds: etree_union 21-22 ms vs 10.8 at RMAT-26
-static const bool g_hook_batch = getenv("SHEEP_HOOK_BATCH") ? atoi(getenv("SHEEP_HOOK_BATCH")) != 0 : false;
-static const bool g_plain_relabel = getenv("SHEEP_PLAIN_RELABEL") != nullptr;   // A/B: k_relabel only
-static int env_int(const char *name, int def) {
-  const char *v = getenv(name);
-  return v && *v ? atoi(v) : def;
-}
 // Finishing block size (log2 positions) of the per-block Liu pass: merges use it; a
 // map's hub blocks would pile onto single lanes, so maps run every level globally.
-// SHEEP_FIN_MERGE / SHEEP_FIN_MAP override (0 = off) for experiments.
-static const int g_fin_merge = env_int("SHEEP_FIN_MERGE", 8);
-static const int g_fin_map = env_int("SHEEP_FIN_MAP", 0);
+constexpr int FIN_MERGE = 8, FIN_MAP = 0;
 
 // spread(x) = floor(x * c / 2^32), c = floor(2^(32+L) / n) in [2^32, 2^33), L = ceil(log2 n):
 // monotone, injective on [0,n), image in [0, 2^L).  clo = c - 2^32.
@@ -946,14 +900,8 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
                          (const uint64_t *)r0, (const uint64_t *)seg, L, tcnt, cstride);
       LAUNCH_CHECK();
       scan_exclusive_u64(c, tcnt, tcnt, 3 * cstride + 1, nullptr);
-      if (g_split_staged)
-        hipLaunchKernelGGL(k_split_write<true>, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s,
-                           clo, (const uint64_t *)r0, (const uint64_t *)seg, L, (const uint64_t *)tcnt, cstride, next,
-                           lbuf, xbuf);
-      else
-        hipLaunchKernelGGL(k_split_write<false>, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s,
-                           clo, (const uint64_t *)r0, (const uint64_t *)seg, L, (const uint64_t *)tcnt, cstride, next,
-                           lbuf, xbuf);
+      hipLaunchKernelGGL(k_split_write, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo,
+                         (const uint64_t *)r0, (const uint64_t *)seg, L, (const uint64_t *)tcnt, cstride, next, lbuf, xbuf);
       LAUNCH_CHECK();
     }
     {
@@ -961,7 +909,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       const uint64_t *in = lbuf, *n_in = st + ST_NL;
       for (int round = 0; round < HOOK_ROUNDS; ++round) {
         uint64_t *dst = hk[round & 1];
-        hipLaunchKernelGGL(g_hook_batch ? k_hook_round<true> : k_hook_round<false>, dim3(gt), dim3(BLOCK), 0, c.stream, in, n_in, uf, alt, cset(CSET_HOOK + round));
+        hipLaunchKernelGGL(k_hook_round, dim3(gt), dim3(BLOCK), 0, c.stream, in, n_in, uf, alt, cset(CSET_HOOK + round));
         LAUNCH_CHECK();
         pack_shards<uint64_t>(c, alt, dst, n_in, cset(CSET_HOOK + round), st + ST_HOOK + round);
         in = dst;
@@ -1089,7 +1037,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   if (nrec) {
     TimedRegion tr(c, "relabel", 20 * nrec);   // record + 2 pos gathers
     // head-bucketed relabel (hist.hip) when the key range fits its LDS buckets
-    m = g_plain_relabel ? UINT64_MAX : relabel_bucketed(c, rec, nrec, pos, pos_size, pst, edges, d + 1);
+    m = relabel_bucketed(c, rec, nrec, pos, pos_size, pst, edges, d + 1);
     if (m == UINT64_MAX) {
       m = nrec;
       hipLaunchKernelGGL(k_relabel, dim3(grid_tiles(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos, pos_size, pst,
@@ -1112,7 +1060,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
       group_edges_by_lo(c, edges, m, n, L, clo, pst, r0, seg);
     }
     TimedRegion tr(c, "etree", 8 * m);
-    etree_from_edges(c, r0, m, n, parent, seg, g_fin_map, 0);
+    etree_from_edges(c, r0, m, n, parent, seg, FIN_MAP, 0);
   } else {
     fill_u32(c, parent, n, INVALID);
   }
@@ -1136,7 +1084,7 @@ void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n,
   if (c.h_scalars[11]) throw Error(SHEEP_ERR_ARG, "merge: a parent is not a later node of the tree");
   {
     TimedRegion tr(c, "merge", 16 * n);
-    etree_from_edges(c, edges, 2 * n, n, parent, nullptr, g_fin_merge, 2);
+    etree_from_edges(c, edges, 2 * n, n, parent, nullptr, FIN_MERGE, 2);
   }
   hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);
   LAUNCH_CHECK();
@@ -1161,7 +1109,7 @@ void merge_trees_many(Ctx &c, const sheep_jnode *trees, uint32_t K, uint64_t n, 
   if (c.h_scalars[11]) throw Error(SHEEP_ERR_ARG, "merge: a parent is not a later node of the tree");
   {
     TimedRegion tr(c, "merge", 8 * (uint64_t)K * n);
-    etree_from_edges(c, edges, (uint64_t)K * n, n, parent, nullptr, g_fin_merge, K);
+    etree_from_edges(c, edges, (uint64_t)K * n, n, parent, nullptr, FIN_MERGE, K);
   }
   hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);
   LAUNCH_CHECK();

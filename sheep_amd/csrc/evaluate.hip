@@ -8,9 +8,24 @@
 //   ECV(up)  : part of the later endpoint
 //   ECV(hash): part of the endpoint with the smaller cormen hash (s odd -> bijective)
 //   Vcom vol : the other endpoint's part (plus X's own part, added per node)
-// so one pass over the records ORs owner bits into per-vertex part bitsets
-// (k bits per vertex, word-interleaved per vertex), and a second pass over vertex
-// slots pops the bits.  Balances and edges-cut are per-block LDS histograms.
+// so one pass over the records ORs owner bits into per-vertex part bitsets and a second
+// pass over vertex slots pops the bits.  Balances and edges-cut are per-block LDS
+// histograms.
+//
+// Layout (HBM), per vertex slot v: M bit arrays (the requested ones, in the order down,
+// up, hash, vcom), each W64 = ceil(nparts / 64) u64 words: bits[(v * M + a) * W64 + w],
+// so one vertex's words share a cache line.  pp[v] = pos << 16 | part packs the two
+// per-vertex gathers a record needs into one 8-B load.
+//
+// Traffic: a record's tail side is near-sequential when records come tail-sorted (runs
+// of equal tails are OR-combined in the wave first); its head side is one random 8-B
+// gather plus, per bit array, a read of the word and an atomicOr only when the bit is
+// still clear — power-law heads saturate their bitsets after a few records, so most
+// head updates end at the (cache-resident) read.
+//
+// The sharded form (one call per edge shard, bitsets OR-combined and accumulators
+// summed across shards, then one node pass) is the distributed evaluator of SURVEY
+// §8(e) step 6.
 #include "common.hpp"
 
 namespace sheep {
@@ -19,115 +34,197 @@ namespace {
 __device__ __forceinline__ uint32_t cormen_hash(uint32_t k) { return k * 2654435769u; }
 
 constexpr int LDS_PARTS = 2048;
+constexpr uint64_t NO_PP = ~0ull;
 
-__device__ __forceinline__ void set_bit(uint32_t *bits, uint32_t W, uint32_t v, int p) {
-  atomicOr(&bits[(uint64_t)v * W + (p >> 5)], 1u << (p & 31));
+// accumulator row: scalars then the three record-side balance histograms
+constexpr int AC_CUT = 0, AC_BAD = 1, AC_LOOPS = 2, AC_RECS = 3, AC_SCAL = 8;
+
+__global__ void k_pp(const uint32_t *__restrict__ pos, const int16_t *__restrict__ parts, uint64_t vs,
+                     uint64_t *__restrict__ pp) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < vs; v += stride) {
+    const uint32_t p = pos[v];
+    const int16_t q = parts[v];
+    pp[v] = (p == INVALID || q < 0) ? NO_PP : ((uint64_t)p << 16) | (uint16_t)q;
+  }
+}
+
+// OR of `m` over the run of consecutive lanes sharing `key` (INVALID: no key), delivered
+// to the run's first lane (returns 0 elsewhere).
+__device__ __forceinline__ uint64_t run_or(uint32_t key, uint64_t m) {
+  const int lane = (int)__lane_id();
+  const uint32_t prev = __shfl_up(key, 1, 64);
+  const bool start = key != INVALID && (lane == 0 || prev != key);
+  const uint64_t starts = __ballot(start);
+  const uint32_t rid = (uint32_t)__popcll(starts & ((lane == 63) ? ~0ull : ((2ull << lane) - 1)));
+  uint64_t v = key != INVALID ? m : 0;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t u = __shfl_down(v, o, 64);
+    const uint32_t ro = __shfl_down(rid, o, 64);
+    const uint32_t ko = __shfl_down(key, o, 64);
+    if (lane + o < 64 && ro == rid && ko == key) v |= u;
+  }
+  return start ? v : 0;
+}
+
+__device__ __forceinline__ void or_bits(unsigned long long *bits, uint64_t idx, uint64_t m) {
+  if (!m) return;
+  if ((bits[idx] & m) != m) atomicOr(&bits[idx], (unsigned long long)m);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_eval_records(const sheep_xs1 *__restrict__ rec, uint64_t nrec,
-                                                        const uint32_t *__restrict__ pos, uint64_t pos_size,
-                                                        const int16_t *__restrict__ parts, int what, uint32_t W,
-                                                        int nparts, uint32_t *__restrict__ bdown,
-                                                        uint32_t *__restrict__ bup, uint32_t *__restrict__ bhash,
-                                                        uint32_t *__restrict__ bvc, unsigned long long *__restrict__ bal,
-                                                        unsigned long long *__restrict__ scal,
-                                                        unsigned long long *__restrict__ selfl) {
-  // bal: [0,nparts) down, [nparts,2n) up, [2n,3n) hash
+                                                        const uint64_t *__restrict__ pp, uint64_t pos_size, int what,
+                                                        int M, uint32_t W64, int nparts,
+                                                        unsigned long long *__restrict__ bits,
+                                                        unsigned long long *__restrict__ acc) {
+  unsigned long long *const bal = acc + AC_SCAL;   // [0,n) down, [n,2n) up, [2n,3n) hash
   __shared__ uint32_t lbal[3][LDS_PARTS];
   const bool lds = nparts <= LDS_PARTS;
   if (lds)
     for (int i = threadIdx.x; i < 3 * LDS_PARTS; i += BLOCK) (&lbal[0][0])[i] = 0;
   __syncthreads();
-  uint64_t cut = 0, bad = 0, sl = 0;
+  // bit-array index of each metric (-1: not requested)
+  const int ad = (what & 2) ? 0 : -1;
+  const int au = (what & 4) ? ((what & 2) ? 1 : 0) : -1;
+  const int ah = (what & 1) ? M - 2 : -1, av = (what & 1) ? M - 1 : -1;
+  uint64_t cut = 0, bad = 0, loops = 0;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nrec; i += stride) {
-    sheep_xs1 r = rec[i];
-    uint32_t t = r.tail, h = r.head;
-    if (t >= pos_size || h >= pos_size) { ++bad; continue; }
-    int tp = parts[t], hp = parts[h];
-    uint32_t pt = pos[t], ph = pos[h];
-    if (tp < 0 || hp < 0 || pt == INVALID || ph == INVALID) { ++bad; continue; }
-    if (t == h) {
-      ++sl;
-      if (what & 2) set_bit(bdown, W, t, tp);
-      if (what & 4) set_bit(bup, W, t, tp);
-      if (what & 1) { set_bit(bhash, W, t, tp); set_bit(bvc, W, t, tp); }
-      continue;
+  const uint64_t iters = (nrec + stride - 1) / stride;
+  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (uint64_t it = 0; it < iters; ++it, i += stride) {   // wave-uniform trip count (run_or)
+    uint32_t t = INVALID, h = INVALID;
+    int tp = 0, hp = 0;
+    bool live = false;
+    uint32_t pt = 0, ph = 0;
+    if (i < nrec) {
+      const sheep_xs1 r = rec[i];
+      if (r.tail >= pos_size || r.head >= pos_size) {
+        ++bad;
+      } else {
+        const uint64_t a = pp[r.tail], b = pp[r.head];
+        if (a == NO_PP || b == NO_PP) {
+          ++bad;
+        } else {
+          t = r.tail;
+          h = r.head;
+          pt = (uint32_t)(a >> 16);
+          ph = (uint32_t)(b >> 16);
+          tp = (int)(uint16_t)a;
+          hp = (int)(uint16_t)b;
+          live = true;
+        }
+      }
     }
-    const int pdown = pt < ph ? tp : hp, pup = pt < ph ? hp : tp;
-    if (what & 2) {
-      set_bit(bdown, W, t, pdown); set_bit(bdown, W, h, pdown);
-      if (lds) atomicAdd(&lbal[0][pdown], 1u); else atomicAdd(&bal[pdown], 1ull);
+    const bool loop = live && t == h;
+    loops += loop;
+    // owner parts (a self-loop's entry X->X owns X's part in every metric)
+    const int pd = loop ? tp : (pt < ph ? tp : hp), pu = loop ? tp : (pt < ph ? hp : tp);
+    const int po = loop ? tp : (cormen_hash(t) < cormen_hash(h) ? tp : hp);
+    if (live && !loop) {
+      if (ad >= 0) { if (lds) atomicAdd(&lbal[0][pd], 1u); else atomicAdd(&bal[pd], 1ull); }
+      if (au >= 0) { if (lds) atomicAdd(&lbal[1][pu], 1u); else atomicAdd(&bal[nparts + pu], 1ull); }
+      if (ah >= 0) {
+        if (lds) atomicAdd(&lbal[2][po], 1u); else atomicAdd(&bal[2 * nparts + po], 1ull);
+        cut += tp != hp;
+      }
     }
-    if (what & 4) {
-      set_bit(bup, W, t, pup); set_bit(bup, W, h, pup);
-      if (lds) atomicAdd(&lbal[1][pup], 1u); else atomicAdd(&bal[nparts + pup], 1ull);
-    }
-    if (what & 1) {
-      const int ph_ = cormen_hash(t) < cormen_hash(h) ? tp : hp;
-      set_bit(bhash, W, t, ph_); set_bit(bhash, W, h, ph_);
-      if (lds) atomicAdd(&lbal[2][ph_], 1u); else atomicAdd(&bal[2 * nparts + ph_], 1ull);
-      set_bit(bvc, W, t, hp); set_bit(bvc, W, h, tp);
-      cut += tp != hp;
+    // the tail side: runs of equal tails combined in the wave (single-word bitsets)
+    const int own_t[4] = {pd, pu, po, hp};   // down, up, hash, vcom owner seen from t
+    const int own_h[4] = {pd, pu, po, tp};
+    const int arr[4] = {ad, au, ah, av};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (arr[q] < 0) continue;   // uniform
+      if (W64 == 1) {
+        const uint64_t m = run_or(live ? t : INVALID, live ? 1ull << own_t[q] : 0);
+        if (m) or_bits(bits, (uint64_t)t * M + arr[q], m);
+      } else if (live) {
+        or_bits(bits, ((uint64_t)t * M + arr[q]) * W64 + (own_t[q] >> 6), 1ull << (own_t[q] & 63));
+      }
+      if (live && !loop) or_bits(bits, ((uint64_t)h * M + arr[q]) * W64 + (own_h[q] >> 6), 1ull << (own_h[q] & 63));
     }
   }
   cut = wave_sum(cut);
   bad = wave_sum(bad);
-  sl = wave_sum(sl);
+  loops = wave_sum(loops);
   if ((threadIdx.x & 63) == 0) {
-    if (sl) atomicAdd(selfl, (unsigned long long)sl);
-    if (cut) atomicAdd(&scal[0], (unsigned long long)cut);
-    if (bad) atomicAdd(&scal[1], (unsigned long long)bad);
+    if (cut) atomicAdd(&acc[AC_CUT], (unsigned long long)cut);
+    if (bad) atomicAdd(&acc[AC_BAD], (unsigned long long)bad);
+    if (loops) atomicAdd(&acc[AC_LOOPS], (unsigned long long)loops);
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&acc[AC_RECS], (unsigned long long)nrec);
   __syncthreads();
   if (lds)
-    for (int i = threadIdx.x; i < 3 * nparts; i += BLOCK) {
-      int a = i / nparts, p = i % nparts;
-      uint32_t v = lbal[a][p];
-      if (v) atomicAdd(&bal[i], (unsigned long long)v);
+    for (int x = threadIdx.x; x < 3 * nparts; x += BLOCK) {
+      const uint32_t v = lbal[x / nparts][x % nparts];
+      if (v) atomicAdd(&bal[x], (unsigned long long)v);
     }
 }
 
-// per vertex slot: nodes are the slots whose Vcom / ECV bitsets are non-empty
-__global__ __launch_bounds__(BLOCK) void k_eval_nodes(uint64_t vs, const int16_t *__restrict__ parts, int what,
-                                                      uint32_t W, int nparts, const uint32_t *__restrict__ bdown,
-                                                      const uint32_t *__restrict__ bup,
-                                                      const uint32_t *__restrict__ bhash,
-                                                      const uint32_t *__restrict__ bvc,
+// dst |= src over the bit words, dst += src over the accumulators (shard combine)
+__global__ void k_eval_combine(unsigned long long *__restrict__ dst, const unsigned long long *__restrict__ src,
+                               uint64_t words, unsigned long long *__restrict__ adst,
+                               const unsigned long long *__restrict__ asrc, uint64_t awords) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < words; i += stride) dst[i] |= src[i];
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < awords; i += stride) adst[i] += asrc[i];
+}
+
+// Per vertex slot: a node is a slot whose first bit array is non-empty (every record
+// sets a bit in every requested array at both endpoints).  out = {ecv down, up, hash,
+// vcom, nodes}; vbal = vertex balance histogram.
+__global__ __launch_bounds__(BLOCK) void k_eval_nodes(uint64_t vs, const int16_t *__restrict__ parts, int what, int M,
+                                                      uint32_t W64, int nparts,
+                                                      const unsigned long long *__restrict__ bits,
                                                       unsigned long long *__restrict__ vbal,
-                                                      unsigned long long *__restrict__ scal) {
-  uint64_t sdown = 0, sup = 0, shash = 0, svc = 0, nodes = 0;
+                                                      unsigned long long *__restrict__ out) {
+  __shared__ uint32_t lv[LDS_PARTS];
+  const bool lds = nparts <= LDS_PARTS;
+  if (lds)
+    for (int i = threadIdx.x; i < LDS_PARTS; i += BLOCK) lv[i] = 0;
+  __syncthreads();
+  const int ad = (what & 2) ? 0 : -1;
+  const int au = (what & 4) ? ((what & 2) ? 1 : 0) : -1;
+  const int ah = (what & 1) ? M - 2 : -1, av = (what & 1) ? M - 1 : -1;
+  uint64_t s[4] = {0, 0, 0, 0}, nodes = 0;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < vs; v += stride) {
-    const uint32_t *any = (what & 2) ? bdown : ((what & 4) ? bup : bhash);
-    uint32_t cd = 0, cu = 0, chh = 0, cv = 0;
+    const unsigned long long *b = bits + v * M * W64;
     bool node = false;
-    for (uint32_t w = 0; w < W; ++w) node |= any[v * W + w] != 0;
+    for (uint32_t w = 0; w < W64; ++w) node |= b[w] != 0;
     if (!node) continue;
     ++nodes;
-    int p = parts[v];
-    for (uint32_t w = 0; w < W; ++w) {
-      uint64_t o = v * W + w;
-      if (what & 2) cd += __popc(bdown[o]);
-      if (what & 4) cu += __popc(bup[o]);
-      if (what & 1) {
-        chh += __popc(bhash[o]);
-        uint32_t x = bvc[o];
-        if ((uint32_t)(p >> 5) == w) x |= 1u << (p & 31);
-        cv += __popc(x);
+    const int p = parts[v];
+    const int arr[4] = {ad, au, ah, av};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (arr[q] < 0) continue;
+      uint32_t cnt = 0;
+      for (uint32_t w = 0; w < W64; ++w) {
+        uint64_t x = b[arr[q] * W64 + w];
+        if (q == 3 && p >= 0 && (uint32_t)(p >> 6) == w) x |= 1ull << (p & 63);   // Vcom: own part
+        cnt += __popcll(x);
       }
+      s[q] += cnt - 1;
     }
-    sdown += cd - 1; sup += cu - 1; shash += chh - 1; svc += cv - 1;
-    if ((what & 1) && p >= 0 && p < nparts) atomicAdd(&vbal[p], 1ull);
+    if (av >= 0 && p >= 0 && p < nparts) {
+      if (lds) atomicAdd(&lv[p], 1u); else atomicAdd(&vbal[p], 1ull);
+    }
   }
-  sdown = wave_sum(sdown); sup = wave_sum(sup); shash = wave_sum(shash); svc = wave_sum(svc); nodes = wave_sum(nodes);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) s[q] = wave_sum(s[q]);
+  nodes = wave_sum(nodes);
   if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&scal[2], (unsigned long long)sdown);
-    atomicAdd(&scal[3], (unsigned long long)sup);
-    atomicAdd(&scal[4], (unsigned long long)shash);
-    atomicAdd(&scal[5], (unsigned long long)svc);
-    atomicAdd(&scal[6], (unsigned long long)nodes);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (s[q]) atomicAdd(&out[q], (unsigned long long)s[q]);
+    if (nodes) atomicAdd(&out[4], (unsigned long long)nodes);
   }
+  __syncthreads();
+  if (lds)
+    for (int x = threadIdx.x; x < nparts; x += BLOCK)
+      if (lv[x]) atomicAdd(&vbal[x], (unsigned long long)lv[x]);
 }
 
 __global__ void k_max_part(const int16_t *__restrict__ parts, uint64_t vs, unsigned long long *__restrict__ out) {
@@ -138,62 +235,122 @@ __global__ void k_max_part(const int16_t *__restrict__ parts, uint64_t vs, unsig
   if ((threadIdx.x & 63) == 0 && m >= 0) atomicMax(out, (unsigned long long)m);
 }
 
+int eval_arrays(int what) { return ((what & 2) ? 1 : 0) + ((what & 4) ? 1 : 0) + ((what & 1) ? 2 : 0); }
+
 }  // namespace
 
-// `what` bitmask: 1 = evaluate(graph) metrics, 2 = ECV(down), 4 = ECV(up).
-void evaluate(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
-              const int16_t *parts, int what, sheep_eval *out) {
+// Layout of the evaluator state for `what` (0 = all) and nparts parts (max part + 1).
+void eval_sizes(int what, int nparts, uint64_t pos_size, uint64_t *bits_words, uint64_t *acc_words) {
+  if (what == 0) what = 7;
+  if (what & ~7) throw Error(SHEEP_ERR_ARG, "evaluate: unknown metric bits");
+  if (nparts < 1) nparts = 1;
+  const uint64_t W64 = ((uint64_t)nparts + 63) / 64;
+  *bits_words = pos_size * (uint64_t)eval_arrays(what) * W64;
+  *acc_words = AC_SCAL + 3 * (uint64_t)nparts;
+}
+
+int eval_num_parts(Ctx &c, const int16_t *parts, uint64_t pos_size) {
+  unsigned long long *d = (unsigned long long *)c.d_scalars + 55;
+  HIP_CHECK(hipMemsetAsync(d, 0, sizeof(uint64_t), c.stream));
+  if (pos_size) {
+    hipLaunchKernelGGL(k_max_part, dim3(grid_for(pos_size)), dim3(BLOCK), 0, c.stream, parts, pos_size, d);
+    LAUNCH_CHECK();
+  }
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 55, d, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  return (int)c.h_scalars[55] + 1;   // max part + 1 (partition.cpp:433-435)
+}
+
+// One shard's records: owner bits ORed into bits, counts added into acc (both zeroed by
+// the caller before the first shard).  Asynchronous.
+void eval_shard(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
+                const int16_t *parts, int what, int nparts, uint64_t *bits, uint64_t *acc) {
+  if (what == 0) what = 7;
+  const int M = eval_arrays(what);
+  const uint32_t W64 = (uint32_t)((nparts + 63) / 64);
+  if (!nrec) return;
+  if (pos_size == 0) {   // every record is out of range
+    hipLaunchKernelGGL(k_eval_records, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, (const uint64_t *)nullptr,
+                       (uint64_t)0, what, M, W64, nparts, (unsigned long long *)bits, (unsigned long long *)acc);
+    LAUNCH_CHECK();
+    return;
+  }
+  uint64_t *pp = c.get_as<uint64_t>("ev_pp", pos_size);
+  hipLaunchKernelGGL(k_pp, dim3(grid_for(pos_size)), dim3(BLOCK), 0, c.stream, pos, parts, pos_size, pp);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_eval_records, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, (const uint64_t *)pp,
+                     pos_size, what, M, W64, nparts, (unsigned long long *)bits, (unsigned long long *)acc);
+  LAUNCH_CHECK();
+}
+
+void eval_combine(Ctx &c, uint64_t *bits, const uint64_t *bits_src, uint64_t words, uint64_t *acc,
+                  const uint64_t *acc_src, uint64_t acc_words) {
+  const uint64_t mx = words > acc_words ? words : acc_words;
+  if (!mx) return;
+  hipLaunchKernelGGL(k_eval_combine, dim3(grid_for(mx)), dim3(BLOCK), 0, c.stream, (unsigned long long *)bits,
+                     (const unsigned long long *)bits_src, words, (unsigned long long *)acc,
+                     (const unsigned long long *)acc_src, acc_words);
+  LAUNCH_CHECK();
+}
+
+// The node pass over the (combined) state and the result; synchronises.
+void eval_finish(Ctx &c, const uint64_t *bits, const uint64_t *acc, uint64_t pos_size, const int16_t *parts, int what,
+                 int nparts, sheep_eval *out) {
   *out = sheep_eval();
   if (what == 0) what = 7;
-  unsigned long long *scal = (unsigned long long *)c.d_scalars + 48;
-  HIP_CHECK(hipMemsetAsync(scal, 0, 9 * sizeof(uint64_t), c.stream));
+  const int M = eval_arrays(what);
+  const uint32_t W64 = (uint32_t)((nparts + 63) / 64);
+  unsigned long long *vbal = c.get_as<unsigned long long>("ev_vbal", (uint64_t)nparts);
+  unsigned long long *res = (unsigned long long *)c.d_scalars + 48;   // ecv down, up, hash, vcom, nodes
+  HIP_CHECK(hipMemsetAsync(vbal, 0, (uint64_t)nparts * sizeof(uint64_t), c.stream));
+  HIP_CHECK(hipMemsetAsync(res, 0, 5 * sizeof(uint64_t), c.stream));
   if (pos_size) {
-    hipLaunchKernelGGL(k_max_part, dim3(grid_for(pos_size)), dim3(BLOCK), 0, c.stream, parts, pos_size, scal + 7);
+    hipLaunchKernelGGL(k_eval_nodes, dim3(grid_for(pos_size)), dim3(BLOCK), 0, c.stream, pos_size, parts, what, M, W64,
+                       nparts, (const unsigned long long *)bits, vbal, res);
     LAUNCH_CHECK();
   }
-  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 55, scal + 7, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  const uint64_t aw = AC_SCAL + 3 * (uint64_t)nparts;
+  std::vector<uint64_t> ha(aw), hv(nparts);
+  HIP_CHECK(hipMemcpyAsync(ha.data(), acc, aw * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipMemcpyAsync(hv.data(), vbal, (uint64_t)nparts * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 48, res, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
-  const int nparts = (int)c.h_scalars[55] + 1;   // max part + 1 (partition.cpp:433-435)
-  const uint32_t W = (uint32_t)((nparts + 31) / 32);
-  const uint64_t words = pos_size * W;
-  uint32_t *bd = c.get_as<uint32_t>("ev_bdown", words ? words : 1);
-  uint32_t *bu = (what & 4) ? c.get_as<uint32_t>("ev_bup", words) : bd;
-  uint32_t *bh = (what & 1) ? c.get_as<uint32_t>("ev_bhash", words) : bd;
-  uint32_t *bv = (what & 1) ? c.get_as<uint32_t>("ev_bvc", words) : bd;
-  if (!(what & 2)) bd = (what & 4) ? bu : bh;
-  for (uint32_t *b : {bd, bu, bh, bv}) HIP_CHECK(hipMemsetAsync(b, 0, words * sizeof(uint32_t), c.stream));
-  unsigned long long *bal = c.get_as<unsigned long long>("ev_bal", 4 * (uint64_t)nparts);
-  HIP_CHECK(hipMemsetAsync(bal, 0, 4 * (uint64_t)nparts * sizeof(uint64_t), c.stream));
+  if (ha[AC_BAD]) throw Error(SHEEP_ERR_RANGE, "evaluate: a vertex is unsequenced or unassigned");
+  auto mx = [&](const uint64_t *h) { uint64_t m = 0; for (int p = 0; p < nparts; ++p) m = h[p] > m ? h[p] : m; return m; };
+  const uint64_t *bal = ha.data() + AC_SCAL;
+  out->nodes = c.h_scalars[52];
+  // adjacency entries = 2 per record, 1 per self-loop (LLAMA stores a self-loop once)
+  out->edges = (2 * ha[AC_RECS] - ha[AC_LOOPS]) / 2;
+  if (what & 2) { out->ecv_down = c.h_scalars[48]; out->max_down_bal = mx(bal); }
+  if (what & 4) { out->ecv_up = c.h_scalars[49]; out->max_up_bal = mx(bal + nparts); }
+  if (what & 1) {
+    out->ecv_hash = c.h_scalars[50];
+    out->vcom_vol = c.h_scalars[51];
+    out->edges_cut = ha[AC_CUT];
+    out->max_hash_bal = mx(bal + 2 * (uint64_t)nparts);
+    out->max_vertex_bal = mx(hv.data());
+  }
+}
+
+// `what` bitmask: 1 = evaluate(graph) metrics, 2 = ECV(down), 4 = ECV(up); 0 = all.
+// Metrics outside the mask come back 0.
+void evaluate(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
+              const int16_t *parts, int what, sheep_eval *out) {
+  uint64_t words = 0, aw = 0;
+  eval_sizes(what, 1, pos_size, &words, &aw);   // validates `what`
+  const int nparts = eval_num_parts(c, parts, pos_size);
+  eval_sizes(what, nparts, pos_size, &words, &aw);
+  uint64_t *bits = c.get_as<uint64_t>("ev_bits", words ? words : 1);
+  uint64_t *acc = c.get_as<uint64_t>("ev_acc", aw);
+  HIP_CHECK(hipMemsetAsync(bits, 0, words * sizeof(uint64_t), c.stream));
+  HIP_CHECK(hipMemsetAsync(acc, 0, aw * sizeof(uint64_t), c.stream));
   {
     // B_eval: record read + 2 pos + 2 part gathers, bitset write + read
-    TimedRegion tr(c, "evaluate", 28 * nrec + 8 * words);
-    if (nrec) {
-      hipLaunchKernelGGL(k_eval_records, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos, pos_size,
-                         parts, what, W, nparts, bd, bu, bh, bv, bal, scal, scal + 8);
-      LAUNCH_CHECK();
-    }
-    hipLaunchKernelGGL(k_eval_nodes, dim3(grid_for(pos_size)), dim3(BLOCK), 0, c.stream, pos_size, parts, what, W,
-                       nparts, bd, bu, bh, bv, bal + 3 * (uint64_t)nparts, scal);
-    LAUNCH_CHECK();
+    // (2 B per slot per 8 parts, per bit array)
+    TimedRegion tr(c, "evaluate", 28 * nrec + 2 * words * 8);
+    eval_shard(c, rec, nrec, pos, pos_size, parts, what, nparts, bits, acc);
+    eval_finish(c, bits, acc, pos_size, parts, what, nparts, out);
   }
-  std::vector<uint64_t> hb(4 * (uint64_t)nparts);
-  HIP_CHECK(hipMemcpyAsync(hb.data(), bal, hb.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 48, scal, 9 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-  c.sync();
-  if (c.h_scalars[49]) throw Error(SHEEP_ERR_RANGE, "evaluate: a vertex is unsequenced or unassigned");
-  auto mx = [&](int a) { uint64_t m = 0; for (int p = 0; p < nparts; ++p) m = std::max(m, hb[(uint64_t)a * nparts + p]); return m; };
-  out->edges_cut = c.h_scalars[48];
-  out->ecv_down = c.h_scalars[50];
-  out->ecv_up = c.h_scalars[51];
-  out->ecv_hash = c.h_scalars[52];
-  out->vcom_vol = c.h_scalars[53];
-  out->nodes = c.h_scalars[54];
-  // adjacency entries = 2 per record, 1 per self-loop (LLAMA stores a self-loop once)
-  out->edges = (2 * nrec - c.h_scalars[56]) / 2;
-  out->max_down_bal = mx(0);
-  out->max_up_bal = mx(1);
-  out->max_hash_bal = mx(2);
-  out->max_vertex_bal = mx(3);
 }
 
 }  // namespace sheep

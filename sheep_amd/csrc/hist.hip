@@ -170,54 +170,11 @@ __global__ __launch_bounds__(HB) void k_hist_scatter(Src src, uint64_t n, uint32
 }
 
 // k_hist_scatter for tree edges grouped by padded lo: besides the u16 key runs it moves
-// each edge to the same position of `grouped` (the thread still holds it), so the
-// elimination tree's input comes out in lo-bucket order at no extra read.
-__global__ __launch_bounds__(HB) void k_lo_scatter(EdgeLoPadded src, uint64_t n, uint32_t nb,
-                                                   const uint32_t *__restrict__ offsets, uint64_t ntiles,
-                                                   uint16_t *__restrict__ out, uint64_t *__restrict__ grouped) {
-  extern __shared__ uint32_t lds[];
-  uint32_t *cur = lds;
-  uint32_t *start = lds + nb;
-  uint32_t *wsum = lds + 2 * nb;
-  uint32_t *stage = lds + 2 * nb + HB / WAVE;
-  for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
-  __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x << TLOG;
-  uint64_t e[KPT];
-  uint32_t k[KPT];
-#pragma unroll
-  for (int j = 0; j < KPT; ++j) {
-    const uint64_t i = base + (uint64_t)j * HB + threadIdx.x;
-    e[j] = i < n ? src.edges[i] : ~0ull;
-  }
-#pragma unroll
-  for (int j = 0; j < KPT; ++j) {
-    k[j] = src.key(e[j]);
-    if (k[j] != NO_KEY) atomicAdd(&cur[k[j] >> WBITS], 1u);
-  }
-  __syncthreads();
-  const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
-  for (uint32_t b = threadIdx.x; b < nb; b += HB) start[b] = cur[b];
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < KPT; ++j)
-    if (k[j] != NO_KEY) {
-      const uint32_t b = k[j] >> WBITS;
-      const uint32_t p = atomicAdd(&cur[b], 1u);
-      stage[p] = (b << 16) | (k[j] & (W - 1));
-      grouped[offsets[(uint64_t)b * ntiles + blockIdx.x] + (p - start[b])] = e[j];
-    }
-  __syncthreads();
-  for (uint32_t j = threadIdx.x; j < total; j += HB) {
-    const uint32_t x = stage[j], b = x >> 16;
-    out[offsets[(uint64_t)b * ntiles + blockIdx.x] + (j - start[b])] = (uint16_t)(x & 0xFFFF);
-  }
-}
-
-// k_lo_scatter with LDS-staged edges: SUB = PER * HB edges at a time are counting-sorted
-// by bucket in LDS and each bucket's run is written with consecutive lanes (the u16 key
-// beside it), instead of one scattered 8-B store per lane.  Same offsets, same result
-// (within a (bucket, tile) run the order is the counting sort's, as in k_lo_scatter).
+// each edge into `grouped` at the same position, so the elimination tree's input comes
+// out in lo-bucket order at no extra read.  SUB = PER * HB edges at a time are
+// counting-sorted by bucket in LDS and each bucket's run is written with consecutive
+// lanes (the u16 key beside it); one scattered 8-B store per lane took 15.4 ms at RMAT-26
+// against 9.8.
 template <int PER>
 __global__ __launch_bounds__(HB) void k_lo_scatter_staged(EdgeLoPadded src, uint64_t n, uint32_t nb,
                                                           const uint32_t *__restrict__ offsets, uint64_t ntiles,
@@ -341,14 +298,10 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
       return;
     }
   }
-  static bool attr_set = false;   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
-  if (!attr_set) {
-    HIP_CHECK(hipFuncSetAttribute((const void *)k_hist_scatter<HeadKeys>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_CHECK(hipFuncSetAttribute((const void *)k_hist_scatter<EdgeLoKeys>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_CHECK(hipFuncSetAttribute((const void *)k_hist_final, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_CHECK(hipFuncSetAttribute((const void *)k_lo_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
-  }
+  for (const void *f : {(const void *)k_hist_scatter<HeadKeys>, (const void *)k_hist_scatter<EdgeLoKeys>,
+                        (const void *)k_hist_final, (const void *)k_lo_scatter_staged<16>,
+                        (const void *)k_lo_scatter_staged<8>})
+    allow_full_lds(f);
   uint32_t *tile_hist = c.get_as<uint32_t>("hist_tiles", ntiles * nb + 1);
   uint16_t *keys = c.get_as<uint16_t>("hist_keys", n);
   if (!counted) {   // (counted: degree_fused already wrote tile_hist, >= nb bucket rows)
@@ -363,23 +316,12 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
     HIP_CHECK(hipMemcpyAsync(save_offsets + ntiles * nb, total, sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
   }
   if constexpr (std::is_same<Src, EdgeLoPadded>::value) {
-    static const bool direct = getenv("SHEEP_LO_DIRECT") != nullptr;   // A/B: one scattered store per lane
-    static bool staged_attr = false;
-    if (!staged_attr) {
-      HIP_CHECK(hipFuncSetAttribute((const void *)k_lo_scatter_staged<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      HIP_CHECK(hipFuncSetAttribute((const void *)k_lo_scatter_staged<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      staged_attr = true;
-    }
-    if (!direct && lds_staged16 <= 160 * 1024) {
+    if (lds_staged16 <= 160 * 1024)
       hipLaunchKernelGGL(k_lo_scatter_staged<16>, dim3((unsigned)ntiles), dim3(HB), lds_staged16, c.stream, src, n, nb,
                          (const uint32_t *)tile_hist, ntiles, keys, grouped);
-    } else if (!direct || lds_scatter > 160 * 1024) {
+    else
       hipLaunchKernelGGL(k_lo_scatter_staged<8>, dim3((unsigned)ntiles), dim3(HB), lds_staged8, c.stream, src, n, nb,
                          (const uint32_t *)tile_hist, ntiles, keys, grouped);
-    } else {
-      hipLaunchKernelGGL(k_lo_scatter, dim3((unsigned)ntiles), dim3(HB), lds_scatter, c.stream, src, n, nb,
-                         (const uint32_t *)tile_hist, ntiles, keys, grouped);
-    }
   } else {
     hipLaunchKernelGGL(k_hist_scatter<Src>, dim3((unsigned)ntiles), dim3(HB), lds_scatter, c.stream, src, n, nb,
                        (const uint32_t *)tile_hist, ntiles, keys);
@@ -494,7 +436,7 @@ struct RelabelKeys {
 // a whole tile does not fit LDS).  gb[b] walks the tile's region of bucket b; every write
 // is bounded by the region's end and a region not filled exactly raises flags[1] (stale
 // offsets) so the host recounts.  flags[0]: a sequenced endpoint's neighbour >= pos_size.
-template <int PER, bool NT>
+template <int PER>
 __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restrict__ rec, uint64_t n,
                                                         const uint32_t *__restrict__ pos, uint64_t pos_size, uint32_t nb,
                                                         const uint32_t *__restrict__ offsets, uint64_t ntiles,
@@ -522,14 +464,7 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
       hd[j] = INVALID;
       pt[j] = INVALID;
       if (i < n) {
-        uint32_t t, h;
-        if constexpr (NT) {   // records stream through once: keep pos resident in the caches
-          t = __builtin_nontemporal_load(&rec[i].tail);
-          h = __builtin_nontemporal_load(&rec[i].head);
-        } else {
-          t = rec[i].tail;
-          h = rec[i].head;
-        }
+        const uint32_t t = rec[i].tail, h = rec[i].head;
         if (t != h) { hd[j] = h; pt[j] = t; }
       }
     }
@@ -557,12 +492,8 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
     for (uint32_t j = threadIdx.x; j < total; j += HB) {
       const uint64_t v = stage[j];
       const uint32_t b = (uint32_t)v >> WBITS, dst = gb[b] + j;
-      if (dst < end[b]) {
-        if constexpr (NT) __builtin_nontemporal_store(v, &out[dst]);
-        else out[dst] = v;
-      } else {
-        lost = true;
-      }
+      if (dst < end[b]) out[dst] = v;
+      else lost = true;
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += cur[b];   // past this sub-tile's run
@@ -577,7 +508,6 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
 // One workgroup per (bucket, slice of <= CHUNK pairs): the bucket's pos slice in LDS.
 // Same outcomes as k_relabel: both endpoints sequenced -> tree edge (hi << 32 | lo);
 // one sequenced, the other an unsequenced slot -> POSTORDER pst for the sequenced one.
-template <bool NT>
 __global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restrict__ pairs, const Chunk *__restrict__ chunks,
                                                        const uint32_t *__restrict__ pos, uint64_t pos_size,
                                                        uint32_t *__restrict__ pst, uint64_t *__restrict__ edges,
@@ -593,7 +523,7 @@ __global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restric
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
-      x[j] = i >= ch.end ? NO_PAIR : NT ? __builtin_nontemporal_load(&pairs[i]) : pairs[i];
+      x[j] = i >= ch.end ? NO_PAIR : pairs[i];
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -650,22 +580,13 @@ void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uin
   hl.valid = hl.bstart.size() == nb + 1;
 }
 
-// SHEEP_RL_NT=0/1: plain or non-temporal record/pair streams in the relabel passes (A/B)
-static const bool g_rl_nt = getenv("SHEEP_RL_NT") ? atoi(getenv("SHEEP_RL_NT")) != 0 : false;   // NT: 18.4 vs 13.9 ms at RMAT-26
-
 uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
                           uint32_t *pst, uint64_t *edges, unsigned long long *err) {
   const uint64_t nb = (pos_size + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
   if (nrec == 0 || nb == 0 || nb > 4096 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return UINT64_MAX;
-  static bool attr_set = false;
-  if (!attr_set) {
-    for (const void *f : {(const void *)k_relabel_scatter<16, false>, (const void *)k_relabel_scatter<8, false>,
-                          (const void *)k_relabel_scatter<4, false>, (const void *)k_relabel_gather<false>,
-                          (const void *)k_relabel_scatter<16, true>, (const void *)k_relabel_scatter<8, true>,
-                          (const void *)k_relabel_scatter<4, true>, (const void *)k_relabel_gather<true>})
-      HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
-  }
+  for (const void *f : {(const void *)k_relabel_scatter<8>, (const void *)k_relabel_scatter<4>,
+                        (const void *)k_relabel_gather})
+    allow_full_lds(f);
   Ctx::HeadLayout &hl = c.head_layout;
   unsigned long long *flags = c.get_as<unsigned long long>("rl_flags", 2);
   auto recount = [&]() -> uint32_t * {   // the relabel's own (bucket, tile) offsets
@@ -692,20 +613,16 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   const size_t fixed = ((3 * nb + HB / WAVE + 1) & ~1ull) * 4;
   auto scatter = [&]() {
     HIP_CHECK(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c.stream));
-    static const int per_max = getenv("SHEEP_RL_PER") ? atoi(getenv("SHEEP_RL_PER")) : 8;   // experiments
-    const int per = per_max >= 16 && fixed + 16 * HB * 8 <= 160 * 1024 ? 16
-                  : per_max >= 8 && fixed + 8 * HB * 8 <= 160 * 1024 ? 8 : 4;
+    // 8K-record sub-tiles (4K / 16K measured 15.8 / 15.3 ms against 14.3 at RMAT-26)
+    const int per = fixed + 8 * HB * 8 <= 160 * 1024 ? 8 : 4;
     const size_t lds = fixed + (size_t)per * HB * 8;
     const dim3 g((unsigned)ntiles), b(HB);
     const uint32_t nb32 = (uint32_t)nb;
     const uint32_t *o = off;
-#define SHEEP_RL_SCATTER(P, N) hipLaunchKernelGGL((k_relabel_scatter<P, N>), g, b, lds, c.stream, rec, nrec, pos, pos_size, nb32, o, ntiles, pairs, flags)
-    if (g_rl_nt) {
-      if (per == 16) SHEEP_RL_SCATTER(16, true); else if (per == 8) SHEEP_RL_SCATTER(8, true); else SHEEP_RL_SCATTER(4, true);
-    } else {
-      if (per == 16) SHEEP_RL_SCATTER(16, false); else if (per == 8) SHEEP_RL_SCATTER(8, false); else SHEEP_RL_SCATTER(4, false);
-    }
-#undef SHEEP_RL_SCATTER
+    if (per == 8)
+      hipLaunchKernelGGL(k_relabel_scatter<8>, g, b, lds, c.stream, rec, nrec, pos, pos_size, nb32, o, ntiles, pairs, flags);
+    else
+      hipLaunchKernelGGL(k_relabel_scatter<4>, g, b, lds, c.stream, rec, nrec, pos, pos_size, nb32, o, ntiles, pairs, flags);
     LAUNCH_CHECK();
     HIP_CHECK(hipMemcpyAsync(c.h_scalars + 12, flags, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   };
@@ -735,12 +652,8 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   if (!chunks.empty()) {
     Chunk *dch = c.get_as<Chunk>("rl_chunks", chunks.size());
     HIP_CHECK(hipMemcpyAsync(dch, chunks.data(), chunks.size() * sizeof(Chunk), hipMemcpyHostToDevice, c.stream));
-    if (g_rl_nt)
-      hipLaunchKernelGGL(k_relabel_gather<true>, dim3((unsigned)chunks.size()), dim3(HB), W * 4, c.stream,
-                         (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err);
-    else
-      hipLaunchKernelGGL(k_relabel_gather<false>, dim3((unsigned)chunks.size()), dim3(HB), W * 4, c.stream,
-                         (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err);
+    hipLaunchKernelGGL(k_relabel_gather, dim3((unsigned)chunks.size()), dim3(HB), W * 4, c.stream,
+                       (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err);
     LAUNCH_CHECK();
     c.sync();   // `chunks` is a pageable host buffer
   }

@@ -151,7 +151,7 @@ __global__ void k_push_down(const uint32_t *__restrict__ parent, const uint32_t 
                             int16_t *__restrict__ parts, unsigned long long *__restrict__ err) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride) {
-    if (parent[v] == INVALID) continue;   // roots are scattered directly
+    if (parent[v] == INVALID) continue;   // roots are scattered directly; the fringe goes next
     uint32_t p = tD[v];
     uint32_t lo = 0, hi = na;              // last interval with start <= p
     while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (ast[mid] <= p) lo = mid + 1; else hi = mid; }
@@ -174,83 +174,225 @@ __global__ void k_fill_i16(int16_t *__restrict__ p, uint64_t n, int16_t v) {
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) p[i] = v;
 }
 
-__global__ void k_parts_to_vid(const uint32_t *__restrict__ seq, uint64_t n, const int16_t *__restrict__ parts,
+// jnid -> vid over the sequence's seq_n entries (partition.cpp:62-66); cnt = {#part 0,
+// #part 1, max part + 1} over the converted entries (the print counts, partition.h:135-143;
+// slots left INVALID_PART count for neither).  Out-of-range vids are the caller's check
+// (pos_size = max(seq) + 1).
+__global__ void k_parts_to_vid(const uint32_t *__restrict__ seq, uint64_t seq_n, const int16_t *__restrict__ parts,
                                int16_t *__restrict__ pv, unsigned long long *__restrict__ cnt) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  uint64_t c0 = 0, c1 = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
-    int16_t p = parts[i];
+  uint64_t c0 = 0, c1 = 0, mx = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < seq_n; i += stride) {
+    const int16_t p = parts[i];
     pv[seq[i]] = p;
     c0 += p == 0;
     c1 += p == 1;
+    mx = (uint64_t)(p + 1) > mx ? (uint64_t)(p + 1) : mx;
   }
   c0 = wave_sum(c0);
   c1 = wave_sum(c1);
+  mx = wave_max(mx);
   if ((threadIdx.x & 63) == 0) {
     if (c0) atomicAdd(&cnt[0], (unsigned long long)c0);
     if (c1) atomicAdd(&cnt[1], (unsigned long long)c1);
+    if (mx) atomicMax(&cnt[2], (unsigned long long)mx);
   }
 }
 
-// One packing event over H: the last packing (node v, tour position vpos, removed
-// weight delta) lowers R of v and of its ancestors; then the lowest id with R > max.
-__global__ __launch_bounds__(BLOCK) void k_pack_event(const uint32_t *__restrict__ hids, uint64_t nh,
-                                                      const uint32_t *__restrict__ hst, const uint32_t *__restrict__ hen,
-                                                      uint64_t *__restrict__ R, uint32_t v, uint32_t vpos,
-                                                      uint64_t delta, uint64_t maxc, const uint64_t *__restrict__ prev,
-                                                      unsigned long long *__restrict__ next) {
-  // hids ascends and nodes below the last packing node v are final: start at v's index
-  const uint64_t start = *prev == ~0ull ? 0 : (uint32_t)*prev;
+// ---- raking: exact subtree sums of the light fringe -------------------------------
+// Round r finishes every node whose kids are all finished and whose accumulated weight
+// acc (own weight + finished kids' sums) is <= max_component: acc is then its subtree sum
+// S, it cannot pack (only S > max can), and it is added into its parent.  Elimination
+// trees of power-law graphs are mostly fringe (RMAT: 66% leaves; three rounds finish
+// ~77% of the nodes), so the Euler tour below only ranks the remaining core T'.
+constexpr int RAKE_ROUNDS = 3;
+
+__global__ void k_rake_init(const uint32_t *__restrict__ koff, const uint64_t *__restrict__ w, uint64_t n,
+                            uint32_t *__restrict__ pend, uint64_t *__restrict__ acc, uint8_t *__restrict__ fin) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  uint64_t best = ~0ull;   // (id << 32) | index of the next packing node
-  for (uint64_t h = start + (uint64_t)blockIdx.x * BLOCK + threadIdx.x; h < nh; h += stride) {
-    const uint32_t a = hids[h];
-    uint64_t r = R[a];
-    if (delta && (a == v || (vpos != INVALID && hst[h] <= vpos && vpos <= hen[h]))) {
-      r -= delta;
-      R[a] = r;
-    }
-    if (r > maxc && (v == INVALID || a > v)) {
-      const uint64_t key = ((uint64_t)a << 32) | h;
-      best = key < best ? key : best;
-    }
+  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride) {
+    pend[v] = koff[v + 1] - koff[v];
+    acc[v] = w[v];
+    fin[v] = 0;
   }
-  best = wave_min(best);
-  if ((threadIdx.x & 63) == 0 && best != ~0ull) atomicMin(next, (unsigned long long)best);
+}
+// mark, then push: the two phases keep a round's finished set independent of timing
+__global__ void k_rake_mark(const uint32_t *__restrict__ pend, const uint64_t *__restrict__ acc, uint64_t n,
+                            uint64_t maxc, uint8_t round, uint8_t *__restrict__ fin) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride)
+    if (!fin[v] && pend[v] == 0 && acc[v] <= maxc) fin[v] = round;
+}
+__global__ void k_rake_push(const uint32_t *__restrict__ parent, const uint8_t *__restrict__ fin, uint64_t n,
+                            uint8_t round, uint64_t *__restrict__ acc, uint32_t *__restrict__ pend) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride) {
+    if (fin[v] != round) continue;
+    const uint32_t p = parent[v];
+    if (p == INVALID) continue;
+    atomicAdd((unsigned long long *)&acc[p], (unsigned long long)acc[v]);
+    atomicSub(&pend[p], 1u);
+  }
+}
+
+// The core's kid table: the kid table's segments with finished kids dropped (order kept);
+// finished nodes become isolated (parent INVALID, no kids) so the tour skips them.
+__global__ void k_core_flags(const uint32_t *__restrict__ kids, uint64_t nk, const uint8_t *__restrict__ fin,
+                             uint32_t *__restrict__ flag) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < nk; j += stride) flag[j] = fin[kids[j]] == 0;
+}
+__global__ void k_core_build(const uint32_t *__restrict__ kids, uint64_t nk, const uint32_t *__restrict__ koff,
+                             const uint32_t *__restrict__ parent, const uint8_t *__restrict__ fin, uint64_t n,
+                             const uint32_t *__restrict__ pref, uint32_t *__restrict__ ckids,
+                             uint32_t *__restrict__ ckoff, uint32_t *__restrict__ cparent) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const uint64_t t0 = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (uint64_t j = t0; j < nk; j += stride) {
+    const uint32_t kid = kids[j];
+    if (!fin[kid]) ckids[pref[j]] = kid;
+  }
+  for (uint64_t v = t0; v <= n; v += stride) {
+    ckoff[v] = pref[koff[v]];
+    if (v < n) cparent[v] = fin[v] ? INVALID : parent[v];
+  }
+}
+
+// ---- packing events with lazily computed residuals ------------------------------------
+// R(a) = cb(a) when forwardPartition's ascending pass reaches a = S(a) minus the weight
+// removed by every earlier packing at a or below a.  A packing event e at node v_e
+// removes delta_e from v_e and its ancestors: a is hit iff v_e == a or tD(v_e) lies in
+// a's tour interval.  Events are few (one per packing node), so R is evaluated on the
+// fly from the event list instead of being pushed up the (10^6-deep) ancestor chains.
+struct PackEv {
+  uint32_t v, vpos;   // packed node, tD(v) (INVALID for a root)
+  uint64_t delta;     // weight its packing removed
+};
+constexpr int EV_LDS = 2048;
+
+// a's tour interval in the core: [tD, tU] for a non-root, its kids' span for a core root
+__device__ __forceinline__ void node_interval(uint32_t a, const uint32_t *cparent, const uint32_t *ckoff,
+                                              const uint32_t *tD, const uint32_t *tU, const uint32_t *rst,
+                                              const uint32_t *ren, uint32_t &lo, uint32_t &hi) {
+  if (cparent[a] != INVALID) { lo = tD[a]; hi = tU[a]; }
+  else if (ckoff[a] < ckoff[a + 1]) { lo = rst[a]; hi = ren[a]; }
+  else { lo = INVALID; hi = INVALID; }
+}
+__device__ __forceinline__ uint64_t lazy_r(uint32_t a, uint64_t r, uint32_t lo, uint32_t hi, const PackEv *ev,
+                                           uint32_t nev) {
+  for (uint32_t e = 0; e < nev; ++e) {
+    const PackEv x = ev[e];
+    if (x.v == a || (lo != INVALID && x.vpos != INVALID && lo <= x.vpos && x.vpos <= hi)) r -= x.delta;
+  }
+  return r;
+}
+
+// The next packing node: the lowest-index heavy node after the last packing node whose
+// residual exceeds max_component.  Workgroups take 2048-entry chunks in index order and
+// stop once a hit below their chunk is known, so an event reads about the distance to
+// the next packing node instead of the whole heavy set.  Block 0 also stores the last
+// event's delta (computed by the host) into the device event list.
+constexpr int EVI = 8, EV_CH = BLOCK * EVI;
+__global__ __launch_bounds__(BLOCK) void k_next_event(const uint32_t *__restrict__ hids, uint64_t nh,
+                                                      const uint64_t *__restrict__ S, const uint32_t *__restrict__ hst,
+                                                      const uint32_t *__restrict__ hen, PackEv *__restrict__ evl,
+                                                      uint32_t nev, uint64_t last_delta, uint64_t maxc,
+                                                      const uint64_t *__restrict__ evprev,
+                                                      unsigned long long *__restrict__ found) {
+  __shared__ PackEv sev[EV_LDS];
+  __shared__ unsigned long long s_best[BLOCK / WAVE];
+  if (nev && blockIdx.x == 0 && threadIdx.x == 0) evl[nev - 1].delta = last_delta;
+  const uint32_t nl = nev < EV_LDS ? nev : EV_LDS;
+  for (uint32_t e = threadIdx.x; e < nl; e += BLOCK) {
+    PackEv x = evl[e];
+    if (e == nev - 1) x.delta = last_delta;
+    sev[e] = x;
+  }
+  __syncthreads();
+  const uint64_t prev = *evprev;
+  const uint64_t start = prev == ~0ull ? 0 : (uint32_t)prev;
+  const uint32_t vlast = prev == ~0ull ? INVALID : (uint32_t)(prev >> 32);
+  for (uint64_t ch = blockIdx.x;; ch += gridDim.x) {
+    const uint64_t base = start + ch * EV_CH;
+    if (base >= nh) break;
+    const unsigned long long f = __hip_atomic_load(found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (f != ~0ull && (uint32_t)f < base) break;   // a hit below this chunk is known
+    unsigned long long best = ~0ull;
+#pragma unroll
+    for (int j = 0; j < EVI; ++j) {
+      const uint64_t h = base + (uint64_t)j * BLOCK + threadIdx.x;
+      if (h >= nh) continue;
+      const uint32_t a = hids[h];
+      if (vlast != INVALID && a <= vlast) continue;
+      uint64_t r = S[a];
+      const uint32_t lo = hst[h], hi = hen[h];
+      for (uint32_t e = 0; e < nev && r > maxc; ++e) {
+        const PackEv x = e < EV_LDS ? sev[e] : evl[e];
+        const uint64_t d = e == nev - 1 ? last_delta : x.delta;
+        if (x.v == a || (lo != INVALID && x.vpos != INVALID && lo <= x.vpos && x.vpos <= hi)) r -= d;
+      }
+      if (r > maxc) {
+        const unsigned long long key = ((unsigned long long)a << 32) | h;
+        best = key < best ? key : best;
+      }
+    }
+    best = wave_min(best);
+    if ((threadIdx.x & 63) == 0) s_best[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long b = s_best[0];
+      for (int w = 1; w < BLOCK / WAVE; ++w) b = s_best[w] < b ? s_best[w] : b;
+      if (b != ~0ull) atomicMin(found, b);
+    }
+    __syncthreads();
+  }
 }
 
 // Everything the host needs for one packing event, stored straight into mapped host
-// memory: hdr = {v, koff[v], #kids, tD(v) (INVALID for a root), R[v] lo, R[v] hi}, then
-// the node's kids in their current order and their R (the first `cap` of them).
+// memory: hdr = {v, koff[v], #kids, R[v] lo, R[v] hi}, then the node's kids in their
+// current order and their residuals (the first `cap` of them).  The event is appended
+// to the device list (delta filled in by the next k_next_event).
 constexpr uint32_t EV_STAGE = 1u << 16;
-__global__ __launch_bounds__(BLOCK) void k_event_stage(const uint64_t *__restrict__ ev, uint64_t *__restrict__ prev,
-                                                       const uint32_t *__restrict__ koff,
-                                                       const uint32_t *__restrict__ parent, const uint32_t *__restrict__ tD,
-                                                       const uint32_t *__restrict__ kids, const uint64_t *__restrict__ R,
-                                                       uint32_t *__restrict__ hdr, uint32_t *__restrict__ kid_out,
-                                                       uint64_t *__restrict__ r_out, uint32_t cap) {
-  const uint64_t e = *ev;
+__global__ __launch_bounds__(BLOCK) void k_event_stage(const unsigned long long *__restrict__ found,
+                                                       uint64_t *__restrict__ evprev, PackEv *__restrict__ evl,
+                                                       uint32_t nev, const uint32_t *__restrict__ koff,
+                                                       const uint32_t *__restrict__ kids, const uint64_t *__restrict__ S,
+                                                       const uint32_t *__restrict__ cparent,
+                                                       const uint32_t *__restrict__ ckoff, const uint32_t *__restrict__ tD,
+                                                       const uint32_t *__restrict__ tU, const uint32_t *__restrict__ rst,
+                                                       const uint32_t *__restrict__ ren, uint32_t *__restrict__ hdr,
+                                                       uint32_t *__restrict__ kid_out, uint64_t *__restrict__ r_out,
+                                                       uint32_t beg_j, uint32_t cap) {
+  const uint64_t e = *found;
   const uint32_t v = e == ~0ull ? INVALID : (uint32_t)(e >> 32);
   if (v == INVALID) {
     if (blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = INVALID;
     return;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) *prev = e;
   const uint32_t beg = koff[v], cnt = koff[v + 1] - beg;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    const uint64_t r = R[v];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && beg_j == 0) {
+    *evprev = e;
+    uint32_t lo, hi;
+    node_interval(v, cparent, ckoff, tD, tU, rst, ren, lo, hi);
+    const uint64_t r = lazy_r(v, S[v], lo, hi, evl, nev);
+    PackEv x;
+    x.v = v;
+    x.vpos = cparent[v] == INVALID ? INVALID : tD[v];
+    x.delta = 0;
+    evl[nev] = x;
     hdr[0] = v;
     hdr[1] = beg;
     hdr[2] = cnt;
-    hdr[3] = parent[v] == INVALID ? INVALID : tD[v];
-    hdr[4] = (uint32_t)r;
-    hdr[5] = (uint32_t)(r >> 32);
+    hdr[3] = (uint32_t)r;
+    hdr[4] = (uint32_t)(r >> 32);
   }
-  const uint32_t lim = cnt < cap ? cnt : cap;
+  const uint32_t lim = cnt - beg_j < cap ? cnt - beg_j : cap;
   for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < lim; j += gridDim.x * BLOCK) {
-    const uint32_t kid = kids[beg + j];
+    const uint32_t kid = kids[beg + beg_j + j];
+    uint32_t lo, hi;
+    node_interval(kid, cparent, ckoff, tD, tU, rst, ren, lo, hi);
     kid_out[j] = kid;
-    r_out[j] = R[kid];
+    r_out[j] = lazy_r(kid, S[kid], lo, hi, evl, nev);
   }
 }
 
@@ -262,15 +404,39 @@ __global__ void k_scatter_u32(const uint32_t *__restrict__ pos, const uint32_t *
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) out[pos[i]] = val[i];
 }
 
-__global__ void k_kid_r(const uint32_t *__restrict__ kids, uint32_t beg, uint32_t cnt, const uint64_t *__restrict__ R,
-                        uint64_t *__restrict__ out) {
-  for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < cnt; j += gridDim.x * BLOCK) out[j] = R[kids[beg + j]];
+// every root's final residual (after all events)
+__global__ void k_roots_r(const uint32_t *__restrict__ ids, uint64_t m, const uint64_t *__restrict__ S,
+                          const uint32_t *__restrict__ cparent, const uint32_t *__restrict__ ckoff,
+                          const uint32_t *__restrict__ tD, const uint32_t *__restrict__ tU,
+                          const uint32_t *__restrict__ rst, const uint32_t *__restrict__ ren,
+                          const PackEv *__restrict__ evl, uint32_t nev, uint64_t *__restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) {
+    const uint32_t a = ids[i];
+    uint32_t lo, hi;
+    node_interval(a, cparent, ckoff, tD, tU, rst, ren, lo, hi);
+    out[i] = lazy_r(a, S[a], lo, hi, evl, nev);
+  }
 }
 
-__global__ void k_gather_r(const uint32_t *__restrict__ ids, uint64_t m, const uint64_t *__restrict__ R,
-                           uint64_t *__restrict__ out) {
+// push-down for the raked fringe: a finished node takes the part of its nearest
+// ancestor-or-self that has one (an assigned kid or the core node its chain reaches;
+// chains of finished ancestors are at most RAKE_ROUNDS long)
+__global__ void k_push_fringe(const uint32_t *__restrict__ parent, const uint8_t *__restrict__ fin, uint64_t n,
+                              int16_t *__restrict__ parts, unsigned long long *__restrict__ err) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) out[i] = R[ids[i]];
+  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride) {
+    if (!fin[v] || parts[v] != SHEEP_INVALID_PART) continue;
+    uint32_t u = (uint32_t)v;
+    int16_t p = SHEEP_INVALID_PART;
+    for (int d = 0; d <= RAKE_ROUNDS + 1 && u != INVALID; ++d) {
+      p = parts[u];
+      if (p != SHEEP_INVALID_PART) break;
+      u = parent[u];
+    }
+    if (p == SHEEP_INVALID_PART) atomicAdd(err, 1ull);
+    else parts[v] = p;
+  }
 }
 
 // ---- facts ---------------------------------------------------------------------------
@@ -366,11 +532,12 @@ uint64_t compact_pred(Ctx &c, int which, const uint64_t *S, uint64_t mx, const u
 
 void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
 
-void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t *seq, uint64_t pos_size,
+void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t *seq, uint64_t seq_n, uint64_t pos_size,
                     sheep_kids *k, int16_t np, double balance, int vtx, int pstw, int16_t *parts_vid,
                     sheep_partition_info *info) {
   if (np <= 0) throw Error(SHEEP_ERR_ARG, "number of parts must be positive");
   if (!k || k->n != n) throw Error(SHEEP_ERR_ARG, "kid table does not belong to this tree");
+  if (seq_n > n) throw Error(SHEEP_ERR_RANGE, "vector::_M_range_check: the sequence is longer than the tree (partition.cpp:65 parts.at)");
   *info = sheep_partition_info();
   if (pos_size) {
     hipLaunchKernelGGL(k_fill_i16, dim3(grid_for(pos_size)), dim3(BLOCK), 0, c.stream, parts_vid, pos_size,
@@ -386,60 +553,91 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   HIP_CHECK(hipMemsetAsync(d, 0, 4 * sizeof(uint64_t), c.stream));
   hipLaunchKernelGGL(k_weights, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, tree, n, vtx, pstw, w, d);
   LAUNCH_CHECK();
-
-  // 2. Euler tour + subtree sums
-  Tour t;
-  build_tour(c, k, t);
   d2h(c, c.h_scalars + 32, c.d_scalars + 32, 1);
   c.sync();
   const uint64_t total = c.h_scalars[32];
   const uint64_t max_component = (uint64_t)((double)(total / (uint64_t)(int64_t)np) * balance);
   info->total_weight = total;
   info->max_component = max_component;
-  uint64_t *S = c.get_as<uint64_t>("pt_S", n);
-  uint32_t *rst = c.get_as<uint32_t>("pt_rst", n), *ren = c.get_as<uint32_t>("pt_ren", n);
-  if (t.nrk) {
-    hipLaunchKernelGGL(k_root_intervals, dim3(grid_for(t.nrk)), dim3(BLOCK), 0, c.stream, t.rk, t.nrk, k->koff,
-                       k->kids, t.tD, t.tU, rst, ren);
+
+  // 2. rake the light fringe (exact subtree sums), then the core T' as its own forest
+  uint64_t *S = c.get_as<uint64_t>("pt_S", n);   // the rake's acc, then every node's subtree sum
+  uint32_t *pend = c.get_as<uint32_t>("pt_pend", n);
+  uint8_t *fin = c.get_as<uint8_t>("pt_fin", n);
+  hipLaunchKernelGGL(k_rake_init, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->koff,
+                     (const uint64_t *)w, n, pend, S, fin);
+  LAUNCH_CHECK();
+  for (int r = 1; r <= RAKE_ROUNDS; ++r) {
+    hipLaunchKernelGGL(k_rake_mark, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)pend,
+                       (const uint64_t *)S, n, max_component, (uint8_t)r, fin);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_rake_push, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->parent,
+                       (const uint8_t *)fin, n, (uint8_t)r, S, pend);
     LAUNCH_CHECK();
   }
-  if (t.A) {
+  sheep_kids core;
+  core.ctx = &c;
+  core.n = n;
+  core.parent = c.get_as<uint32_t>("pt_cparent", n);
+  core.koff = c.get_as<uint32_t>("pt_ckoff", n + 1);
+  core.kids = c.get_as<uint32_t>("pt_ckids", k->nkids + 1);
+  {
+    uint32_t *pref = c.get_as<uint32_t>("pt_cpref", k->nkids + 1);
+    uint32_t *tot = (uint32_t *)(c.d_scalars + 31);
+    if (k->nkids) {
+      hipLaunchKernelGGL(k_core_flags, dim3(grid_for(k->nkids)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->kids,
+                         k->nkids, (const uint8_t *)fin, pref);
+      LAUNCH_CHECK();
+    }
+    HIP_CHECK(hipMemsetAsync(pref + k->nkids, 0, sizeof(uint32_t), c.stream));
+    scan_exclusive_u32(c, pref, pref, k->nkids + 1, tot);
+    hipLaunchKernelGGL(k_core_build, dim3(grid_for(n + 1)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->kids,
+                       k->nkids, (const uint32_t *)k->koff, (const uint32_t *)k->parent, (const uint8_t *)fin, n,
+                       (const uint32_t *)pref, core.kids, core.koff, core.parent);
+    LAUNCH_CHECK();
+    d2h(c, c.h_scalars + 31, c.d_scalars + 31, 1);
+    c.sync();
+    core.nkids = (uint32_t)c.h_scalars[31];
+  }
+  Tour t;
+  build_tour(c, &core, t);
+  uint32_t *rst = c.get_as<uint32_t>("pt_rst", n), *ren = c.get_as<uint32_t>("pt_ren", n);
+  if (t.nrk) {
+    hipLaunchKernelGGL(k_root_intervals, dim3(grid_for(t.nrk)), dim3(BLOCK), 0, c.stream, t.rk, t.nrk, core.koff,
+                       core.kids, t.tD, t.tU, rst, ren);
+    LAUNCH_CHECK();
+  }
+  if (t.A) {   // core subtree sums over the tour, the raked acc as node weights
     uint64_t *val = c.get_as<uint64_t>("pt_tourval", t.A);
-    hipLaunchKernelGGL(k_tour_vals, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, t.tD, t.tU, n, (const uint64_t *)w,
+    hipLaunchKernelGGL(k_tour_vals, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, t.tD, t.tU, n, (const uint64_t *)S,
                        (const uint64_t *)nullptr, 0, val);
     LAUNCH_CHECK();
     scan_exclusive_u64(c, val, val, t.A, nullptr);
-    hipLaunchKernelGGL(k_subtree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, k->parent, t.tD, t.tU, n,
-                       (const uint64_t *)w, (const uint64_t *)val, S);
+    uint64_t *S2 = c.get_as<uint64_t>("pt_S2", n);
+    hipLaunchKernelGGL(k_subtree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, core.parent, t.tD, t.tU, n,
+                       (const uint64_t *)S, (const uint64_t *)val, S2);
     LAUNCH_CHECK();
-  } else {
-    HIP_CHECK(hipMemcpyAsync(S, w, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, c.stream));
+    hipLaunchKernelGGL(k_root_sums, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, core.parent, n, S2);
+    LAUNCH_CHECK();
+    S = S2;
   }
-  hipLaunchKernelGGL(k_root_sums, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, k->parent, n, S);
-  LAUNCH_CHECK();
 
-  // 3. packing events (partition.cpp:97-135).  R(v) = cb(v) when the ascending pass
-  // reaches v = S(v) minus what packings below v removed.  Ascending order means the
-  // next packing node is the LOWEST id with R > max: every node below it already has
-  // its final cb.  Only H = {v : S(v) > max} (ancestor-closed, R <= S) can pack, so each
-  // event is one pass over H: subtract the last packing's removed weight from the
-  // packed node and its ancestors (tour-interval test), then atomicMin the next id
-  // with R > max.  The host runs the packing itself with the reference's own
-  // std::sort on the node's current kid order and first-fit (order persists across k).
-  uint64_t *R = c.get_as<uint64_t>("pt_R", n);
-  HIP_CHECK(hipMemcpyAsync(R, S, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, c.stream));
+  // 3. packing events (partition.cpp:97-135).  Only H = {v : S(v) > max} (ancestor-
+  // closed, in the core) can pack; the next packing node is the LOWEST id whose residual
+  // exceeds max — every node below it already has its final cb.  The host runs each
+  // packing with the reference's own std::sort on the node's current kid order and
+  // first-fit (the order persists across k).
   uint32_t *hids = c.get_as<uint32_t>("pt_hids", n);
-  const uint64_t nh = compact_pred(c, 0, S, max_component, k->parent, n, hids, nullptr, "h");
+  const uint64_t nh = compact_pred(c, 0, S, max_component, core.parent, n, hids, nullptr, "h");
   info->heavy_nodes = nh;
   uint32_t *hst = c.get_as<uint32_t>("pt_hst", nh ? nh : 1), *hen = c.get_as<uint32_t>("pt_hen", nh ? nh : 1);
   if (nh) {
-    hipLaunchKernelGGL(k_intervals, dim3(grid_for(nh)), dim3(BLOCK), 0, c.stream, hids, nh, k->parent, k->koff,
+    hipLaunchKernelGGL(k_intervals, dim3(grid_for(nh)), dim3(BLOCK), 0, c.stream, hids, nh, core.parent, core.koff,
                        (const uint32_t *)rst, (const uint32_t *)ren, t.tD, t.tU, hst, hen);
     LAUNCH_CHECK();
   }
-  // ev = (next packing node << 32) | its index in hids (~0: none); evprev = the last one.
-  // One stream sync per event.
-  unsigned long long *ev = (unsigned long long *)(c.d_scalars + 44);
+  PackEv *evl = c.get_as<PackEv>("pt_events", nh + 1);
+  unsigned long long *found = (unsigned long long *)(c.d_scalars + 44);
   uint64_t *evprev = c.d_scalars + 46;
   HIP_CHECK(hipMemsetAsync(evprev, 0xFF, sizeof(uint64_t), c.stream));
   uint8_t *stage = (uint8_t *)c.get_pinned("pt_event", 64 + (size_t)EV_STAGE * 12);
@@ -456,41 +654,46 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   std::vector<uint32_t> seg, order, sorted, upl_pos, upl_ids;
   std::vector<uint64_t> segR, scb;
   std::vector<char> done;
-  uint32_t v = INVALID, vpos = INVALID;
+  uint32_t nev = 0;
   uint64_t delta = 0;
+  const unsigned gev = nh ? (unsigned)std::min<uint64_t>((nh + EV_CH - 1) / EV_CH, 256) : 1;
+  auto stage_event = [&](uint32_t beg_j, uint32_t cap, uint32_t *o_kids, uint64_t *o_r) {
+    hipLaunchKernelGGL(k_event_stage, dim3(64), dim3(BLOCK), 0, c.stream, (const unsigned long long *)found, evprev, evl,
+                       nev, (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
+                       (const uint32_t *)core.parent, (const uint32_t *)core.koff, (const uint32_t *)t.tD,
+                       (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren, d_hdr, o_kids, o_r, beg_j,
+                       cap);
+    LAUNCH_CHECK();
+  };
   {
     TimedRegion tr(c, "partition_events");
     for (;;) {
-      HIP_CHECK(hipMemsetAsync(ev, 0xFF, sizeof(uint64_t), c.stream));
+      HIP_CHECK(hipMemsetAsync(found, 0xFF, sizeof(uint64_t), c.stream));
       if (nh) {
-        hipLaunchKernelGGL(k_pack_event, dim3(grid_for(nh)), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh,
-                           (const uint32_t *)hst, (const uint32_t *)hen, R, v, vpos, delta, max_component,
-                           (const uint64_t *)evprev, ev);
+        hipLaunchKernelGGL(k_next_event, dim3(gev), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh,
+                           (const uint64_t *)S, (const uint32_t *)hst, (const uint32_t *)hen, evl, nev, delta,
+                           max_component, (const uint64_t *)evprev, found);
         LAUNCH_CHECK();
       }
-      hipLaunchKernelGGL(k_event_stage, dim3(64), dim3(BLOCK), 0, c.stream, (const uint64_t *)ev, evprev, k->koff,
-                         k->parent,
-                         t.tD, (const uint32_t *)k->kids, (const uint64_t *)R, d_hdr, d_kids, d_r, EV_STAGE);
-      LAUNCH_CHECK();
+      stage_event(0, EV_STAGE, d_kids, d_r);
       c.sync();
-      v = hdr[0];
+      const uint32_t v = hdr[0];
       if (v == INVALID) break;
       info->packing_nodes++;
       const uint32_t beg = hdr[1], cnt = hdr[2];
-      vpos = hdr[3];
-      uint64_t cb = (uint64_t)hdr[4] | ((uint64_t)hdr[5] << 32);
+      uint64_t cb = (uint64_t)hdr[3] | ((uint64_t)hdr[4] << 32);
       seg.assign(st_kids, st_kids + std::min(cnt, EV_STAGE));
       segR.assign(st_r, st_r + std::min(cnt, EV_STAGE));
       if (cnt > EV_STAGE) {   // a node with more kids than the staging area: fetch the rest
         seg.resize(cnt); segR.resize(cnt);
+        uint32_t *kk = c.get_as<uint32_t>("pt_kK", cnt);
         uint64_t *kR = c.get_as<uint64_t>("pt_kR", cnt);
-        hipLaunchKernelGGL(k_kid_r, dim3(grid_for(cnt)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->kids, beg, cnt,
-                           (const uint64_t *)R, kR);
-        LAUNCH_CHECK();
-        d2h(c, seg.data() + EV_STAGE, (const uint32_t *)k->kids + beg + EV_STAGE, cnt - EV_STAGE);
-        d2h(c, segR.data() + EV_STAGE, (const uint64_t *)kR + EV_STAGE, cnt - EV_STAGE);
+        stage_event(EV_STAGE, cnt - EV_STAGE, kk, kR);
+        d2h(c, seg.data() + EV_STAGE, (const uint32_t *)kk, cnt - EV_STAGE);
+        d2h(c, segR.data() + EV_STAGE, (const uint64_t *)kR, cnt - EV_STAGE);
         c.sync();
       }
+      ++nev;   // the event k_event_stage appended
       const uint64_t cb0 = cb;
       // std::sort on the current kid order with the reference comparator (:104-106);
       // sorting positions with a comparator on their keys is the same sort.
@@ -538,7 +741,6 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
     hipLaunchKernelGGL(k_scatter_u32, dim3(grid_for(mu)), dim3(BLOCK), 0, c.stream, (const uint32_t *)dp,
                        (const uint32_t *)dv, mu, k->kids);
     LAUNCH_CHECK();
-    c.sync();   // the host vectors die with this call
   }
   // roots (ascending) with their final cb
   uint32_t *rids = c.get_as<uint32_t>("pt_roots", n);
@@ -547,13 +749,15 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   std::vector<uint64_t> r_cb(nroots);
   if (nroots) {
     uint64_t *rR = c.get_as<uint64_t>("pt_rR", nroots);
-    hipLaunchKernelGGL(k_gather_r, dim3(grid_for(nroots)), dim3(BLOCK), 0, c.stream, (const uint32_t *)rids, nroots,
-                       (const uint64_t *)R, rR);
+    hipLaunchKernelGGL(k_roots_r, dim3(grid_for(nroots)), dim3(BLOCK), 0, c.stream, (const uint32_t *)rids, nroots,
+                       (const uint64_t *)S, (const uint32_t *)core.parent, (const uint32_t *)core.koff,
+                       (const uint32_t *)t.tD, (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren,
+                       (const PackEv *)evl, nev, rR);
     LAUNCH_CHECK();
     d2h(c, r_ids.data(), (const uint32_t *)rids, nroots);
     d2h(c, r_cb.data(), (const uint64_t *)rR, nroots);
-    c.sync();
   }
+  c.sync();   // the kid-order upload vectors die with this call
 
   // 4. descending pass: roots into the highest bin that fits (:146-152)
   std::vector<int16_t> root_part(nroots);
@@ -571,15 +775,19 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
     }
     root_part[ri] = got;
   }
-  info->created = (int32_t)part_size.size();
 
-  // 6. push down: assigned = packed kids + roots, as laminar tour intervals
+  // 5. push down: assigned = packed kids + roots; core nodes through the laminar tour
+  // intervals of the assigned core nodes, then the fringe up its short parent chains
+  HIP_CHECK(hipMemsetAsync(c.d_scalars + 36, 0, 4 * sizeof(uint64_t), c.stream));   // push-down error, print counts
   const uint64_t na = asg_ids.size() + nroots;
   std::vector<uint32_t> all_ids(asg_ids);
   all_ids.insert(all_ids.end(), r_ids.begin(), r_ids.end());
   std::vector<int16_t> all_part(asg_part);
   all_part.insert(all_part.end(), root_part.begin(), root_part.end());
   int16_t *parts = c.get_as<int16_t>("pt_parts", n);
+  unsigned long long *e = (unsigned long long *)c.d_scalars + 36;
+  hipLaunchKernelGGL(k_fill_i16, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parts, n, SHEEP_INVALID_PART);
+  LAUNCH_CHECK();
   {
     uint32_t *aid = c.get_as<uint32_t>("pt_aid", na);
     int16_t *ap = c.get_as<int16_t>("pt_ap", na);
@@ -588,7 +796,7 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
     hipLaunchKernelGGL(k_scatter_parts, dim3(grid_for(na)), dim3(BLOCK), 0, c.stream, aid, ap, na, parts);
     LAUNCH_CHECK();
     uint32_t *st = c.get_as<uint32_t>("pt_ast", na), *en = c.get_as<uint32_t>("pt_aen", na);
-    hipLaunchKernelGGL(k_intervals, dim3(grid_for(na)), dim3(BLOCK), 0, c.stream, aid, na, k->parent, k->koff,
+    hipLaunchKernelGGL(k_intervals, dim3(grid_for(na)), dim3(BLOCK), 0, c.stream, aid, na, core.parent, core.koff,
                        (const uint32_t *)rst, (const uint32_t *)ren, t.tD, t.tU, st, en);
     LAUNCH_CHECK();
     std::vector<uint32_t> hs(na), he(na);
@@ -619,25 +827,27 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
       h2d(c, den, sen.data(), m);
       h2d(c, dencl, encl.data(), m);
       h2d(c, dsp, sp.data(), m);
-      unsigned long long *e = (unsigned long long *)c.d_scalars + 36;
-      HIP_CHECK(hipMemsetAsync(e, 0, sizeof(uint64_t), c.stream));
-      hipLaunchKernelGGL(k_push_down, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, k->parent, t.tD, n, dst_, den, dsp,
+      hipLaunchKernelGGL(k_push_down, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, core.parent, t.tD, n, dst_, den, dsp,
                          dencl, m, parts, e);
       LAUNCH_CHECK();
-      d2h(c, c.h_scalars + 36, c.d_scalars + 36, 1);
-      c.sync();   // the staged host vectors die with this block
     }
+    hipLaunchKernelGGL(k_push_fringe, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->parent,
+                       (const uint8_t *)fin, n, parts, e);
+    LAUNCH_CHECK();
+    c.sync();   // the staged host vectors die with this block
   }
-  // 7. jnid -> vid (:62-66) and print counts (partition.h:138-139)
-  unsigned long long *cnt = (unsigned long long *)c.d_scalars + 38;
-  HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(uint64_t), c.stream));
-  hipLaunchKernelGGL(k_parts_to_vid, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, seq, n, parts, parts_vid, cnt);
-  LAUNCH_CHECK();
-  d2h(c, c.h_scalars + 38, c.d_scalars + 38, 2);
+  // 6. jnid -> vid (:62-66) and print counts (partition.h:138-139)
+  unsigned long long *cnt = (unsigned long long *)c.d_scalars + 37;
+  if (seq_n) {
+    hipLaunchKernelGGL(k_parts_to_vid, dim3(grid_for(seq_n)), dim3(BLOCK), 0, c.stream, seq, seq_n, parts, parts_vid, cnt);
+    LAUNCH_CHECK();
+  }
+  d2h(c, c.h_scalars + 36, c.d_scalars + 36, 4);
   c.sync();
-  if (asg_ids.size() + nroots && c.h_scalars[36]) throw Error(SHEEP_ERR_HIP, "partition push-down: unassigned node");
-  info->first_size = c.h_scalars[38];
-  info->second_size = c.h_scalars[39];
+  if (c.h_scalars[36]) throw Error(SHEEP_ERR_HIP, "partition push-down: unassigned node");
+  info->first_size = c.h_scalars[37];
+  info->second_size = c.h_scalars[38];
+  info->created = (int32_t)c.h_scalars[39];   // max part + 1 over the vid-indexed vector
 }
 
 void tree_facts(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_facts_t *out) {

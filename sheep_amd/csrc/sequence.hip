@@ -125,8 +125,6 @@ void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v) {
   LAUNCH_CHECK();
 }
 
-static const bool g_split_degree = getenv("SHEEP_SPLIT_DEGREE") != nullptr;   // A/B: k_degree + separate head count
-
 void degree_count(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap,
                   uint64_t *max_slot) {
   if (mode < 0 || mode > 2) throw Error(SHEEP_ERR_ARG, "bad degree mode");
@@ -135,7 +133,7 @@ void degree_count(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_
   bool counted = false;   // heads' (bucket, tile) counts made by the same pass (hist.hip)
   if (nrec) {
     TimedRegion tr(c, "degree", 12 * nrec);   // one read of the 12-B records
-    counted = !g_split_degree && degree_fused(c, rec, nrec, mode, deg, cap, d, d + 1);
+    counted = degree_fused(c, rec, nrec, mode, deg, cap, d, d + 1);
     if (!counted) {
       hipLaunchKernelGGL(k_degree, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, mode, deg, cap, d, d + 1);
       LAUNCH_CHECK();

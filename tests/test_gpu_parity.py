@@ -266,3 +266,83 @@ def test_tree_above_2e27_nodes(gpu_ctx):
     del d
     op, ow = oracle.build_tree(t_, h_, seq)
     assert np.array_equal(p, op) and np.array_equal(w, ow)
+
+
+@pytest.mark.parametrize("what", [0, 1, 2, 4, 6])
+def test_evaluate_masks_and_shards(gpu_ctx, what):
+    """sheep_evaluate computes only the metrics its mask asks for (the others come back 0),
+    and the sharded evaluator (shards ORed into one state, or two states combined as
+    another device's would be) gives the same counts as one call over all records."""
+    import sheep_amd
+    d = sheep_amd.rmat(16, 16, 9)
+    h = sheep_amd.to_numpy_u32(d).reshape(-1, 3)
+    s = sheep_amd.degree_sequence(d)
+    tree = sheep_amd.build_tree(d, s)
+    res = sheep_amd.partition(s, tree, 100)
+    full = oracle.evaluate(h[:, 0], h[:, 1], s.numpy(), res.numpy())
+    ev = sheep_amd.evaluate(d, s, res.parts, what=what)
+    m = what or 7
+    keep = {"edges", "nodes"}
+    if m & 1:
+        keep |= {"edges_cut", "vcom_vol", "max_vertex_bal", "ecv_hash", "max_hash_bal"}
+    if m & 2:
+        keep |= {"ecv_down", "max_down_bal"}
+    if m & 4:
+        keep |= {"ecv_up", "max_up_bal"}
+    assert ev.__dict__ == {k: (v if k in keep else 0) for k, v in full.items()}
+    R = d.shape[0]
+    a = sheep_amd.ShardedEvaluator(s, res.parts, what)
+    b = sheep_amd.ShardedEvaluator(s, res.parts, what, nparts=a.nparts)
+    for i in range(5):
+        (a if i % 2 else b).add(d[i * R // 5:(i + 1) * R // 5])
+    a.combine(b.bits, b.acc)
+    assert a.finish() == ev
+
+
+def test_evaluate_wide_parts(gpu_ctx):
+    """More than 64 parts (several bitset words per vertex), against the oracle."""
+    import sheep_amd
+    d = sheep_amd.rmat(15, 16, 4)
+    h = sheep_amd.to_numpy_u32(d).reshape(-1, 3)
+    s = sheep_amd.degree_sequence(d)
+    tree = sheep_amd.build_tree(d, s)
+    res = sheep_amd.partition(s, tree, 300)
+    assert res.created > 128
+    assert sheep_amd.evaluate(d, s, res.parts).__dict__ == oracle.evaluate(h[:, 0], h[:, 1], s.numpy(), res.numpy())
+
+
+def test_partition_sequence_length(gpu_ctx):
+    """Partition(seq, jnodes, k) (partition.cpp:62-66): a sequence longer than the tree is
+    the reference's parts.at() throw; a shorter one converts only its own entries, and
+    the printed counts come from the vid-indexed vector (partition.h:135-143)."""
+    import sheep_amd
+    seq = golden_seq("hep")
+    p, w = golden_tree("hep")
+    tree = sheep_amd.tree_to_device(p, w)
+    longer = sheep_amd.sequence_from_host(np.append(seq, np.uint32(seq.max() + 1)))
+    with pytest.raises(IndexError):
+        sheep_amd.partition(longer, tree, 4)
+    short = seq[:-100]
+    res = sheep_amd.partition(sheep_amd.sequence_from_host(short), tree, 4)
+    oparts, oinfo = oracle.partition(p, w, short, 4)
+    assert np.array_equal(res.numpy(), oparts)
+    assert res.created == oinfo["created"]
+    assert res.first_size == np.count_nonzero(oparts == 0) and res.second_size == np.count_nonzero(oparts == 1)
+
+
+def test_context_on_another_device(gpu_ctx):
+    """Calls run on the context's device whatever device the calling thread has current."""
+    import torch
+    import sheep_amd
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one HIP device")
+    ctx1 = sheep_amd.Context(1)
+    torch.cuda.set_device(0)
+    with torch.cuda.device(1):
+        d = sheep_amd.rmat(12, 16, 12, ctx=ctx1)
+        deg = torch.zeros(1 << 12, dtype=torch.int32, device="cuda:1")
+    torch.cuda.set_device(0)
+    _, vs = sheep_amd.degree_count(d, deg=deg, ctx=ctx1)
+    s = sheep_amd.sequence_from_degrees(deg, vs, ctx=ctx1)
+    h = sheep_amd.to_numpy_u32(d).reshape(-1, 3)
+    assert np.array_equal(s.numpy(), oracle.sequence(h[:, 0], h[:, 1]))

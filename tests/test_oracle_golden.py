@@ -106,3 +106,46 @@ def test_hep_cost_table():
         parts, _ = oracle.partition(p, w, seq, k, kids=kids)
         assert oracle.evaluate(r["tail"], r["head"], seq, parts)["ecv_down"] == down, f"k={k}"
     assert len(rows) >= 29
+
+
+@pytest.mark.parametrize("name", GRAPHS)
+def test_threaded_oracle_matches_golden(name):
+    """The OpenMP graph build / evaluators (used for the BASELINE-size parity checks)
+    give the single-threaded results: sequences (both LLAMA forms), tree, every
+    evaluator line."""
+    r = golden_records(name)
+    seq = golden_seq(name)
+    oracle.set_threads(4)
+    try:
+        assert np.array_equal(oracle.sequence(r["tail"], r["head"], "llama"), seq)
+        assert np.array_equal(oracle.sequence(r["tail"], r["head"], "records"), seq)
+        p, w = oracle.build_tree(r["tail"], r["head"], seq)
+        gp, gw = golden_tree(name)
+        assert np.array_equal(p, gp) and np.array_equal(w, gw)
+        _, blocks = golden_part_text(name)
+        kids = oracle.Kids(p)
+        for k, block in zip(ks(name), blocks):
+            parts, info = oracle.partition(p, w, seq, k, kids=kids)
+            ev = oracle.evaluate(r["tail"], r["head"], seq, parts)
+            assert oracle.eval_text(ev, k) in block, f"k={k}"
+    finally:
+        oracle.set_threads(1)
+
+
+def test_partition_sequence_length_semantics():
+    """Partition ctor (partition.cpp:62-66): a sequence longer than the tree throws
+    (parts.at); a shorter one converts only its own entries."""
+    r = golden_records("edge")
+    seq = golden_seq("edge")
+    p, w = golden_tree("edge")
+    longer = np.append(seq, np.uint32(seq.max() + 1))
+    with pytest.raises(RuntimeError, match="range"):
+        oracle.partition(p, w, longer, 2)
+    parts_full, _ = oracle.partition(p, w, seq, 2)
+    short = seq[:-1]
+    parts, info = oracle.partition(p, w, short, 2)
+    vs = int(short.max()) + 1
+    want = np.full(vs, -1, np.int16)
+    want[short] = parts_full[short]
+    assert np.array_equal(parts, want)
+    assert info["created"] == int(want.max()) + 1
