@@ -27,7 +27,7 @@ build/hip/%.o: sheep_amd/csrc/%.hip $(HIPHDR)
 
 $(LIB): $(HIPOBJ)
 	@mkdir -p sheep_amd/lib
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIPOBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIPOBJ) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 cli: $(CLIBIN)
 

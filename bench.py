@@ -8,17 +8,22 @@ One step = the whole hot path over one synthetic graph already resident in HBM:
   -> makeKids + partition_tree forwardPartition (k parts) on rank 0
 
 (reference: graph2tree.cpp:161-216 `-ir` + partition_tree.cpp:130-143).
-Every computation runs in libsheep_hip.so's HIP kernels; the CPU oracle is only timed
-as the `cpu_baseline` leg (rank 0, N=1) on a bounded sample.
+After the timed steps the ECV(down)/balance evaluator (partition.cpp:475-521) is timed
+on its own ("timed and rooflined separately"): on one GPU over all
+records; on N GPUs sharded — parts broadcast (Partition::mpi_sync), per-shard owner
+bitsets, a binomial OR-reduction to rank 0, one node pass.
 
-    python bench.py [--gpus N --steps K --warmup W --scale 26 --ef 16 --k 64]
+Every computation runs in libsheep_hip.so's HIP kernels; the reference's own lib/ code
+(oracle/_ref, built from /root/reference) is only timed as the `cpu_baseline` leg
+(rank 0, N=1) on a bounded sample.
+
+    python bench.py [--gpus N --steps K --warmup W --scale 26 --ef 16 --k 64 --shuffle]
 
 For N > 1 launch with torch.distributed.run (one process per GPU, RCCL over xGMI).
 The graph is fixed as N grows (edge shards of one RMAT graph): "scaling": "strong".
 """
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -27,16 +32,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level table)
-# Leaf regions (one kernel or one fused kernel family per launch); aggregates such as
-# "etree" / "partition" / "sequence" are reported in phases but not rooflined.
-LEAF = ("degree", "degree_heads", "relabel", "pst_group", "etree_split", "etree_union", "etree_cross",
-        "etree_apply", "etree_compact", "evaluate")
-# kernels of a region, for roofline.traffic from the committed PMC passes (tools/pmc_traffic.py);
-# regions whose kernels are shared with other regions (histograms, packs) get traffic null
-REGION_KERNELS = {"relabel": ["k_relabel_scatter", "k_relabel_gather"], "degree": ["k_degree"], "etree_split": ["k_split_count", "k_split_write"],
+# Leaf regions (one kernel family per region, HIP events on the context stream) and the
+# kernels each runs, for roofline.traffic from the committed PMC file (tools/pmc_traffic.py).
+# Algorithmic bytes per region: DESIGN.md §5 (a stated per-region extension of SURVEY
+# §8(d), whose B_alg covers the whole path).  Regions whose kernels are shared with other
+# regions (scans, radix passes) get traffic null.
+LEAF = ("degree", "degree_heads", "sequence", "relabel", "pst_group", "etree_split", "etree_union", "etree_cross",
+        "etree_apply", "merge", "kids", "partition")
+REGION_KERNELS = {"degree": ["k_degree_fused"], "relabel": ["k_relabel_scatter", "k_relabel_gather"],
+                  "etree_split": ["k_split_count", "k_split_write"], "etree_union": ["k_hook_round", "k_hook_finish", "k_light_top"],
                   "etree_cross": ["k_cross_find"], "etree_apply": ["k_cross_apply", "k_level_clean"],
-                  "etree_compact": ["k_compact_edges"], "etree_bucket": ["k_bucket_count", "k_bucket_scatter"]}
-PMC_FILE = os.path.join(ROOT, "profiles", "r1", "pmc_traffic_rmat{scale}.json")
+                  "evaluate": ["k_pp", "k_eval_records", "k_eval_nodes"]}
+PMC_FILE = os.path.join(ROOT, "profiles", "r2", "pmc_traffic_rmat{scale}_k{k}.json")
 
 
 def parse():
@@ -48,7 +55,11 @@ def parse():
     ap.add_argument("--ef", type=int, default=16)
     ap.add_argument("--k", type=int, default=64)
     ap.add_argument("--seed", type=int, default=None, help="RMAT seed (default: the scale, SURVEY §8d)")
+    ap.add_argument("--shuffle", action="store_true",
+                    help="records in a random order, half with tail/head swapped (a generic edge list)")
+    ap.add_argument("--eval-reps", type=int, default=3, help="timed evaluator runs (0: skip)")
     ap.add_argument("--cpu-scale", type=int, default=22, help="RMAT scale of the CPU-baseline sample")
+    ap.add_argument("--cpu-ranks", type=int, default=16, help="MPI ranks of the reference CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo stages the exchanges through host memory (rehearsal)")
@@ -60,6 +71,19 @@ def parse():
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 also builds the whole-graph tree and checks the merged one against it")
     return ap.parse_args()
+
+
+def shuffled(d, seed):
+    """The records in a random order, half of them with tail and head swapped."""
+    import torch
+    g = torch.Generator(device=d.device)
+    g.manual_seed(seed)
+    out = d[torch.randperm(d.shape[0], device=d.device, generator=g)]
+    flip = torch.rand(out.shape[0], device=d.device, generator=g) < 0.5
+    tail = out[:, 0].clone()
+    out[flip, 0] = out[flip, 1]
+    out[flip, 1] = tail[flip]
+    return out
 
 
 def main():
@@ -88,11 +112,15 @@ def main():
 
     ctx = sheep_amd.Context(local)
     rec = sheep_amd.rmat(a.scale, a.ef, seed, ctx=ctx)          # whole graph, identical on every rank
+    if a.shuffle:
+        rec = shuffled(rec, 1000 + seed)
     R = rec.shape[0]
     beg, end = sdist.shard_bounds(R, rank, world)               # contiguous edge shard (graph2tree -l)
-    shard = rec[beg:end]
+    shard = rec[beg:end].contiguous()
+    del rec
+    torch.cuda.empty_cache()
     vs_cap = 1 << a.scale
-    deg = torch.zeros(vs_cap, dtype=torch.int32, device="cuda")
+    deg = torch.zeros(vs_cap, dtype=torch.int32, device=f"cuda:{local}")
 
     def step():
         deg.zero_()
@@ -118,6 +146,13 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    def max_over_ranks(t):
+        if world > 1:
+            tt = torch.tensor([t], dtype=torch.float64, device=f"cuda:{local}" if a.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t = float(tt.item())
+        return t
+
     for _ in range(a.warmup):
         step()
     barrier()
@@ -128,36 +163,29 @@ def main():
     for _ in range(a.steps):
         s, tree, res = step()
     barrier()
-    t = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([t], dtype=torch.float64, device="cuda" if a.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t = float(tt.item())
+    t = max_over_ranks(time.perf_counter() - t0)
 
-    # per-region device timings (HIP events on the context stream)
+    # per-region device timings (HIP events on the context stream), timed steps only
     phases = {}
     for name in ctx.timer_names():
         ms, launches, nbytes = ctx.timer(name)
         phases[name] = {"ms_per_step": round(ms / a.steps, 4), "launches": launches, "alg_bytes": nbytes}
+    ctx.timer_reset()
+
+    evaluator = None
+    if a.eval_reps > 0:
+        evaluator = time_evaluator(a, ctx, shard, s, res, rank, world, local, barrier, max_over_ranks)
     ctx.timing(False)
-    roof = None
-    leaf = [(phases[n]["ms_per_step"], n) for n in LEAF if n in phases and phases[n]["launches"]]
-    if leaf:
-        _, dom = max(leaf)
-        p = phases[dom]
-        ms_launch = p["ms_per_step"] * a.steps / p["launches"]
-        b_launch = p["alg_bytes"] / p["launches"]
-        ach = b_launch / (ms_launch * 1e-3) / 1e9
-        roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                "alg_bytes_per_launch": int(b_launch), "ms_per_launch": round(ms_launch, 4)}
-        roof.update(pmc_traffic(a, dom, p["launches"] / a.steps))
 
     verified = None
     if a.verify and rank == 0:                                  # merged tree == whole-graph tree
-        whole = sheep_amd.build_tree(rec, s, ctx=ctx)
-        verified = bool(torch.equal(whole, tree))
-        del whole
+        if world == 1:
+            verified = True
+        else:
+            whole = sheep_amd.build_tree(sheep_amd.rmat(a.scale, a.ef, seed, ctx=ctx) if not a.shuffle else
+                                         shuffled(sheep_amd.rmat(a.scale, a.ef, seed, ctx=ctx), 1000 + seed), s, ctx=ctx)
+            verified = bool(torch.equal(whole, tree))
+            del whole
         if not verified:
             print("bench: merged tree differs from the whole-graph tree", file=sys.stderr, flush=True)
 
@@ -166,6 +194,21 @@ def main():
         n = s.n
         b_alg = 32 * R + 14 * s.pos_size + 20 * n
         value = R * a.steps / t
+        leaf = [(phases[x]["ms_per_step"], x) for x in LEAF if x in phases and phases[x]["launches"]]
+        roof = None
+        if leaf:
+            _, dom = max(leaf)
+            p = phases[dom]
+            ms_launch = p["ms_per_step"] * a.steps / p["launches"]
+            b_launch = p["alg_bytes"] / p["launches"]
+            ach = b_launch / (ms_launch * 1e-3) / 1e9
+            roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "alg_bytes_per_launch": int(b_launch), "ms_per_launch": round(ms_launch, 4)}
+            roof.update(pmc_region(a, world, dom, p["launches"] / a.steps))
+        path = {"alg_bytes": b_alg, "achieved_GBs": round(b_alg * a.steps / t / 1e9, 2),
+                "frac": round(b_alg * a.steps / t / 1e9 / (HBM_PEAK_GBS * world), 4)}
+        path.update(pmc_path(a, world, b_alg))
         out = {
             "metric": "edges/s seq+tree+partition",
             "value": round(value, 1),
@@ -178,23 +221,24 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (Graph500 RMAT, seeded, self-loops/duplicates removed)",
+            "data": "synthetic (Graph500 RMAT, seeded, self-loops/duplicates removed"
+                    + (", records shuffled and half of them reversed)" if a.shuffle else ", records (tail, head)-sorted)"),
             "config": {"workload": f"RMAT-{a.scale} ef{a.ef}, k={a.k}", "records": R, "vertex_slots": s.pos_size,
                        "tree_nodes": n, "k": a.k, "created": res.created, "packing_nodes": res.packing_nodes,
-                       "heavy_nodes": res.heavy_nodes, "seed": seed,
+                       "heavy_nodes": res.heavy_nodes, "seed": seed, "shuffled": a.shuffle,
                        "parallelism": f"edge-shards x{world}" + (f", {a.reduce} reduce" if world > 1 else "")
                        + ("" if a.dist_backend == "nccl" else f" ({a.dist_backend}"
                           + (", one device" if a.same_device else "") + ")")},
-            "path_roofline": {"alg_bytes": b_alg, "achieved_GBs": round(b_alg * a.steps / t / 1e9, 2),
-                              "frac": round(b_alg * a.steps / t / 1e9 / (HBM_PEAK_GBS * world), 4)},
             "roofline": roof,
+            "path_roofline": path,
+            "evaluator": evaluator,
             "phases": phases,
         }
         if verified is not None:
             out["verified_vs_whole_graph"] = verified
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a, ctx)
-    del rec, shard
+    del shard
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -202,67 +246,163 @@ def main():
         print(json.dumps(out), flush=True)
 
 
-def pmc_traffic(a, region, launches_per_step):
-    """roofline.traffic: HBM bytes per launch of the region's kernels from the committed
-    rocprofv3 PMC passes for this workload (FETCH_SIZE and WRITE_SIZE, separate passes);
-    null when there is no profile for it or the kernels are shared between regions."""
-    path = PMC_FILE.format(scale=a.scale)
-    ks = REGION_KERNELS.get(region)
-    if not ks or not os.path.exists(path):
-        return {}
+def time_evaluator(a, ctx, shard, s, res, rank, world, local, barrier, max_over_ranks):
+    """ECV(down) + balance (evaluate(graph, seq), partition.cpp:475-521), timed on its own:
+    one GPU — sheep_evaluate over all records; N GPUs — parts broadcast, per-shard
+    bitsets, binomial OR-reduction to rank 0, node pass there.  B_eval per SURVEY §8(d)."""
+    import torch
+    import sheep_amd
+    from sheep_amd import dist as sdist
+    R_total = shard.shape[0] * world if world > 1 else shard.shape[0]
+    times, ev = [], None
+    parts0 = res.parts if rank == 0 else None
+    for _ in range(a.eval_reps):
+        barrier()
+        t0 = time.perf_counter()
+        if world == 1:
+            ev = sheep_amd.evaluate(shard, s, parts0, what=sheep_amd.EVAL_DOWN, ctx=ctx)
+        else:
+            parts = sdist.sync_parts(parts0, s.pos_size, torch.device("cuda", local))
+            nparts = torch.tensor([0 if rank else sheep_amd.ShardedEvaluator.num_parts(parts, s, ctx)],
+                                  dtype=torch.int64, device=f"cuda:{local}" if a.dist_backend == "nccl" else "cpu")
+            dist_broadcast(nparts)
+            e = sheep_amd.ShardedEvaluator(s, parts, sheep_amd.EVAL_DOWN, nparts=int(nparts.item()), ctx=ctx)
+            e.add(shard)
+            e = sdist.reduce_eval(e, rank, world)
+            ev = e.finish() if rank == 0 else None
+        barrier()
+        times.append(max_over_ranks(time.perf_counter() - t0))
+    if rank != 0:
+        return None
+    k = res.created
+    b_eval = 24 * R_total + 4 * R_total + 2 * s.pos_size * ((k + 7) // 8)    # SURVEY §8(d)
+    best = min(times)
+    out = {"what": "ECV(down) + down balance", "ecv_down": ev.ecv_down, "max_down_bal": ev.max_down_bal,
+           "ms": round(1e3 * best, 3), "reps": a.eval_reps, "alg_bytes": b_eval,
+           "achieved_GBs": round(b_eval / best / 1e9, 2), "peak": HBM_PEAK_GBS * world,
+           "frac": round(b_eval / best / 1e9 / (HBM_PEAK_GBS * world), 4),
+           "edges_per_s": round(R_total / best, 1)}
+    if world == 1:   # device time of the region (HIP events), beside the wall time
+        ms, launches, _ = ctx.timer("evaluate")
+        if launches:
+            out["device_ms"] = round(ms / launches, 3)
+    out.update(pmc_region(a, world, "evaluate", 1))
+    return out
+
+
+def dist_broadcast(t):
+    import torch.distributed as dist
+    from sheep_amd import dist as sdist
+    if sdist._host_staged() and t.is_cuda:
+        h = t.cpu()
+        dist.broadcast(h, 0)
+        t.copy_(h)
+    else:
+        dist.broadcast(t, 0)
+
+
+def _pmc(a, world):
+    path = PMC_FILE.format(scale=a.scale, k=a.k)
+    if world != 1 or a.shuffle or not os.path.exists(path):
+        return None, path
     prof = json.load(open(path))
-    if prof.get("workload") != f"RMAT-{a.scale} ef{a.ef}, k={a.k}" or any(k not in prof["kernels"] for k in ks):
+    if prof.get("workload") != f"RMAT-{a.scale} ef{a.ef}, k={a.k}":
+        return None, path
+    return prof, path
+
+
+def pmc_region(a, world, region, launches_per_step):
+    """roofline.traffic: HBM bytes per launch of the region's kernels from the committed
+    rocprofv3 PMC passes for this workload (FETCH_SIZE and WRITE_SIZE, separate passes,
+    per path step as the difference of a 2-step and a 1-step run); null when there is no
+    profile for it or the kernels are shared between regions."""
+    prof, path = _pmc(a, world)
+    ks = REGION_KERNELS.get(region)
+    if prof is None or not ks:
         return {}
-    raw = sum(prof["kernels"][k]["traffic_raw"] for k in ks) / launches_per_step
-    cor = sum(prof["kernels"][k]["traffic_stream_corrected"] for k in ks) / launches_per_step
+    sel = [v for v in prof["kernels"].values() if v["base"] in ks]
+    if not sel:
+        return {}
+    key = "per_eval" if region == "evaluate" else "per_step"
+    sel = [v for v in sel if key in v]
+    if not sel:
+        return {}
+    raw = sum(v[key]["traffic_raw"] for v in sel) / launches_per_step
+    cor = sum(v[key]["traffic_stream_corrected"] for v in sel) / launches_per_step
     return {"traffic": int(raw), "traffic_stream_corrected": int(cor),
             "traffic_source": os.path.relpath(path, ROOT) + " (FETCH_SIZE + WRITE_SIZE; Infinity-Cache hits included)"}
 
 
-def cpu_baseline(a, ctx):
-    """CPU baseline on a bounded sample: RMAT-<cpu-scale> from the same generator,
-    seq + tree + partition(k), one core, graph already in memory.
+def pmc_path(a, world, b_alg):
+    """The whole step's measured HBM traffic (every kernel of one path step) against B_alg."""
+    prof, path = _pmc(a, world)
+    if prof is None:
+        return {}
+    raw = sum(v["per_step"]["traffic_raw"] for v in prof["kernels"].values())
+    cor = sum(v["per_step"]["traffic_stream_corrected"] for v in prof["kernels"].values())
+    return {"traffic": int(raw), "traffic_stream_corrected": int(cor), "traffic_over_alg": round(raw / b_alg, 3),
+            "traffic_source": os.path.relpath(path, ROOT)}
 
-    kind "reference": the reference's own lib/ code (degreeSequence, JTree + makeKids,
-    Partition -- the graph2tree.cpp:185-208 flow) compiled from /root/reference into
-    oracle/_ref/ref_harness (`time` mode).  The oracle restatement (oracle/sheep_oracle.cpp)
-    is timed beside it as `port`.  Test infrastructure timed as a baseline; never the
+
+def cpu_info():
+    model = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return model, os.cpu_count()
+
+
+def cpu_baseline(a, ctx):
+    """CPU baseline on a bounded sample: RMAT-<cpu-scale> from the same generator.
+
+    kind "reference": the reference's own lib/ code, compiled from /root/reference into
+    oracle/_ref/ref_harness by oracle/ref/Makefile, run as the graph2tree `-r -p k` flow
+    over MPI ranks (mpiexec -n P ref_harness mpi ...): each rank loads its edge shard
+    (graph2tree -l semantics, untimed), then mpiSequence's degree all-reduce with
+    degreeSequence's sort, JTree on the shard (map), JNodeTable::mpi_merge (the custom-op
+    MPI_Reduce), makeKids + Partition(k) + mpi_sync on rank 0.  The timed region starts at
+    a barrier after the load.  Test infrastructure timed as a baseline; never the
     measured path."""
+    import shutil
     import subprocess
     import tempfile
     import numpy as np
     import sheep_amd
-    import oracle
     sc = a.cpu_scale
     d = sheep_amd.rmat(sc, a.ef, sc, ctx=ctx)
     h = sheep_amd.to_numpy_u32(d).reshape(-1, 3)
     del d
-    tail, head = np.ascontiguousarray(h[:, 0]), np.ascontiguousarray(h[:, 1])
-    R = len(tail)
-    sample = f"RMAT-{sc} ef{a.ef} seed {sc} ({R} records), seq+tree+partition k={a.k}, single-threaded"
-    t0 = time.perf_counter()
-    seq = oracle.sequence(tail, head)
-    p, w = oracle.build_tree(tail, head, seq)
-    oracle.partition(p, w, seq, a.k)
-    tp = time.perf_counter() - t0
-    port = {"value": round(R / tp, 1), "unit": "edges/s", "cores": 1, "kind": "port",
-            "sample": f"{sample}, oracle/sheep_oracle.cpp, {tp:.2f} s"}
+    R = len(h)
+    model, ncpu = cpu_info()
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
-    if not os.path.exists(harness):
-        return port
+    mpiexec = shutil.which("mpiexec", path="/opt/conda/bin") or shutil.which("mpiexec")
+    if not os.path.exists(harness) or not mpiexec:
+        return {"value": None, "unit": "edges/s", "cores": 0, "kind": "reference",
+                "sample": "oracle/_ref/ref_harness or mpiexec missing on this host"}
+    ranks = max(1, min(a.cpu_ranks, ncpu or 1))
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, f"rmat{sc}.dat")
         h.tofile(path)
         del h
-        r = subprocess.run([harness, "time", path, str(a.k)], capture_output=True, text=True, timeout=600)
+        env = dict(os.environ, OMP_NUM_THREADS="1")
+        r = subprocess.run([mpiexec, "-n", str(ranks), harness, "mpi", path, str(a.k)], capture_output=True,
+                           text=True, timeout=900, env=env)
     if r.returncode != 0:
-        port["reference_error"] = r.stderr.strip()[-300:]
-        return port
-    tr = json.loads(r.stdout.strip().splitlines()[-1])["seconds"]
-    return {"value": round(R / tr, 1), "unit": "edges/s", "cores": 1, "kind": "reference",
-            "sample": f"{sample}, reference lib/ (degreeSequence + JTree + makeKids + Partition, "
-                      f"graph2tree.cpp:185-208) built by oracle/ref/Makefile, {tr:.2f} s",
-            "port": port}
+        return {"value": None, "unit": "edges/s", "cores": ranks, "kind": "reference",
+                "sample": f"mpiexec failed: {r.stderr.strip()[-300:]}"}
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    sec = res["seconds"]
+    return {"value": round(R / sec, 1), "unit": "edges/s", "cores": ranks, "kind": "reference",
+            "cpu_model": model, "host_cpus": ncpu,
+            "sample": f"RMAT-{sc} ef{a.ef} seed {sc} ({R} records), k={a.k}: reference lib/ graph2tree -r -p flow "
+                      f"(mpiSequence all-reduce + degreeSequence sort, JTree per shard, JNodeTable::mpi_merge, "
+                      f"makeKids + Partition + mpi_sync) on {ranks} MPI ranks x 1 thread, shards loaded untimed, "
+                      f"{sec:.2f} s",
+            "phases_s": {k: round(v, 3) for k, v in res.get("phases", {}).items()}}
 
 
 if __name__ == "__main__":

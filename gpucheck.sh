@@ -1,5 +1,6 @@
-# GPU parity suite + smoke (round 2)
+# GPU parity suite + smoke + a short bench (round 2)
 set -o pipefail
 mkdir -p gpurun_out && export HSA_ENABLE_IPC_MODE_LEGACY=0 && export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gt.log 2>&1 || exit 1
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py --steps 5 --no-cpu-baseline > gpurun_out/b26.log 2>&1 || exit 1

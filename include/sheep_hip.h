@@ -215,8 +215,57 @@ int sheep_eval_finish(sheep_ctx *ctx, const uint64_t *bits_dev, const uint64_t *
 int sheep_edge_parts(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec, const uint32_t *pos_dev,
                      uint64_t pos_size, const int16_t *parts_vid_dev, int16_t *edge_part_dev);
 
+/* ---- several GPUs of one node (graph2tree -i / -r without MPI) ----------------------
+ * One process drives `ndev` ranks, rank r on devices[r] with a context of its own.  Distinct
+ * devices exchange over RCCL (one communicator clique, xGMI); a device listed more than
+ * once (several edge shards rehearsed on one GPU) exchanges by device-to-device copies.
+ * Per-rank arrays (rec_dev[r], deg_dev[r], ...) live on rank r's device.  Every call is
+ * complete (all ranks synchronised) on return.  Replaces (chan150/sheep):
+ *   sheep_group_sequence        mpiSequence (sequence.h:65-93): per-shard LLAMA degrees
+ *                               into deg_dev[r] (zeroed by the caller, capacity cap), the
+ *                               MPI_Allreduce(MAX) of max_slot and MPI_Allreduce(SUM) of the
+ *                               degrees, then the same seq/pos on every rank
+ *   sheep_group_build_tree      JTree per shard (graph2tree.cpp:185-189) + mpi_merge
+ *                               (jnode.cpp:203-250): reduce 0 = partial trees only (tree_dev[r]
+ *                               = rank r's tree), 1 = gather + one K-way merge on rank 0,
+ *                               2 = binomial rounds of pairwise merges on disjoint device pairs;
+ *                               with 1 / 2 the merged tree is in tree_dev[0]
+ *   sheep_group_broadcast_parts Partition::mpi_sync (partition.cpp:69-79): rank 0's parts
+ *   sheep_group_evaluate        Partition::evaluate over the shards: per-rank part bitsets,
+ *                               binomial OR-reduction, the node pass on rank 0 */
+typedef struct sheep_group sheep_group;
+int sheep_group_create(const int *devices, int ndev, sheep_group **out);
+int sheep_group_destroy(sheep_group *g);
+int sheep_group_size(const sheep_group *g);
+sheep_ctx *sheep_group_ctx(sheep_group *g, int rank);
+int sheep_group_uses_rccl(const sheep_group *g);
+int sheep_group_sequence(sheep_group *g, const sheep_xs1 *const *rec_dev, const uint64_t *nrec,
+                         uint32_t *const *deg_dev, uint64_t cap, uint32_t *const *seq_dev,
+                         uint32_t *const *pos_dev, uint64_t *n_out, uint64_t *vs_out);
+int sheep_group_build_tree(sheep_group *g, const sheep_xs1 *const *rec_dev, const uint64_t *nrec,
+                           const uint32_t *const *pos_dev, uint64_t pos_size, uint64_t n,
+                           sheep_jnode *const *tree_dev, int reduce);
+/* the reduction step alone (tree_dev[r] = rank r's partial tree; reduce 1 or 2 as above) */
+int sheep_group_reduce_trees(sheep_group *g, sheep_jnode *const *tree_dev, uint64_t n, int reduce);
+int sheep_group_broadcast_parts(sheep_group *g, int16_t *const *parts_vid_dev, uint64_t pos_size);
+int sheep_device_count(int *out);
+int sheep_group_evaluate(sheep_group *g, const sheep_xs1 *const *rec_dev, const uint64_t *nrec,
+                         const uint32_t *const *pos_dev, uint64_t pos_size,
+                         const int16_t *const *parts_vid_dev, int what, sheep_eval *out);
+
 /* ---- tree facts (TREEFAQS) -------------------------------------------------------- */
 int sheep_facts(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n, sheep_facts_t *out);
+
+/* ---- .net (SNAP text) ingest ---------------------------------------------------------
+ * text_dev[0, bytes): a SNAP text edge list in HBM.  Whitespace-separated unsigned decimal
+ * pairs become records {tail, head, 1.0f} in out_dev (capacity cap records) the way
+ * SNAPReader reads them (readerwriter.h:78-90): the input ends at the first token that is
+ * not a 32-bit unsigned decimal, an incomplete last pair is dropped.  skip_comments = 1
+ * drops lines whose first token starts with '#' or '%' first (the graph loader's
+ * handling of SNAP headers; LLAMA's own loader is un-vendored, so parity-unpinned).
+ * *nrec_out (host, synchronises) = records written. */
+int sheep_parse_net(sheep_ctx *ctx, const char *text_dev, uint64_t bytes, int skip_comments, sheep_xs1 *out_dev,
+                    uint64_t cap, uint64_t *nrec_out);
 
 /* ---- synthetic input ---------------------------------------------------------------
  * Graph500-parameter RMAT (A,B,C,D = .57,.19,.19,.05, no per-level noise), vertex

@@ -42,14 +42,29 @@ class HarnessGraph {
   HarnessGraph(char const *filename, size_t part = 0, size_t num_parts = 0) {
     std::vector<vid_t> t, h;
     vid_t X, Y;
+    size_t base = 0;   // index of the first record held in t/h
     if (strcmp(".dat", filename + strlen(filename) - 4) == 0) {
       std::ifstream s(filename, std::ios::binary);
       xs1 rec;
-      while (s.read((char *)&rec, sizeof rec)) { t.push_back(rec.tail); h.push_back(rec.head); }
+      if (num_parts != 0) {   // a partial load reads only its own contiguous record range
+        s.seekg(0, std::ios::end);
+        const size_t R = (size_t)s.tellg() / sizeof(xs1);
+        const size_t b = (part - 1) * R / num_parts, e = part * R / num_parts;
+        s.seekg((std::streamoff)(b * sizeof(xs1)), std::ios::beg);
+        std::vector<xs1> buf(e - b);
+        s.read((char *)buf.data(), (std::streamsize)(buf.size() * sizeof(xs1)));
+        for (const xs1 &x : buf) { t.push_back(x.tail); h.push_back(x.head); }
+        base = b;
+        part = 1;
+        num_parts = 0;
+      } else {
+        while (s.read((char *)&rec, sizeof rec)) { t.push_back(rec.tail); h.push_back(rec.head); }
+      }
     } else {
       std::ifstream s(filename);
       while ((s >> X) && (s >> Y)) { t.push_back(X); h.push_back(Y); }
     }
+    (void)base;
     size_t R = t.size(), beg = 0, end = R;
     if (num_parts != 0) { beg = (part - 1) * R / num_parts; end = part * R / num_parts; }
     for (size_t i = beg; i < end; ++i) max_nodes = std::max(max_nodes, std::max(t[i], h[i]) + 1);
@@ -90,6 +105,30 @@ class HarnessGraph {
   EdgeItr getEdgeItr(vid_t X) const { return EdgeItr(this, X); }
 };
 
+// The GraphType concept over an all-reduced degree vector: what degreeSequence
+// (sequence.h:52-63) reads (getNodes, getNodeItr, getDeg), so the reference's own sort
+// (by-reference comparator) orders mpiSequence's summed degrees.
+class DegreeGraph {
+  std::vector<esize_t> const &deg;
+  size_t nodes = 0;
+
+ public:
+  explicit DegreeGraph(std::vector<esize_t> const &d) : deg(d) {
+    for (esize_t x : d) nodes += x != 0;
+  }
+  size_t getNodes() const { return nodes; }
+  size_t getDeg(vid_t X) const { return deg[X]; }
+  class NodeItr {
+    DegreeGraph const *g; vid_t n;
+   public:
+    NodeItr(DegreeGraph const *gr) : g(gr), n(0) { while (n != g->deg.size() && g->deg[n] == 0) ++n; }
+    vid_t operator*() const { return n; }
+    vid_t operator++() { do { ++n; } while (n != g->deg.size() && g->deg[n] == 0); return n; }
+    bool isEnd() const { return n == g->deg.size(); }
+  };
+  NodeItr getNodeItr() const { return NodeItr(this); }
+};
+
 static void dump_parts(Partition const &p, char const *path) {
   std::ofstream o(path, std::ios::binary | std::ios::trunc);
   o.write((char const *)p.parts.data(), p.parts.size() * sizeof(part_t));
@@ -102,7 +141,8 @@ static int usage() {
           "ref_harness part G SEQ|- TREE PARTS_PREFIX k.. partition_tree -f -g flow + parts dumps\n"
           "ref_harness write G SEQ|- TREE k PREFIX        Partition + graph-based writePartitionedGraph\n"
           "ref_harness writefile G SEQ|- TREE k PREFIX    Partition + file-based writePartitionedGraph\n"
-          "ref_harness time G k                           seconds for degreeSequence + JTree + Partition(k)\n");
+          "ref_harness time G k                           seconds for degreeSequence + JTree + Partition(k)\n"
+          "mpiexec -n P ref_harness mpi G k              graph2tree -r -p k over P MPI ranks (timed)\n");
   return 1;
 }
 
@@ -168,6 +208,44 @@ int main(int argc, char **argv) {
     double const s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     printf("{\"seconds\": %.6f, \"records\": %zu, \"nodes\": %zu, \"parts\": %zu}\n", s,
            (size_t)g.getEdges(), seq.size(), part.parts.size());
+    return 0;
+  }
+  if (cmd == "mpi" && argc == 4) {   // bench.py cpu_baseline: graph2tree.cpp:134-216 (-i -r -p k)
+    MPI_Init(nullptr, nullptr);
+    int rank = 0, size = 1;
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    MPI_Comm_size(MPI_COMM_WORLD, &size);
+    HarnessGraph g(argv[2], rank + 1, size);   // this rank's edge shard (graph2tree.cpp:162), untimed
+    MPI_Barrier(MPI_COMM_WORLD);
+    auto const t0 = std::chrono::steady_clock::now();
+    // mpiSequence (sequence.h:65-83): the degree all-reduce as the reference does it; the
+    // sort is degreeSequence's (by-reference comparator) over the summed degrees -- the
+    // by-value capture at sequence.h:85 copies the degree vector per comparison and does
+    // not finish at these sizes
+    vid_t max_vid = 0, local_max = g.getMaxVid();
+    MPI_Allreduce(&local_max, &max_vid, 1, MPI_UINT32_T, MPI_MAX, MPI_COMM_WORLD);
+    std::vector<esize_t> degree(max_vid + 1), local_degree(max_vid + 1, 0);
+    for (auto nitr = g.getNodeItr(); !nitr.isEnd(); ++nitr) local_degree[*nitr] = g.getDeg(*nitr);
+    MPI_Allreduce(local_degree.data(), degree.data(), max_vid, MPI_UINT32_T, MPI_SUM, MPI_COMM_WORLD);
+    std::vector<vid_t> seq = degreeSequence(DegreeGraph(degree));
+    auto const t1 = std::chrono::steady_clock::now();
+    JTree tree(g, seq);                                   // map (graph2tree.cpp:185-189)
+    auto const t2 = std::chrono::steady_clock::now();
+    tree.jnodes.mpi_merge(false);                         // reduce (graph2tree.cpp:196)
+    auto const t3 = std::chrono::steady_clock::now();
+    if (rank == 0) tree.jnodes.makeKids();                // graph2tree.cpp:203-210
+    Partition p = rank == 0 ? Partition(seq, tree.jnodes, (short)atoi(argv[3])) : Partition();
+    p.mpi_sync();
+    MPI_Barrier(MPI_COMM_WORLD);
+    auto const t4 = std::chrono::steady_clock::now();
+    auto sec = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double>(b - a).count();
+    };
+    if (rank == 0)
+      printf("{\"seconds\": %.6f, \"ranks\": %d, \"nodes\": %zu, \"phases\": {\"sort\": %.6f, \"map\": %.6f, "
+             "\"reduce\": %.6f, \"partition\": %.6f}}\n", sec(t0, t4), size, seq.size(), sec(t0, t1), sec(t1, t2),
+             sec(t2, t3), sec(t3, t4));
+    MPI_Finalize();
     return 0;
   }
   return usage();

@@ -105,6 +105,16 @@ def lib() -> ctypes.CDLL:
         "sheep_eval_combine": ([P, P, P, U64, P, P, U64], I32),
         "sheep_eval_finish": ([P, P, P, U64, P, I32, I32, ctypes.POINTER(_Eval)], I32),
         "sheep_edge_parts": ([P, P, U64, P, U64, P, P], I32),
+        "sheep_group_create": ([P, I32, ctypes.POINTER(P)], I32),
+        "sheep_group_destroy": ([P], I32),
+        "sheep_group_size": ([P], I32),
+        "sheep_group_ctx": ([P, I32], P),
+        "sheep_group_uses_rccl": ([P], I32),
+        "sheep_group_sequence": ([P, P, P, P, U64, P, P, ctypes.POINTER(U64), ctypes.POINTER(U64)], I32),
+        "sheep_group_build_tree": ([P, P, P, P, U64, U64, P, I32], I32),
+        "sheep_group_broadcast_parts": ([P, P, U64], I32),
+        "sheep_group_evaluate": ([P, P, P, P, U64, P, I32, ctypes.POINTER(_Eval)], I32),
+        "sheep_parse_net": ([P, P, U64, I32, P, U64, ctypes.POINTER(U64)], I32),
         "sheep_rmat_generate": ([P, I32, I32, U64, P, U64, ctypes.POINTER(U64)], I32),
         "sheep_rmat_generate_host": ([I32, I32, U64, P, U64, ctypes.POINTER(U64)], I32),
     }
@@ -451,6 +461,14 @@ class ShardedEvaluator:
         self.acc = t.zeros(aw.value, dtype=t.int64, device=f"cuda:{self.ctx.device}")
         self.bits_words, self.acc_words = bw.value, aw.value
 
+    @staticmethod
+    def num_parts(parts, seq: Sequence, ctx: Context | None = None) -> int:
+        """max part + 1 over the vid-indexed parts (partition.cpp:433-435)."""
+        ctx = ctx or default_context()
+        n = ctypes.c_int32()
+        _check(lib().sheep_eval_num_parts(ctx.handle, _ptr(parts), seq.pos_size, ctypes.byref(n)))
+        return n.value
+
     def add(self, records, nrec: int | None = None):
         nrec = records.shape[0] if nrec is None else nrec
         _check(lib().sheep_eval_shard(self.ctx.handle, _ptr(records), nrec, _ptr(self.seq.pos), self.seq.pos_size,
@@ -508,6 +526,100 @@ def facts(tree, ctx: Context | None = None) -> Facts:
 
 
 # ---------------------------------------------------------------------------------
+# several GPUs in one process (graph2tree -i / -r without MPI)
+# ---------------------------------------------------------------------------------
+def _ptr_array(ts):
+    return (ctypes.c_void_p * len(ts))(*[_ptr(t) for t in ts])
+
+
+class _BorrowedContext(Context):
+    """A rank's context inside a Group (owned by the group)."""
+
+    def __init__(self, device: int, handle):
+        self.device = device
+        self.handle = handle
+
+    def close(self):
+        self.handle = None
+
+
+class Group:
+    """One process driving several devices as the ranks of graph2tree's MPI world
+    (sheep_group_* in include/sheep_hip.h): RCCL between distinct devices, device copies
+    when a device is listed more than once (a rehearsal of several shards on one GPU)."""
+
+    REDUCE = {"none": 0, "kway": 1, "binomial": 2}
+
+    def __init__(self, devices):
+        self.devices = list(devices)
+        arr = (ctypes.c_int * len(self.devices))(*self.devices)
+        h = ctypes.c_void_p()
+        _check(lib().sheep_group_create(arr, len(self.devices), ctypes.byref(h)))
+        self.handle = h
+        self.ctx = [_BorrowedContext(d, ctypes.c_void_p(lib().sheep_group_ctx(h, r)))
+                    for r, d in enumerate(self.devices)]
+
+    @property
+    def rccl(self) -> bool:
+        return bool(lib().sheep_group_uses_rccl(self.handle))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().sheep_group_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _dev(self, r):
+        return f"cuda:{self.devices[r]}"
+
+    def sequence(self, shards, vs_cap: int):
+        """mpiSequence over the ranks' record shards: a Sequence per rank (all equal)."""
+        t = _torch()
+        P = len(self.devices)
+        deg = [t.zeros(max(vs_cap, 1), dtype=t.int32, device=self._dev(r)) for r in range(P)]
+        seq = [t.empty(max(vs_cap, 1), dtype=t.int32, device=self._dev(r)) for r in range(P)]
+        pos = [t.empty(max(vs_cap, 1), dtype=t.int32, device=self._dev(r)) for r in range(P)]
+        nrec = (ctypes.c_uint64 * P)(*[s.shape[0] for s in shards])
+        n, vs = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().sheep_group_sequence(self.handle, _ptr_array(shards), nrec, _ptr_array(deg), vs_cap,
+                                          _ptr_array(seq), _ptr_array(pos), ctypes.byref(n), ctypes.byref(vs)))
+        return [Sequence(seq[r], pos[r], n.value, vs.value) for r in range(P)]
+
+    def build_tree(self, shards, seqs, reduce: str = "kway"):
+        """JTree per shard + mpi_merge: the merged tree (rank 0's device) for kway/binomial,
+        every rank's partial tree for "none"."""
+        t = _torch()
+        P = len(self.devices)
+        n = seqs[0].n
+        trees = [t.empty((max(n, 1), 2), dtype=t.int32, device=self._dev(r)) for r in range(P)]
+        nrec = (ctypes.c_uint64 * P)(*[s.shape[0] for s in shards])
+        _check(lib().sheep_group_build_tree(self.handle, _ptr_array(shards), nrec, _ptr_array([s.pos for s in seqs]),
+                                            seqs[0].pos_size, n, _ptr_array(trees), self.REDUCE[reduce]))
+        return [x[:n] for x in trees] if reduce == "none" else trees[0][:n]
+
+    def broadcast_parts(self, parts0, pos_size: int):
+        """Partition::mpi_sync: rank 0's parts on every rank."""
+        t = _torch()
+        P = len(self.devices)
+        parts = [parts0] + [t.empty(max(pos_size, 1), dtype=t.int16, device=self._dev(r)) for r in range(1, P)]
+        _check(lib().sheep_group_broadcast_parts(self.handle, _ptr_array(parts), pos_size))
+        return [p[:pos_size] for p in parts]
+
+    def evaluate(self, shards, seqs, parts, what: int = 0) -> "EvalResult":
+        P = len(self.devices)
+        nrec = (ctypes.c_uint64 * P)(*[s.shape[0] for s in shards])
+        out = _Eval()
+        _check(lib().sheep_group_evaluate(self.handle, _ptr_array(shards), nrec, _ptr_array([s.pos for s in seqs]),
+                                          seqs[0].pos_size, _ptr_array(parts), what, ctypes.byref(out)))
+        return EvalResult(*[getattr(out, f) for f, _ in _Eval._fields_])
+
+
+# ---------------------------------------------------------------------------------
 # synthetic input
 # ---------------------------------------------------------------------------------
 def rmat(scale: int, edgefactor: int = 16, seed: int = 1, ctx: Context | None = None):
@@ -528,6 +640,21 @@ def rmat_host(scale: int, edgefactor: int = 16, seed: int = 1) -> np.ndarray:
     n = ctypes.c_uint64()
     _check(lib().sheep_rmat_generate_host(scale, edgefactor, seed, buf.ctypes.data, cap, ctypes.byref(n)))
     return buf[: 3 * n.value].reshape(-1, 3)
+
+
+def parse_net(text: bytes, skip_comments: bool = False, ctx: Context | None = None):
+    """A SNAP text edge list parsed on the GPU (sheep_parse_net): [R, 3] int32 device
+    records, SNAPReader semantics (skip_comments: the graph loader's '#'/'%' lines)."""
+    ctx = ctx or default_context()
+    t = _torch()
+    raw = t.frombuffer(bytearray(text), dtype=t.uint8).to(_dev(ctx)) if text else t.empty(1, dtype=t.uint8,
+                                                                                            device=_dev(ctx))
+    cap = len(text) // 4 + 1
+    out = t.empty((cap, 3), dtype=t.int32, device=_dev(ctx))
+    n = ctypes.c_uint64()
+    _check(lib().sheep_parse_net(ctx.handle, _ptr(raw), len(text), int(skip_comments), _ptr(out), cap,
+                                 ctypes.byref(n)))
+    return out[: n.value]
 
 
 XS1 = np.dtype([("tail", "<u4"), ("head", "<u4"), ("weight", "<f4")])

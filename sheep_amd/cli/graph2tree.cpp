@@ -5,21 +5,183 @@
 //
 // Phases (graph2tree.cpp:161-218): load the records into HBM, degree sequence (or -s
 // read), map (JTree on the GPU), [reduce], [partition], [TREEFAQS].  -i / -r select the
-// reference's MPI sort / reduce; here a single process drives one GPU, so they only
-// keep their file-naming and printing behaviour (the multi-GPU edge-shard path is
-// bench.py's torch.distributed + RCCL driver).  Flags of the
-// junction-tree experiments (-e -j -m -w -x) and -t are rejected with a message.
+// reference's MPI sort / reduce: here ONE process plays the MPI world, rank r on device r
+// of SHEEP_DEVICES (default: every visible GPU; a device listed twice rehearses two
+// shards on it) — edge shards, an RCCL all-reduce of the degrees, per-GPU partial trees,
+// the merge on rank 0, the parts broadcast and per-rank partition files, with the
+// reference's file names (sheep/world.hpp, include/sheep_hip.h sheep_group_*).  With one
+// rank the single-GPU path runs.  Flags of the junction-tree experiments (-e -j -m -w -x)
+// and -t are rejected with a message.
 #include <unistd.h>
 
 #include <cassert>
 #include <chrono>
 
 #include "sheep/sheep.hpp"
+#include "sheep/world.hpp"
 
 using namespace sheep;
 
 static double seconds_since(std::chrono::steady_clock::time_point t) {
   return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t).count() / 1000.0;
+}
+
+// JTree::isValid (jtree.cpp:238-300) as far as it checks anything (the per-edge ancestor
+// checks are vacuous there): index count == verts, parents later and in range.
+static bool tree_valid(const std::vector<sheep_jnode> &nodes, uint64_t n, uint64_t vert_cnt) {
+  bool ok = vert_cnt == n;
+  for (uint64_t id = 0; ok && id != n; ++id) {
+    const jnid_t p = nodes[id].parent;
+    ok = p == INVALID_JNID || (p > id && p < n);
+  }
+  return ok;
+}
+
+// The -i / -r MPI world over several GPUs (graph2tree.cpp:134-216).
+static int run_world(const std::vector<int> &devs, const char *graph_filename, bool use_mpi_sort, bool use_mpi_reduce,
+                     size_t partitions, const char *sequence_filename, const char *output_filename, bool verbose,
+                     bool do_faqs, bool do_validate, std::chrono::steady_clock::time_point start_point) {
+  World w(devs);
+  const int P = w.size();
+  if (partitions != 0 && !use_mpi_reduce) {
+    printf("graph2tree: -p with -i needs -r (the ranks' partial trees are merged before partitioning).\n");
+    return 1;
+  }
+  if (!use_mpi_sort && strcmp(sequence_filename, "") == 0) {
+    printf("graph2tree: -r needs -i or -s SEQ (every rank must use the same sequence).\n");
+    return 1;
+  }
+  if (verbose) printf("Loading %s...\n", graph_filename);
+  std::vector<sheep_xs1> all;
+  if (is_dat(graph_filename)) {
+    all = readRecords(graph_filename);
+  } else {   // SNAP text, parsed on rank 0's GPU
+    uint64_t nr = 0;
+    DeviceArray<sheep_xs1> d = parseNet(graph_filename, true, &nr, w.ctx(0));
+    all.resize(nr);
+    if (nr) d.download(all.data(), nr);
+  }
+  const uint64_t R = all.size();
+  std::vector<RankState> rk(P);
+  uint64_t cap = 1;
+  for (int r = 0; r < P; ++r) {   // rank r loads part r+1 of P (graph2tree.cpp:137-143, 162)
+    const uint64_t beg = (uint64_t)r * R / P, end = (uint64_t)(r + 1) * R / P;
+    rk[r].host.assign(all.begin() + beg, all.begin() + end);
+    rk[r].rec = DeviceArray<sheep_xs1>(end - beg, w.ctx(r));
+    if (end > beg) rk[r].rec.upload(rk[r].host.data(), end - beg);
+    for (const sheep_xs1 &x : rk[r].host)
+      rk[r].max_vid = std::max<uint64_t>(rk[r].max_vid, (uint64_t)std::max(x.tail, x.head) + 1);
+    cap = std::max(cap, rk[r].max_vid);
+  }
+  const bool is_leader = true;   // rank 0 prints (graph2tree.cpp:158-159)
+  const double load_s = seconds_since(start_point);
+  if (is_leader) printf("Loaded graph in: %f seconds\n", load_s);
+
+  std::vector<const sheep_xs1 *> recp(P);
+  std::vector<uint64_t> nrec(P);
+  std::vector<uint32_t *> seqp(P), posp(P), degp(P);
+  for (int r = 0; r < P; ++r) { recp[r] = rk[r].rec.get(); nrec[r] = rk[r].host.size(); }
+  uint64_t n = 0, pos_size = 0;
+  if (use_mpi_sort) {   // mpiSequence (sequence.h:65-93)
+    const std::vector<uint32_t> zero(cap, 0);
+    for (int r = 0; r < P; ++r) {
+      rk[r].deg = DeviceArray<uint32_t>(cap, w.ctx(r));
+      rk[r].deg.upload(zero.data(), cap);
+      rk[r].seq = DeviceArray<uint32_t>(cap, w.ctx(r));
+      rk[r].pos = DeviceArray<uint32_t>(cap, w.ctx(r));
+      degp[r] = rk[r].deg.get(); seqp[r] = rk[r].seq.get(); posp[r] = rk[r].pos.get();
+    }
+    check(sheep_group_sequence(w.handle(), recp.data(), nrec.data(), degp.data(), cap, seqp.data(), posp.data(), &n,
+                               &pos_size));
+    if (strcmp(sequence_filename, "") != 0) {   // rank 0 writes it (graph2tree.cpp:177-178)
+      std::vector<vid_t> h(n);
+      if (n) rk[0].seq.download(h.data(), n);
+      writeSequence(h, sequence_filename);
+    }
+  } else {   // readSequence on every rank
+    const std::vector<vid_t> h = readSequence(sequence_filename);
+    n = h.size();
+    pos_size = h.empty() ? 0 : (uint64_t)*std::max_element(h.begin(), h.end()) + 1;
+    for (int r = 0; r < P; ++r) {
+      rk[r].seq = DeviceArray<uint32_t>(n, w.ctx(r));
+      if (n) rk[r].seq.upload(h.data(), n);
+      rk[r].pos = DeviceArray<uint32_t>(pos_size, w.ctx(r));
+      check(sheep_positions(w.ctx(r), rk[r].seq.get(), n, rk[r].pos.get(), pos_size));
+      posp[r] = rk[r].pos.get();
+    }
+  }
+  const double sort_s = seconds_since(start_point) - load_s;
+  if (is_leader && (use_mpi_sort || strcmp(sequence_filename, "") == 0)) printf("Sorted in: %f seconds\n", sort_s);
+
+  std::vector<sheep_jnode *> treep(P);
+  for (int r = 0; r < P; ++r) { rk[r].tree = DeviceArray<sheep_jnode>(n, w.ctx(r)); treep[r] = rk[r].tree.get(); }
+  std::vector<const uint32_t *> cposp(posp.begin(), posp.end());
+  check(sheep_group_build_tree(w.handle(), recp.data(), nrec.data(), cposp.data(), pos_size, n, treep.data(), 0));
+  const double map_s = seconds_since(start_point) - sort_s - load_s;
+  if (is_leader) printf("Mapped in: %f seconds\n", map_s);
+  if (use_mpi_reduce) {   // mpi_merge (jnode.cpp:213-250): gather + one K-way merge on rank 0
+    check(sheep_group_reduce_trees(w.handle(), treep.data(), n, 1));
+    const double reduce_s = seconds_since(start_point) - map_s - sort_s - load_s;
+    if (is_leader) printf("Reduced in: %f seconds\n", reduce_s);
+  }
+
+  if (partitions != 0) {   // graph2tree.cpp:203-213
+    sheep_kids *kids = nullptr;
+    check(sheep_kids_create(w.ctx(0), rk[0].tree.get(), n, &kids));
+    std::vector<int16_t *> partp(P);
+    for (int r = 0; r < P; ++r) { rk[r].parts = DeviceArray<int16_t>(pos_size, w.ctx(r)); partp[r] = rk[r].parts.get(); }
+    sheep_partition_info info{};
+    const int rc = sheep_partition(w.ctx(0), rk[0].tree.get(), n, rk[0].seq.get(), n, pos_size, kids, (int16_t)partitions,
+                                   1.03, 0, 1, rk[0].parts.get(), &info);
+    sheep_kids_destroy(kids);
+    check(rc);
+    check(sheep_group_broadcast_parts(w.handle(), partp.data(), pos_size));   // p.mpi_sync()
+    if (strcmp(output_filename, "") != 0) {   // every rank writes its shard: PREFIX-wRRRR-pPPPP
+      std::vector<int16_t> pv(pos_size);
+      if (pos_size) rk[0].parts.download(pv.data(), pos_size);
+      part_t max_part = -1;
+      for (part_t x : pv) max_part = std::max(max_part, x);
+      for (int r = 0; r < P; ++r) {
+        DeviceArray<int16_t> ep(nrec[r], w.ctx(r));
+        check(sheep_edge_parts(w.ctx(r), rk[r].rec.get(), nrec[r], rk[r].pos.get(), pos_size, rk[r].parts.get(), ep.get()));
+        std::vector<int16_t> eh(nrec[r]);
+        if (nrec[r]) ep.download(eh.data(), nrec[r]);
+        char prefix[4096];
+        snprintf(prefix, sizeof prefix, "%s-w%04d-p", output_filename, r);   // graph2tree.cpp:151-156
+        write_partition_files(rk[r].host, eh, max_part, rk[r].max_vid, prefix, false, false);
+      }
+    } else if (is_leader) {
+      printf("Actually created %d partitions.\n", (int)info.created);
+      printf("First two partition sizes: %zu and %zu\n", (size_t)info.first_size, (size_t)info.second_size);
+    }
+  } else if (strcmp(output_filename, "") != 0) {
+    if (use_mpi_reduce) {   // rank 0 saves the merged tree (graph2tree.cpp:217-218)
+      JNodeTable t;
+      t.assign_from_device(rk[0].tree, (jnid_t)n, (jnid_t)n);
+      t.save(output_filename);
+    } else {   // -i alone: every rank maps its shard into OUTPUTrrr0.tre (graph2tree.cpp:144-149)
+      for (int r = 0; r < P; ++r) {
+        char name[4096];
+        snprintf(name, sizeof name, "%s%02dr0.tre", output_filename, r);
+        JNodeTable t;
+        t.assign_from_device(rk[r].tree, (jnid_t)n, (jnid_t)n);
+        t.save(name);
+      }
+    }
+  }
+  if (verbose) printf("Built in: %f seconds\n", seconds_since(start_point));
+  if (do_faqs || do_validate) {
+    Facts f;
+    check(sheep_facts(w.ctx(0), rk[0].tree.get(), n, &f.f));
+    if (do_faqs) f.print();
+    if (do_validate) {
+      std::vector<sheep_jnode> h(n);
+      if (n) rk[0].tree.download(h.data(), n);
+      printf(tree_valid(h, n, f.f.vert_cnt) ? "Tree is valid.\n" : "ERROR: Tree is not valid.\n");
+    }
+  }
+  if (verbose) printf("Finished in: %f seconds\n", seconds_since(start_point));
+  return 0;
 }
 
 int main(int argc, char *argv[]) {
@@ -68,6 +230,20 @@ int main(int argc, char *argv[]) {
   const char *const graph_filename = argv[optind];
   auto start_point = std::chrono::steady_clock::now();
 
+  if (use_mpi_sort || use_mpi_reduce) {
+    try {
+      const std::vector<int> devs = world_devices();
+      if (devs.size() > 1)
+        return run_world(devs, graph_filename, use_mpi_sort, use_mpi_reduce, partitions, sequence_filename,
+                         output_filename, verbose, do_faqs, do_validate, start_point);
+    } catch (const std::out_of_range &e) {
+      fprintf(stderr, "terminate called after throwing an instance of 'std::out_of_range'\n  what():  %s\n", e.what());
+      return 134;
+    } catch (const std::exception &e) {
+      fprintf(stderr, "graph2tree: %s\n", e.what());
+      return 1;
+    }
+  }
   std::string out_name = output_filename;
   if (use_mpi_sort || use_mpi_reduce) {   // one rank: rank 0 of a size-1 world (graph2tree.cpp:134-157)
     part = 1;
@@ -122,14 +298,9 @@ int main(int argc, char *argv[]) {
     if (verbose) printf("Built in: %f seconds\n", seconds_since(start_point));
     if (do_faqs) tree.jnodes.getFacts().print();
     if (do_validate) {
-      // JTree::isValid (jtree.cpp:238-300): index count == verts, parents later & in range
       const Facts f = tree.jnodes.getFacts();
-      bool ok = f.f.vert_cnt == seq.n;
-      for (jnid_t id = 0; ok && id != tree.size(); ++id) {
-        const jnid_t p = tree.jnodes.parent(id);
-        ok = p == INVALID_JNID || (p > id && p < tree.size());
-      }
-      printf(ok ? "Tree is valid.\n" : "ERROR: Tree is not valid.\n");
+      printf(tree_valid(tree.jnodes.nodes(), tree.size(), f.f.vert_cnt) && f.f.vert_cnt == seq.n
+                 ? "Tree is valid.\n" : "ERROR: Tree is not valid.\n");
     }
     if (verbose) printf("Finished in: %f seconds\n", seconds_since(start_point));
   } catch (const std::out_of_range &e) {

@@ -7,10 +7,6 @@
 #include "common.hpp"
 #include "tree_tour.hpp"
 
-struct sheep_ctx {
-  sheep::Ctx c;
-};
-
 namespace sheep {
 static thread_local std::string g_last_error;
 void set_error(const char *msg) { g_last_error = msg; }
@@ -38,6 +34,7 @@ void eval_finish(Ctx &c, const uint64_t *bits, const uint64_t *acc, uint64_t pos
 void tree_facts(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_facts_t *out);
 void edge_parts(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
                 const int16_t *parts_vid, int16_t *out);
+uint64_t parse_net(Ctx &c, const char *text, uint64_t bytes, int skip_comments, sheep_xs1 *out, uint64_t cap);
 uint64_t rmat_generate(Ctx &c, int scale, int ef, uint64_t seed, sheep_xs1 *out, uint64_t cap);
 uint64_t rmat_generate_host(int scale, int ef, uint64_t seed, sheep_xs1 *out, uint64_t cap);
 }  // namespace sheep
@@ -365,6 +362,15 @@ int sheep_facts(sheep_ctx *ctx, const sheep_jnode *tree, uint64_t n, sheep_facts
   DeviceGuard dg(ctx);
   NEED(ctx && out && (tree || !n), "null argument");
   sheep::tree_facts(ctx->c, tree, n, out);
+  API_END
+}
+
+int sheep_parse_net(sheep_ctx *ctx, const char *text, uint64_t bytes, int skip_comments, sheep_xs1 *out, uint64_t cap,
+                    uint64_t *nrec_out) {
+  API_BEGIN
+  DeviceGuard dg(ctx);
+  NEED(ctx && nrec_out && (text || !bytes) && (out || !cap), "null argument");
+  *nrec_out = sheep::parse_net(ctx->c, text, bytes, skip_comments, out, cap);
   API_END
 }
 

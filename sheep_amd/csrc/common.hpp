@@ -128,6 +128,15 @@ struct Ctx {
   }
 };
 
+}  // namespace sheep
+
+// The C ABI's opaque context handle (include/sheep_hip.h).
+struct sheep_ctx {
+  sheep::Ctx c;
+};
+
+namespace sheep {
+
 // Brackets one instrumented launch with HIP events on the context stream.  `bytes` is
 // the launch's ALGORITHMIC traffic, summed per timer name.
 struct TimedRegion {

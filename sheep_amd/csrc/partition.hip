@@ -203,9 +203,10 @@ __global__ void k_parts_to_vid(const uint32_t *__restrict__ seq, uint64_t seq_n,
 // Round r finishes every node whose kids are all finished and whose accumulated weight
 // acc (own weight + finished kids' sums) is <= max_component: acc is then its subtree sum
 // S, it cannot pack (only S > max can), and it is added into its parent.  Elimination
-// trees of power-law graphs are mostly fringe (RMAT: 66% leaves; three rounds finish
-// ~77% of the nodes), so the Euler tour below only ranks the remaining core T'.
-constexpr int RAKE_ROUNDS = 3;
+// trees of power-law graphs are mostly fringe (RMAT: 66% leaves; two rounds finish ~74%
+// of the nodes, a third only 3% more for its scattered atomics), so the Euler tour below
+// only ranks the remaining core T'.
+constexpr int RAKE_ROUNDS = 2;
 
 __global__ void k_rake_init(const uint32_t *__restrict__ koff, const uint64_t *__restrict__ w, uint64_t n,
                             uint32_t *__restrict__ pend, uint64_t *__restrict__ acc, uint8_t *__restrict__ fin) {
@@ -278,13 +279,19 @@ __device__ __forceinline__ void node_interval(uint32_t a, const uint32_t *cparen
   else if (ckoff[a] < ckoff[a + 1]) { lo = rst[a]; hi = ren[a]; }
   else { lo = INVALID; hi = INVALID; }
 }
-__device__ __forceinline__ uint64_t lazy_r(uint32_t a, uint64_t r, uint32_t lo, uint32_t hi, const PackEv *ev,
-                                           uint32_t nev) {
+// events in LDS (the first EV_LDS; later ones from the device list)
+__device__ __forceinline__ uint64_t lazy_r(uint32_t a, uint64_t r, uint32_t lo, uint32_t hi, const PackEv *sev,
+                                           const PackEv *ev, uint32_t nev) {
   for (uint32_t e = 0; e < nev; ++e) {
-    const PackEv x = ev[e];
+    const PackEv x = e < EV_LDS ? sev[e] : ev[e];
     if (x.v == a || (lo != INVALID && x.vpos != INVALID && lo <= x.vpos && x.vpos <= hi)) r -= x.delta;
   }
   return r;
+}
+__device__ __forceinline__ void load_events(const PackEv *ev, uint32_t nev, PackEv *sev) {
+  const uint32_t nl = nev < EV_LDS ? nev : EV_LDS;
+  for (uint32_t e = threadIdx.x; e < nl; e += blockDim.x) sev[e] = ev[e];
+  __syncthreads();
 }
 
 // The next packing node: the lowest-index heavy node after the last packing node whose
@@ -294,7 +301,7 @@ __device__ __forceinline__ uint64_t lazy_r(uint32_t a, uint64_t r, uint32_t lo, 
 // event's delta (computed by the host) into the device event list.
 constexpr int EVI = 8, EV_CH = BLOCK * EVI;
 __global__ __launch_bounds__(BLOCK) void k_next_event(const uint32_t *__restrict__ hids, uint64_t nh,
-                                                      const uint64_t *__restrict__ S, const uint32_t *__restrict__ hst,
+                                                      const uint64_t *__restrict__ SH, const uint32_t *__restrict__ hst,
                                                       const uint32_t *__restrict__ hen, PackEv *__restrict__ evl,
                                                       uint32_t nev, uint64_t last_delta, uint64_t maxc,
                                                       const uint64_t *__restrict__ evprev,
@@ -324,7 +331,7 @@ __global__ __launch_bounds__(BLOCK) void k_next_event(const uint32_t *__restrict
       if (h >= nh) continue;
       const uint32_t a = hids[h];
       if (vlast != INVALID && a <= vlast) continue;
-      uint64_t r = S[a];
+      uint64_t r = SH[h];
       const uint32_t lo = hst[h], hi = hen[h];
       for (uint32_t e = 0; e < nev && r > maxc; ++e) {
         const PackEv x = e < EV_LDS ? sev[e] : evl[e];
@@ -363,18 +370,20 @@ __global__ __launch_bounds__(BLOCK) void k_event_stage(const unsigned long long 
                                                        const uint32_t *__restrict__ ren, uint32_t *__restrict__ hdr,
                                                        uint32_t *__restrict__ kid_out, uint64_t *__restrict__ r_out,
                                                        uint32_t beg_j, uint32_t cap) {
+  __shared__ PackEv sev[EV_LDS];
   const uint64_t e = *found;
   const uint32_t v = e == ~0ull ? INVALID : (uint32_t)(e >> 32);
   if (v == INVALID) {
     if (blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = INVALID;
     return;
   }
+  load_events(evl, nev, sev);
   const uint32_t beg = koff[v], cnt = koff[v + 1] - beg;
   if (blockIdx.x == 0 && threadIdx.x == 0 && beg_j == 0) {
     *evprev = e;
     uint32_t lo, hi;
     node_interval(v, cparent, ckoff, tD, tU, rst, ren, lo, hi);
-    const uint64_t r = lazy_r(v, S[v], lo, hi, evl, nev);
+    const uint64_t r = lazy_r(v, S[v], lo, hi, sev, evl, nev);
     PackEv x;
     x.v = v;
     x.vpos = cparent[v] == INVALID ? INVALID : tD[v];
@@ -389,10 +398,14 @@ __global__ __launch_bounds__(BLOCK) void k_event_stage(const unsigned long long 
   const uint32_t lim = cnt - beg_j < cap ? cnt - beg_j : cap;
   for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < lim; j += gridDim.x * BLOCK) {
     const uint32_t kid = kids[beg + beg_j + j];
-    uint32_t lo, hi;
-    node_interval(kid, cparent, ckoff, tD, tU, rst, ren, lo, hi);
+    uint64_t r = S[kid];
+    if (cparent[kid] != INVALID) {   // a fringe kid never packed and has no packing below it
+      uint32_t lo, hi;
+      node_interval(kid, cparent, ckoff, tD, tU, rst, ren, lo, hi);
+      r = lazy_r(kid, r, lo, hi, sev, evl, nev);
+    }
     kid_out[j] = kid;
-    r_out[j] = lazy_r(kid, S[kid], lo, hi, evl, nev);
+    r_out[j] = r;
   }
 }
 
@@ -404,18 +417,26 @@ __global__ void k_scatter_u32(const uint32_t *__restrict__ pos, const uint32_t *
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) out[pos[i]] = val[i];
 }
 
+__global__ void k_gather_u64(const uint64_t *__restrict__ src, const uint32_t *__restrict__ idx, uint64_t m,
+                             uint64_t *__restrict__ dst) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) dst[i] = src[idx[i]];
+}
+
 // every root's final residual (after all events)
 __global__ void k_roots_r(const uint32_t *__restrict__ ids, uint64_t m, const uint64_t *__restrict__ S,
                           const uint32_t *__restrict__ cparent, const uint32_t *__restrict__ ckoff,
                           const uint32_t *__restrict__ tD, const uint32_t *__restrict__ tU,
                           const uint32_t *__restrict__ rst, const uint32_t *__restrict__ ren,
                           const PackEv *__restrict__ evl, uint32_t nev, uint64_t *__restrict__ out) {
+  __shared__ PackEv sev[EV_LDS];
+  load_events(evl, nev, sev);
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) {
     const uint32_t a = ids[i];
     uint32_t lo, hi;
     node_interval(a, cparent, ckoff, tD, tU, rst, ren, lo, hi);
-    out[i] = lazy_r(a, S[a], lo, hi, evl, nev);
+    out[i] = lazy_r(a, S[a], lo, hi, sev, evl, nev);
   }
 }
 
@@ -636,6 +657,12 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
                        (const uint32_t *)rst, (const uint32_t *)ren, t.tD, t.tU, hst, hen);
     LAUNCH_CHECK();
   }
+  uint64_t *SH = c.get_as<uint64_t>("pt_SH", nh ? nh : 1);   // S of the heavy nodes, in hids order
+  if (nh) {
+    hipLaunchKernelGGL(k_gather_u64, dim3(grid_for(nh)), dim3(BLOCK), 0, c.stream, (const uint64_t *)S,
+                       (const uint32_t *)hids, nh, SH);
+    LAUNCH_CHECK();
+  }
   PackEv *evl = c.get_as<PackEv>("pt_events", nh + 1);
   unsigned long long *found = (unsigned long long *)(c.d_scalars + 44);
   uint64_t *evprev = c.d_scalars + 46;
@@ -656,9 +683,9 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   std::vector<char> done;
   uint32_t nev = 0;
   uint64_t delta = 0;
-  const unsigned gev = nh ? (unsigned)std::min<uint64_t>((nh + EV_CH - 1) / EV_CH, 256) : 1;
+  const unsigned gev = nh ? (unsigned)std::min<uint64_t>((nh + EV_CH - 1) / EV_CH, 128) : 1;
   auto stage_event = [&](uint32_t beg_j, uint32_t cap, uint32_t *o_kids, uint64_t *o_r) {
-    hipLaunchKernelGGL(k_event_stage, dim3(64), dim3(BLOCK), 0, c.stream, (const unsigned long long *)found, evprev, evl,
+    hipLaunchKernelGGL(k_event_stage, dim3(256), dim3(BLOCK), 0, c.stream, (const unsigned long long *)found, evprev, evl,
                        nev, (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
                        (const uint32_t *)core.parent, (const uint32_t *)core.koff, (const uint32_t *)t.tD,
                        (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren, d_hdr, o_kids, o_r, beg_j,
@@ -671,7 +698,7 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
       HIP_CHECK(hipMemsetAsync(found, 0xFF, sizeof(uint64_t), c.stream));
       if (nh) {
         hipLaunchKernelGGL(k_next_event, dim3(gev), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh,
-                           (const uint64_t *)S, (const uint32_t *)hst, (const uint32_t *)hen, evl, nev, delta,
+                           (const uint64_t *)SH, (const uint32_t *)hst, (const uint32_t *)hen, evl, nev, delta,
                            max_component, (const uint64_t *)evprev, found);
         LAUNCH_CHECK();
       }
@@ -806,8 +833,13 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
     std::vector<uint32_t> ord;
     ord.reserve(na);
     for (uint32_t i = 0; i < na; ++i) if (hs[i] != INVALID) ord.push_back(i);
+    // outer intervals first; a root's span can equal its only core kid's interval, and
+    // the root is the outer one (assigned roots follow the packed kids in all_ids)
+    const uint32_t nasg = (uint32_t)asg_ids.size();
     std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
-      return hs[a] != hs[b] ? hs[a] < hs[b] : he[a] > he[b];
+      if (hs[a] != hs[b]) return hs[a] < hs[b];
+      if (he[a] != he[b]) return he[a] > he[b];
+      return (a >= nasg) > (b >= nasg);
     });
     const uint32_t m = (uint32_t)ord.size();
     std::vector<uint32_t> sst(m), sen(m), encl(m);

@@ -211,6 +211,7 @@ void build_kids(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_kids *k) {
   HIP_CHECK(hipMalloc(&k->koff, (n + 2) * sizeof(uint32_t)));
   HIP_CHECK(hipMalloc(&k->kids, (n + 1) * sizeof(uint32_t)));
   if (n == 0) { HIP_CHECK(hipMemsetAsync(k->koff, 0, sizeof(uint32_t), c.stream)); return; }
+  TimedRegion tr(c, "kids", 8 * n + 12 * n);   // tree read; parent copy, offsets, kid ids written
   uint32_t *keys = c.get_as<uint32_t>("kid_keys", n), *vals = c.get_as<uint32_t>("kid_vals", n);
   uint32_t *kalt = c.get_as<uint32_t>("kid_kalt", n), *valt = c.get_as<uint32_t>("kid_valt", n);
   HIP_CHECK(hipMemsetAsync(k->koff, 0, (n + 1) * sizeof(uint32_t), c.stream));

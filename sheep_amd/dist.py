@@ -11,6 +11,8 @@ path (graph2tree.cpp:161-216).
                         rank i with i % 2r == r sends to i - r, which merges.  Merging is
                         associative and commutative (the elimination tree of the union of
                         the parent edges), so the tree at rank 0 equals the serial one.
+  * reduce_eval       — the evaluator's per-shard part bitsets ORed (and its counts
+                        summed) to rank 0 in the same binomial shape;
   * reduce_trees_kway — the same reduction as ONE gather + ONE K-way merge on rank 0
                         (sheep_merge_trees_many): every rank sends its tree straight to
                         rank 0 (each over its own xGMI link, all at once), and the merge
@@ -111,6 +113,26 @@ def reduce_trees_kway(tree: torch.Tensor, merge_many, rank: int, world: int):
     None elsewhere."""
     stacked = gather_trees(tree, rank, world)
     return None if stacked is None else merge_many(stacked)
+
+
+def reduce_eval(ev, rank: int, world: int):
+    """Binomial reduction of ShardedEvaluator states to rank 0: at
+    hop r, rank i with i % 2r == r sends its bitsets and counts to i - r, which ORs / adds
+    them in (sheep_eval_combine; RCCL has no bitwise-OR reduction).  Returns the combined
+    evaluator on rank 0, None elsewhere."""
+    r = 1
+    while r < world:
+        if rank % (2 * r) == r:
+            _send(ev.bits, rank - r)
+            _send(ev.acc, rank - r)
+            return None
+        if rank + r < world:
+            bits = _recv_like(ev.bits, rank + r)
+            acc = _recv_like(ev.acc, rank + r)
+            ev.combine(bits, acc)
+            del bits, acc
+        r *= 2
+    return ev
 
 
 def sync_parts(parts: torch.Tensor | None, pos_size: int, device) -> torch.Tensor:

@@ -69,35 +69,37 @@ class Context {
 };
 inline sheep_ctx *ctx() { return Context::get().handle(); }
 
-// Owning device buffer (move-only).
+// Owning device buffer (move-only), on the process context's device or a given one.
 template <typename T>
 class DeviceArray {
  public:
   DeviceArray() = default;
-  explicit DeviceArray(size_t n) : n_(n) {
+  explicit DeviceArray(size_t n, sheep_ctx *c = nullptr) : n_(n), c_(c ? c : ctx()) {
     void *p = nullptr;
-    check(sheep_malloc(ctx(), (n ? n : 1) * sizeof(T), &p));
+    check(sheep_malloc(c_, (n ? n : 1) * sizeof(T), &p));
     p_ = (T *)p;
   }
-  DeviceArray(DeviceArray &&o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }
+  DeviceArray(DeviceArray &&o) noexcept : p_(o.p_), n_(o.n_), c_(o.c_) { o.p_ = nullptr; o.n_ = 0; }
   DeviceArray &operator=(DeviceArray &&o) noexcept {
     std::swap(p_, o.p_);
     std::swap(n_, o.n_);
+    std::swap(c_, o.c_);
     return *this;
   }
   DeviceArray(const DeviceArray &) = delete;
   DeviceArray &operator=(const DeviceArray &) = delete;
   ~DeviceArray() {
-    if (p_) sheep_free(ctx(), p_);
+    if (p_) sheep_free(c_, p_);
   }
   T *get() const { return p_; }
   size_t size() const { return n_; }
-  void upload(const T *h, size_t cnt) { check(sheep_memcpy_h2d(ctx(), p_, h, cnt * sizeof(T))); }
-  void download(T *h, size_t cnt) const { check(sheep_memcpy_d2h(ctx(), h, p_, cnt * sizeof(T))); }
+  void upload(const T *h, size_t cnt) { check(sheep_memcpy_h2d(c_, p_, h, cnt * sizeof(T))); }
+  void download(T *h, size_t cnt) const { check(sheep_memcpy_d2h(c_, h, p_, cnt * sizeof(T))); }
 
  private:
   T *p_ = nullptr;
   size_t n_ = 0;
+  sheep_ctx *c_ = nullptr;
 };
 
 inline bool is_dat(const char *filename) {
@@ -106,8 +108,11 @@ inline bool is_dat(const char *filename) {
 }
 
 // XS1 records of a .dat file, or pairs of a SNAP text file read the way SNAPReader does
-// (readerwriter.h:166-178: stop at the first pair that does not parse).
-inline std::vector<sheep_xs1> readRecords(const char *filename) {
+// (readerwriter.h:78-90: whitespace-separated pairs, stop at the first pair that does not
+// parse).  skip_comments: lines starting with '#' or '%' are skipped first, as the graph
+// loader does for SNAP / edge-list headers (LLAMA's text loader is un-vendored: that
+// behaviour is parity-unpinned); SNAPReader itself (fileSequence) does not skip them.
+inline std::vector<sheep_xs1> readRecords(const char *filename, bool skip_comments = false) {
   std::vector<sheep_xs1> rec;
   if (is_dat(filename)) {
     FILE *f = fopen(filename, "rb");
@@ -122,9 +127,39 @@ inline std::vector<sheep_xs1> readRecords(const char *filename) {
   } else {
     std::ifstream s(filename);
     if (!s) throw std::bad_alloc();
+    if (skip_comments) {
+      for (int ch = (s >> std::ws).peek(); ch == '#' || ch == '%'; ch = (s >> std::ws).peek()) {
+        std::string line;
+        std::getline(s, line);
+      }
+    }
     vid_t X, Y;
     while ((s >> X) && (s >> Y)) rec.push_back(sheep_xs1{X, Y, 1.0f});
   }
+  return rec;
+}
+
+inline std::vector<char> readBytes(const char *filename) {
+  FILE *f = fopen(filename, "rb");
+  if (!f) throw std::bad_alloc();   // the reference's loaders fail with bad_alloc / abort
+  fseek(f, 0, SEEK_END);
+  const long bytes = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  std::vector<char> b(bytes > 0 ? (size_t)bytes : 0);
+  const size_t got = b.empty() ? 0 : fread(b.data(), 1, b.size(), f);
+  fclose(f);
+  b.resize(got);
+  return b;
+}
+
+// A .net (SNAP text) file parsed on the GPU (sheep_parse_net): the records in HBM.
+// skip_comments: the graph loader's '#' / '%' header lines (see readRecords).
+inline DeviceArray<sheep_xs1> parseNet(const char *filename, bool skip_comments, uint64_t *nrec, sheep_ctx *c = nullptr) {
+  const std::vector<char> text = readBytes(filename);
+  DeviceArray<char> dtext(text.size(), c);
+  if (!text.empty()) dtext.upload(text.data(), text.size());
+  DeviceArray<sheep_xs1> rec(text.size() / 4 + 1, c);   // a record takes >= 4 bytes ("a b\n")
+  check(sheep_parse_net(c ? c : ctx(), dtext.get(), text.size(), skip_comments ? 1 : 0, rec.get(), rec.size(), nrec));
   return rec;
 }
 
@@ -134,7 +169,15 @@ inline std::vector<sheep_xs1> readRecords(const char *filename) {
 class GraphWrapper {
  public:
   GraphWrapper(const char *filename, size_t part = 0, size_t num_parts = 0) {
-    std::vector<sheep_xs1> all = readRecords(filename);
+    std::vector<sheep_xs1> all;
+    if (is_dat(filename)) {
+      all = readRecords(filename);
+    } else {   // SNAP text: parsed on the GPU, the records brought back for the metadata
+      uint64_t n = 0;
+      DeviceArray<sheep_xs1> d = parseNet(filename, true, &n);
+      all.resize(n);
+      if (n) d.download(all.data(), n);
+    }
     size_t beg = 0, end = all.size();
     if (num_parts != 0) {
       beg = (part - 1) * all.size() / num_parts;
@@ -209,11 +252,20 @@ inline size_t GraphWrapper::getNodes() const {
 // fileSequence (sequence.h:95-128): degrees straight from the file records (self-loop
 // +2; XS1Reader hands the last record out twice, readerwriter.h:138-146).
 inline std::vector<vid_t> fileSequence(const char *filename) {
-  std::vector<sheep_xs1> all = readRecords(filename);
+  std::vector<sheep_xs1> all;
+  DeviceArray<sheep_xs1> rec;
+  if (is_dat(filename)) {
+    all = readRecords(filename);
+    rec = DeviceArray<sheep_xs1>(all.size());
+    if (!all.empty()) rec.upload(all.data(), all.size());
+  } else {   // SNAPReader semantics, parsed on the GPU
+    uint64_t n = 0;
+    rec = parseNet(filename, false, &n);
+    all.resize(n);
+    if (n) rec.download(all.data(), n);
+  }
   uint64_t cap = 1;
   for (const sheep_xs1 &r : all) cap = std::max<uint64_t>(cap, (uint64_t)std::max(r.tail, r.head) + 1);
-  DeviceArray<sheep_xs1> rec(all.size());
-  if (!all.empty()) rec.upload(all.data(), all.size());
   DeviceArray<uint32_t> deg(cap);
   std::vector<uint32_t> zero(cap, 0);
   deg.upload(zero.data(), cap);
@@ -357,6 +409,58 @@ class JTree {
   jnid_t size() const { return jnodes.size(); }
 };
 
+// The text files of writePartitionedGraph (partition.cpp:588-670): one SNAP text file per
+// part, PREFIX%04d, lines "X Y"; record i goes to part ep[i].
+//   file_order = true  — partition_tree -o (:632-670): the records as the input file is
+//                        read; an XS1 file repeats its last record (XS1Reader tests eof
+//                        before the read that fails, readerwriter.h:50-57).
+//   file_order = false — graph2tree -p -o (:588-630): the graph's node order, X ascending,
+//                        its adjacency in load (record) order, only X < Y.  LLAMA's own
+//                        edge-iterator order is not in the reference, so the order of lines
+//                        within a file is parity-unpinned here (the line multiset is pinned).
+inline void write_partition_files(const std::vector<sheep_xs1> &rec, const std::vector<int16_t> &ep, part_t max_part,
+                                  uint64_t vmax, const char *prefix, bool file_order, bool is_dat) {
+  const uint64_t R = rec.size();
+  if (max_part >= 10000) throw std::runtime_error("writePartitionedGraph: more than 9999 parts (partition.cpp:599)");
+  std::vector<FILE *> files;
+  std::vector<std::string> bufs(max_part + 1);
+  for (part_t p = 0; p <= max_part; ++p) {
+    char name[4096];
+    snprintf(name, sizeof name, "%s%04d", prefix, (int)p);
+    FILE *f = fopen(name, "w");
+    if (!f) {
+      for (FILE *o : files) fclose(o);
+      throw std::runtime_error(std::string("cannot create ") + name);
+    }
+    files.push_back(f);
+  }
+  auto put = [&](part_t p, uint32_t x, uint32_t y) {
+    std::string &b = bufs.at(p);
+    char line[32];
+    const int len = snprintf(line, sizeof line, "%u %u\n", x, y);
+    b.append(line, len);
+    if (b.size() > (1u << 20)) { fwrite(b.data(), 1, b.size(), files[p]); b.clear(); }
+  };
+  if (file_order) {
+    for (uint64_t i = 0; i < R; ++i) put(ep[i], rec[i].tail, rec[i].head);
+    if (is_dat && R) put(ep[R - 1], rec[R - 1].tail, rec[R - 1].head);
+  } else {
+    // counting sort of the non-loop records by their smaller vid, stable in record order
+    std::vector<uint64_t> start(vmax + 1, 0);
+    for (uint64_t i = 0; i < R; ++i)
+      if (rec[i].tail != rec[i].head) ++start[std::min(rec[i].tail, rec[i].head) + 1];
+    for (uint64_t v = 0; v < vmax; ++v) start[v + 1] += start[v];
+    std::vector<uint64_t> order(start[vmax]);
+    for (uint64_t i = 0; i < R; ++i)
+      if (rec[i].tail != rec[i].head) order[start[std::min(rec[i].tail, rec[i].head)]++] = i;
+    for (uint64_t i : order) put(ep[i], std::min(rec[i].tail, rec[i].head), std::max(rec[i].tail, rec[i].head));
+  }
+  for (part_t p = 0; p <= max_part; ++p) {
+    fwrite(bufs[p].data(), 1, bufs[p].size(), files[p]);
+    fclose(files[p]);
+  }
+}
+
 inline void print_ratio_line(const char *label, uint64_t v, double denom) {
   printf("%s%zu (%f%%)\n", label, (size_t)v, (double)v / denom);
 }
@@ -418,50 +522,10 @@ class Partition {
     check(sheep_edge_parts(ctx(), g.records(), R, seq.pos.get(), seq.pos_size, parts_.get(), dpart.get()));
     std::vector<int16_t> ep(R);
     if (R) dpart.download(ep.data(), R);
-    const std::vector<sheep_xs1> rec = g.hostRecords();
     const std::vector<part_t> pv = parts();
     part_t max_part = -1;
     for (part_t x : pv) max_part = std::max(max_part, x);
-    if (max_part >= 10000) throw std::runtime_error("writePartitionedGraph: more than 9999 parts (partition.cpp:599)");
-    std::vector<FILE *> files;
-    std::vector<std::string> bufs(max_part + 1);
-    for (part_t p = 0; p <= max_part; ++p) {
-      char name[4096];
-      snprintf(name, sizeof name, "%s%04d", prefix, (int)p);
-      FILE *f = fopen(name, "w");
-      if (!f) {
-        for (FILE *o : files) fclose(o);
-        throw std::runtime_error(std::string("cannot create ") + name);
-      }
-      files.push_back(f);
-    }
-    auto put = [&](part_t p, uint32_t x, uint32_t y) {
-      std::string &b = bufs.at(p);
-      char line[32];
-      const int len = snprintf(line, sizeof line, "%u %u\n", x, y);
-      b.append(line, len);
-      if (b.size() > (1u << 20)) { fwrite(b.data(), 1, b.size(), files[p]); b.clear(); }
-    };
-    if (file_order) {
-      for (uint64_t i = 0; i < R; ++i) put(ep[i], rec[i].tail, rec[i].head);
-      if (g.isDat() && R) put(ep[R - 1], rec[R - 1].tail, rec[R - 1].head);
-    } else {
-      // counting sort of the non-loop records by their smaller vid, stable in record order
-      const uint64_t vmax = g.getMaxVid();
-      std::vector<uint64_t> start(vmax + 1, 0);
-      for (uint64_t i = 0; i < R; ++i)
-        if (rec[i].tail != rec[i].head) ++start[std::min(rec[i].tail, rec[i].head) + 1];
-      for (uint64_t v = 0; v < vmax; ++v) start[v + 1] += start[v];
-      std::vector<uint64_t> order(start[vmax]);
-      for (uint64_t i = 0; i < R; ++i)
-        if (rec[i].tail != rec[i].head) order[start[std::min(rec[i].tail, rec[i].head)]++] = i;
-      for (uint64_t i : order)
-        put(ep[i], std::min(rec[i].tail, rec[i].head), std::max(rec[i].tail, rec[i].head));
-    }
-    for (part_t p = 0; p <= max_part; ++p) {
-      fwrite(bufs[p].data(), 1, bufs[p].size(), files[p]);
-      fclose(files[p]);
-    }
+    write_partition_files(g.hostRecords(), ep, max_part, g.getMaxVid(), prefix, file_order, g.isDat());
   }
 
  private:

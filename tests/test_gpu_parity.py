@@ -346,3 +346,82 @@ def test_context_on_another_device(gpu_ctx):
     s = sheep_amd.sequence_from_degrees(deg, vs, ctx=ctx1)
     h = sheep_amd.to_numpy_u32(d).reshape(-1, 3)
     assert np.array_equal(s.numpy(), oracle.sequence(h[:, 0], h[:, 1]))
+
+
+@pytest.mark.parametrize("ranks", [2, 3, 4])
+def test_group_rehearsal_matches_single_gpu(gpu_ctx, ranks):
+    """sheep_group_* (graph2tree -i -r without MPI) with `ranks` edge shards rehearsed on
+    device 0 (device copies stand in for RCCL): the all-reduced sequence, the K-way and
+    the binomial reduce, the parts broadcast and the sharded evaluator all equal the
+    single-GPU results."""
+    import torch
+    import sheep_amd
+    d = sheep_amd.rmat(16, 16, 16)
+    s = sheep_amd.degree_sequence(d)
+    whole = sheep_amd.build_tree(d, s)
+    res = sheep_amd.partition(s, whole, 32)
+    ev = sheep_amd.evaluate(d, s, res.parts)
+    g = sheep_amd.Group([0] * ranks)
+    assert not g.rccl
+    R = d.shape[0]
+    shards = [d[r * R // ranks:(r + 1) * R // ranks].contiguous() for r in range(ranks)]
+    seqs = g.sequence(shards, 1 << 16)
+    for q in seqs:
+        assert q.n == s.n and torch.equal(q.seq[: q.n], s.seq[: s.n])
+    for mode in ("kway", "binomial"):
+        assert torch.equal(g.build_tree(shards, seqs, mode), whole), mode
+    partial = g.build_tree(shards, seqs, "none")
+    assert torch.equal(sheep_amd.merge_trees_many(torch.stack(partial)), whole)
+    parts = g.broadcast_parts(res.parts.clone(), s.pos_size)
+    for p in parts:
+        assert torch.equal(p, res.parts)
+    assert g.evaluate(shards, seqs, parts) == ev
+    g.close()
+
+
+def _snapreader(text: bytes, skip_comments: bool):
+    """SNAPReader (readerwriter.h:78-90) restated on the host: `>> X` then `>> Y` until one
+    fails; with skip_comments, lines whose first token starts with '#'/'%' are dropped first."""
+    toks = []
+    for line in text.decode().splitlines():
+        parts = line.split()
+        if skip_comments and parts and parts[0][0] in "#%":
+            continue
+        toks += parts
+    vals = []
+    for tok in toks:
+        if not tok.isdigit() or int(tok) > 0xFFFFFFFF:
+            break
+        vals.append(int(tok))
+    vals = vals[: len(vals) // 2 * 2]
+    return np.array(vals, dtype=np.uint64).reshape(-1, 2)
+
+
+@pytest.mark.parametrize("skip", [False, True])
+@pytest.mark.parametrize("text", [
+    b"1 2\n3 4\n5 6\n",
+    b"1 2\n3 4\n5",                                   # incomplete last pair
+    b"  10\t20\r\n30    40\r\n\n\n50 60",             # tabs, CRLF, blank lines
+    b"# header\n% more\n1 2\n3 4\n",                  # comment header
+    b"1 2\n# mid comment 7 8\n3 4\n",                 # comment line inside
+    b"1 2\n3 x\n5 6\n",                               # garbage stops the input
+    b"1 2\n4294967295 0\n4294967296 1\n7 8\n",        # u32 overflow stops it
+    b"",
+    b"\n \n",
+])
+def test_parse_net(gpu_ctx, text, skip):
+    import sheep_amd
+    want = _snapreader(text, skip)
+    got = sheep_amd.to_numpy_u32(sheep_amd.parse_net(text, skip)).reshape(-1, 3)
+    assert got.shape[0] == want.shape[0]
+    assert np.array_equal(got[:, :2].astype(np.uint64), want)
+    assert np.all(got[:, 2].view(np.float32) == 1.0)
+
+
+def test_parse_net_large_vs_dat(gpu_ctx):
+    """RMAT-16 written as SNAP text parses back to the same records."""
+    import sheep_amd
+    h = sheep_amd.rmat_host(16, 16, 3)
+    text = "".join(f"{t} {u}\n" for t, u in h[:, :2]).encode()
+    got = sheep_amd.to_numpy_u32(sheep_amd.parse_net(text)).reshape(-1, 3)
+    assert np.array_equal(got[:, :2], h[:, :2])
