@@ -17,7 +17,8 @@ __global__ __launch_bounds__(BLOCK) void k_pack(const T *__restrict__ src, T *__
                                                 const uint64_t *__restrict__ n_in,
                                                 const unsigned long long *__restrict__ counters,
                                                 uint64_t *__restrict__ total_out, const uint64_t *__restrict__ cond,
-                                                unsigned long long *__restrict__ zero_after) {
+                                                unsigned long long *__restrict__ zero_after,
+                                                const uint64_t *__restrict__ dst_off) {
   if (cond && *cond == 0) return;
   __shared__ uint64_t s_prefix, s_count;
   const uint32_t k = blockIdx.x / PACK_SLICES, slice = blockIdx.x % PACK_SLICES;
@@ -36,7 +37,7 @@ __global__ __launch_bounds__(BLOCK) void k_pack(const T *__restrict__ src, T *__
   const uint64_t cnt = s_count, per = (cnt + PACK_SLICES - 1) / PACK_SLICES;
   const uint64_t beg = (uint64_t)slice * per, end = beg + per < cnt ? beg + per : cnt;
   const T *s = src + shard_base(ntiles, k, 1);
-  T *d = dst + s_prefix;
+  T *d = dst + (dst_off ? *dst_off : 0) + s_prefix;
   for (uint64_t i = beg + threadIdx.x; i < end; i += BLOCK) d[i] = s[i];
 }
 
@@ -50,15 +51,17 @@ unsigned long long *shard_counters(Ctx &c, const char *tag) {
 
 template <typename T>
 void pack_shards(Ctx &c, const T *src, T *dst, const uint64_t *n_in, const unsigned long long *counters,
-                 uint64_t *total_out, const uint64_t *cond, unsigned long long *zero_after) {
+                 uint64_t *total_out, const uint64_t *cond, unsigned long long *zero_after, const uint64_t *dst_off) {
   hipLaunchKernelGGL(k_pack<T>, dim3(NSHARD * PACK_SLICES), dim3(BLOCK), 0, c.stream, src, dst, n_in, counters,
-                     total_out, cond, zero_after);
+                     total_out, cond, zero_after, dst_off);
   LAUNCH_CHECK();
 }
 
 template void pack_shards<uint32_t>(Ctx &, const uint32_t *, uint32_t *, const uint64_t *,
-                                    const unsigned long long *, uint64_t *, const uint64_t *, unsigned long long *);
+                                    const unsigned long long *, uint64_t *, const uint64_t *, unsigned long long *,
+                                    const uint64_t *);
 template void pack_shards<uint64_t>(Ctx &, const uint64_t *, uint64_t *, const uint64_t *,
-                                    const unsigned long long *, uint64_t *, const uint64_t *, unsigned long long *);
+                                    const unsigned long long *, uint64_t *, const uint64_t *, unsigned long long *,
+                                    const uint64_t *);
 
 }  // namespace sheep

@@ -304,9 +304,11 @@ void spread_params(uint64_t n, int *L, uint32_t *clo);
 // append.hip — sharded appends: counters (NSHARD * SHARD_STRIDE u64, zeroed).  The pack
 // step moves the shard regions of a producer that streamed *n_in items together in dst
 // and writes the total to *total_out (device; must not alias n_in).  With cond, it runs
-// only if *cond != 0, and then also zeroes the counter set zero_after.  No host sync.
+// only if *cond != 0, and then also zeroes the counter set zero_after.  With dst_off the
+// packed items start at dst + *dst_off (a device count).  No host sync.
 unsigned long long *shard_counters(Ctx &c, const char *tag);
 template <typename T>
 void pack_shards(Ctx &c, const T *src, T *dst, const uint64_t *n_in, const unsigned long long *counters,
-                 uint64_t *total_out, const uint64_t *cond = nullptr, unsigned long long *zero_after = nullptr);
+                 uint64_t *total_out, const uint64_t *cond = nullptr, unsigned long long *zero_after = nullptr,
+                 const uint64_t *dst_off = nullptr);
 }  // namespace sheep

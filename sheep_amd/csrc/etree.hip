@@ -155,12 +155,13 @@ __global__ __launch_bounds__(BLOCK) void k_relabel(const sheep_xs1 *__restrict__
 // stale or dead entries for long and needs no separate compaction.
 //
 // stats row of level l (u64): [0] list length entering the level, [1] light edges,
-// [2] cross edges, [3] entries that stayed, [5..7] unresolved light edges after hooking
-// round 0..2, [10] edges activated from the level's bucket.
-constexpr int ST_ROW = 16, ST_LIVE = 0, ST_NL = 1, ST_NX = 2, ST_KEPT = 3, ST_HOOK = 5, ST_R0 = 10;
+// [2] cross edges, [3] entries that stayed, [4] contractions that survived, [5..7]
+// unresolved light edges after hooking round 0..2, [10] edges activated from the
+// level's bucket.
+constexpr int ST_ROW = 16, ST_LIVE = 0, ST_NL = 1, ST_NX = 2, ST_KEPT = 3, ST_CONTR = 4, ST_HOOK = 5, ST_R0 = 10;
 constexpr int HOOK_ROUNDS = 3;
-// counter sets zeroed at every level: hook rounds (sharded appends)
-constexpr int CSET_HOOK = 0, NCSET = CSET_HOOK + HOOK_ROUNDS;
+// counter sets zeroed at every level: hook rounds and the contractions (sharded appends)
+constexpr int CSET_HOOK = 0, CSET_APPLY = CSET_HOOK + HOOK_ROUNDS, NCSET = CSET_APPLY + 1;
 constexpr uint64_t CSET_WORDS = (uint64_t)NSHARD * SHARD_STRIDE;
 
 // ---- first-activity buckets ---------------------------------------------------------
@@ -373,66 +374,49 @@ __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict
 // edges into one hub, all carry the same m.)  claim is n x u32, L3-resident, unlike a
 // global hash table of the pairs.
 //
-// The contracted edges are APPENDED to the next list, after the entries k_split kept:
-// cross edge j goes to next[kept + j] (DEAD if it died) — a sequential write.
-// RMAT-26 (~49M cross edges per level): batched 18.8 -> 18.3 ms per step; RMAT-22 (a few
-// million): batched 2.0 -> 2.9 ms, so small levels keep one edge per lane
-constexpr uint64_t CROSS_APPLY_BATCH_MIN = 1ull << 24;
+// The surviving contractions are APPENDED to the next list, after the entries k_split
+// kept: each 2048-edge tile reserves its survivors' slots in a sharded append (one
+// atomic per tile on one of 64 counters) and k_pack moves the shard regions behind the
+// kept entries, so the next level reads no dead slots (at RMAT-26 most contractions die
+// as duplicates: 80% of a level's list was dead slots).  Every gather stage is issued
+// for all of a thread's 8 edges before the next (xtop/xbuf, then mt, then claim).
 __global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restrict__ xbuf, const uint32_t *__restrict__ xtop,
                                                        const uint64_t *__restrict__ st, const uint32_t *__restrict__ mt,
                                                        const uint32_t *__restrict__ top, uint32_t *__restrict__ claim,
-                                                       uint64_t *__restrict__ next, uint32_t *__restrict__ parent,
-                                                       uint64_t n) {
+                                                       uint64_t *__restrict__ scratch,
+                                                       unsigned long long *__restrict__ counters,
+                                                       uint32_t *__restrict__ parent, uint64_t n) {
   const uint64_t nx = st[ST_NX];
   const bool sparse = level_sparse(st[ST_NL], nx, n);
-  uint64_t *out = next + st[ST_KEPT];
-  if (nx < CROSS_APPLY_BATCH_MIN) {   // small levels: one edge per lane keeps more waves busy
-    const uint64_t stride1 = (uint64_t)gridDim.x * BLOCK;
-    for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < nx; j += stride1) {
-      const uint32_t r = xtop[j], m = mt[r];
-      if (sparse) parent[top[r]] = m;   // jnode.h:158-162 adopt (all cross edges of r store the same m)
-      const uint32_t b = (uint32_t)(xbuf[j] >> 32);
-      bool kill = b == m;
-      if (!kill) {
-        uint32_t c = claim[b];
-        if (c == INVALID) c = atomicCAS(&claim[b], INVALID, m);
-        kill = c == m;   // someone else's (m, b) is kept (our own successful CAS returned INVALID)
-      }
-      out[j] = kill ? DEAD : ((uint64_t)b << 32) | m;
-    }
-    return;
-  }
-  // large levels: XK edges per thread with every gather stage issued for all of them
-  // before the next (xtop/xbuf, then mt, then claim): XK independent chains per lane
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK * XK;
-  for (uint64_t j0 = (uint64_t)blockIdx.x * BLOCK * XK + threadIdx.x; j0 < nx; j0 += stride) {
-    uint32_t r[XK], b[XK], m[XK], cl[XK];
-    bool live[XK];
+  const uint64_t ntiles = (nx + TILE - 1) / TILE;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    uint32_t r[TILE_ITEMS], b[TILE_ITEMS], m[TILE_ITEMS], cl[TILE_ITEMS];
+    uint32_t keep = 0;
 #pragma unroll
-    for (int k = 0; k < XK; ++k) {
-      const uint64_t j = j0 + (uint64_t)k * BLOCK;
-      live[k] = j < nx;
-      r[k] = live[k] ? xtop[j] : 0;
-      b[k] = live[k] ? (uint32_t)(xbuf[j] >> 32) : 0;
+    for (int k = 0; k < TILE_ITEMS; ++k) {
+      const uint64_t j = tile * TILE + (uint64_t)k * BLOCK + threadIdx.x;
+      const bool live = j < nx;
+      r[k] = live ? xtop[j] : INVALID;
+      b[k] = live ? (uint32_t)(xbuf[j] >> 32) : 0;
     }
 #pragma unroll
-    for (int k = 0; k < XK; ++k) m[k] = live[k] ? mt[r[k]] : INVALID;
+    for (int k = 0; k < TILE_ITEMS; ++k) m[k] = r[k] != INVALID ? mt[r[k]] : INVALID;
 #pragma unroll
-    for (int k = 0; k < XK; ++k) {
-      if (live[k] && sparse) parent[top[r[k]]] = m[k];   // jnode.h:158-162 adopt (all cross edges of r store the same m)
-      cl[k] = live[k] && b[k] != m[k] ? claim[b[k]] : 0;
+    for (int k = 0; k < TILE_ITEMS; ++k) {
+      if (r[k] != INVALID && sparse) parent[top[r[k]]] = m[k];   // jnode.h:158-162 adopt (every cross edge of r stores the same m)
+      cl[k] = r[k] != INVALID && b[k] != m[k] ? claim[b[k]] : 0;
     }
 #pragma unroll
-    for (int k = 0; k < XK; ++k) {
-      if (!live[k]) continue;
-      bool kill = b[k] == m[k];
-      if (!kill) {
-        uint32_t c = cl[k];
-        if (c == INVALID) c = atomicCAS(&claim[b[k]], INVALID, m[k]);
-        kill = c == m[k];   // someone else's (m, b) is kept (our own successful CAS returned INVALID)
-      }
-      out[j0 + (uint64_t)k * BLOCK] = kill ? DEAD : ((uint64_t)b[k] << 32) | m[k];
+    for (int k = 0; k < TILE_ITEMS; ++k) {
+      if (r[k] == INVALID || b[k] == m[k]) continue;
+      uint32_t c = cl[k];
+      if (c == INVALID) c = atomicCAS(&claim[b[k]], INVALID, m[k]);
+      if (c != m[k]) keep |= 1u << k;   // someone else's (m, b) is kept (our own successful CAS returned INVALID)
     }
+    uint64_t slot = shard_reserve((uint32_t)__popc(keep), counters, tile, ntiles, 1);
+#pragma unroll
+    for (int k = 0; k < TILE_ITEMS; ++k)
+      if (keep & (1u << k)) scratch[slot++] = ((uint64_t)b[k] << 32) | m[k];
   }
 }
 
@@ -462,7 +446,7 @@ struct SplitIn {
   uint64_t len, rb, m;
   __device__ SplitIn(const uint64_t *l, const uint64_t *prev, const uint64_t *r, const uint64_t *seg, int s, int L)
       : list(l), r0(r) {
-    len = prev ? prev[ST_KEPT] + prev[ST_NX] : 0;
+    len = prev ? prev[ST_KEPT] + prev[ST_CONTR] : 0;
     rb = seg[s];
     m = len + (seg[L + s] - rb);
   }
@@ -588,7 +572,7 @@ __global__ void k_fin_gather(const uint64_t *__restrict__ list, const uint64_t *
                              const uint64_t *__restrict__ r0, uint64_t rb, uint64_t re, uint64_t *__restrict__ out,
                              uint64_t *__restrict__ n_out) {
   // out = list ++ r0[rb, re), halves swapped (lo << 32 | hi) so a sort on the low bits sorts by hi
-  const uint64_t len = prev ? prev[ST_KEPT] + prev[ST_NX] : 0, m = len + (re - rb);
+  const uint64_t len = prev ? prev[ST_KEPT] + prev[ST_CONTR] : 0, m = len + (re - rb);
   if (blockIdx.x == 0 && threadIdx.x == 0) *n_out = m;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
@@ -819,8 +803,8 @@ void spread_params(uint64_t n, int *L_out, uint32_t *clo_out) {
   *clo_out = (uint32_t)(cfull - (((unsigned __int128)1) << 32));
 }
 
-// A level's next list holds the entries that stayed (alive, <= m) plus one contraction
-// slot per cross edge (<= m).
+// A level's next list holds the entries that stayed (alive, <= m) plus the surviving
+// contractions (<= one per cross edge, <= m).
 static uint64_t list_capacity(uint64_t m) { return 2 * m + TILE; }
 
 // Elimination tree of `m` edges ((hi<<32)|lo, lo < hi < n, DEAD holes allowed), grouped
@@ -929,9 +913,11 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     }
     {
       TimedRegion tr(c, "etree_apply");
-      hipLaunchKernelGGL(k_cross_apply, dim3(grid_for(m)), dim3(BLOCK), 0, c.stream, (const uint64_t *)xbuf,
-                         (const uint32_t *)xtop, (const uint64_t *)st, (const uint32_t *)mt, (const uint32_t *)top, claim, next, parent, n);
+      hipLaunchKernelGGL(k_cross_apply, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)xbuf,
+                         (const uint32_t *)xtop, (const uint64_t *)st, (const uint32_t *)mt, (const uint32_t *)top, claim,
+                         alt, cset(CSET_APPLY), parent, n);
       LAUNCH_CHECK();
+      pack_shards<uint64_t>(c, alt, next, st + ST_NX, cset(CSET_APPLY), st + ST_CONTR, nullptr, nullptr, st + ST_KEPT);
       hipLaunchKernelGGL(k_level_clean, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
                          (const uint64_t *)xbuf, (const uint32_t *)xtop, (const uint64_t *)st, uf, mt, top, claim, n,
                          parent, csets);
@@ -1018,9 +1004,9 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     c.add_bytes("etree_cross", 12 * r[ST_NX]);
     c.add_bytes("etree_apply", 20 * r[ST_NX]);
     if (g_debug_etree)
-      fprintf(stderr, "etree lvl %d s %d list %lu bucket %lu kept %lu light %lu cross %lu hook-left %lu %lu %lu\n", lvl,
-              L - 1 - lvl, (unsigned long)r[ST_LIVE], (unsigned long)r[ST_R0], (unsigned long)r[ST_KEPT],
-              (unsigned long)r[ST_NL], (unsigned long)r[ST_NX], (unsigned long)r[ST_HOOK],
+      fprintf(stderr, "etree lvl %d s %d list %lu bucket %lu kept %lu light %lu cross %lu contractions %lu hook-left %lu %lu %lu\n",
+              lvl, L - 1 - lvl, (unsigned long)r[ST_LIVE], (unsigned long)r[ST_R0], (unsigned long)r[ST_KEPT],
+              (unsigned long)r[ST_NL], (unsigned long)r[ST_NX], (unsigned long)r[ST_CONTR], (unsigned long)r[ST_HOOK],
               (unsigned long)r[ST_HOOK + 1], (unsigned long)r[ST_HOOK + 2]);
   }
 }

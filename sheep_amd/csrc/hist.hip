@@ -169,6 +169,51 @@ __global__ __launch_bounds__(HB) void k_hist_scatter(Src src, uint64_t n, uint32
   }
 }
 
+// k_hist_scatter for key ranges whose bucket counters and a whole staged tile do not fit
+// LDS together (more than ~4087 buckets, vertex ids above 2^27): the tile's keys are
+// counting-sorted SUB = PER * HB at a time, each bucket's run of a sub-tile written at the
+// bucket's running cursor (the same (bucket, tile) regions as k_hist_scatter).
+template <typename Src, int PER>
+__global__ __launch_bounds__(HB) void k_hist_scatter_staged(Src src, uint64_t n, uint32_t nb,
+                                                            const uint32_t *__restrict__ offsets, uint64_t ntiles,
+                                                            uint16_t *__restrict__ out) {
+  constexpr uint32_t SUB = PER * HB;
+  extern __shared__ uint32_t lds[];
+  uint32_t *cur = lds, *gb = lds + nb, *wsum = lds + 2 * nb;
+  uint32_t *stage = lds + 2 * nb + HB / WAVE;
+  const uint64_t tile = blockIdx.x;
+  for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] = offsets[(uint64_t)b * ntiles + tile];
+  const uint64_t base = tile << TLOG;
+  for (uint32_t s0 = 0; s0 < TKEYS; s0 += SUB) {
+    for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
+    __syncthreads();
+    uint32_t k[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint64_t i = base + s0 + (uint64_t)j * HB + threadIdx.x;
+      k[j] = i < n ? src(i) : NO_KEY;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      if (k[j] != NO_KEY) atomicAdd(&cur[k[j] >> WBITS], 1u);
+    __syncthreads();
+    const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
+    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] -= cur[b];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      if (k[j] != NO_KEY) stage[atomicAdd(&cur[k[j] >> WBITS], 1u)] = k[j];
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < total; j += HB) {
+      const uint32_t key = stage[j];
+      out[gb[key >> WBITS] + j] = (uint16_t)(key & (W - 1));
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += cur[b];
+    __syncthreads();
+  }
+}
+
 // k_hist_scatter for tree edges grouped by padded lo: besides the u16 key runs it moves
 // each edge into `grouped` at the same position, so the elimination tree's input comes
 // out in lo-bucket order at no extra read.  SUB = PER * HB edges at a time are
@@ -283,12 +328,13 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
   const uint32_t nb = (uint32_t)((K + W - 1) >> WBITS);
   const uint64_t ntiles = (n + TKEYS - 1) >> TLOG;
   const size_t lds_scatter = (2 * (size_t)nb + HB / WAVE + TKEYS) * 4;   // <= 160 KiB for nb <= 4087
+  const size_t lds_scatter16 = (2 * (size_t)nb + HB / WAVE + 16 * HB) * 4;   // staged: nb <= 8192
   // the staged grouping scatter holds 2 nb counters + PER * HB staged edges: nb <= 8192
   // (lds_exclusive_scan's limit) with PER = 8, i.e. padded lo ranges up to 2^28
   const size_t lds_staged16 = ((2 * (size_t)nb + HB / WAVE + 1) & ~(size_t)1) * 4 + 16 * HB * 8;
   const size_t lds_staged8 = lds_staged16 - 8 * HB * 8;
   const bool fits = std::is_same<Src, EdgeLoPadded>::value ? (nb <= 8 * HB && lds_staged8 <= 160 * 1024)
-                                                            : lds_scatter <= 160 * 1024;
+                                                            : (nb <= 8 * HB && lds_scatter16 <= 160 * 1024);
   if (!fits || ntiles * nb >= (1ull << 32) || n >= (1ull << 32)) {
     if constexpr (std::is_same<Src, EdgeLoPadded>::value) {
       throw Error(SHEEP_ERR_ARG, "group_edges_by_lo: padded lo range above 2^28 or 2^32 edges");
@@ -299,8 +345,9 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
     }
   }
   for (const void *f : {(const void *)k_hist_scatter<HeadKeys>, (const void *)k_hist_scatter<EdgeLoKeys>,
-                        (const void *)k_hist_final, (const void *)k_lo_scatter_staged<16>,
-                        (const void *)k_lo_scatter_staged<8>})
+                        (const void *)k_hist_scatter_staged<HeadKeys, 16>,
+                        (const void *)k_hist_scatter_staged<EdgeLoKeys, 16>, (const void *)k_hist_final,
+                        (const void *)k_lo_scatter_staged<16>, (const void *)k_lo_scatter_staged<8>})
     allow_full_lds(f);
   uint32_t *tile_hist = c.get_as<uint32_t>("hist_tiles", ntiles * nb + 1);
   uint16_t *keys = c.get_as<uint16_t>("hist_keys", n);
@@ -322,9 +369,12 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
     else
       hipLaunchKernelGGL(k_lo_scatter_staged<8>, dim3((unsigned)ntiles), dim3(HB), lds_staged8, c.stream, src, n, nb,
                          (const uint32_t *)tile_hist, ntiles, keys, grouped);
-  } else {
+  } else if (lds_scatter <= 160 * 1024) {
     hipLaunchKernelGGL(k_hist_scatter<Src>, dim3((unsigned)ntiles), dim3(HB), lds_scatter, c.stream, src, n, nb,
                        (const uint32_t *)tile_hist, ntiles, keys);
+  } else {
+    hipLaunchKernelGGL((k_hist_scatter_staged<Src, 16>), dim3((unsigned)ntiles), dim3(HB), lds_scatter16, c.stream, src, n,
+                       nb, (const uint32_t *)tile_hist, ntiles, keys);
   }
   LAUNCH_CHECK();
   // bucket starts (column 0 of the bucket-major offsets) -> chunk list
@@ -555,7 +605,7 @@ __global__ void k_seg_from_buckets(const uint32_t *__restrict__ bstart, const ui
 bool degree_fused(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap,
                   unsigned long long *d_max, unsigned long long *d_err) {
   const uint64_t nb = (cap + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
-  if (nrec == 0 || nb == 0 || nb > 4096 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return false;
+  if (nrec == 0 || nb == 0 || nb > 8192 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return false;
   uint32_t *tile_hist = c.get_as<uint32_t>("hist_tiles", ntiles * nb + 1);
   hipLaunchKernelGGL(k_degree_fused, dim3((unsigned)ntiles), dim3(CB), nb * 4, c.stream, rec, nrec, mode, deg, cap,
                      (uint32_t)nb, tile_hist, ntiles, d_max, d_err);
@@ -568,7 +618,7 @@ void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uin
   hl.valid = false;
   hl.bstart.clear();
   const uint64_t nb = (K + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
-  if (!llama || nb == 0 || nb > 4096 || ntiles * nb + 1 >= (1ull << 32)) {
+  if (!llama || nb == 0 || nb > 8192 || ntiles * nb + 1 >= (1ull << 32)) {
     histogram_add(c, HeadKeys{rec, llama}, nrec, K, cnt, nullptr, nullptr, nullptr, nullptr, nullptr, counted);
     return;
   }
@@ -583,7 +633,7 @@ void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uin
 uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
                           uint32_t *pst, uint64_t *edges, unsigned long long *err) {
   const uint64_t nb = (pos_size + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
-  if (nrec == 0 || nb == 0 || nb > 4096 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return UINT64_MAX;
+  if (nrec == 0 || nb == 0 || nb > 8192 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return UINT64_MAX;
   for (const void *f : {(const void *)k_relabel_scatter<8>, (const void *)k_relabel_scatter<4>,
                         (const void *)k_relabel_gather})
     allow_full_lds(f);
@@ -613,8 +663,10 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   const size_t fixed = ((3 * nb + HB / WAVE + 1) & ~1ull) * 4;
   auto scatter = [&]() {
     HIP_CHECK(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c.stream));
-    // 8K-record sub-tiles (4K / 16K measured 15.8 / 15.3 ms against 14.3 at RMAT-26)
+    // 8K-record sub-tiles (4K / 16K measured 15.8 / 15.3 ms against 14.3 at RMAT-26);
+    // 4K when the bucket cursors take more LDS (vertex ids above 2^27)
     const int per = fixed + 8 * HB * 8 <= 160 * 1024 ? 8 : 4;
+    if (fixed + (size_t)per * HB * 8 > 160 * 1024) throw Error(SHEEP_ERR_ARG, "relabel: bucket layout exceeds LDS");
     const size_t lds = fixed + (size_t)per * HB * 8;
     const dim3 g((unsigned)ntiles), b(HB);
     const uint32_t nb32 = (uint32_t)nb;

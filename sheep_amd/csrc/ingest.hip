@@ -22,7 +22,6 @@ namespace {
 
 constexpr int NB_PER = 16;                  // bytes per thread
 constexpr int NB_TILE = BLOCK * NB_PER;     // 4 KiB per workgroup tile
-constexpr uint32_t BAD = 0xFFFFFFFFu;
 
 __device__ __forceinline__ bool blank(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f'; }
 
@@ -69,8 +68,9 @@ __global__ __launch_bounds__(BLOCK) void k_tok_write(const char *__restrict__ te
     if (base + j < bytes && tok_start(text, base + j)) tpos[off++] = base + j;
 }
 
-// value (BAD when not an unsigned 32-bit decimal); flags: 1 = a newline precedes the token
-// (or it is the first), 2 = it opens a comment line ('#' or '%' first on its line)
+// value; flags: 1 = a newline precedes the token (or it is the first), 2 = it opens a
+// comment line ('#' or '%' first on its line), 4 = not an unsigned 32-bit decimal
+// (4294967295 is a valid value, so validity is a flag, not a sentinel)
 __global__ __launch_bounds__(BLOCK) void k_tok_parse(const char *__restrict__ text, uint64_t bytes,
                                                      const uint64_t *__restrict__ tpos, uint64_t ntok,
                                                      uint32_t *__restrict__ val, uint32_t *__restrict__ linestart,
@@ -91,10 +91,10 @@ __global__ __launch_bounds__(BLOCK) void k_tok_parse(const char *__restrict__ te
       else { v = v * 10 + (uint32_t)(ch - '0'); ++digits; }
     }
     ok = ok && digits > 0 && v <= 0xFFFFFFFFull;
-    val[t] = ok ? (uint32_t)v : BAD;
+    val[t] = (uint32_t)v;
     const char c0 = text[p];
     linestart[t] = nl ? 1u : 0u;
-    flags[t] = (nl ? 1 : 0) | (nl && (c0 == '#' || c0 == '%') ? 2 : 0);
+    flags[t] = (nl ? 1 : 0) | (nl && (c0 == '#' || c0 == '%') ? 2 : 0) | (ok ? 0 : 4);
   }
 }
 
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(BLOCK) void k_tok_keep(const uint32_t *__restrict__
     // lineid: inclusive count of line starts up to t, so the token's line is lineid - 1
     const bool dropped = skip_comments && comment[lineid[t] - 1];
     keep[t] = dropped ? 0u : 1u;
-    if (!dropped && val[t] == BAD && t < fb) fb = t;
+    if (!dropped && (flags[t] & 4) && t < fb) fb = t;
   }
   fb = wave_min(fb);
   if ((threadIdx.x & 63) == 0 && fb != ~0ull) atomicMin(first_bad, (unsigned long long)fb);

@@ -22,6 +22,7 @@
 //      ancestor-or-self (assigned = packed kids + roots), found by binary search over
 //      the assigned nodes' Euler-tour intervals (laminar), then re-indexes jnid -> vid.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <vector>
 
@@ -261,15 +262,14 @@ __global__ void k_core_build(const uint32_t *__restrict__ kids, uint64_t nk, con
 
 // ---- packing events with lazily computed residuals ------------------------------------
 // R(a) = cb(a) when forwardPartition's ascending pass reaches a = S(a) minus the weight
-// removed by every earlier packing at a or below a.  A packing event e at node v_e
-// removes delta_e from v_e and its ancestors: a is hit iff v_e == a or tD(v_e) lies in
-// a's tour interval.  Events are few (one per packing node), so R is evaluated on the
-// fly from the event list instead of being pushed up the (10^6-deep) ancestor chains.
-struct PackEv {
-  uint32_t v, vpos;   // packed node, tD(v) (INVALID for a root)
-  uint64_t delta;     // weight its packing removed
-};
-constexpr int EV_LDS = 2048;
+// removed by every earlier packing at a or below a.  A packing at a non-root v removes
+// delta from v and its ancestors: a is hit iff tD(v) lies in a's tour interval.  The host
+// keeps the events sorted by tD(v) with prefix sums of their deltas (EvTable, copied to
+// the device before each scan), so R(a) = S(a) - (prefix sum over the events inside a's
+// interval): two binary searches, whatever the number of events.  A packing at a root
+// changes only that root, which no later candidate is (candidates have larger ids), and
+// the host subtracts it from the root's final residual itself.
+constexpr int EV_LDS = 4096;   // event table entries held in LDS (larger tables: global reads)
 
 // a's tour interval in the core: [tD, tU] for a non-root, its kids' span for a core root
 __device__ __forceinline__ void node_interval(uint32_t a, const uint32_t *cparent, const uint32_t *ckoff,
@@ -279,43 +279,51 @@ __device__ __forceinline__ void node_interval(uint32_t a, const uint32_t *cparen
   else if (ckoff[a] < ckoff[a + 1]) { lo = rst[a]; hi = ren[a]; }
   else { lo = INVALID; hi = INVALID; }
 }
-// events in LDS (the first EV_LDS; later ones from the device list)
-__device__ __forceinline__ uint64_t lazy_r(uint32_t a, uint64_t r, uint32_t lo, uint32_t hi, const PackEv *sev,
-                                           const PackEv *ev, uint32_t nev) {
-  for (uint32_t e = 0; e < nev; ++e) {
-    const PackEv x = e < EV_LDS ? sev[e] : ev[e];
-    if (x.v == a || (lo != INVALID && x.vpos != INVALID && lo <= x.vpos && x.vpos <= hi)) r -= x.delta;
+
+// event table: m sorted positions, prefix sums pre[0..m] (pre[i] = sum of deltas before i)
+struct EvView {
+  const uint32_t *pos;
+  const uint64_t *pre;
+  uint32_t m;
+  __device__ uint32_t lower(uint32_t x) const {   // first i with pos[i] >= x
+    uint32_t a = 0, b = m;
+    while (a < b) { const uint32_t c = (a + b) >> 1; if (pos[c] < x) a = c + 1; else b = c; }
+    return a;
   }
-  return r;
-}
-__device__ __forceinline__ void load_events(const PackEv *ev, uint32_t nev, PackEv *sev) {
-  const uint32_t nl = nev < EV_LDS ? nev : EV_LDS;
-  for (uint32_t e = threadIdx.x; e < nl; e += blockDim.x) sev[e] = ev[e];
+  __device__ uint64_t removed(uint32_t lo, uint32_t hi) const {   // deltas with lo <= pos <= hi
+    if (lo == INVALID || m == 0) return 0;
+    const uint32_t i = lower(lo), j = hi == INVALID ? m : lower(hi + 1);
+    return j > i ? pre[j] - pre[i] : 0;
+  }
+};
+
+// loads the table into LDS when it fits (every thread of the block must call it)
+__device__ __forceinline__ EvView load_table(const uint32_t *gpos, const uint64_t *gpre, uint32_t m, uint32_t *spos,
+                                             uint64_t *spre) {
+  if (m > EV_LDS) return EvView{gpos, gpre, m};
+  for (uint32_t i = threadIdx.x; i <= m; i += blockDim.x) {
+    if (i < m) spos[i] = gpos[i];
+    spre[i] = gpre[i];
+  }
   __syncthreads();
+  return EvView{spos, spre, m};
 }
 
 // The next packing node: the lowest-index heavy node after the last packing node whose
 // residual exceeds max_component.  Workgroups take 2048-entry chunks in index order and
 // stop once a hit below their chunk is known, so an event reads about the distance to
-// the next packing node instead of the whole heavy set.  Block 0 also stores the last
-// event's delta (computed by the host) into the device event list.
+// the next packing node instead of the whole heavy set.
 constexpr int EVI = 8, EV_CH = BLOCK * EVI;
 __global__ __launch_bounds__(BLOCK) void k_next_event(const uint32_t *__restrict__ hids, uint64_t nh,
                                                       const uint64_t *__restrict__ SH, const uint32_t *__restrict__ hst,
-                                                      const uint32_t *__restrict__ hen, PackEv *__restrict__ evl,
-                                                      uint32_t nev, uint64_t last_delta, uint64_t maxc,
+                                                      const uint32_t *__restrict__ hen, const uint32_t *__restrict__ epos,
+                                                      const uint64_t *__restrict__ epre, uint32_t m, uint64_t maxc,
                                                       const uint64_t *__restrict__ evprev,
                                                       unsigned long long *__restrict__ found) {
-  __shared__ PackEv sev[EV_LDS];
+  __shared__ uint32_t spos[EV_LDS];
+  __shared__ uint64_t spre[EV_LDS + 1];
   __shared__ unsigned long long s_best[BLOCK / WAVE];
-  if (nev && blockIdx.x == 0 && threadIdx.x == 0) evl[nev - 1].delta = last_delta;
-  const uint32_t nl = nev < EV_LDS ? nev : EV_LDS;
-  for (uint32_t e = threadIdx.x; e < nl; e += BLOCK) {
-    PackEv x = evl[e];
-    if (e == nev - 1) x.delta = last_delta;
-    sev[e] = x;
-  }
-  __syncthreads();
+  const EvView ev = load_table(epos, epre, m, spos, spre);
   const uint64_t prev = *evprev;
   const uint64_t start = prev == ~0ull ? 0 : (uint32_t)prev;
   const uint32_t vlast = prev == ~0ull ? INVALID : (uint32_t)(prev >> 32);
@@ -331,13 +339,7 @@ __global__ __launch_bounds__(BLOCK) void k_next_event(const uint32_t *__restrict
       if (h >= nh) continue;
       const uint32_t a = hids[h];
       if (vlast != INVALID && a <= vlast) continue;
-      uint64_t r = SH[h];
-      const uint32_t lo = hst[h], hi = hen[h];
-      for (uint32_t e = 0; e < nev && r > maxc; ++e) {
-        const PackEv x = e < EV_LDS ? sev[e] : evl[e];
-        const uint64_t d = e == nev - 1 ? last_delta : x.delta;
-        if (x.v == a || (lo != INVALID && x.vpos != INVALID && lo <= x.vpos && x.vpos <= hi)) r -= d;
-      }
+      const uint64_t r = SH[h] - ev.removed(hst[h], hen[h]);
       if (r > maxc) {
         const unsigned long long key = ((unsigned long long)a << 32) | h;
         best = key < best ? key : best;
@@ -356,56 +358,63 @@ __global__ __launch_bounds__(BLOCK) void k_next_event(const uint32_t *__restrict
 }
 
 // Everything the host needs for one packing event, stored straight into mapped host
-// memory: hdr = {v, koff[v], #kids, R[v] lo, R[v] hi}, then the node's kids in their
-// current order and their residuals (the first `cap` of them).  The event is appended
-// to the device list (delta filled in by the next k_next_event).
+// memory: hdr = {v, koff[v], #kids, R[v] lo, R[v] hi, tD(v) (INVALID for a root)}, then
+// the node's kids in their current order and their residuals (the first `cap` of them).
+// The last workgroup to finish raises hdr[7] = seq (system-scope), which the host polls
+// instead of synchronising the stream.
 constexpr uint32_t EV_STAGE = 1u << 16;
 __global__ __launch_bounds__(BLOCK) void k_event_stage(const unsigned long long *__restrict__ found,
-                                                       uint64_t *__restrict__ evprev, PackEv *__restrict__ evl,
-                                                       uint32_t nev, const uint32_t *__restrict__ koff,
+                                                       uint64_t *__restrict__ evprev, const uint32_t *__restrict__ epos,
+                                                       const uint64_t *__restrict__ epre, uint32_t m,
+                                                       const uint32_t *__restrict__ koff,
                                                        const uint32_t *__restrict__ kids, const uint64_t *__restrict__ S,
                                                        const uint32_t *__restrict__ cparent,
                                                        const uint32_t *__restrict__ ckoff, const uint32_t *__restrict__ tD,
                                                        const uint32_t *__restrict__ tU, const uint32_t *__restrict__ rst,
                                                        const uint32_t *__restrict__ ren, uint32_t *__restrict__ hdr,
                                                        uint32_t *__restrict__ kid_out, uint64_t *__restrict__ r_out,
-                                                       uint32_t beg_j, uint32_t cap) {
-  __shared__ PackEv sev[EV_LDS];
+                                                       uint32_t beg_j, uint32_t cap, unsigned *__restrict__ done,
+                                                       uint32_t seq) {
+  __shared__ uint32_t spos[EV_LDS];
+  __shared__ uint64_t spre[EV_LDS + 1];
+  __shared__ bool last;
   const uint64_t e = *found;
   const uint32_t v = e == ~0ull ? INVALID : (uint32_t)(e >> 32);
-  if (v == INVALID) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = INVALID;
-    return;
-  }
-  load_events(evl, nev, sev);
-  const uint32_t beg = koff[v], cnt = koff[v + 1] - beg;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && beg_j == 0) {
-    *evprev = e;
-    uint32_t lo, hi;
-    node_interval(v, cparent, ckoff, tD, tU, rst, ren, lo, hi);
-    const uint64_t r = lazy_r(v, S[v], lo, hi, sev, evl, nev);
-    PackEv x;
-    x.v = v;
-    x.vpos = cparent[v] == INVALID ? INVALID : tD[v];
-    x.delta = 0;
-    evl[nev] = x;
-    hdr[0] = v;
-    hdr[1] = beg;
-    hdr[2] = cnt;
-    hdr[3] = (uint32_t)r;
-    hdr[4] = (uint32_t)(r >> 32);
-  }
-  const uint32_t lim = cnt - beg_j < cap ? cnt - beg_j : cap;
-  for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < lim; j += gridDim.x * BLOCK) {
-    const uint32_t kid = kids[beg + beg_j + j];
-    uint64_t r = S[kid];
-    if (cparent[kid] != INVALID) {   // a fringe kid never packed and has no packing below it
+  if (v != INVALID) {
+    const EvView ev = load_table(epos, epre, m, spos, spre);
+    const uint32_t beg = koff[v], cnt = koff[v + 1] - beg;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && beg_j == 0) {
+      *evprev = e;
       uint32_t lo, hi;
-      node_interval(kid, cparent, ckoff, tD, tU, rst, ren, lo, hi);
-      r = lazy_r(kid, r, lo, hi, sev, evl, nev);
+      node_interval(v, cparent, ckoff, tD, tU, rst, ren, lo, hi);
+      const uint64_t r = S[v] - ev.removed(lo, hi);
+      hdr[0] = v;
+      hdr[1] = beg;
+      hdr[2] = cnt;
+      hdr[3] = (uint32_t)r;
+      hdr[4] = (uint32_t)(r >> 32);
+      hdr[5] = cparent[v] == INVALID ? INVALID : tD[v];
     }
-    kid_out[j] = kid;
-    r_out[j] = r;
+    const uint32_t lim = cnt - beg_j < cap ? cnt - beg_j : cap;
+    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < lim; j += gridDim.x * BLOCK) {
+      const uint32_t kid = kids[beg + beg_j + j];
+      uint64_t r = S[kid];
+      if (cparent[kid] != INVALID) r -= ev.removed(tD[kid], tU[kid]);   // fringe kids never had a packing below
+      kid_out[j] = kid;
+      r_out[j] = r;
+    }
+  } else if (blockIdx.x == 0 && threadIdx.x == 0) {
+    hdr[0] = INVALID;
+  }
+  // completion flag: the last workgroup publishes it after every store is visible
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    *done = 0;
+    __threadfence_system();
+    __hip_atomic_store(&hdr[7], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -423,20 +432,22 @@ __global__ void k_gather_u64(const uint64_t *__restrict__ src, const uint32_t *_
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) dst[i] = src[idx[i]];
 }
 
-// every root's final residual (after all events)
+// every root's final residual (after all events; a root's own packing is the host's)
 __global__ void k_roots_r(const uint32_t *__restrict__ ids, uint64_t m, const uint64_t *__restrict__ S,
                           const uint32_t *__restrict__ cparent, const uint32_t *__restrict__ ckoff,
                           const uint32_t *__restrict__ tD, const uint32_t *__restrict__ tU,
                           const uint32_t *__restrict__ rst, const uint32_t *__restrict__ ren,
-                          const PackEv *__restrict__ evl, uint32_t nev, uint64_t *__restrict__ out) {
-  __shared__ PackEv sev[EV_LDS];
-  load_events(evl, nev, sev);
+                          const uint32_t *__restrict__ epos, const uint64_t *__restrict__ epre, uint32_t me,
+                          uint64_t *__restrict__ out) {
+  __shared__ uint32_t spos[EV_LDS];
+  __shared__ uint64_t spre[EV_LDS + 1];
+  const EvView ev = load_table(epos, epre, me, spos, spre);
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) {
     const uint32_t a = ids[i];
     uint32_t lo, hi;
     node_interval(a, cparent, ckoff, tD, tU, rst, ren, lo, hi);
-    out[i] = lazy_r(a, S[a], lo, hi, sev, evl, nev);
+    out[i] = S[a] - ev.removed(lo, hi);
   }
 }
 
@@ -663,51 +674,80 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
                        (const uint32_t *)hids, nh, SH);
     LAUNCH_CHECK();
   }
-  PackEv *evl = c.get_as<PackEv>("pt_events", nh + 1);
   unsigned long long *found = (unsigned long long *)(c.d_scalars + 44);
   uint64_t *evprev = c.d_scalars + 46;
+  unsigned *done_ctr = (unsigned *)(c.d_scalars + 47);
   HIP_CHECK(hipMemsetAsync(evprev, 0xFF, sizeof(uint64_t), c.stream));
+  HIP_CHECK(hipMemsetAsync(done_ctr, 0, sizeof(uint64_t), c.stream));
   uint8_t *stage = (uint8_t *)c.get_pinned("pt_event", 64 + (size_t)EV_STAGE * 12);
-  uint32_t *hdr = (uint32_t *)stage, *st_kids = (uint32_t *)(stage + 64);
+  volatile uint32_t *hdr = (volatile uint32_t *)stage;
+  uint32_t *st_kids = (uint32_t *)(stage + 64);
   uint64_t *st_r = (uint64_t *)(stage + 64 + (size_t)EV_STAGE * 4);
   uint32_t *d_hdr, *d_kids;
   uint64_t *d_r;
-  HIP_CHECK(hipHostGetDevicePointer((void **)&d_hdr, hdr, 0));
+  HIP_CHECK(hipHostGetDevicePointer((void **)&d_hdr, stage, 0));
   HIP_CHECK(hipHostGetDevicePointer((void **)&d_kids, st_kids, 0));
   HIP_CHECK(hipHostGetDevicePointer((void **)&d_r, st_r, 0));
+  // the event table (sorted tD of the non-root packings, prefix sums of their deltas):
+  // host copy -> pinned staging -> device, one async copy per event
+  std::vector<std::pair<uint32_t, uint64_t>> evs;
+  uint32_t *ev_pos = c.get_as<uint32_t>("pt_evpos", nh + 1);
+  uint64_t *ev_pre = c.get_as<uint64_t>("pt_evpre", nh + 2);
+  uint8_t *ev_stage = (uint8_t *)c.get_pinned("pt_evtable", (size_t)(nh + 2) * 12 + 16);
+  uint32_t m_ev = 0;
+  HIP_CHECK(hipMemsetAsync(ev_pre, 0, sizeof(uint64_t), c.stream));
+  auto upload_table = [&]() {
+    m_ev = (uint32_t)evs.size();
+    uint32_t *hp = (uint32_t *)ev_stage;
+    uint64_t *hs = (uint64_t *)(ev_stage + ((size_t)(m_ev * 4 + 15) & ~(size_t)7));
+    uint64_t run = 0;
+    for (uint32_t i = 0; i < m_ev; ++i) { hp[i] = evs[i].first; hs[i] = run; run += evs[i].second; }
+    hs[m_ev] = run;
+    if (m_ev) HIP_CHECK(hipMemcpyAsync(ev_pos, hp, m_ev * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
+    HIP_CHECK(hipMemcpyAsync(ev_pre, hs, (m_ev + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+  };
+  std::vector<std::pair<uint32_t, uint64_t>> root_own;   // a root's own packing delta
+  uint32_t seq_no = 0;
+  // waits for k_event_stage's completion flag (hdr[7]): a poll of mapped memory wakes the
+  // host sooner than a stream synchronisation
+  auto wait_stage = [&](uint32_t want) {
+    for (long spin = 0; hdr[7] != want; ++spin)
+      if (spin > (1l << 22)) { c.sync(); break; }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  };
   std::vector<uint64_t> part_size;
   std::vector<uint32_t> asg_ids;
   std::vector<int16_t> asg_part;
   std::vector<uint32_t> seg, order, sorted, upl_pos, upl_ids;
   std::vector<uint64_t> segR, scb;
   std::vector<char> done;
-  uint32_t nev = 0;
-  uint64_t delta = 0;
   const unsigned gev = nh ? (unsigned)std::min<uint64_t>((nh + EV_CH - 1) / EV_CH, 128) : 1;
   auto stage_event = [&](uint32_t beg_j, uint32_t cap, uint32_t *o_kids, uint64_t *o_r) {
-    hipLaunchKernelGGL(k_event_stage, dim3(256), dim3(BLOCK), 0, c.stream, (const unsigned long long *)found, evprev, evl,
-                       nev, (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
-                       (const uint32_t *)core.parent, (const uint32_t *)core.koff, (const uint32_t *)t.tD,
-                       (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren, d_hdr, o_kids, o_r, beg_j,
-                       cap);
+    ++seq_no;
+    hipLaunchKernelGGL(k_event_stage, dim3(256), dim3(BLOCK), 0, c.stream, (const unsigned long long *)found, evprev,
+                       (const uint32_t *)ev_pos, (const uint64_t *)ev_pre, m_ev, (const uint32_t *)k->koff,
+                       (const uint32_t *)k->kids, (const uint64_t *)S, (const uint32_t *)core.parent,
+                       (const uint32_t *)core.koff, (const uint32_t *)t.tD, (const uint32_t *)t.tU, (const uint32_t *)rst,
+                       (const uint32_t *)ren, d_hdr, o_kids, o_r, beg_j, cap, done_ctr, seq_no);
     LAUNCH_CHECK();
   };
   {
     TimedRegion tr(c, "partition_events");
+    hdr[7] = 0;
     for (;;) {
       HIP_CHECK(hipMemsetAsync(found, 0xFF, sizeof(uint64_t), c.stream));
       if (nh) {
         hipLaunchKernelGGL(k_next_event, dim3(gev), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh,
-                           (const uint64_t *)SH, (const uint32_t *)hst, (const uint32_t *)hen, evl, nev, delta,
-                           max_component, (const uint64_t *)evprev, found);
+                           (const uint64_t *)SH, (const uint32_t *)hst, (const uint32_t *)hen, (const uint32_t *)ev_pos,
+                           (const uint64_t *)ev_pre, m_ev, max_component, (const uint64_t *)evprev, found);
         LAUNCH_CHECK();
       }
       stage_event(0, EV_STAGE, d_kids, d_r);
-      c.sync();
+      wait_stage(seq_no);
       const uint32_t v = hdr[0];
       if (v == INVALID) break;
       info->packing_nodes++;
-      const uint32_t beg = hdr[1], cnt = hdr[2];
+      const uint32_t beg = hdr[1], cnt = hdr[2], vpos = hdr[5];
       uint64_t cb = (uint64_t)hdr[3] | ((uint64_t)hdr[4] << 32);
       seg.assign(st_kids, st_kids + std::min(cnt, EV_STAGE));
       segR.assign(st_r, st_r + std::min(cnt, EV_STAGE));
@@ -720,7 +760,6 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
         d2h(c, segR.data() + EV_STAGE, (const uint64_t *)kR, cnt - EV_STAGE);
         c.sync();
       }
-      ++nev;   // the event k_event_stage appended
       const uint64_t cb0 = cb;
       // std::sort on the current kid order with the reference comparator (:104-106);
       // sorting positions with a comparator on their keys is the same sort.
@@ -757,7 +796,12 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
           part_size.push_back(0);
         }
       } while (cb > max_component);
-      delta = cb0 - cb;
+      // the event into the table for the next scan (sorted by tD; a root keeps its own)
+      if (vpos != INVALID)
+        evs.insert(std::upper_bound(evs.begin(), evs.end(), std::make_pair(vpos, (uint64_t)~0ull)), {vpos, cb0 - cb});
+      else
+        root_own.push_back({v, cb0 - cb});
+      upload_table();   // (the previous upload is complete: the stage kernel after it has finished)
     }
   }
   if (!upl_pos.empty()) {   // persist the sorted kid orders (forwardPartition mutates kids, :104-106)
@@ -779,12 +823,16 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
     hipLaunchKernelGGL(k_roots_r, dim3(grid_for(nroots)), dim3(BLOCK), 0, c.stream, (const uint32_t *)rids, nroots,
                        (const uint64_t *)S, (const uint32_t *)core.parent, (const uint32_t *)core.koff,
                        (const uint32_t *)t.tD, (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren,
-                       (const PackEv *)evl, nev, rR);
+                       (const uint32_t *)ev_pos, (const uint64_t *)ev_pre, m_ev, rR);
     LAUNCH_CHECK();
     d2h(c, r_ids.data(), (const uint32_t *)rids, nroots);
     d2h(c, r_cb.data(), (const uint64_t *)rR, nroots);
   }
   c.sync();   // the kid-order upload vectors die with this call
+  for (const auto &ro : root_own) {   // a packed root's own removed weight
+    const auto it = std::lower_bound(r_ids.begin(), r_ids.end(), ro.first);
+    if (it != r_ids.end() && *it == ro.first) r_cb[it - r_ids.begin()] -= ro.second;
+  }
 
   // 4. descending pass: roots into the highest bin that fits (:146-152)
   std::vector<int16_t> root_part(nroots);

@@ -215,14 +215,16 @@ def test_unsequenced_and_out_of_range(gpu_ctx):
         sheep_amd.build_tree(_dev_records(swapped), s2)
 
 
-def test_wide_vertex_ids_fallback_kernels(gpu_ctx):
-    """Vertex ids above 2^27 exceed the LDS bucket layout (4096 buckets of 2^15 slots):
-    the degree pass and the relabel take their unbucketed kernels (k_degree + separate
-    head count, k_relabel).  Same results as the oracle."""
+@pytest.mark.parametrize("stretch", [40000, 150000])
+def test_wide_vertex_ids(gpu_ctx, stretch):
+    """Vertex ids up to 1.6e8 (above 2^27: more than 4087 LDS buckets of 2^15 slots, the
+    staged heads histogram and 4K-record relabel sub-tiles) and up to 6e8 (above 2^28:
+    beyond the bucket layout, the unbucketed kernels k_degree + scattered head atomics and
+    the one-pass k_relabel).  Same results as the oracle."""
     import sheep_amd
     h = sheep_amd.rmat_host(12, 16, 12)
-    t_ = h[:, 0].astype(np.uint64) * 40000 + 7
-    h_ = h[:, 1].astype(np.uint64) * 40000 + 7
+    t_ = h[:, 0].astype(np.uint64) * stretch + 7
+    h_ = h[:, 1].astype(np.uint64) * stretch + 7
     assert h_.max() >= (1 << 27)
     t_, h_ = t_.astype(np.uint32), h_.astype(np.uint32)
     w = np.ones(len(t_), np.float32)
@@ -253,7 +255,8 @@ def test_empty_and_tiny(gpu_ctx):
 def test_tree_above_2e27_nodes(gpu_ctx):
     """A path of 1.4e8 vertices: 1.4e8 tree nodes, so the pst grouping's padded lo range
     needs more than 4087 LDS buckets (staged scatter with 8K-edge sub-tiles); vertex ids
-    above 2^27 also take the atomic heads histogram and k_relabel.  Tree vs the oracle."""
+    above 2^27 also take the staged heads histogram and 4K-record relabel sub-tiles.  Tree
+    vs the oracle."""
     import sheep_amd
     N = 140_000_000
     t_ = np.arange(N, dtype=np.uint32)
