@@ -54,7 +54,14 @@ def parse():
     ap.add_argument("--scale", type=int, default=26)
     ap.add_argument("--ef", type=int, default=16)
     ap.add_argument("--k", type=int, default=64)
-    ap.add_argument("--seed", type=int, default=None, help="RMAT seed (default: the scale, SURVEY §8d)")
+    ap.add_argument("--seed", type=int, default=None, help="generator seed (default: the RMAT scale; 2010 for powerlaw)")
+    ap.add_argument("--graph", default="rmat", choices=("rmat", "powerlaw"),
+                    help="rmat: Graph500 RMAT (C2/C3/C5); powerlaw: Chung-Lu at twitter-2010 scale (C4)")
+    ap.add_argument("--draws", type=int, default=1_560_000_000,
+                    help="powerlaw edge draws (about 1.468e9 records survive the dedup, twitter-2010's count)")
+    ap.add_argument("--shards", type=int, default=1,
+                    help="one GPU: edge shards mapped one after another and merged K-way (graphs of >= 2^32 "
+                         "records, e.g. RMAT-28; C5 on one GPU)")
     ap.add_argument("--shuffle", action="store_true",
                     help="records in a random order, half with tail/head swapped (a generic edge list)")
     ap.add_argument("--eval-reps", type=int, default=3, help="timed evaluator runs (0: skip)")
@@ -108,28 +115,47 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
-    seed = a.scale if a.seed is None else a.seed
+    seed = (a.scale if a.graph == "rmat" else 2010) if a.seed is None else a.seed
+    if a.shards > 1 and world > 1:
+        raise SystemExit("--shards is the one-GPU form of the edge-shard path")
 
     ctx = sheep_amd.Context(local)
-    rec = sheep_amd.rmat(a.scale, a.ef, seed, ctx=ctx)          # whole graph, identical on every rank
+    if a.graph == "rmat":                                       # whole graph, identical on every rank
+        rec = sheep_amd.rmat(a.scale, a.ef, seed, ctx=ctx)
+        vs_cap, workload = 1 << a.scale, f"RMAT-{a.scale} ef{a.ef}, k={a.k}"
+    else:
+        rec = sheep_amd.powerlaw(sheep_amd.TWITTER_VERTICES, a.draws, 1.9, seed, ctx=ctx)
+        vs_cap, workload = sheep_amd.TWITTER_VERTICES, f"Chung-Lu power law (twitter-2010 scale), k={a.k}"
+    if a.shards > 1:
+        workload += f", {a.shards} shards on 1 GPU"
     if a.shuffle:
         rec = shuffled(rec, 1000 + seed)
     R = rec.shape[0]
     beg, end = sdist.shard_bounds(R, rank, world)               # contiguous edge shard (graph2tree -l)
-    shard = rec[beg:end].contiguous()
+    shard = rec[beg:end].contiguous() if world > 1 else rec
     del rec
     torch.cuda.empty_cache()
-    vs_cap = 1 << a.scale
     deg = torch.zeros(vs_cap, dtype=torch.int32, device=f"cuda:{local}")
+    subs = [shard[i * shard.shape[0] // a.shards:(i + 1) * shard.shape[0] // a.shards] for i in range(a.shards)]
+    stack = [None]
 
     def step():
         deg.zero_()
-        _, max_slot = sheep_amd.degree_count(shard, mode="llama", deg=deg, ctx=ctx)
-        vs = max_slot
+        vs = 0
+        for sub in subs:                                        # shards accumulate into one histogram
+            _, max_slot = sheep_amd.degree_count(sub, mode="llama", deg=deg, ctx=ctx)
+            vs = max(vs, max_slot)
         if world > 1:                                           # sequence.h:72,78 MPI_Allreduce
-            vs = sdist.allreduce_degrees(deg, max_slot)
+            vs = sdist.allreduce_degrees(deg, vs)
         s = sheep_amd.sequence_from_degrees(deg, vs, ctx=ctx)
-        tree = sheep_amd.build_tree(shard, s, ctx=ctx)
+        if a.shards > 1:                                        # map per shard, then ONE K-way merge
+            if stack[0] is None or stack[0].shape[1] != s.n:
+                stack[0] = torch.empty((a.shards, s.n, 2), dtype=torch.int32, device=f"cuda:{local}")
+            for i, sub in enumerate(subs):
+                sheep_amd.build_tree(sub, s, ctx=ctx, out=stack[0][i])
+            tree = sheep_amd.merge_trees_many(stack[0], ctx=ctx)
+        else:
+            tree = sheep_amd.build_tree(shard, s, ctx=ctx)
         if world > 1 and a.reduce == "kway":                    # reduce to rank 0 (jnode.cpp:241) in one pass
             tree = sdist.reduce_trees_kway(tree, lambda t: sheep_amd.merge_trees_many(t, ctx=ctx), rank, world)
         elif world > 1:                                         # binomial reduce to rank 0 (jnode.cpp:241)
@@ -174,13 +200,15 @@ def main():
 
     evaluator = None
     if a.eval_reps > 0:
-        evaluator = time_evaluator(a, ctx, shard, s, res, rank, world, local, barrier, max_over_ranks)
+        evaluator = time_evaluator(a, ctx, shard, subs, s, res, rank, world, local, barrier, max_over_ranks)
     ctx.timing(False)
 
     verified = None
     if a.verify and rank == 0:                                  # merged tree == whole-graph tree
-        if world == 1:
+        if world == 1 and a.shards == 1:
             verified = True
+        elif world == 1:
+            verified = bool(torch.equal(sheep_amd.build_tree(shard, s, ctx=ctx), tree)) if R < (1 << 32) else None
         else:
             whole = sheep_amd.build_tree(sheep_amd.rmat(a.scale, a.ef, seed, ctx=ctx) if not a.shuffle else
                                          shuffled(sheep_amd.rmat(a.scale, a.ef, seed, ctx=ctx), 1000 + seed), s, ctx=ctx)
@@ -221,11 +249,13 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (Graph500 RMAT, seeded, self-loops/duplicates removed"
+            "data": ("synthetic (Graph500 RMAT, seeded" if a.graph == "rmat" else
+                     f"synthetic (Chung-Lu power law, gamma 1.9, {sheep_amd.TWITTER_VERTICES} vertices, seeded")
+                    + ", self-loops/duplicates removed"
                     + (", records shuffled and half of them reversed)" if a.shuffle else ", records (tail, head)-sorted)"),
-            "config": {"workload": f"RMAT-{a.scale} ef{a.ef}, k={a.k}", "records": R, "vertex_slots": s.pos_size,
+            "config": {"workload": workload, "records": R, "vertex_slots": s.pos_size,
                        "tree_nodes": n, "k": a.k, "created": res.created, "packing_nodes": res.packing_nodes,
-                       "heavy_nodes": res.heavy_nodes, "seed": seed, "shuffled": a.shuffle,
+                       "heavy_nodes": res.heavy_nodes, "seed": seed, "shuffled": a.shuffle, "shards": a.shards,
                        "parallelism": f"edge-shards x{world}" + (f", {a.reduce} reduce" if world > 1 else "")
                        + ("" if a.dist_backend == "nccl" else f" ({a.dist_backend}"
                           + (", one device" if a.same_device else "") + ")")},
@@ -246,7 +276,7 @@ def main():
         print(json.dumps(out), flush=True)
 
 
-def time_evaluator(a, ctx, shard, s, res, rank, world, local, barrier, max_over_ranks):
+def time_evaluator(a, ctx, shard, subs, s, res, rank, world, local, barrier, max_over_ranks):
     """ECV(down) + balance (evaluate(graph, seq), partition.cpp:475-521), timed on its own:
     one GPU — sheep_evaluate over all records; N GPUs — parts broadcast, per-shard
     bitsets, binomial OR-reduction to rank 0, node pass there.  B_eval per SURVEY §8(d)."""
@@ -259,8 +289,13 @@ def time_evaluator(a, ctx, shard, s, res, rank, world, local, barrier, max_over_
     for _ in range(a.eval_reps):
         barrier()
         t0 = time.perf_counter()
-        if world == 1:
+        if world == 1 and a.shards == 1:
             ev = sheep_amd.evaluate(shard, s, parts0, what=sheep_amd.EVAL_DOWN, ctx=ctx)
+        elif world == 1:                                         # the shards' bitsets, then one node pass
+            e = sheep_amd.ShardedEvaluator(s, parts0, sheep_amd.EVAL_DOWN, ctx=ctx)
+            for sub in subs:
+                e.add(sub)
+            ev = e.finish()
         else:
             parts = sdist.sync_parts(parts0, s.pos_size, torch.device("cuda", local))
             nparts = torch.tensor([0 if rank else sheep_amd.ShardedEvaluator.num_parts(parts, s, ctx)],
@@ -303,7 +338,7 @@ def dist_broadcast(t):
 
 def _pmc(a, world):
     path = PMC_FILE.format(scale=a.scale, k=a.k)
-    if world != 1 or a.shuffle or not os.path.exists(path):
+    if world != 1 or a.shuffle or a.graph != "rmat" or a.shards != 1 or not os.path.exists(path):
         return None, path
     prof = json.load(open(path))
     if prof.get("workload") != f"RMAT-{a.scale} ef{a.ef}, k={a.k}":

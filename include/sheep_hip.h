@@ -219,8 +219,9 @@ int sheep_edge_parts(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec, co
  * One process drives `ndev` ranks, rank r on devices[r] with a context of its own.  Distinct
  * devices exchange over RCCL (one communicator clique, xGMI); a device listed more than
  * once (several edge shards rehearsed on one GPU) exchanges by device-to-device copies.
- * Per-rank arrays (rec_dev[r], deg_dev[r], ...) live on rank r's device.  Every call is
- * complete (all ranks synchronised) on return.  Replaces (chan150/sheep):
+ * Per-rank arrays (rec_dev[r], deg_dev[r], ...) live on rank r's device.  The ranks run on
+ * streams of their own: inputs written on other streams must be complete before a call
+ * (synchronise them first); every call is complete (all ranks synchronised) on return.  Replaces (chan150/sheep):
  *   sheep_group_sequence        mpiSequence (sequence.h:65-93): per-shard LLAMA degrees
  *                               into deg_dev[r] (zeroed by the caller, capacity cap), the
  *                               MPI_Allreduce(MAX) of max_slot and MPI_Allreduce(SUM) of the
@@ -277,6 +278,13 @@ int sheep_rmat_generate(sheep_ctx *ctx, int scale, int edgefactor, uint64_t seed
                         sheep_xs1 *out_dev, uint64_t cap, uint64_t *nrec_out);
 int sheep_rmat_generate_host(int scale, int edgefactor, uint64_t seed, sheep_xs1 *out_host,
                              uint64_t cap, uint64_t *nrec_out);
+/* Chung-Lu power law (BASELINE config C4, twitter-2010 scale): `draws` edges whose two
+ * endpoints are drawn independently with probability ~ (rank + x0)^-1/(gamma-1) over
+ * `nverts` vertices (x0: the top vertex takes 0.1% of the draws), labels permuted,
+ * self-loops and duplicates removed, tail > head, sorted by (tail, head), weight 1.0f.
+ * out_dev needs capacity `draws` records; *nrec_out (host) = records kept. */
+int sheep_powerlaw_generate(sheep_ctx *ctx, uint64_t nverts, uint64_t draws, double gamma, uint64_t seed,
+                            sheep_xs1 *out_dev, uint64_t cap, uint64_t *nrec_out);
 
 #ifdef __cplusplus
 }

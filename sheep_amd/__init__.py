@@ -115,6 +115,7 @@ def lib() -> ctypes.CDLL:
         "sheep_group_broadcast_parts": ([P, P, U64], I32),
         "sheep_group_evaluate": ([P, P, P, P, U64, P, I32, ctypes.POINTER(_Eval)], I32),
         "sheep_parse_net": ([P, P, U64, I32, P, U64, ctypes.POINTER(U64)], I32),
+        "sheep_powerlaw_generate": ([P, U64, U64, D, U64, P, U64, ctypes.POINTER(U64)], I32),
         "sheep_rmat_generate": ([P, I32, I32, U64, P, U64, ctypes.POINTER(U64)], I32),
         "sheep_rmat_generate_host": ([I32, I32, U64, P, U64, ctypes.POINTER(U64)], I32),
     }
@@ -287,12 +288,13 @@ def sequence_from_host(seq: np.ndarray, ctx: Context | None = None) -> Sequence:
 # ---------------------------------------------------------------------------------
 # jtree / jnode
 # ---------------------------------------------------------------------------------
-def build_tree(records, seq: Sequence, nrec: int | None = None, ctx: Context | None = None):
-    """JTree(graph, seq): device tensor [n, 2] int32 = JNode {parent, pst_weight}."""
+def build_tree(records, seq: Sequence, nrec: int | None = None, ctx: Context | None = None, out=None):
+    """JTree(graph, seq): device tensor [n, 2] int32 = JNode {parent, pst_weight}
+    (written into `out`, an [n, 2] int32 tensor, when given)."""
     ctx = ctx or default_context()
     t = _torch()
     nrec = records.shape[0] if nrec is None else nrec
-    tree = t.empty((max(seq.n, 1), 2), dtype=t.int32, device=_dev(ctx))
+    tree = out if out is not None else t.empty((max(seq.n, 1), 2), dtype=t.int32, device=_dev(ctx))
     _check(lib().sheep_build_tree(ctx.handle, _ptr(records), nrec, _ptr(seq.pos), seq.pos_size, seq.n, _ptr(tree)))
     return tree[: seq.n]
 
@@ -577,6 +579,13 @@ class Group:
     def _dev(self, r):
         return f"cuda:{self.devices[r]}"
 
+    def _ready(self):
+        """The ranks run on streams of their own: finish torch's work on every device
+        (inputs, zero-filled outputs) before a group call reads it."""
+        t = _torch()
+        for d in sorted(set(self.devices)):
+            t.cuda.synchronize(d)
+
     def sequence(self, shards, vs_cap: int):
         """mpiSequence over the ranks' record shards: a Sequence per rank (all equal)."""
         t = _torch()
@@ -586,6 +595,7 @@ class Group:
         pos = [t.empty(max(vs_cap, 1), dtype=t.int32, device=self._dev(r)) for r in range(P)]
         nrec = (ctypes.c_uint64 * P)(*[s.shape[0] for s in shards])
         n, vs = ctypes.c_uint64(), ctypes.c_uint64()
+        self._ready()
         _check(lib().sheep_group_sequence(self.handle, _ptr_array(shards), nrec, _ptr_array(deg), vs_cap,
                                           _ptr_array(seq), _ptr_array(pos), ctypes.byref(n), ctypes.byref(vs)))
         return [Sequence(seq[r], pos[r], n.value, vs.value) for r in range(P)]
@@ -598,6 +608,7 @@ class Group:
         n = seqs[0].n
         trees = [t.empty((max(n, 1), 2), dtype=t.int32, device=self._dev(r)) for r in range(P)]
         nrec = (ctypes.c_uint64 * P)(*[s.shape[0] for s in shards])
+        self._ready()
         _check(lib().sheep_group_build_tree(self.handle, _ptr_array(shards), nrec, _ptr_array([s.pos for s in seqs]),
                                             seqs[0].pos_size, n, _ptr_array(trees), self.REDUCE[reduce]))
         return [x[:n] for x in trees] if reduce == "none" else trees[0][:n]
@@ -607,6 +618,7 @@ class Group:
         t = _torch()
         P = len(self.devices)
         parts = [parts0] + [t.empty(max(pos_size, 1), dtype=t.int16, device=self._dev(r)) for r in range(1, P)]
+        self._ready()
         _check(lib().sheep_group_broadcast_parts(self.handle, _ptr_array(parts), pos_size))
         return [p[:pos_size] for p in parts]
 
@@ -614,6 +626,7 @@ class Group:
         P = len(self.devices)
         nrec = (ctypes.c_uint64 * P)(*[s.shape[0] for s in shards])
         out = _Eval()
+        self._ready()
         _check(lib().sheep_group_evaluate(self.handle, _ptr_array(shards), nrec, _ptr_array([s.pos for s in seqs]),
                                           seqs[0].pos_size, _ptr_array(parts), what, ctypes.byref(out)))
         return EvalResult(*[getattr(out, f) for f, _ in _Eval._fields_])
@@ -630,6 +643,21 @@ def rmat(scale: int, edgefactor: int = 16, seed: int = 1, ctx: Context | None = 
     out = t.empty((cap, 3), dtype=t.int32, device=_dev(ctx))
     n = ctypes.c_uint64()
     _check(lib().sheep_rmat_generate(ctx.handle, scale, edgefactor, seed, _ptr(out), cap, ctypes.byref(n)))
+    return out[: n.value]
+
+
+TWITTER_VERTICES = 41_652_230      # twitter-2010 (slurm-fen-twitter.out:2)
+
+
+def powerlaw(nverts: int = TWITTER_VERTICES, draws: int = 1_600_000_000, gamma: float = 1.9, seed: int = 2010,
+             ctx: Context | None = None):
+    """Chung-Lu power-law records generated in HBM (BASELINE config C4): [R, 3] int32."""
+    ctx = ctx or default_context()
+    t = _torch()
+    out = t.empty((draws, 3), dtype=t.int32, device=_dev(ctx))
+    n = ctypes.c_uint64()
+    _check(lib().sheep_powerlaw_generate(ctx.handle, nverts, draws, float(gamma), seed, _ptr(out), draws,
+                                         ctypes.byref(n)))
     return out[: n.value]
 
 

@@ -36,6 +36,7 @@ void edge_parts(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos
                 const int16_t *parts_vid, int16_t *out);
 uint64_t parse_net(Ctx &c, const char *text, uint64_t bytes, int skip_comments, sheep_xs1 *out, uint64_t cap);
 uint64_t rmat_generate(Ctx &c, int scale, int ef, uint64_t seed, sheep_xs1 *out, uint64_t cap);
+uint64_t powerlaw_generate(Ctx &c, uint64_t V, uint64_t M, double gamma, uint64_t seed, sheep_xs1 *out, uint64_t cap);
 uint64_t rmat_generate_host(int scale, int ef, uint64_t seed, sheep_xs1 *out, uint64_t cap);
 }  // namespace sheep
 
@@ -380,6 +381,15 @@ int sheep_rmat_generate(sheep_ctx *ctx, int scale, int ef, uint64_t seed, sheep_
   DeviceGuard dg(ctx);
   NEED(ctx && out && nrec_out, "null argument");
   *nrec_out = sheep::rmat_generate(ctx->c, scale, ef, seed, out, cap);
+  API_END
+}
+
+int sheep_powerlaw_generate(sheep_ctx *ctx, uint64_t nverts, uint64_t draws, double gamma, uint64_t seed,
+                            sheep_xs1 *out, uint64_t cap, uint64_t *nrec_out) {
+  API_BEGIN
+  DeviceGuard dg(ctx);
+  NEED(ctx && out && nrec_out, "null argument");
+  *nrec_out = sheep::powerlaw_generate(ctx->c, nverts, draws, gamma, seed, out, cap);
   API_END
 }
 

@@ -351,7 +351,9 @@ __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict
     // Power-law graphs send most cross edges of a level to one giant component's top:
     // combine in the wave first (lanes sharing the first lane's top) and skip atomics a
     // plain read already shows useless (mt only decreases; a stale read is >= the true
-    // value, so skipping stays exact).
+    // value, so skipping stays exact).  Measured: issuing the other lanes' atomics
+    // without the read (no-return atomics) costs 25x at RMAT-28 / Chung-Lu, where
+    // lanes beside the first still hit hub tops.
 #pragma unroll
     for (int k = 0; k < XK; ++k) {
       const uint64_t cm = __ballot(cross[k]);

@@ -249,7 +249,10 @@ int sheep_group_sequence(sheep_group *g, const sheep_xs1 *const *rec, const uint
   uint64_t vs = 0;
   for (uint64_t m : ms) vs = m > vs ? m : vs;                         // MPI_Allreduce(MAX), sequence.h:72
   sheep::allreduce_sum_u32(g, deg, vs);                               // MPI_Allreduce(SUM), sequence.h:78
-  sheep::per_rank(g, [&](int r) { n[r] = sheep::sequence_from_degrees(sheep::C(g, r), deg[r], vs, seq[r], pos[r]); });
+  sheep::per_rank(g, [&](int r) {
+    n[r] = sheep::sequence_from_degrees(sheep::C(g, r), deg[r], vs, seq[r], pos[r]);
+    sheep::C(g, r).sync();
+  });
   *n_out = n[0];
   *vs_out = vs;
   GAPI_END
