@@ -189,7 +189,9 @@ int sheep_evaluate(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec,
  * split over devices or passes):
  *   sheep_eval_sizes      u64 words of the bitset and accumulator state for (what,
  *                         nparts, pos_size); nparts = max part + 1
- *                         (sheep_eval_num_parts);
+ *                         (sheep_eval_num_parts).  The bitset state holds one row per
+ *                         vertex slot: (pos << 16 | part), then the owner bit words;
+ *                         every shard writes the same row heads, so OR-combining keeps them;
  *   sheep_eval_shard      ORs one shard's owner bits into bits_dev and adds its counts into
  *                         acc_dev (both zeroed by the caller before the first shard);
  *   sheep_eval_combine    bits_dev |= bits_src, acc_dev += acc_src (state of another

@@ -351,7 +351,9 @@ __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict
     // Power-law graphs send most cross edges of a level to one giant component's top:
     // combine in the wave first (lanes sharing the first lane's top) and skip atomics a
     // plain read already shows useless (mt only decreases; a stale read is >= the true
-    // value, so skipping stays exact).  Measured: issuing the other lanes' atomics
+    // value, so skipping stays exact).  (Issuing the other lanes' atomics without the
+    // read, as no-return atomics, cost 25x at RMAT-28 and Chung-Lu, where lanes beside
+    // the first still hit hub tops.)  Measured: issuing the other lanes' atomics
     // without the read (no-return atomics) costs 25x at RMAT-28 / Chung-Lu, where
     // lanes beside the first still hit hub tops.
 #pragma unroll
@@ -791,9 +793,11 @@ __global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t 
 void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
 
 static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
-// Finishing block size (log2 positions) of the per-block Liu pass: merges use it; a
-// map's hub blocks would pile onto single lanes, so maps run every level globally.
-constexpr int FIN_MERGE = 8, FIN_MAP = 0;
+// Finishing block size (log2 positions) of the per-block Liu pass.  The last levels of a
+// map keep ~5M list entries each at RMAT-26 (0.6 ms per level for a dozen launches);
+// one sort + the per-block pass replaces the last 8 (RMAT-26: 49.7 -> 45.9 ms; B = 7:
+// 46.4).  Hub blocks go to whole waves (k_fin_heavy).
+constexpr int FIN_MERGE = 8, FIN_MAP = 8;
 
 // spread(x) = floor(x * c / 2^32), c = floor(2^(32+L) / n) in [2^32, 2^33), L = ceil(log2 n):
 // monotone, injective on [0,n), image in [0, 2^L).  clo = c - 2^32.

@@ -12,16 +12,18 @@
 // pass over vertex slots pops the bits.  Balances and edges-cut are per-block LDS
 // histograms.
 //
-// Layout (HBM), per vertex slot v: M bit arrays (the requested ones, in the order down,
-// up, hash, vcom), each W64 = ceil(nparts / 64) u64 words: bits[(v * M + a) * W64 + w],
-// so one vertex's words share a cache line.  pp[v] = pos << 16 | part packs the two
-// per-vertex gathers a record needs into one 8-B load.
+// Layout (HBM): one row of RW = 1 + M * W64 u64 words per vertex slot v.  Word 0 is
+// pp = pos << 16 | part (the two per-vertex gathers a record needs, in one 8-B load);
+// then M bit arrays (the requested ones, in the order down, up, hash, vcom), each
+// W64 = ceil(nparts / 64) words: row[v][1 + a * W64 + w].
 //
 // Traffic: a record's tail side is near-sequential when records come tail-sorted (runs
-// of equal tails are OR-combined in the wave first); its head side is one random 8-B
-// gather plus, per bit array, a read of the word and an atomicOr only when the bit is
-// still clear — power-law heads saturate their bitsets after a few records, so most
-// head updates end at the (cache-resident) read.
+// of equal tails are OR-combined in the wave first).  Its head side is random over a
+// 0.5-1 GB array at RMAT-26, far above the Infinity Cache: with pp and the bits in
+// separate arrays it cost two random lines per record (37.8 ms at RMAT-26); in one row
+// the bit word shares the line the pp gather already brought in (k <= 64, one array: a
+// 16-B row, one 16-B load).  The atomicOr is issued only when the bit is still clear —
+// power-law heads saturate their bitsets after a few records.
 //
 // The sharded form (one call per edge shard, bitsets OR-combined and accumulators
 // summed across shards, then one node pass) is the distributed evaluator of SURVEY
@@ -39,13 +41,14 @@ constexpr uint64_t NO_PP = ~0ull;
 // accumulator row: scalars then the three record-side balance histograms
 constexpr int AC_CUT = 0, AC_BAD = 1, AC_LOOPS = 2, AC_RECS = 3, AC_SCAL = 8;
 
-__global__ void k_pp(const uint32_t *__restrict__ pos, const int16_t *__restrict__ parts, uint64_t vs,
-                     uint64_t *__restrict__ pp) {
+// row heads (identical for every shard, so the OR-combine of states keeps them)
+__global__ void k_pp(const uint32_t *__restrict__ pos, const int16_t *__restrict__ parts, uint64_t vs, uint32_t RW,
+                     uint64_t *__restrict__ rows) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < vs; v += stride) {
     const uint32_t p = pos[v];
     const int16_t q = parts[v];
-    pp[v] = (p == INVALID || q < 0) ? NO_PP : ((uint64_t)p << 16) | (uint16_t)q;
+    rows[v * RW] = (p == INVALID || q < 0) ? NO_PP : ((uint64_t)p << 16) | (uint16_t)q;
   }
 }
 
@@ -73,11 +76,12 @@ __device__ __forceinline__ void or_bits(unsigned long long *bits, uint64_t idx, 
   if ((bits[idx] & m) != m) atomicOr(&bits[idx], (unsigned long long)m);
 }
 
+template <bool ROW16>   // ROW16: one bit array of one word (RW == 2), loaded with the head's pp
 __global__ __launch_bounds__(BLOCK) void k_eval_records(const sheep_xs1 *__restrict__ rec, uint64_t nrec,
-                                                        const uint64_t *__restrict__ pp, uint64_t pos_size, int what,
-                                                        int M, uint32_t W64, int nparts,
-                                                        unsigned long long *__restrict__ bits,
+                                                        uint64_t pos_size, int what, int M, uint32_t W64, int nparts,
+                                                        unsigned long long *__restrict__ rows,
                                                         unsigned long long *__restrict__ acc) {
+  const uint32_t RW = 1 + (uint32_t)M * W64;
   unsigned long long *const bal = acc + AC_SCAL;   // [0,n) down, [n,2n) up, [2n,3n) hash
   __shared__ uint32_t lbal[3][LDS_PARTS];
   const bool lds = nparts <= LDS_PARTS;
@@ -97,12 +101,21 @@ __global__ __launch_bounds__(BLOCK) void k_eval_records(const sheep_xs1 *__restr
     int tp = 0, hp = 0;
     bool live = false;
     uint32_t pt = 0, ph = 0;
+    uint64_t hw = 0;   // ROW16: the head's bit word, read with its pp
     if (i < nrec) {
       const sheep_xs1 r = rec[i];
       if (r.tail >= pos_size || r.head >= pos_size) {
         ++bad;
       } else {
-        const uint64_t a = pp[r.tail], b = pp[r.head];
+        const uint64_t a = rows[(uint64_t)r.tail * RW];
+        uint64_t b;
+        if (ROW16) {
+          const ulonglong2 hr = *reinterpret_cast<const ulonglong2 *>(rows + (uint64_t)r.head * 2);
+          b = hr.x;
+          hw = hr.y;
+        } else {
+          b = rows[(uint64_t)r.head * RW];
+        }
         if (a == NO_PP || b == NO_PP) {
           ++bad;
         } else {
@@ -138,11 +151,18 @@ __global__ __launch_bounds__(BLOCK) void k_eval_records(const sheep_xs1 *__restr
       if (arr[q] < 0) continue;   // uniform
       if (W64 == 1) {
         const uint64_t m = run_or(live ? t : INVALID, live ? 1ull << own_t[q] : 0);
-        if (m) or_bits(bits, (uint64_t)t * M + arr[q], m);
+        if (m) or_bits(rows, (uint64_t)t * RW + 1 + arr[q], m);
       } else if (live) {
-        or_bits(bits, ((uint64_t)t * M + arr[q]) * W64 + (own_t[q] >> 6), 1ull << (own_t[q] & 63));
+        or_bits(rows, (uint64_t)t * RW + 1 + arr[q] * W64 + (own_t[q] >> 6), 1ull << (own_t[q] & 63));
       }
-      if (live && !loop) or_bits(bits, ((uint64_t)h * M + arr[q]) * W64 + (own_h[q] >> 6), 1ull << (own_h[q] & 63));
+      if (live && !loop) {
+        if (ROW16) {
+          const uint64_t m = 1ull << own_h[q];
+          if ((hw & m) != m) atomicOr(&rows[(uint64_t)h * 2 + 1], (unsigned long long)m);
+        } else {
+          or_bits(rows, (uint64_t)h * RW + 1 + arr[q] * W64 + (own_h[q] >> 6), 1ull << (own_h[q] & 63));
+        }
+      }
     }
   }
   cut = wave_sum(cut);
@@ -176,7 +196,7 @@ __global__ void k_eval_combine(unsigned long long *__restrict__ dst, const unsig
 // vcom, nodes}; vbal = vertex balance histogram.
 __global__ __launch_bounds__(BLOCK) void k_eval_nodes(uint64_t vs, const int16_t *__restrict__ parts, int what, int M,
                                                       uint32_t W64, int nparts,
-                                                      const unsigned long long *__restrict__ bits,
+                                                      const unsigned long long *__restrict__ rows,
                                                       unsigned long long *__restrict__ vbal,
                                                       unsigned long long *__restrict__ out) {
   __shared__ uint32_t lv[LDS_PARTS];
@@ -190,7 +210,7 @@ __global__ __launch_bounds__(BLOCK) void k_eval_nodes(uint64_t vs, const int16_t
   uint64_t s[4] = {0, 0, 0, 0}, nodes = 0;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < vs; v += stride) {
-    const unsigned long long *b = bits + v * M * W64;
+    const unsigned long long *b = rows + v * (1 + (uint64_t)M * W64) + 1;
     bool node = false;
     for (uint32_t w = 0; w < W64; ++w) node |= b[w] != 0;
     if (!node) continue;
@@ -245,7 +265,7 @@ void eval_sizes(int what, int nparts, uint64_t pos_size, uint64_t *bits_words, u
   if (what & ~7) throw Error(SHEEP_ERR_ARG, "evaluate: unknown metric bits");
   if (nparts < 1) nparts = 1;
   const uint64_t W64 = ((uint64_t)nparts + 63) / 64;
-  *bits_words = pos_size * (uint64_t)eval_arrays(what) * W64;
+  *bits_words = pos_size * (1 + (uint64_t)eval_arrays(what) * W64);
   *acc_words = AC_SCAL + 3 * (uint64_t)nparts;
 }
 
@@ -270,16 +290,17 @@ void eval_shard(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos
   const uint32_t W64 = (uint32_t)((nparts + 63) / 64);
   if (!nrec) return;
   if (pos_size == 0) {   // every record is out of range
-    hipLaunchKernelGGL(k_eval_records, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, (const uint64_t *)nullptr,
-                       (uint64_t)0, what, M, W64, nparts, (unsigned long long *)bits, (unsigned long long *)acc);
+    hipLaunchKernelGGL(k_eval_records<false>, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, (uint64_t)0,
+                       what, M, W64, nparts, (unsigned long long *)bits, (unsigned long long *)acc);
     LAUNCH_CHECK();
     return;
   }
-  uint64_t *pp = c.get_as<uint64_t>("ev_pp", pos_size);
-  hipLaunchKernelGGL(k_pp, dim3(grid_for(pos_size)), dim3(BLOCK), 0, c.stream, pos, parts, pos_size, pp);
+  const uint32_t RW = 1 + (uint32_t)M * W64;
+  hipLaunchKernelGGL(k_pp, dim3(grid_for(pos_size)), dim3(BLOCK), 0, c.stream, pos, parts, pos_size, RW, bits);
   LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_eval_records, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, (const uint64_t *)pp,
-                     pos_size, what, M, W64, nparts, (unsigned long long *)bits, (unsigned long long *)acc);
+  auto kern = RW == 2 ? k_eval_records<true> : k_eval_records<false>;
+  hipLaunchKernelGGL(kern, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos_size, what, M, W64, nparts,
+                     (unsigned long long *)bits, (unsigned long long *)acc);
   LAUNCH_CHECK();
 }
 
@@ -347,7 +368,7 @@ void evaluate(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, 
   {
     // B_eval: record read + 2 pos + 2 part gathers, bitset write + read
     // (2 B per slot per 8 parts, per bit array)
-    TimedRegion tr(c, "evaluate", 28 * nrec + 2 * words * 8);
+    TimedRegion tr(c, "evaluate", 28 * nrec + 2 * (words - pos_size) * 8);
     eval_shard(c, rec, nrec, pos, pos_size, parts, what, nparts, bits, acc);
     eval_finish(c, bits, acc, pos_size, parts, what, nparts, out);
   }
