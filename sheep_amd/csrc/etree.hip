@@ -33,51 +33,80 @@ constexpr uint64_t DEAD = ~0ull;
 
 __device__ __forceinline__ uint32_t spread(uint32_t x, uint32_t clo) { return x + __umulhi(x, clo); }
 
+// ---- per-level state: level-tagged words -------------------------------------------
+// uf, top, mt and claim are rebuilt at every D&C level.  For n < 2^27 - 1 a word carries
+// the level that wrote it in its top 5 bits (Tg): a word of another level reads as the
+// reset value (uf / top: the vertex itself, mt / claim: none), so no pass restores the
+// arrays between levels (the dense reset wrote 16 B per vertex per level: 9 GB of the
+// RMAT-26 step).  Larger trees keep untagged words and the per-level reset.
+//   uf, top, claim: tag = level + 1 (top's atomicMax: older words are smaller);
+//   mt: tag = 31 - level (atomicMin: older words are larger; the reset value ~0 is larger
+//       still, and at level 0, where it carries the current tag, its value is >= n).
+constexpr int TAG_SHIFT = 27;
+constexpr uint32_t VAL_MASK = (1u << TAG_SHIFT) - 1;
+constexpr uint64_t TAG_MAX_N = VAL_MASK;   // n < 2^27 - 1: every position is < VAL_MASK
+
+struct Tg {
+  uint32_t cur, mcur;   // (level + 1) << 27, (31 - level) << 27
+  bool on;
+  __device__ __forceinline__ uint32_t get(uint32_t w, uint32_t self) const {   // uf / top
+    return !on ? w : (w & ~VAL_MASK) == cur ? (w & VAL_MASK) : self;
+  }
+  __device__ __forceinline__ uint32_t enc(uint32_t v) const { return on ? (cur | v) : v; }
+  __device__ __forceinline__ uint32_t claim_get(uint32_t w) const {
+    return !on ? w : (w & ~VAL_MASK) == cur ? (w & VAL_MASK) : INVALID;
+  }
+  __device__ __forceinline__ uint32_t m_enc(uint32_t v) const { return on ? (mcur | v) : v; }
+  __device__ __forceinline__ uint32_t m_get(uint32_t w) const {
+    return !on ? w : ((w & ~VAL_MASK) == mcur && (w & VAL_MASK) != VAL_MASK) ? (w & VAL_MASK) : INVALID;
+  }
+};
+__host__ __device__ inline Tg make_tag(int lvl, bool on) {
+  return Tg{(uint32_t)(lvl + 1) << TAG_SHIFT, (uint32_t)(31 - lvl) << TAG_SHIFT, on};
+}
+
 // ---- union-find ---------------------------------------------------------------------
 // The forest is monotone: uf[x] only ever changes from x to a smaller root (CAS hook,
 // only on a current root, so no link is ever lost) or to a smaller ancestor (path
 // splitting), so every value a thread can read — even a stale L1 copy — is an ancestor
-// of x.  Plain loads/stores are therefore safe while other threads hook: a stale root
-// only makes its CAS fail, and the edge is simply kept for the next round.  The
-// component's top (its largest id, which the etree needs) is tracked separately.
+// of x (a word of an older level reads as x itself, the level's start value).  Plain
+// loads/stores are therefore safe while other threads hook: a stale root only makes its
+// CAS fail, and the edge is simply kept for the next round.  The component's top (its
+// largest id, which the etree needs) is tracked separately.
 // (Linking under the larger root instead, so root = top, measured 2x slower hooking.)
 
 // Path splitting on two chains in lockstep (both loads in flight at once).
-__device__ __forceinline__ void find2(uint32_t *uf, uint32_t &x, uint32_t &y) {
-  uint32_t px = uf[x], py = uf[y];
+__device__ __forceinline__ void find2(uint32_t *uf, Tg g, uint32_t &x, uint32_t &y) {
+  uint32_t px = g.get(uf[x], x), py = g.get(uf[y], y);
   while (px != x || py != y) {
     if (px != x) {
-      const uint32_t g = uf[px];
-      if (g != px) uf[x] = g;
+      const uint32_t gg = g.get(uf[px], px);
+      if (gg != px) uf[x] = g.enc(gg);
       x = px;
-      px = g;
+      px = gg;
     }
     if (py != y) {
-      const uint32_t g = uf[py];
-      if (g != py) uf[y] = g;
+      const uint32_t gg = g.get(uf[py], py);
+      if (gg != py) uf[y] = g.enc(gg);
       y = py;
-      py = g;
+      py = gg;
     }
   }
 }
-__device__ __forceinline__ uint32_t find_plain(uint32_t *uf, uint32_t x) {
-  uint32_t p = uf[x];
-  while (p != x) {
-    const uint32_t g = uf[p];
-    if (g != p) uf[x] = g;
-    x = p;
-    p = g;
-  }
-  return x;
-}
 
+// Hooks root hi under lo: succeeds only while hi is still a root (its word unchanged).
+__device__ __forceinline__ bool hook(uint32_t *uf, Tg g, uint32_t hi, uint32_t lo) {
+  const uint32_t w = uf[hi];
+  if (g.get(w, hi) != hi) return false;
+  return atomicCAS(&uf[hi], w, g.enc(lo)) == w;
+}
 
 // K independent chains in lockstep: each round issues one load per unfinished chain,
 // so a thread keeps K pointer chases in flight instead of one.
-template <int K> __device__ __forceinline__ void find_many(uint32_t *uf, uint32_t (&x)[K], const bool (&v)[K]) {
+template <int K> __device__ __forceinline__ void find_many(uint32_t *uf, Tg g, uint32_t (&x)[K], const bool (&v)[K]) {
   uint32_t p[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) p[k] = v[k] ? uf[x[k]] : x[k];
+  for (int k = 0; k < K; ++k) p[k] = v[k] ? g.get(uf[x[k]], x[k]) : x[k];
   for (;;) {
     bool any = false;
 #pragma unroll
@@ -86,10 +115,10 @@ template <int K> __device__ __forceinline__ void find_many(uint32_t *uf, uint32_
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       if (p[k] != x[k]) {
-        const uint32_t g = uf[p[k]];
-        if (g != p[k]) uf[x[k]] = g;
+        const uint32_t gg = g.get(uf[p[k]], p[k]);
+        if (gg != p[k]) uf[x[k]] = g.enc(gg);
         x[k] = p[k];
-        p[k] = g;
+        p[k] = gg;
       }
     }
   }
@@ -187,31 +216,34 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t *__restrict__ uf, uint
   for (uint64_t i = t0; i < NCSET * CSET_WORDS; i += stride) csets[i] = 0;
 }
 
-// End of a level: back to the reset state for the next one.  Only light endpoints (uf,
-// top), cross roots (mt) and cross hi ends (claim) were written, so when those lists are
-// short against n they are undone entry by entry (k_cross_apply then also stored the
-// parents); otherwise a dense pass assigns parent(top of every component with a cross
-// edge) = m_r (jnode.h:158-162 adopt) and rewrites the arrays whole.  The choice is made
-// on the device from the level's counts (no host round trip).
-__device__ __forceinline__ bool level_sparse(uint64_t nl, uint64_t nx, uint64_t n) {
-  return (nl + nx) * 8 < n;   // a scattered 4-B store costs about a line; a dense pass 16 B per vertex
-}
-
+// End of a level: the counter sets back to zero.  Tagged state: parent(top(r)) = m_r for
+// every root with a cross edge, from one streaming read of mt (a random store per cross
+// edge in k_cross_apply cost more).  Untagged state (n >= 2^27 - 1): back to the reset
+// values — entry by entry when the level's lists are short against n (only light
+// endpoints, cross roots and cross hi ends were written), else densely; the choice is
+// made on the device from the level's counts (no host round trip).
 __global__ __launch_bounds__(BLOCK) void k_level_clean(const uint64_t *__restrict__ lbuf, const uint64_t *__restrict__ xbuf,
                                                        const uint32_t *__restrict__ xtop,
                                                        const uint64_t *__restrict__ st, uint32_t *__restrict__ uf,
                                                        uint32_t *__restrict__ mt, uint32_t *__restrict__ top,
-                                                       uint32_t *__restrict__ claim, uint64_t n,
+                                                       uint32_t *__restrict__ claim, uint64_t n, bool tagged, int lvl,
                                                        uint32_t *__restrict__ parent,
                                                        unsigned long long *__restrict__ csets) {
   const uint64_t nl = st[ST_NL], nx = st[ST_NX];
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   const uint64_t t0 = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
   for (uint64_t i = t0; i < NCSET * CSET_WORDS; i += stride) csets[i] = 0;
-  if (!level_sparse(nl, nx, n)) {
+  if (tagged) {   // parent(top(r)) = m_r for every root r with a cross edge (jnode.h:158-162 adopt)
+    const Tg g = make_tag(lvl, true);
+    if (nx == 0) return;
     for (uint64_t i = t0; i < n; i += stride) {
-      const uint32_t m = mt[i];
-      if (m != INVALID && uf[i] == i) parent[top[i]] = m;
+      const uint32_t m = g.m_get(mt[i]);
+      if (m != INVALID) parent[g.get(top[i], (uint32_t)i)] = m;
+    }
+    return;
+  }
+  if ((nl + nx) * 8 >= n) {   // a scattered 4-B store costs about a line; a dense pass 16 B per vertex
+    for (uint64_t i = t0; i < n; i += stride) {
       uf[i] = (uint32_t)i;
       mt[i] = INVALID;
       top[i] = (uint32_t)i;
@@ -239,7 +271,7 @@ constexpr int XK = 4;   // items per thread in the gather kernels (independent c
 // component is an endpoint of a light edge and its maximum is the hi end of one, so a
 // max over the light edges' hi ends suffices (singletons keep top = self).
 __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict__ lbuf, const uint64_t *__restrict__ n_l,
-                                                     uint32_t *uf, uint32_t *__restrict__ top) {
+                                                     uint32_t *uf, uint32_t *__restrict__ top, Tg g) {
   const uint64_t nl = *n_l;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK * XK;
   const uint64_t iters = (nl + stride - 1) / stride;
@@ -255,8 +287,9 @@ __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict_
       r[k] = (uint32_t)e;
       b[k] = (uint32_t)(e >> 32);
     }
-    find_many<XK>(uf, r, live);
+    find_many<XK>(uf, g, r, live);
     // top only grows: combine lanes sharing the first lane's root, skip useless atomics
+    // (tagged words: an older level's word is smaller than any of this level's)
 #pragma unroll
     for (int k = 0; k < XK; ++k) {
       const uint64_t lm = __ballot(live[k]);
@@ -265,8 +298,8 @@ __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict_
       const uint32_t r0 = __shfl(r[k], first, 64);
       const bool same = live[k] && r[k] == r0;
       const uint32_t v = wave_max(same ? b[k] : 0u);
-      if ((int)__lane_id() == first && v > top[r0]) atomicMax(&top[r0], v);
-      if (live[k] && !same && b[k] > top[r[k]]) atomicMax(&top[r[k]], b[k]);
+      if ((int)__lane_id() == first && v > g.get(top[r0], r0)) atomicMax(&top[r0], g.enc(v));
+      if (live[k] && !same && b[k] > g.get(top[r[k]], r[k])) atomicMax(&top[r[k]], g.enc(b[k]));
     }
   }
 }
@@ -280,7 +313,7 @@ __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict_
 // (Batched finds of all the thread's edges before any hook left more hooks to later
 // rounds: 21-22 ms against 10.8 ms at RMAT-26.)
 __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict__ in, const uint64_t *__restrict__ n_in,
-                                                      uint32_t *uf, uint64_t *__restrict__ out,
+                                                      uint32_t *uf, Tg g, uint64_t *__restrict__ out,
                                                       unsigned long long *__restrict__ counter) {
   const uint64_t nin = *n_in;
   const uint64_t ntiles = (nin + TILE - 1) / TILE;
@@ -296,10 +329,10 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
     for (int j = 0; j < TILE_ITEMS; ++j) {
       if (ev[j] == DEAD) continue;
       uint32_t a = (uint32_t)ev[j], b = (uint32_t)(ev[j] >> 32);
-      find2(uf, a, b);
+      find2(uf, g, a, b);
       if (a == b) continue;
       const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-      if (atomicCAS(&uf[hi], hi, lo) != hi) keep |= 1u << j;
+      if (!hook(uf, g, hi, lo)) keep |= 1u << j;
     }
     uint64_t slot = shard_reserve((uint32_t)__popc(keep), counter, tile, ntiles, 1);
 #pragma unroll
@@ -312,24 +345,25 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
 // hooked in place, retrying until each one's roots agree.  Lock-free: a failed CAS
 // means another hook made progress.
 __global__ __launch_bounds__(BLOCK) void k_hook_finish(const uint64_t *__restrict__ in, const uint64_t *__restrict__ n_in,
-                                                       uint32_t *uf) {
+                                                       uint32_t *uf, Tg g) {
   const uint64_t nin = *n_in;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nin; i += stride) {
     const uint64_t e = in[i];
     uint32_t a = (uint32_t)e, b = (uint32_t)(e >> 32);
     for (;;) {
-      find2(uf, a, b);
+      find2(uf, g, a, b);
       if (a == b) break;
       const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-      if (atomicCAS(&uf[hi], hi, lo) == hi) break;
+      if (hook(uf, g, hi, lo)) break;
     }
   }
 }
 
 // For every cross edge (a,b): r = root of a's light component; m_r = min b (atomicMin).
 __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict__ xbuf, const uint64_t *__restrict__ n_x,
-                                                      uint32_t *uf, uint32_t *__restrict__ mt, uint32_t *__restrict__ xtop) {
+                                                      uint32_t *uf, uint32_t *__restrict__ mt, uint32_t *__restrict__ xtop,
+                                                      Tg g) {
   const uint64_t nx = *n_x;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK * XK;
   const uint64_t iters = (nx + stride - 1) / stride;
@@ -344,18 +378,16 @@ __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict
       t[k] = (uint32_t)e;
       b[k] = (uint32_t)(e >> 32);
     }
-    find_many<XK>(uf, t, cross);
+    find_many<XK>(uf, g, t, cross);
 #pragma unroll
     for (int k = 0; k < XK; ++k)
       if (cross[k]) xtop[base + (uint64_t)k * BLOCK] = t[k];
     // Power-law graphs send most cross edges of a level to one giant component's top:
     // combine in the wave first (lanes sharing the first lane's top) and skip atomics a
     // plain read already shows useless (mt only decreases; a stale read is >= the true
-    // value, so skipping stays exact).  (Issuing the other lanes' atomics without the
-    // read, as no-return atomics, cost 25x at RMAT-28 and Chung-Lu, where lanes beside
-    // the first still hit hub tops.)  Measured: issuing the other lanes' atomics
-    // without the read (no-return atomics) costs 25x at RMAT-28 / Chung-Lu, where
-    // lanes beside the first still hit hub tops.
+    // value, so skipping stays exact; the tagged words compare the same way).  (Issuing
+    // the other lanes' atomics without the read, as no-return atomics, cost 25x at
+    // RMAT-28 and Chung-Lu, where lanes beside the first still hit hub tops.)
 #pragma unroll
     for (int k = 0; k < XK; ++k) {
       const uint64_t cm = __ballot(cross[k]);
@@ -364,19 +396,20 @@ __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict
       const uint32_t t0 = __shfl(t[k], first, 64);
       const bool same = cross[k] && t[k] == t0;
       const uint32_t v = wave_min(same ? b[k] : INVALID);
-      if ((int)__lane_id() == first && v < mt[t0]) atomicMin(&mt[t0], v);
-      if (cross[k] && !same && b[k] < mt[t[k]]) atomicMin(&mt[t[k]], b[k]);
+      if ((int)__lane_id() == first && g.m_enc(v) < mt[t0]) atomicMin(&mt[t0], g.m_enc(v));
+      if (cross[k] && !same && g.m_enc(b[k]) < mt[t[k]]) atomicMin(&mt[t[k]], g.m_enc(b[k]));
     }
   }
 }
 
 // Contract every cross edge (a,b) -> (m_r, b) where r = a's light component; drop it
-// when b == m_r.  Dedup: claim[b] holds the first contracted lo seen for b; an edge that
-// finds its own m_r there is a duplicate of a kept edge and dies.  (Exact: only equal
-// (m_r, b) pairs die, and the claimant itself is kept.  Lossy: a second distinct m for
-// the same b is kept without a check — the common duplicates, a giant component's many
-// edges into one hub, all carry the same m.)  claim is n x u32, L3-resident, unlike a
-// global hash table of the pairs.
+// when b == m_r.  parent(top(r)) = m_r (jnode.h:158-162 adopt) is stored by k_level_clean
+// in one pass over mt (tagged state) or here by the edges with b == m_r.  Dedup: claim[b] holds
+// the first contracted lo seen for b; an edge that finds its own m_r there is a duplicate
+// of a kept edge and dies.  (Exact: only equal (m_r, b) pairs die, and the claimant
+// itself is kept.  Lossy: a second distinct m for the same b is kept without a check —
+// the common duplicates, a giant component's many edges into one hub, all carry the same
+// m.)  claim is n x u32, L3-resident, unlike a global hash table of the pairs.
 //
 // The surviving contractions are APPENDED to the next list, after the entries k_split
 // kept: each 2048-edge tile reserves its survivors' slots in a sharded append (one
@@ -389,9 +422,8 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restric
                                                        const uint32_t *__restrict__ top, uint32_t *__restrict__ claim,
                                                        uint64_t *__restrict__ scratch,
                                                        unsigned long long *__restrict__ counters,
-                                                       uint32_t *__restrict__ parent, uint64_t n) {
+                                                       uint32_t *__restrict__ parent, Tg g) {
   const uint64_t nx = st[ST_NX];
-  const bool sparse = level_sparse(st[ST_NL], nx, n);
   const uint64_t ntiles = (nx + TILE - 1) / TILE;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     uint32_t r[TILE_ITEMS], b[TILE_ITEMS], m[TILE_ITEMS], cl[TILE_ITEMS];
@@ -404,18 +436,21 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restric
       b[k] = live ? (uint32_t)(xbuf[j] >> 32) : 0;
     }
 #pragma unroll
-    for (int k = 0; k < TILE_ITEMS; ++k) m[k] = r[k] != INVALID ? mt[r[k]] : INVALID;
+    for (int k = 0; k < TILE_ITEMS; ++k) m[k] = r[k] != INVALID ? g.m_get(mt[r[k]]) : INVALID;
 #pragma unroll
     for (int k = 0; k < TILE_ITEMS; ++k) {
-      if (r[k] != INVALID && sparse) parent[top[r[k]]] = m[k];   // jnode.h:158-162 adopt (every cross edge of r stores the same m)
+      if (r[k] != INVALID && b[k] == m[k] && !g.on) parent[top[r[k]]] = m[k];   // untagged: here (tagged: k_level_clean)
       cl[k] = r[k] != INVALID && b[k] != m[k] ? claim[b[k]] : 0;
     }
 #pragma unroll
     for (int k = 0; k < TILE_ITEMS; ++k) {
       if (r[k] == INVALID || b[k] == m[k]) continue;
-      uint32_t c = cl[k];
-      if (c == INVALID) c = atomicCAS(&claim[b[k]], INVALID, m[k]);
-      if (c != m[k]) keep |= 1u << k;   // someone else's (m, b) is kept (our own successful CAS returned INVALID)
+      uint32_t c = g.claim_get(cl[k]);
+      if (c == INVALID) {
+        const uint32_t old = atomicCAS(&claim[b[k]], cl[k], g.enc(m[k]));
+        c = old == cl[k] ? INVALID : g.claim_get(old);
+      }
+      if (c != m[k]) keep |= 1u << k;   // someone else's (m, b) is kept (our own successful CAS left INVALID)
     }
     uint64_t slot = shard_reserve((uint32_t)__popc(keep), counters, tile, ntiles, 1);
 #pragma unroll
@@ -875,13 +910,16 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   const unsigned gt = grid_tiles(m), gt2 = grid_tiles(lcap + m), gf = grid_for(m, BLOCK * XK), gn = grid_for(n);
   const int FINB = fin_bits < 0 ? 0 : fin_bits > FIN_BITS_MAX ? FIN_BITS_MAX : fin_bits;   // levels s < FINB: Liu per block (0: none)
   const int nglobal = L > FINB ? L - FINB : 0;
-  // the union-find state starts clean; each level restores it at its end (k_level_clean)
+  // the per-level state starts clean; tagged words need no restore between levels,
+  // untagged ones are restored at each level's end (k_level_clean)
+  const bool tagged = n < TAG_MAX_N;
   hipLaunchKernelGGL(k_reset, dim3(gn), dim3(BLOCK), 0, c.stream, uf, mt, top, claim, n, csets);
   LAUNCH_CHECK();
   for (int lvl = 0; lvl < nglobal; ++lvl) {
     const int s = L - 1 - lvl;
     uint64_t *st = stats + (uint64_t)lvl * ST_ROW;
     const uint64_t *prev = lvl ? st - ST_ROW : nullptr;
+    const Tg g = make_tag(lvl, tagged);
     uint64_t *cur = lists[lvl & 1], *next = lists[(lvl + 1) & 1];
     {
       TimedRegion tr(c, "etree_split");
@@ -899,34 +937,34 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       const uint64_t *in = lbuf, *n_in = st + ST_NL;
       for (int round = 0; round < HOOK_ROUNDS; ++round) {
         uint64_t *dst = hk[round & 1];
-        hipLaunchKernelGGL(k_hook_round, dim3(gt), dim3(BLOCK), 0, c.stream, in, n_in, uf, alt, cset(CSET_HOOK + round));
+        hipLaunchKernelGGL(k_hook_round, dim3(gt), dim3(BLOCK), 0, c.stream, in, n_in, uf, g, alt, cset(CSET_HOOK + round));
         LAUNCH_CHECK();
         pack_shards<uint64_t>(c, alt, dst, n_in, cset(CSET_HOOK + round), st + ST_HOOK + round);
         in = dst;
         n_in = st + ST_HOOK + round;
       }
-      hipLaunchKernelGGL(k_hook_finish, dim3(gf), dim3(BLOCK), 0, c.stream, in, n_in, uf);
+      hipLaunchKernelGGL(k_hook_finish, dim3(gf), dim3(BLOCK), 0, c.stream, in, n_in, uf, g);
       LAUNCH_CHECK();
       hipLaunchKernelGGL(k_light_top, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
-                         (const uint64_t *)(st + ST_NL), uf, top);
+                         (const uint64_t *)(st + ST_NL), uf, top, g);
       LAUNCH_CHECK();
     }
     {
       TimedRegion tr(c, "etree_cross");
       hipLaunchKernelGGL(k_cross_find, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)xbuf,
-                         (const uint64_t *)(st + ST_NX), uf, mt, xtop);
+                         (const uint64_t *)(st + ST_NX), uf, mt, xtop, g);
       LAUNCH_CHECK();
     }
     {
       TimedRegion tr(c, "etree_apply");
       hipLaunchKernelGGL(k_cross_apply, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)xbuf,
                          (const uint32_t *)xtop, (const uint64_t *)st, (const uint32_t *)mt, (const uint32_t *)top, claim,
-                         alt, cset(CSET_APPLY), parent, n);
+                         alt, cset(CSET_APPLY), parent, g);
       LAUNCH_CHECK();
       pack_shards<uint64_t>(c, alt, next, st + ST_NX, cset(CSET_APPLY), st + ST_CONTR, nullptr, nullptr, st + ST_KEPT);
       hipLaunchKernelGGL(k_level_clean, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
                          (const uint64_t *)xbuf, (const uint32_t *)xtop, (const uint64_t *)st, uf, mt, top, claim, n,
-                         parent, csets);
+                         tagged, lvl, parent, csets);
       LAUNCH_CHECK();
     }
   }
