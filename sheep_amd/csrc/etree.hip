@@ -103,19 +103,26 @@ __device__ __forceinline__ bool hook(uint32_t *uf, Tg g, uint32_t hi, uint32_t l
 
 // K independent chains in lockstep: each round issues one load per unfinished chain,
 // so a thread keeps K pointer chases in flight instead of one.
+// (Loads are issued for all K chains before any word is decoded — a chain that is done
+// reloads its own root's word — so the K loads stay in flight together: decoding each
+// word inside its chain's branch made the compiler wait for every load in turn.)
 template <int K> __device__ __forceinline__ void find_many(uint32_t *uf, Tg g, uint32_t (&x)[K], const bool (&v)[K]) {
-  uint32_t p[K];
+  uint32_t p[K], w[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) p[k] = v[k] ? g.get(uf[x[k]], x[k]) : x[k];
+  for (int k = 0; k < K; ++k) w[k] = uf[x[k]];
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k] = v[k] ? g.get(w[k], x[k]) : x[k];
   for (;;) {
     bool any = false;
 #pragma unroll
     for (int k = 0; k < K; ++k) any |= p[k] != x[k];
     if (!any) break;
 #pragma unroll
+    for (int k = 0; k < K; ++k) w[k] = uf[p[k]];
+#pragma unroll
     for (int k = 0; k < K; ++k) {
       if (p[k] != x[k]) {
-        const uint32_t gg = g.get(uf[p[k]], p[k]);
+        const uint32_t gg = g.get(w[k], p[k]);
         if (gg != p[k]) uf[x[k]] = g.enc(gg);
         x[k] = p[k];
         p[k] = gg;
@@ -435,12 +442,18 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restric
       r[k] = live ? xtop[j] : INVALID;
       b[k] = live ? (uint32_t)(xbuf[j] >> 32) : 0;
     }
+    // every gather stage issued for all 8 edges before any word is decoded (a decode
+    // inside each edge's branch serialised the loads: 2x slower at RMAT-22)
 #pragma unroll
-    for (int k = 0; k < TILE_ITEMS; ++k) m[k] = r[k] != INVALID ? g.m_get(mt[r[k]]) : INVALID;
+    for (int k = 0; k < TILE_ITEMS; ++k) m[k] = mt[r[k] != INVALID ? r[k] : 0];
 #pragma unroll
-    for (int k = 0; k < TILE_ITEMS; ++k) {
-      if (r[k] != INVALID && b[k] == m[k] && !g.on) parent[top[r[k]]] = m[k];   // untagged: here (tagged: k_level_clean)
-      cl[k] = r[k] != INVALID && b[k] != m[k] ? claim[b[k]] : 0;
+    for (int k = 0; k < TILE_ITEMS; ++k) m[k] = r[k] != INVALID ? g.m_get(m[k]) : INVALID;
+#pragma unroll
+    for (int k = 0; k < TILE_ITEMS; ++k) cl[k] = claim[b[k]];
+    if (!g.on) {   // untagged state: the adoption here (tagged: k_level_clean)
+#pragma unroll
+      for (int k = 0; k < TILE_ITEMS; ++k)
+        if (r[k] != INVALID && b[k] == m[k]) parent[top[r[k]]] = m[k];
     }
 #pragma unroll
     for (int k = 0; k < TILE_ITEMS; ++k) {
