@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=None, help="generator seed (default: the RMAT scale; 2010 for powerlaw)")
     ap.add_argument("--graph", default="rmat", choices=("rmat", "powerlaw"),
                     help="rmat: Graph500 RMAT (C2/C3/C5); powerlaw: Chung-Lu at twitter-2010 scale (C4)")
-    ap.add_argument("--draws", type=int, default=1_560_000_000,
+    ap.add_argument("--draws", type=int, default=2_222_000_000,
                     help="powerlaw edge draws (about 1.468e9 records survive the dedup, twitter-2010's count)")
     ap.add_argument("--shards", type=int, default=1,
                     help="one GPU: edge shards mapped one after another and merged K-way (graphs of >= 2^32 "

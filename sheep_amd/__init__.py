@@ -649,7 +649,7 @@ def rmat(scale: int, edgefactor: int = 16, seed: int = 1, ctx: Context | None = 
 TWITTER_VERTICES = 41_652_230      # twitter-2010 (slurm-fen-twitter.out:2)
 
 
-def powerlaw(nverts: int = TWITTER_VERTICES, draws: int = 1_600_000_000, gamma: float = 1.9, seed: int = 2010,
+def powerlaw(nverts: int = TWITTER_VERTICES, draws: int = 2_222_000_000, gamma: float = 1.9, seed: int = 2010,
              ctx: Context | None = None):
     """Chung-Lu power-law records generated in HBM (BASELINE config C4): [R, 3] int32."""
     ctx = ctx or default_context()
