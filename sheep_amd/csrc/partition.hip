@@ -209,32 +209,46 @@ __global__ void k_parts_to_vid(const uint32_t *__restrict__ seq, uint64_t seq_n,
 // only ranks the remaining core T'.
 constexpr int RAKE_ROUNDS = 2;
 
-__global__ void k_rake_init(const uint32_t *__restrict__ koff, const uint64_t *__restrict__ w, uint64_t n,
-                            uint32_t *__restrict__ pend, uint64_t *__restrict__ acc, uint8_t *__restrict__ fin) {
+// The rake state of a node is ONE u64: acc << 24 | kids not yet finished, so a finished
+// kid's push is a single atomicAdd(acc_kid << 24 - 1) on its parent (no borrow: the
+// count is >= 1 while the kid is unfinished).  Needs every node's kid count < 2^24 and
+// the total weight < 2^40 (else the partition runs without raking: all nodes are core).
+constexpr int RAKE_CNT_BITS = 24;
+constexpr uint64_t RAKE_CNT_MASK = (1ull << RAKE_CNT_BITS) - 1;
+
+// round 1's mark fused in: a leaf finishes when its weight is <= max_component
+__global__ void k_rake_init(const uint32_t *__restrict__ koff, const uint64_t *__restrict__ w, uint64_t n, uint64_t maxc,
+                            bool rake, uint64_t *__restrict__ pk, uint8_t *__restrict__ fin) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride) {
-    pend[v] = koff[v + 1] - koff[v];
-    acc[v] = w[v];
-    fin[v] = 0;
+    const uint32_t nk = koff[v + 1] - koff[v];
+    pk[v] = (w[v] << RAKE_CNT_BITS) | nk;
+    fin[v] = rake && nk == 0 && w[v] <= maxc;
   }
 }
 // mark, then push: the two phases keep a round's finished set independent of timing
-__global__ void k_rake_mark(const uint32_t *__restrict__ pend, const uint64_t *__restrict__ acc, uint64_t n,
-                            uint64_t maxc, uint8_t round, uint8_t *__restrict__ fin) {
+__global__ void k_rake_mark(const uint64_t *__restrict__ pk, uint64_t n, uint64_t maxc, uint8_t round,
+                            uint8_t *__restrict__ fin) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride)
-    if (!fin[v] && pend[v] == 0 && acc[v] <= maxc) fin[v] = round;
+  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride) {
+    const uint64_t x = pk[v];
+    if (!fin[v] && (x & RAKE_CNT_MASK) == 0 && (x >> RAKE_CNT_BITS) <= maxc) fin[v] = round;
+  }
 }
 __global__ void k_rake_push(const uint32_t *__restrict__ parent, const uint8_t *__restrict__ fin, uint64_t n,
-                            uint8_t round, uint64_t *__restrict__ acc, uint32_t *__restrict__ pend) {
+                            uint8_t round, uint64_t *__restrict__ pk) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride) {
     if (fin[v] != round) continue;
     const uint32_t p = parent[v];
     if (p == INVALID) continue;
-    atomicAdd((unsigned long long *)&acc[p], (unsigned long long)acc[v]);
-    atomicSub(&pend[p], 1u);
+    atomicAdd((unsigned long long *)&pk[p], (unsigned long long)(((pk[v] >> RAKE_CNT_BITS) << RAKE_CNT_BITS) - 1));
   }
+}
+// acc out of the packed words, in place
+__global__ void k_rake_acc(uint64_t *__restrict__ pk, uint64_t n) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride) pk[v] >>= RAKE_CNT_BITS;
 }
 
 // The core's kid table: the kid table's segments with finished kids dropped (order kept);
@@ -309,20 +323,49 @@ __device__ __forceinline__ EvView load_table(const uint32_t *gpos, const uint64_
   return EvView{spos, spre, m};
 }
 
-// The next packing node: the lowest-index heavy node after the last packing node whose
-// residual exceeds max_component.  Workgroups take 2048-entry chunks in index order and
-// stop once a hit below their chunk is known, so an event reads about the distance to
-// the next packing node instead of the whole heavy set.
+// One packing event in one launch.  Every workgroup scans 2048-entry chunks of the heavy
+// set in index order for the lowest-index node after the last packing node whose
+// residual exceeds max_component, and stops once a hit below its chunk is known (an
+// event reads about the distance to the next packing node, not the whole heavy set).
+// The last workgroup to finish then knows the node and stages the event straight into
+// mapped host memory: hdr = {v, koff[v], #kids, R[v] lo, R[v] hi, tD(v) (INVALID for a
+// root), kids staged?}, the node's kids in their current order and their residuals (up
+// to EV_INLINE of them; larger kid lists go through k_event_kids).  It resets the
+// search state for the next event and raises hdr[7] = seq (system scope), which the
+// host polls instead of synchronising the stream.  The event table is read from mapped
+// host memory too (the host rewrites it between events), so an event is ONE launch.
 constexpr int EVI = 8, EV_CH = BLOCK * EVI;
-__global__ __launch_bounds__(BLOCK) void k_next_event(const uint32_t *__restrict__ hids, uint64_t nh,
-                                                      const uint64_t *__restrict__ SH, const uint32_t *__restrict__ hst,
-                                                      const uint32_t *__restrict__ hen, const uint32_t *__restrict__ epos,
-                                                      const uint64_t *__restrict__ epre, uint32_t m, uint64_t maxc,
-                                                      const uint64_t *__restrict__ evprev,
-                                                      unsigned long long *__restrict__ found) {
+constexpr uint32_t EV_STAGE = 1u << 16;   // mapped staging area (kids)
+constexpr uint32_t EV_INLINE = 4096;      // kid lists staged by the event kernel itself
+
+__device__ __forceinline__ void stage_kids(const EvView &ev, uint32_t beg, uint32_t lim, uint32_t j0, uint32_t stride,
+                                           const uint32_t *kids, const uint64_t *S, const uint32_t *cparent,
+                                           const uint32_t *tD, const uint32_t *tU, uint32_t *kid_out, uint64_t *r_out) {
+  for (uint32_t j = j0; j < lim; j += stride) {
+    const uint32_t kid = kids[beg + j];
+    uint64_t r = S[kid];
+    if (cparent[kid] != INVALID) r -= ev.removed(tD[kid], tU[kid]);   // fringe kids never had a packing below
+    kid_out[j] = kid;
+    r_out[j] = r;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hids, uint64_t nh,
+                                                 const uint64_t *__restrict__ SH, const uint32_t *__restrict__ hst,
+                                                 const uint32_t *__restrict__ hen, const uint32_t *__restrict__ epos,
+                                                 const uint64_t *__restrict__ epre, uint32_t m, uint64_t maxc,
+                                                 uint64_t *__restrict__ evprev, unsigned long long *__restrict__ found,
+                                                 unsigned *__restrict__ done, const uint32_t *__restrict__ koff,
+                                                 const uint32_t *__restrict__ kids, const uint64_t *__restrict__ S,
+                                                 const uint32_t *__restrict__ cparent, const uint32_t *__restrict__ ckoff,
+                                                 const uint32_t *__restrict__ tD, const uint32_t *__restrict__ tU,
+                                                 const uint32_t *__restrict__ rst, const uint32_t *__restrict__ ren,
+                                                 uint32_t *__restrict__ hdr, uint32_t *__restrict__ kid_out,
+                                                 uint64_t *__restrict__ r_out, uint32_t seq) {
   __shared__ uint32_t spos[EV_LDS];
   __shared__ uint64_t spre[EV_LDS + 1];
   __shared__ unsigned long long s_best[BLOCK / WAVE];
+  __shared__ bool last;
   const EvView ev = load_table(epos, epre, m, spos, spre);
   const uint64_t prev = *evprev;
   const uint64_t start = prev == ~0ull ? 0 : (uint32_t)prev;
@@ -355,35 +398,18 @@ __global__ __launch_bounds__(BLOCK) void k_next_event(const uint32_t *__restrict
     }
     __syncthreads();
   }
-}
-
-// Everything the host needs for one packing event, stored straight into mapped host
-// memory: hdr = {v, koff[v], #kids, R[v] lo, R[v] hi, tD(v) (INVALID for a root)}, then
-// the node's kids in their current order and their residuals (the first `cap` of them).
-// The last workgroup to finish raises hdr[7] = seq (system-scope), which the host polls
-// instead of synchronising the stream.
-constexpr uint32_t EV_STAGE = 1u << 16;
-__global__ __launch_bounds__(BLOCK) void k_event_stage(const unsigned long long *__restrict__ found,
-                                                       uint64_t *__restrict__ evprev, const uint32_t *__restrict__ epos,
-                                                       const uint64_t *__restrict__ epre, uint32_t m,
-                                                       const uint32_t *__restrict__ koff,
-                                                       const uint32_t *__restrict__ kids, const uint64_t *__restrict__ S,
-                                                       const uint32_t *__restrict__ cparent,
-                                                       const uint32_t *__restrict__ ckoff, const uint32_t *__restrict__ tD,
-                                                       const uint32_t *__restrict__ tU, const uint32_t *__restrict__ rst,
-                                                       const uint32_t *__restrict__ ren, uint32_t *__restrict__ hdr,
-                                                       uint32_t *__restrict__ kid_out, uint64_t *__restrict__ r_out,
-                                                       uint32_t beg_j, uint32_t cap, unsigned *__restrict__ done,
-                                                       uint32_t seq) {
-  __shared__ uint32_t spos[EV_LDS];
-  __shared__ uint64_t spre[EV_LDS + 1];
-  __shared__ bool last;
-  const uint64_t e = *found;
+  // the last workgroup to finish sees every other workgroup's atomicMin
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  const unsigned long long e = __hip_atomic_load(found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t v = e == ~0ull ? INVALID : (uint32_t)(e >> 32);
   if (v != INVALID) {
-    const EvView ev = load_table(epos, epre, m, spos, spre);
     const uint32_t beg = koff[v], cnt = koff[v + 1] - beg;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && beg_j == 0) {
+    if (cnt <= EV_INLINE) stage_kids(ev, beg, cnt, threadIdx.x, BLOCK, kids, S, cparent, tD, tU, kid_out, r_out);
+    if (threadIdx.x == 0) {
       *evprev = e;
       uint32_t lo, hi;
       node_interval(v, cparent, ckoff, tD, tU, rst, ren, lo, hi);
@@ -394,19 +420,41 @@ __global__ __launch_bounds__(BLOCK) void k_event_stage(const unsigned long long 
       hdr[3] = (uint32_t)r;
       hdr[4] = (uint32_t)(r >> 32);
       hdr[5] = cparent[v] == INVALID ? INVALID : tD[v];
+      hdr[6] = cnt <= EV_INLINE;
     }
-    const uint32_t lim = cnt - beg_j < cap ? cnt - beg_j : cap;
-    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < lim; j += gridDim.x * BLOCK) {
-      const uint32_t kid = kids[beg + beg_j + j];
-      uint64_t r = S[kid];
-      if (cparent[kid] != INVALID) r -= ev.removed(tD[kid], tU[kid]);   // fringe kids never had a packing below
-      kid_out[j] = kid;
-      r_out[j] = r;
-    }
-  } else if (blockIdx.x == 0 && threadIdx.x == 0) {
+  } else if (threadIdx.x == 0) {
     hdr[0] = INVALID;
   }
-  // completion flag: the last workgroup publishes it after every store is visible
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *found = ~0ull;   // the next event's search starts clean
+    *done = 0;
+    __threadfence_system();
+    __hip_atomic_store(&hdr[7], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// The kids [beg_j, beg_j + cap) of the last event's node (evprev) with their residuals,
+// for kid lists above EV_INLINE; the last workgroup raises hdr[7] = seq.
+__global__ __launch_bounds__(BLOCK) void k_event_kids(const uint64_t *__restrict__ evprev,
+                                                      const uint32_t *__restrict__ epos,
+                                                      const uint64_t *__restrict__ epre, uint32_t m,
+                                                      const uint32_t *__restrict__ koff,
+                                                      const uint32_t *__restrict__ kids, const uint64_t *__restrict__ S,
+                                                      const uint32_t *__restrict__ cparent,
+                                                      const uint32_t *__restrict__ tD, const uint32_t *__restrict__ tU,
+                                                      uint32_t *__restrict__ hdr, uint32_t *__restrict__ kid_out,
+                                                      uint64_t *__restrict__ r_out, uint32_t beg_j, uint32_t cap,
+                                                      unsigned *__restrict__ done, uint32_t seq) {
+  __shared__ uint32_t spos[EV_LDS];
+  __shared__ uint64_t spre[EV_LDS + 1];
+  __shared__ bool last;
+  const uint32_t v = (uint32_t)(*evprev >> 32);
+  const EvView ev = load_table(epos, epre, m, spos, spre);
+  const uint32_t beg = koff[v] + beg_j, cnt = koff[v + 1] - koff[v];
+  const uint32_t lim = cnt - beg_j < cap ? cnt - beg_j : cap;
+  stage_kids(ev, beg, lim, blockIdx.x * BLOCK + threadIdx.x, gridDim.x * BLOCK, kids, S, cparent, tD, tU, kid_out,
+             r_out);
   __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
@@ -593,20 +641,24 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   info->max_component = max_component;
 
   // 2. rake the light fringe (exact subtree sums), then the core T' as its own forest
-  uint64_t *S = c.get_as<uint64_t>("pt_S", n);   // the rake's acc, then every node's subtree sum
-  uint32_t *pend = c.get_as<uint32_t>("pt_pend", n);
+  uint64_t *S = c.get_as<uint64_t>("pt_S", n);   // the rake's packed state, then acc, then every node's subtree sum
   uint8_t *fin = c.get_as<uint8_t>("pt_fin", n);
+  const bool rake = k->max_kids <= RAKE_CNT_MASK && total < (1ull << (64 - RAKE_CNT_BITS));
   hipLaunchKernelGGL(k_rake_init, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->koff,
-                     (const uint64_t *)w, n, pend, S, fin);
+                     (const uint64_t *)w, n, max_component, rake, S, fin);
   LAUNCH_CHECK();
-  for (int r = 1; r <= RAKE_ROUNDS; ++r) {
-    hipLaunchKernelGGL(k_rake_mark, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)pend,
-                       (const uint64_t *)S, n, max_component, (uint8_t)r, fin);
-    LAUNCH_CHECK();
+  for (int r = 1; rake && r <= RAKE_ROUNDS; ++r) {
+    if (r > 1) {
+      hipLaunchKernelGGL(k_rake_mark, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint64_t *)S, n, max_component,
+                         (uint8_t)r, fin);
+      LAUNCH_CHECK();
+    }
     hipLaunchKernelGGL(k_rake_push, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->parent,
-                       (const uint8_t *)fin, n, (uint8_t)r, S, pend);
+                       (const uint8_t *)fin, n, (uint8_t)r, S);
     LAUNCH_CHECK();
   }
+  hipLaunchKernelGGL(k_rake_acc, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, S, n);
+  LAUNCH_CHECK();
   sheep_kids core;
   core.ctx = &c;
   core.n = n;
@@ -679,6 +731,7 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   unsigned *done_ctr = (unsigned *)(c.d_scalars + 47);
   HIP_CHECK(hipMemsetAsync(evprev, 0xFF, sizeof(uint64_t), c.stream));
   HIP_CHECK(hipMemsetAsync(done_ctr, 0, sizeof(uint64_t), c.stream));
+  HIP_CHECK(hipMemsetAsync(found, 0xFF, sizeof(uint64_t), c.stream));   // k_event resets it after each event
   uint8_t *stage = (uint8_t *)c.get_pinned("pt_event", 64 + (size_t)EV_STAGE * 12);
   volatile uint32_t *hdr = (volatile uint32_t *)stage;
   uint32_t *st_kids = (uint32_t *)(stage + 64);
@@ -688,28 +741,41 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   HIP_CHECK(hipHostGetDevicePointer((void **)&d_hdr, stage, 0));
   HIP_CHECK(hipHostGetDevicePointer((void **)&d_kids, st_kids, 0));
   HIP_CHECK(hipHostGetDevicePointer((void **)&d_r, st_r, 0));
-  // the event table (sorted tD of the non-root packings, prefix sums of their deltas):
-  // host copy -> pinned staging -> device, one async copy per event
+  // the event table (sorted tD of the non-root packings, prefix sums of their deltas),
+  // written by the host into mapped memory between events; the kernels read it there
+  // (into LDS) — a device copy only when it outgrows the LDS copy, and once at the end
   std::vector<std::pair<uint32_t, uint64_t>> evs;
   uint32_t *ev_pos = c.get_as<uint32_t>("pt_evpos", nh + 1);
   uint64_t *ev_pre = c.get_as<uint64_t>("pt_evpre", nh + 2);
   uint8_t *ev_stage = (uint8_t *)c.get_pinned("pt_evtable", (size_t)(nh + 2) * 12 + 16);
+  uint8_t *d_ev_stage;
+  HIP_CHECK(hipHostGetDevicePointer((void **)&d_ev_stage, ev_stage, 0));
   uint32_t m_ev = 0;
-  HIP_CHECK(hipMemsetAsync(ev_pre, 0, sizeof(uint64_t), c.stream));
-  auto upload_table = [&]() {
+  const uint32_t *t_pos = (const uint32_t *)d_ev_stage;   // the table the next launch reads
+  const uint64_t *t_pre = (const uint64_t *)(d_ev_stage + 8);
+  *(uint64_t *)(ev_stage + 8) = 0;   // empty table: pre[0] = 0
+  auto write_table = [&](bool to_device) {
     m_ev = (uint32_t)evs.size();
+    const size_t pre_off = ((size_t)m_ev * 4 + 15) & ~(size_t)7;
     uint32_t *hp = (uint32_t *)ev_stage;
-    uint64_t *hs = (uint64_t *)(ev_stage + ((size_t)(m_ev * 4 + 15) & ~(size_t)7));
+    uint64_t *hs = (uint64_t *)(ev_stage + pre_off);
     uint64_t run = 0;
     for (uint32_t i = 0; i < m_ev; ++i) { hp[i] = evs[i].first; hs[i] = run; run += evs[i].second; }
     hs[m_ev] = run;
-    if (m_ev) HIP_CHECK(hipMemcpyAsync(ev_pos, hp, m_ev * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
-    HIP_CHECK(hipMemcpyAsync(ev_pre, hs, (m_ev + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+    if (to_device || m_ev > (uint32_t)EV_LDS) {
+      if (m_ev) HIP_CHECK(hipMemcpyAsync(ev_pos, hp, m_ev * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
+      HIP_CHECK(hipMemcpyAsync(ev_pre, hs, (m_ev + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+      t_pos = ev_pos;
+      t_pre = ev_pre;
+    } else {
+      t_pos = (const uint32_t *)d_ev_stage;
+      t_pre = (const uint64_t *)(d_ev_stage + pre_off);
+    }
   };
   std::vector<std::pair<uint32_t, uint64_t>> root_own;   // a root's own packing delta
   uint32_t seq_no = 0;
-  // waits for k_event_stage's completion flag (hdr[7]): a poll of mapped memory wakes the
-  // host sooner than a stream synchronisation
+  // waits for the event kernels' completion flag (hdr[7]): a poll of mapped memory wakes
+  // the host sooner than a stream synchronisation
   auto wait_stage = [&](uint32_t want) {
     for (long spin = 0; hdr[7] != want; ++spin)
       if (spin > (1l << 22)) { c.sync(); break; }
@@ -722,40 +788,40 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   std::vector<uint64_t> segR, scb;
   std::vector<char> done;
   const unsigned gev = nh ? (unsigned)std::min<uint64_t>((nh + EV_CH - 1) / EV_CH, 128) : 1;
-  auto stage_event = [&](uint32_t beg_j, uint32_t cap, uint32_t *o_kids, uint64_t *o_r) {
+  auto stage_kids_of = [&](uint32_t beg_j, uint32_t cap, uint32_t *o_kids, uint64_t *o_r) {
     ++seq_no;
-    hipLaunchKernelGGL(k_event_stage, dim3(256), dim3(BLOCK), 0, c.stream, (const unsigned long long *)found, evprev,
-                       (const uint32_t *)ev_pos, (const uint64_t *)ev_pre, m_ev, (const uint32_t *)k->koff,
-                       (const uint32_t *)k->kids, (const uint64_t *)S, (const uint32_t *)core.parent,
-                       (const uint32_t *)core.koff, (const uint32_t *)t.tD, (const uint32_t *)t.tU, (const uint32_t *)rst,
-                       (const uint32_t *)ren, d_hdr, o_kids, o_r, beg_j, cap, done_ctr, seq_no);
+    hipLaunchKernelGGL(k_event_kids, dim3(256), dim3(BLOCK), 0, c.stream, (const uint64_t *)evprev, t_pos, t_pre, m_ev,
+                       (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
+                       (const uint32_t *)core.parent, (const uint32_t *)t.tD, (const uint32_t *)t.tU, d_hdr, o_kids, o_r,
+                       beg_j, cap, done_ctr, seq_no);
     LAUNCH_CHECK();
+    wait_stage(seq_no);
   };
   {
     TimedRegion tr(c, "partition_events");
     hdr[7] = 0;
     for (;;) {
-      HIP_CHECK(hipMemsetAsync(found, 0xFF, sizeof(uint64_t), c.stream));
-      if (nh) {
-        hipLaunchKernelGGL(k_next_event, dim3(gev), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh,
-                           (const uint64_t *)SH, (const uint32_t *)hst, (const uint32_t *)hen, (const uint32_t *)ev_pos,
-                           (const uint64_t *)ev_pre, m_ev, max_component, (const uint64_t *)evprev, found);
-        LAUNCH_CHECK();
-      }
-      stage_event(0, EV_STAGE, d_kids, d_r);
+      ++seq_no;
+      hipLaunchKernelGGL(k_event, dim3(gev), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh, (const uint64_t *)SH,
+                         (const uint32_t *)hst, (const uint32_t *)hen, t_pos, t_pre, m_ev, max_component, evprev, found,
+                         done_ctr, (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
+                         (const uint32_t *)core.parent, (const uint32_t *)core.koff, (const uint32_t *)t.tD,
+                         (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren, d_hdr, d_kids, d_r, seq_no);
+      LAUNCH_CHECK();
       wait_stage(seq_no);
       const uint32_t v = hdr[0];
       if (v == INVALID) break;
       info->packing_nodes++;
       const uint32_t beg = hdr[1], cnt = hdr[2], vpos = hdr[5];
       uint64_t cb = (uint64_t)hdr[3] | ((uint64_t)hdr[4] << 32);
+      if (!hdr[6]) stage_kids_of(0, EV_STAGE, d_kids, d_r);   // more kids than the event kernel stages
       seg.assign(st_kids, st_kids + std::min(cnt, EV_STAGE));
       segR.assign(st_r, st_r + std::min(cnt, EV_STAGE));
       if (cnt > EV_STAGE) {   // a node with more kids than the staging area: fetch the rest
         seg.resize(cnt); segR.resize(cnt);
         uint32_t *kk = c.get_as<uint32_t>("pt_kK", cnt);
         uint64_t *kR = c.get_as<uint64_t>("pt_kR", cnt);
-        stage_event(EV_STAGE, cnt - EV_STAGE, kk, kR);
+        stage_kids_of(EV_STAGE, cnt - EV_STAGE, kk, kR);
         d2h(c, seg.data() + EV_STAGE, (const uint32_t *)kk, cnt - EV_STAGE);
         d2h(c, segR.data() + EV_STAGE, (const uint64_t *)kR, cnt - EV_STAGE);
         c.sync();
@@ -801,9 +867,10 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
         evs.insert(std::upper_bound(evs.begin(), evs.end(), std::make_pair(vpos, (uint64_t)~0ull)), {vpos, cb0 - cb});
       else
         root_own.push_back({v, cb0 - cb});
-      upload_table();   // (the previous upload is complete: the stage kernel after it has finished)
+      write_table(false);   // (no kernel reads the table now: the last one has finished)
     }
   }
+  write_table(true);   // the device copy k_roots_r reads
   if (!upl_pos.empty()) {   // persist the sorted kid orders (forwardPartition mutates kids, :104-106)
     const uint64_t mu = upl_pos.size();
     uint32_t *dp = c.get_as<uint32_t>("pt_uplpos", mu), *dv = c.get_as<uint32_t>("pt_uplids", mu);

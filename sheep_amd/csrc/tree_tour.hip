@@ -12,6 +12,14 @@
 namespace sheep {
 namespace {
 
+__global__ void k_max_u32(const uint32_t *__restrict__ x, uint64_t n, unsigned long long *__restrict__ out) {
+  uint32_t m = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) m = x[i] > m ? x[i] : m;
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(out, (unsigned long long)m);
+}
+
 __global__ void k_kid_keys(const sheep_jnode *__restrict__ tree, uint64_t n, uint32_t *__restrict__ keys,
                            uint32_t *__restrict__ vals, uint32_t *__restrict__ parent,
                            uint32_t *__restrict__ cnt, unsigned long long *__restrict__ err) {
@@ -216,20 +224,23 @@ void build_kids(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_kids *k) {
   uint32_t *kalt = c.get_as<uint32_t>("kid_kalt", n), *valt = c.get_as<uint32_t>("kid_valt", n);
   HIP_CHECK(hipMemsetAsync(k->koff, 0, (n + 1) * sizeof(uint32_t), c.stream));
   unsigned long long *d = (unsigned long long *)c.d_scalars + 16;
-  HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
+  HIP_CHECK(hipMemsetAsync(d, 0, 3 * sizeof(uint64_t), c.stream));
   hipLaunchKernelGGL(k_kid_keys, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, tree, n, keys, vals, k->parent,
                      k->koff, d);
   LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_max_u32, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->koff, n, d + 2);
+  LAUNCH_CHECK();   // the largest kid count (the partition's packed rake state needs it < 2^24)
   // counts -> offsets; total = number of kids
   scan_exclusive_u32(c, k->koff, k->koff, n + 1, (uint32_t *)(d + 1));
   int bits = 0;
   while (bits < 32 && (n >> bits)) ++bits;
   radix_sort_pairs_u32(c, keys, vals, n, bits, kalt, valt);   // stable: kids ascending per parent
   HIP_CHECK(hipMemcpyAsync(k->kids, vals, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
-  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 16, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 16, d, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
   if (c.h_scalars[16]) throw Error(SHEEP_ERR_RANGE, "tree: parent out of range or not later than its kid");
   k->nkids = (uint32_t)c.h_scalars[17];
+  k->max_kids = c.h_scalars[18];
 }
 
 void build_tour(Ctx &c, sheep_kids *k, Tour &t) {

@@ -10,6 +10,7 @@ struct sheep_kids {
   uint32_t *kids = nullptr;    // child lists, initially ascending id (jnode.h:190-204);
                                // FFD sorts segments in place (persistent, partition.cpp:104-106)
   uint64_t nkids = 0;
+  uint64_t max_kids = 0;       // the largest kid count
 };
 
 namespace sheep {
