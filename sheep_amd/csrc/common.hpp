@@ -292,11 +292,27 @@ bool degree_fused(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_
                   unsigned long long *d_max, unsigned long long *d_err);
 // relabel (jtree.cpp:72-91) in head-bucket order; returns the number of edges written, or
 // UINT64_MAX when the key range / record count does not fit the bucket layout.
+// The padded-lo bucket layout of the first-activity grouping (group_edges_by_lo): host
+// copy + the device padding offsets / bucket bases.
+struct LoGroup {
+  int L = 0;
+  uint32_t clo = 0, mask = 0, nb = 0;
+  uint64_t K = 0;
+  std::vector<uint32_t> padoff, kbase;
+  std::vector<uint64_t> pstart, plen;
+  uint32_t *d_pad = nullptr, *d_kbase = nullptr;
+};
+void lo_group_prepare(Ctx &c, uint64_t n, int L, uint32_t clo, LoGroup &g);
+// relabel (jtree.cpp:72-91) in head-bucket order; returns the number of edges written, or
+// UINT64_MAX when the key range / record count does not fit the bucket layout.  With lg,
+// the gather also writes the edges' (padded-lo bucket, tile) counts for the grouping
+// (*counted = true), so group_edges_by_lo skips its count pass.
 uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
-                          uint32_t *pst, uint64_t *edges, unsigned long long *err);
+                          uint32_t *pst, uint64_t *edges, unsigned long long *err, const LoGroup *lg = nullptr,
+                          bool *counted = nullptr);
 void histogram_edge_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t K, uint32_t *cnt);
-void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, int L, uint32_t clo, uint32_t *pst,
-                       uint64_t *r0, uint64_t *seg);
+void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGroup &g, uint32_t *pst, uint64_t *r0,
+                       uint64_t *seg, bool counted);
 // etree.hip
 void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
                       int fin_bits, uint32_t per_lo);

@@ -1077,10 +1077,19 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   unsigned long long *d = (unsigned long long *)c.d_scalars + 8;
   HIP_CHECK(hipMemsetAsync(d + 1, 0, sizeof(uint64_t), c.stream));
   uint64_t m = nrec;   // edges[i] per record, DEAD holes included (k_relabel)
+  int L = 0;
+  uint32_t clo = 0;
+  LoGroup lg;
+  bool counted = false;
+  if (n >= 2) {
+    spread_params(n, &L, &clo);
+    lo_group_prepare(c, n, L, clo, lg);
+  }
   if (nrec) {
     TimedRegion tr(c, "relabel", 20 * nrec);   // record + 2 pos gathers
-    // head-bucketed relabel (hist.hip) when the key range fits its LDS buckets
-    m = relabel_bucketed(c, rec, nrec, pos, pos_size, pst, edges, d + 1);
+    // head-bucketed relabel (hist.hip) when the key range fits its LDS buckets; it also
+    // counts the edges for the grouping below
+    m = relabel_bucketed(c, rec, nrec, pos, pos_size, pst, edges, d + 1, n >= 2 ? &lg : nullptr, &counted);
     if (m == UINT64_MAX) {
       m = nrec;
       hipLaunchKernelGGL(k_relabel, dim3(grid_tiles(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos, pos_size, pst,
@@ -1092,15 +1101,12 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   c.sync();
   if (c.h_scalars[9]) throw Error(SHEEP_ERR_RANGE, "vector::_M_range_check: neighbour vid beyond the sequence's index (jtree.cpp:75)");
   if (n >= 2 && m) {
-    int L;
-    uint32_t clo;
-    spread_params(n, &L, &clo);
     uint64_t *r0 = c.get_as<uint64_t>("bt_grouped", m);
     uint64_t *seg = c.get_as<uint64_t>("bt_seg", 2 * (uint64_t)L);
     {
       // pst = histogram of the edges' lo; the same passes group the edges by lo
       TimedRegion tr(c, "pst_group", 20 * m);
-      group_edges_by_lo(c, edges, m, n, L, clo, pst, r0, seg);
+      group_edges_by_lo(c, edges, m, lg, pst, r0, seg, counted);
     }
     TimedRegion tr(c, "etree", 8 * m);
     etree_from_edges(c, r0, m, n, parent, seg, FIN_MAP, 0);

@@ -558,38 +558,60 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
 // One workgroup per (bucket, slice of <= CHUNK pairs): the bucket's pos slice in LDS.
 // Same outcomes as k_relabel: both endpoints sequenced -> tree edge (hi << 32 | lo);
 // one sequenced, the other an unsequenced slot -> POSTORDER pst for the sequenced one.
+// COUNT: also the edges' (padded-lo bucket, 32K-edge tile) counts of the grouping's
+// count pass (k_hist_count<EdgeLoPadded> over the same edges, which then does not run):
+// the chunk is walked one output tile at a time with the tile's counts in LDS after the
+// pos slice, flushed with one atomicAdd per non-zero bucket (a tile can span two chunks).
+template <bool COUNT>
 __global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restrict__ pairs, const Chunk *__restrict__ chunks,
                                                        const uint32_t *__restrict__ pos, uint64_t pos_size,
                                                        uint32_t *__restrict__ pst, uint64_t *__restrict__ edges,
-                                                       unsigned long long *__restrict__ flags) {
+                                                       unsigned long long *__restrict__ flags, EdgeLoPadded lk,
+                                                       uint32_t lnb, uint32_t *__restrict__ tile_hist, uint64_t ntiles) {
   extern __shared__ uint32_t lds[];
+  uint32_t *const lcnt = lds + W;
   const Chunk ch = chunks[blockIdx.x];
   const uint64_t v0 = (uint64_t)ch.bucket << WBITS;
   for (uint32_t i = threadIdx.x; i < W; i += HB) lds[i] = v0 + i < pos_size ? pos[v0 + i] : INVALID;
-  __syncthreads();
   bool bad = false;
-  for (uint64_t i0 = ch.beg; i0 < ch.end; i0 += 8 * HB) {
-    uint64_t x[8];
+  for (uint64_t t0 = ch.beg; t0 < ch.end;) {
+    const uint64_t t1 = COUNT ? ((t0 >> TLOG) + 1) << TLOG : ch.end;   // this output tile's part of the chunk
+    const uint64_t s1 = t1 < ch.end ? t1 : ch.end;
+    if (COUNT)
+      for (uint32_t b = threadIdx.x; b < lnb; b += HB) lcnt[b] = 0;
+    __syncthreads();
+    for (uint64_t i0 = t0; i0 < s1; i0 += 8 * HB) {
+      uint64_t x[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
-      x[j] = i >= ch.end ? NO_PAIR : pairs[i];
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
-      if (i >= ch.end) continue;
-      const uint32_t ptm = (uint32_t)(x[j] >> 32), ph = lds[(uint32_t)x[j] & (W - 1)];
-      uint64_t e = ~0ull;   // DEAD
-      if (ph != INVALID) {
-        if (ptm == PT_OOR) bad = true;                       // index.at(tail) throws
-        else if (ptm != INVALID) e = ptm < ph ? ((uint64_t)ph << 32) | ptm : ((uint64_t)ptm << 32) | ph;
-        else atomicAdd(&pst[ph], 1u);
-      } else if (ptm < PT_OOR) {
-        atomicAdd(&pst[ptm], 1u);
+      for (int j = 0; j < 8; ++j) {
+        const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
+        x[j] = i >= s1 ? NO_PAIR : pairs[i];
       }
-      edges[i] = e;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
+        if (i >= s1) continue;
+        const uint32_t ptm = (uint32_t)(x[j] >> 32), ph = lds[(uint32_t)x[j] & (W - 1)];
+        uint64_t e = ~0ull;   // DEAD
+        if (ph != INVALID) {
+          if (ptm == PT_OOR) bad = true;                       // index.at(tail) throws
+          else if (ptm != INVALID) e = ptm < ph ? ((uint64_t)ph << 32) | ptm : ((uint64_t)ptm << 32) | ph;
+          else atomicAdd(&pst[ph], 1u);
+        } else if (ptm < PT_OOR) {
+          atomicAdd(&pst[ptm], 1u);
+        }
+        edges[i] = e;
+        if (COUNT && e != ~0ull) atomicAdd(&lcnt[lk.key(e) >> WBITS], 1u);
+      }
     }
+    if (COUNT) {
+      __syncthreads();
+      const uint64_t tile = t0 >> TLOG;
+      for (uint32_t b = threadIdx.x; b < lnb; b += HB)
+        if (lcnt[b]) atomicAdd(&tile_hist[(uint64_t)b * ntiles + tile], lcnt[b]);
+      __syncthreads();   // lcnt is cleared for the next tile
+    }
+    t0 = s1;
   }
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(&flags[0], 1ull);
 }
@@ -631,11 +653,12 @@ void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uin
 }
 
 uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
-                          uint32_t *pst, uint64_t *edges, unsigned long long *err) {
+                          uint32_t *pst, uint64_t *edges, unsigned long long *err, const LoGroup *lg, bool *counted) {
+  if (counted) *counted = false;
   const uint64_t nb = (pos_size + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
   if (nrec == 0 || nb == 0 || nb > 8192 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return UINT64_MAX;
   for (const void *f : {(const void *)k_relabel_scatter<8>, (const void *)k_relabel_scatter<4>,
-                        (const void *)k_relabel_gather})
+                        (const void *)k_relabel_gather<false>, (const void *)k_relabel_gather<true>})
     allow_full_lds(f);
   Ctx::HeadLayout &hl = c.head_layout;
   unsigned long long *flags = c.get_as<unsigned long long>("rl_flags", 2);
@@ -701,14 +724,31 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   }
   const uint64_t m = hl.bstart[nb];
   if (c.h_scalars[12]) HIP_CHECK(hipMemsetAsync(err, 0xFF, 1, c.stream));   // range error (reported by the caller)
+  // the grouping's count pass fused in when its bucket counters fit beside the pos slice
+  const uint64_t ntiles_e = (m + TKEYS - 1) >> TLOG;
+  const bool count = lg && m && lg->nb && ((size_t)W + lg->nb) * 4 <= 160 * 1024 && ntiles_e * lg->nb + 1 < (1ull << 32) &&
+                     m < (1ull << 32);
+  uint32_t *tile_hist = nullptr;
+  if (count) {
+    tile_hist = c.get_as<uint32_t>("hist_tiles", ntiles_e * lg->nb + 1);
+    HIP_CHECK(hipMemsetAsync(tile_hist, 0, ntiles_e * lg->nb * sizeof(uint32_t), c.stream));
+  }
   if (!chunks.empty()) {
     Chunk *dch = c.get_as<Chunk>("rl_chunks", chunks.size());
     HIP_CHECK(hipMemcpyAsync(dch, chunks.data(), chunks.size() * sizeof(Chunk), hipMemcpyHostToDevice, c.stream));
-    hipLaunchKernelGGL(k_relabel_gather, dim3((unsigned)chunks.size()), dim3(HB), W * 4, c.stream,
-                       (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err);
+    const EdgeLoPadded lk{edges, lg ? lg->d_pad : nullptr, lg ? lg->clo : 0, lg ? lg->mask : 0};
+    if (count)
+      hipLaunchKernelGGL(k_relabel_gather<true>, dim3((unsigned)chunks.size()), dim3(HB), (W + lg->nb) * 4, c.stream,
+                         (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err, lk, lg->nb,
+                         tile_hist, ntiles_e);
+    else
+      hipLaunchKernelGGL(k_relabel_gather<false>, dim3((unsigned)chunks.size()), dim3(HB), W * 4, c.stream,
+                         (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err, lk, 0u,
+                         (uint32_t *)nullptr, (uint64_t)0);
     LAUNCH_CHECK();
     c.sync();   // `chunks` is a pageable host buffer
   }
+  if (counted) *counted = count;
   return m;
 }
 
@@ -719,8 +759,7 @@ void histogram_edge_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t K, ui
 // pst[lo] += edges with that lo, and the edges grouped for the elimination tree: r0 holds
 // them in padded-lo bucket order and seg[s] / seg[L + s] delimit the edges whose first
 // active level is s ("first-activity buckets").
-void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, int L, uint32_t clo, uint32_t *pst,
-                       uint64_t *r0, uint64_t *seg) {
+void lo_group_prepare(Ctx &c, uint64_t n, int L, uint32_t clo, LoGroup &g) {
   // lo range of level s: ya = spread(lo) in [2^L - 2^(s+1), 2^L - 2^s)
   auto first_lo = [&](uint64_t y) {
     uint64_t a = 0, b = n;
@@ -730,39 +769,49 @@ void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, in
     }
     return a;
   };
-  std::vector<uint32_t> padoff(32, 0);
-  std::vector<uint64_t> pstart(L), plen(L);
+  g.L = L;
+  g.clo = clo;
+  g.mask = (uint32_t)((1ull << L) - 1);
+  g.padoff.assign(32, 0);
+  g.pstart.assign(L, 0);
+  g.plen.assign(L, 0);
   uint64_t run = 0;
   for (int s = L - 1; s >= 0; --s) {   // ranges in increasing lo
     const uint64_t beg = first_lo((1ull << L) - (2ull << s)), end = first_lo((1ull << L) - (1ull << s));
     const uint64_t len = end > beg ? end - beg : 0;
-    pstart[s] = run;
-    plen[s] = (len + W - 1) / W * W;
-    padoff[s] = (uint32_t)(run - beg);
-    run += plen[s];
+    g.pstart[s] = run;
+    g.plen[s] = (len + W - 1) / W * W;
+    g.padoff[s] = (uint32_t)(run - beg);
+    run += g.plen[s];
   }
-  const uint64_t K = run ? run : W;
-  if (K >= (1ull << 32)) throw Error(SHEEP_ERR_ARG, "group_edges_by_lo: key range too large");
-  const uint32_t nb = (uint32_t)(K / W);
-  std::vector<uint32_t> kbase(nb);
+  g.K = run ? run : W;
+  if (g.K >= (1ull << 32)) throw Error(SHEEP_ERR_ARG, "group_edges_by_lo: key range too large");
+  g.nb = (uint32_t)(g.K / W);
+  g.kbase.assign(g.nb, 0);
   for (int s = 0; s < L; ++s)
-    for (uint64_t b = pstart[s] / W; b < (pstart[s] + plen[s]) / W; ++b) kbase[b] = (uint32_t)(b * W - padoff[s]);
-  uint32_t *d_pad = c.get_as<uint32_t>("grp_padoff", 32);
-  uint32_t *d_kbase = c.get_as<uint32_t>("grp_kbase", nb);
-  uint32_t *d_bstart = c.get_as<uint32_t>("grp_bstart", nb + 1);
-  HIP_CHECK(hipMemcpyAsync(d_pad, padoff.data(), 32 * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
-  HIP_CHECK(hipMemcpyAsync(d_kbase, kbase.data(), nb * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
-  HIP_CHECK(hipMemsetAsync(d_bstart, 0, (nb + 1) * sizeof(uint32_t), c.stream));
-  const uint32_t mask = (uint32_t)((1ull << L) - 1);
-  histogram_add(c, EdgeLoPadded{edges, d_pad, clo, mask}, m, K, pst, r0, d_kbase, d_bstart);
+    for (uint64_t b = g.pstart[s] / W; b < (g.pstart[s] + g.plen[s]) / W; ++b) g.kbase[b] = (uint32_t)(b * W - g.padoff[s]);
+  g.d_pad = c.get_as<uint32_t>("grp_padoff", 32);
+  g.d_kbase = c.get_as<uint32_t>("grp_kbase", g.nb);
+  HIP_CHECK(hipMemcpyAsync(g.d_pad, g.padoff.data(), 32 * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
+  HIP_CHECK(hipMemcpyAsync(g.d_kbase, g.kbase.data(), g.nb * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
+  c.sync();   // the layout's host vectors are the copies' sources
+}
+
+void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGroup &g, uint32_t *pst, uint64_t *r0,
+                       uint64_t *seg, bool counted) {
+  const int L = g.L;
+  uint32_t *d_bstart = c.get_as<uint32_t>("grp_bstart", g.nb + 1);
+  HIP_CHECK(hipMemsetAsync(d_bstart, 0, (g.nb + 1) * sizeof(uint32_t), c.stream));
+  histogram_add(c, EdgeLoPadded{edges, g.d_pad, g.clo, g.mask}, m, g.K, pst, r0, g.d_kbase, d_bstart, nullptr, nullptr,
+                counted);
   std::vector<uint64_t> hseg(2 * (size_t)L);
-  for (int s = 0; s < L; ++s) { hseg[s] = pstart[s] / W; hseg[L + s] = (pstart[s] + plen[s]) / W; }
+  for (int s = 0; s < L; ++s) { hseg[s] = g.pstart[s] / W; hseg[L + s] = (g.pstart[s] + g.plen[s]) / W; }
   uint64_t *d_sb = c.get_as<uint64_t>("grp_segb", 2 * (size_t)L);
   HIP_CHECK(hipMemcpyAsync(d_sb, hseg.data(), 2 * (size_t)L * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
   hipLaunchKernelGGL(k_seg_from_buckets, dim3(1), dim3(64), 0, c.stream, (const uint32_t *)d_bstart,
                      (const uint64_t *)d_sb, L, seg);
   LAUNCH_CHECK();
-  c.sync();   // the host vectors above are pageable
+  c.sync();   // the host vector above is pageable
 }
 
 }  // namespace sheep
