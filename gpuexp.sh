@@ -1,5 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out && export HSA_ENABLE_IPC_MODE_LEGACY=0 && export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_scale_parity.py tests/test_cli.py -m gpu -x -q --timeout 400 --timeout-method thread > gpurun_out/gt_all.log 2>&1 || exit 1
-timeout -k 10 300 python -u bench.py --steps 5 --no-cpu-baseline --eval-reps 1 > gpurun_out/new26.log 2>&1 || exit 1
-timeout -k 10 300 python -u bench.py --scale 22 --k 16 --steps 5 --no-cpu-baseline --eval-reps 1 > gpurun_out/new22.log 2>&1 || exit 1
+T="timeout -k 10"
+$T 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "partition or oracle or c2 or c3 or cli or group" > gpurun_out/e1.log 2>&1 || exit 1
+SHEEP_DEBUG_PART=1 $T 300 python -u bench.py --steps 3 --no-cpu-baseline --eval-reps 0 > gpurun_out/b1.log 2> gpurun_out/b1.err || exit 1
+SHEEP_DEBUG_PART=1 $T 300 python -u bench.py --graph powerlaw --k 128 --steps 2 --no-cpu-baseline --eval-reps 0 > gpurun_out/b4.log 2> gpurun_out/b4.err || exit 1

@@ -200,6 +200,41 @@ template <typename T> __device__ __forceinline__ T wave_min(T v) {
   return v;
 }
 
+// One atomic per workgroup for a value every thread contributes (every thread of the
+// workgroup calls; blockDim.x a multiple of 64, <= 1024).  Per-wave atomics on one word
+// serialise a launch of ~1e5 workgroups (k_compact_count: 1.5 ms for 1.3e5 of them).
+// The max skips its atomic when a plain read already shows a value >= v (the word only
+// grows; a stale read is smaller, so nothing is lost).
+__device__ __forceinline__ uint64_t block_reduce_u64(uint64_t v, bool is_max) {
+  __shared__ uint64_t s_red[16];
+  v = is_max ? wave_max(v) : wave_sum(v);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t r = 0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) r = is_max ? (s_red[w] > r ? s_red[w] : r) : r + s_red[w];
+  __syncthreads();   // s_red is reused by the next call
+  return r;          // meaningful in thread 0
+}
+__device__ __forceinline__ void block_atomic_max(unsigned long long *dst, uint64_t v) {
+  const uint64_t m = block_reduce_u64(v, true);
+  if (threadIdx.x == 0 && m && m > __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMax(dst, (unsigned long long)m);
+}
+__device__ __forceinline__ void block_atomic_add(unsigned long long *dst, uint64_t v) {
+  const uint64_t m = block_reduce_u64(v, false);
+  if (threadIdx.x == 0 && m) atomicAdd(dst, (unsigned long long)m);
+}
+
+// The tile of this workgroup in a grid of one workgroup per tile.  Workgroups are dealt
+// round-robin over the 8 XCDs (b and b + 8 share one), so this gives XCD x a contiguous
+// run of tiles: the tiles running at once on one XCD then share the lines of their
+// (bucket, tile) counter columns in that XCD's L2.  A bijection on [0, gridDim.x).
+__device__ __forceinline__ uint32_t xcd_tile() {
+  const uint32_t g = gridDim.x, b = blockIdx.x, x = b & 7, q = g >> 3, r = g & 7;
+  return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 // Workgroup-aggregated append: reserves `cnt` consecutive slots for every thread with
 // ONE device atomic per workgroup call (a single hot counter takes ~0.1 G atomics/s, so
 // per-wave appends serialise a streaming kernel).  Every thread of the workgroup must
@@ -315,7 +350,7 @@ void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGroup 
                        uint64_t *seg, bool counted);
 // etree.hip
 void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
-                      int fin_bits, uint32_t per_lo);
+                      int fin_bits);
 void spread_params(uint64_t n, int *L, uint32_t *clo);
 // append.hip — sharded appends: counters (NSHARD * SHARD_STRIDE u64, zeroed).  The pack
 // step moves the shard regions of a producer that streamed *n_in items together in dst

@@ -23,6 +23,7 @@
 // ranges are dyadic in a monotone spread of [0,n) onto [0,2^L) so halves are balanced.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -617,7 +618,8 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
 // A block with more than FIN_HEAVY edges (a hub's block) is handed to a whole wave
 // instead, which takes the edges of one hi 64 at a time.  Used for merges, whose edges
 // (two parent edges per node plus contractions) spread evenly over the blocks.
-constexpr int FIN_BITS_MAX = 8;     // 2^8 one-byte entries x 64 lanes = 16 KB of LDS per wave
+constexpr int FIN_LANE_BITS = 8;   // lane-per-block: 2^8 one-byte entries x 64 lanes = 16 KB of LDS per wave
+constexpr int FIN_BITS_MAX = 13;   // wave-per-block: 2^13 two-byte entries = 16 KB
 constexpr uint64_t FIN_HEAVY = 256;
 
 __global__ void k_fin_gather(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
@@ -643,7 +645,7 @@ __global__ __launch_bounds__(BLOCK) void k_fin_bounds(const uint64_t *__restrict
                                                       uint32_t clo, int B, uint64_t nb, uint64_t n,
                                                       uint64_t *__restrict__ eb, uint32_t *__restrict__ vb,
                                                       uint32_t *__restrict__ light, uint32_t *__restrict__ heavy,
-                                                      unsigned long long *__restrict__ n_lh) {
+                                                      unsigned long long *__restrict__ n_lh, uint64_t heavy_min) {
   const uint64_t nf = *n_fin;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   const uint64_t t0 = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -667,7 +669,7 @@ __global__ __launch_bounds__(BLOCK) void k_fin_bounds(const uint64_t *__restrict
       eb[b] = e0;
       if (b + 1 == nb) eb[nb] = e1;
     }
-    const bool big = e1 - e0 > FIN_HEAVY, small = e1 > e0 && !big;
+    const bool big = e1 - e0 > heavy_min, small = e1 > e0 && !big;
     const uint64_t sl = wave_append(small, n_lh), sh = wave_append(big, n_lh + 1);
     if (small) light[sl] = (uint32_t)b;
     if (big) heavy[sh] = (uint32_t)b;
@@ -719,28 +721,30 @@ __global__ __launch_bounds__(WAVE) void k_fin_lanes(const uint64_t *__restrict__
   }
 }
 
-__device__ __forceinline__ uint32_t fin_find(uint8_t *uf, uint32_t x) {
+template <typename U> __device__ __forceinline__ uint32_t fin_find(U *uf, uint32_t x) {
   uint32_t p = uf[x];
   while (p != x) {   // path halving (pointers only move up: safe with other lanes)
     const uint32_t g = uf[p];
-    uf[x] = (uint8_t)g;
+    uf[x] = (U)g;
     x = g;
     p = uf[x];
   }
   return x;
 }
 
-// A heavy block: one wave, its edges staged through LDS FIN_STAGE at a time (coalesced),
-// then taken one hi at a time, 64 edges per step.  Lanes with the same root store the
-// same link; distinct roots link under v side by side, as Liu's loop over v's
-// neighbours would.
-constexpr int FIN_STAGE = 2048;
+// A heavy block (and every block when B > FIN_LANE_BITS): one wave, its edges staged
+// through LDS FIN_STAGE at a time (coalesced), then taken one hi at a time, 64 edges per
+// step.  Lanes with the same root store the same link; distinct roots link under v side
+// by side, as Liu's loop over v's neighbours would.  Entries: one byte up to 2^8
+// positions, two bytes above.
+constexpr int FIN_STAGE = 1024;
 template <int B>
 __global__ __launch_bounds__(WAVE) void k_fin_heavy(const uint64_t *__restrict__ fin, const uint64_t *__restrict__ eb,
                                                     const uint32_t *__restrict__ vb, const uint32_t *__restrict__ heavy,
                                                     const unsigned long long *__restrict__ n_heavy,
                                                     uint32_t *__restrict__ parent) {
-  __shared__ uint8_t uf[1 << B];
+  using U = typename std::conditional<(B <= 8), uint8_t, uint16_t>::type;
+  __shared__ U uf[1 << B];
   __shared__ uint64_t stage[FIN_STAGE];
   const int lane = threadIdx.x;
   const unsigned long long nh = *n_heavy;
@@ -749,7 +753,7 @@ __global__ __launch_bounds__(WAVE) void k_fin_heavy(const uint64_t *__restrict__
     const uint32_t v0 = vb[b], cnt = vb[b + 1] - v0;
     const uint64_t e0 = eb[b], e1 = eb[b + 1];
     __syncthreads();   // the previous block is done with uf and stage
-    for (uint32_t i = lane; i < cnt; i += WAVE) uf[i] = (uint8_t)i;
+    for (uint32_t i = lane; i < cnt; i += WAVE) uf[i] = (U)i;
     for (uint64_t base = e0; base < e1; base += FIN_STAGE) {
       const uint32_t len = (uint32_t)(e1 - base < FIN_STAGE ? e1 - base : FIN_STAGE);
       __syncthreads();
@@ -763,10 +767,10 @@ __global__ __launch_bounds__(WAVE) void k_fin_heavy(const uint64_t *__restrict__
         const uint64_t mask = __ballot(mine);
         const uint32_t x = (uint32_t)(e >> 32) - v0, vv = v - v0;
         if (mine && x < cnt && vv < cnt) {
-          const uint32_t r = fin_find(uf, x);
+          const uint32_t r = fin_find<U>(uf, x);
           if (r != vv) {
             parent[v0 + r] = v;
-            uf[r] = (uint8_t)vv;
+            uf[r] = (U)vv;
           }
         }
         __syncthreads();   // this v's links before the next v's finds
@@ -776,53 +780,84 @@ __global__ __launch_bounds__(WAVE) void k_fin_heavy(const uint64_t *__restrict__
   }
 }
 
-// Parent edges of both trees, in place: edges[2i] from a, edges[2i+1] from b (DEAD when
-// absent or equal to a's).
-__global__ __launch_bounds__(BLOCK) void k_tree_edges(const sheep_jnode *__restrict__ a, const sheep_jnode *__restrict__ b,
-                                                      uint64_t n, uint64_t *__restrict__ edges,
+// ---- merge input ------------------------------------------------------------------
+// K trees: tree 0 at t0, tree k >= 1 at t1 + (k - 1) * stride (two separate trees, or K
+// stacked ones).  Node i contributes its DISTINCT parents over the K trees as edges
+// (parent << 32 | i), compacted in node order — so the edges come sorted by lo and the
+// first-activity groups are ranges of them (seg from the node offsets, k_seg_at).  The
+// parents are deduplicated in registers; most of the K x n slots are empty or repeats
+// (RMAT-26, 8 shard trees: ~47M edges in 262M slots), which the levels no longer read.
+struct TreeSet {
+  const sheep_jnode *t0, *t1;
+  uint64_t stride;
+  __device__ __forceinline__ const sheep_jnode *at(uint32_t k) const { return k == 0 ? t0 : t1 + (uint64_t)(k - 1) * stride; }
+};
+constexpr uint32_t MERGE_KMAX = 64;   // trees per pass (a larger K is merged in passes)
+
+// p[k] = node i's parent in tree k, INVALID when absent or equal to an earlier tree's;
+// returns the summed pst weight.  A parent that is not a later node of the tree flags bad.
+template <int KM>
+__device__ __forceinline__ uint32_t tree_parents(const TreeSet &ts, uint32_t K, uint64_t n, uint64_t i,
+                                                 uint32_t (&p)[KM], bool &bad) {
+  uint32_t w = 0;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    p[k] = INVALID;
+    if ((uint32_t)k < K) {
+      const sheep_jnode x = ts.at(k)[i];
+      w += x.pst_weight;
+      p[k] = x.parent;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    // a parent must be a later, existing node (jnode.cpp kids(current) via makeKids)
+    if (p[k] != INVALID && (p[k] <= i || p[k] >= n)) {
+      bad = true;
+      p[k] = INVALID;
+    }
+#pragma unroll
+    for (int j = 0; j < k; ++j)
+      if (p[j] == p[k]) p[k] = INVALID;
+  }
+  return w;
+}
+
+template <int KM>
+__global__ __launch_bounds__(BLOCK) void k_tree_count(TreeSet ts, uint32_t K, uint64_t n, uint32_t *__restrict__ cnt,
                                                       uint32_t *__restrict__ pst_out, unsigned long long *__restrict__ err) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   bool bad = false;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
-    const sheep_jnode x = a[i], y = b[i];
-    uint32_t pa = x.parent, pb = y.parent;
-    pst_out[i] = x.pst_weight + y.pst_weight;
-    // a parent must be a later, existing node (jnode.cpp kids(current) via makeKids)
-    if ((pa != INVALID && (pa <= i || pa >= n)) || (pb != INVALID && (pb <= i || pb >= n))) {
-      bad = true;
-      pa = pb = INVALID;
-    }
-    edges[2 * i] = pa != INVALID ? ((uint64_t)pa << 32) | (uint32_t)i : DEAD;
-    edges[2 * i + 1] = pb != INVALID && pb != pa ? ((uint64_t)pb << 32) | (uint32_t)i : DEAD;
+    uint32_t p[KM];
+    pst_out[i] = tree_parents<KM>(ts, K, n, i, p, bad);
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) c += p[k] != INVALID;
+    cnt[i] = c;
   }
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(err, 1ull);
 }
 
-// K trees stored one after another (trees[k * n + i]): edges[K i + k] = node i's parent
-// edge in tree k, DEAD when absent or equal to an earlier tree's; pst = the sum.
-__global__ __launch_bounds__(BLOCK) void k_tree_edges_many(const sheep_jnode *__restrict__ trees, uint32_t K,
-                                                           uint64_t n, uint64_t *__restrict__ edges,
-                                                           uint32_t *__restrict__ pst_out,
-                                                           unsigned long long *__restrict__ err) {
+template <int KM>
+__global__ __launch_bounds__(BLOCK) void k_tree_write(TreeSet ts, uint32_t K, uint64_t n, const uint32_t *__restrict__ off,
+                                                      uint64_t *__restrict__ edges) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   bool bad = false;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
-    uint32_t w = 0;
-    for (uint32_t k = 0; k < K; ++k) {
-      const sheep_jnode x = trees[(uint64_t)k * n + i];
-      w += x.pst_weight;
-      uint32_t p = x.parent;
-      if (p != INVALID && (p <= i || p >= n)) {
-        bad = true;
-        p = INVALID;
-      }
-      for (uint32_t j = 0; j < k && p != INVALID; ++j)
-        if ((uint32_t)(edges[K * i + j] >> 32) == p) p = INVALID;
-      edges[K * i + k] = p != INVALID ? ((uint64_t)p << 32) | (uint32_t)i : DEAD;
-    }
-    pst_out[i] = w;
+    uint32_t p[KM];
+    tree_parents<KM>(ts, K, n, i, p, bad);
+    uint64_t o = off[i];
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+      if (p[k] != INVALID) edges[o++] = ((uint64_t)p[k] << 32) | (uint32_t)i;
   }
-  if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(err, 1ull);
+}
+
+// seg[j] = off[node[j]]: the first-activity group bounds of lo-sorted edges.
+struct SegNodes { uint32_t node[64]; };
+__global__ void k_seg_at(const uint32_t *__restrict__ off, SegNodes sn, int cnt, uint64_t *__restrict__ seg) {
+  if ((int)threadIdx.x < cnt) seg[threadIdx.x] = off[sn.node[threadIdx.x]];
 }
 
 __global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t *__restrict__ pst, uint64_t n,
@@ -844,8 +879,11 @@ static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
 // Finishing block size (log2 positions) of the per-block Liu pass.  The last levels of a
 // map keep ~5M list entries each at RMAT-26 (0.6 ms per level for a dozen launches);
 // one sort + the per-block pass replaces the last 8 (RMAT-26: 49.7 -> 45.9 ms; B = 7:
-// 46.4).  Hub blocks go to whole waves (k_fin_heavy).
-constexpr int FIN_MERGE = 8, FIN_MAP = 8;
+// 46.4; B = 10: 42.7 against 39.9, B = 12: 82.5 — hub blocks serialise on one wave).
+// Hub blocks go to whole waves (k_fin_heavy).  A merge's edges spread evenly over the
+// blocks, so its finish takes 11 bits (RMAT-26, 8 shard trees: K-way merge 19.5 -> 17.9
+// ms; 10: 18.1, 12: 18.2).
+constexpr int FIN_MERGE = 11, FIN_MAP = 8;
 
 // spread(x) = floor(x * c / 2^32), c = floor(2^(32+L) / n) in [2^32, 2^33), L = ceil(log2 n):
 // monotone, injective on [0,n), image in [0, 2^L).  clo = c - 2^32.
@@ -862,13 +900,12 @@ void spread_params(uint64_t n, int *L_out, uint32_t *clo_out) {
 static uint64_t list_capacity(uint64_t m) { return 2 * m + TILE; }
 
 // Elimination tree of `m` edges ((hi<<32)|lo, lo < hi < n, DEAD holes allowed), grouped
-// by first active level: seg[s] / seg[L + s] (device) delimit group s.  seg == nullptr:
-// the edges are a merge's parent edges (entries per_lo * lo + k), whose groups are
-// computed here.  The edges are read only.
+// by first active level: seg[s] / seg[L + s] (device) delimit group s.  The edges are
+// read only.
 // One pass of launches per level, no host synchronisation inside the loop (see the
 // stats row above); the stats come back once at the end for the timers / debug log.
-void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg_in,
-                      int fin_bits, uint32_t per_lo) {
+void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
+                      int fin_bits) {
   fill_u32(c, parent, n, INVALID);
   if (n < 2 || m == 0) return;
   if (m >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "too many edges for one shard");
@@ -888,28 +925,6 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   // the two list buffers (level l reads one and writes the other) and the bucketed input r0
   uint64_t *lists[2] = {c.get_as<uint64_t>("et_list1", lcap), c.get_as<uint64_t>("et_list2", lcap)};
   const uint64_t *r0 = edges;
-  const uint64_t *seg = seg_in;
-  if (!seg) {
-    uint64_t *dseg = c.get_as<uint64_t>("et_seg", 2 * (uint64_t)L);
-    seg = dseg;
-    // bucket s = lo with ya in [2^L - 2^(s+1), 2^L - 2^s): a range of lo, entries per_lo * lo + k
-    auto first_lo = [&](uint64_t y) {   // min lo with spread(lo) >= y
-      uint64_t a = 0, b = n;
-      while (a < b) {
-        const uint64_t x = (a + b) / 2;
-        if (x + ((x * (uint64_t)clo) >> 32) >= y) b = x; else a = x + 1;
-      }
-      return a;
-    };
-    uint64_t *h = (uint64_t *)c.get_pinned("et_seg_host", 2 * (size_t)L * sizeof(uint64_t));
-    for (int b = 0; b < L; ++b) {
-      h[b] = per_lo * first_lo((1ull << L) - (2ull << b));
-      h[L + b] = per_lo * first_lo((1ull << L) - (1ull << b));
-      if (h[L + b] > m) h[L + b] = m;
-      if (h[b] > h[L + b]) h[b] = h[L + b];
-    }
-    HIP_CHECK(hipMemcpyAsync(dseg, h, 2 * (size_t)L * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
-  }
   // a split reads at most the list plus a bucket: (lcap + m) entries, in TILE tiles
   const uint64_t cstride = (lcap + m + TILE - 1) / TILE + 1;
   uint64_t *tcnt = c.get_as<uint64_t>("et_tilecnt", 3 * cstride + 1);
@@ -1009,22 +1024,28 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       uint32_t *light = c.get_as<uint32_t>("et_fin_light", nb), *heavy = c.get_as<uint32_t>("et_fin_heavy", nb);
       unsigned long long *n_lh = (unsigned long long *)(n_fin + 1);   // light, heavy counts (zeroed with stats)
       hipLaunchKernelGGL(k_fin_bounds, dim3(grid_for(nb > n ? nb + 1 : n + 1)), dim3(BLOCK), 0, c.stream,
-                         (const uint64_t *)fin, (const uint64_t *)n_fin, clo, FINB, nb, n, eb, vb, light, heavy, n_lh);
+                         (const uint64_t *)fin, (const uint64_t *)n_fin, clo, FINB, nb, n, eb, vb, light, heavy, n_lh,
+                         FINB <= FIN_LANE_BITS ? FIN_HEAVY : 0);
       LAUNCH_CHECK();
-      const unsigned gl = (unsigned)((nb + WAVE - 1) / WAVE), gh = (unsigned)(nb < 4096 ? nb : 4096);
+      const unsigned gl = (unsigned)((nb + WAVE - 1) / WAVE), gh = (unsigned)(nb < 8192 ? nb : 8192);
       switch (FINB) {
-#define SHEEP_FIN_CASE(B)                                                                                        \
-  case B:                                                                                                        \
+#define SHEEP_FIN_LANES(B)                                                                                       \
     hipLaunchKernelGGL(k_fin_lanes<B>, dim3(gl), dim3(WAVE), 0, c.stream, (const uint64_t *)fin, (const uint64_t *)eb, \
                        (const uint32_t *)vb, (const uint32_t *)light, (const unsigned long long *)n_lh, parent);  \
-    LAUNCH_CHECK();                                                                                              \
+    LAUNCH_CHECK();
+#define SHEEP_FIN_HEAVY(B)                                                                                       \
     hipLaunchKernelGGL(k_fin_heavy<B>, dim3(gh), dim3(WAVE), 0, c.stream, (const uint64_t *)fin, (const uint64_t *)eb, \
                        (const uint32_t *)vb, (const uint32_t *)heavy, (const unsigned long long *)(n_lh + 1), parent); \
-    LAUNCH_CHECK();                                                                                              \
-    break;
+    LAUNCH_CHECK();
+#define SHEEP_FIN_CASE(B) case B: SHEEP_FIN_LANES(B) SHEEP_FIN_HEAVY(B) break;
+#define SHEEP_FIN_WAVE(B) case B: SHEEP_FIN_HEAVY(B) break;
         SHEEP_FIN_CASE(1) SHEEP_FIN_CASE(2) SHEEP_FIN_CASE(3) SHEEP_FIN_CASE(4)
         SHEEP_FIN_CASE(5) SHEEP_FIN_CASE(6) SHEEP_FIN_CASE(7) SHEEP_FIN_CASE(8)
+        SHEEP_FIN_WAVE(9) SHEEP_FIN_WAVE(10) SHEEP_FIN_WAVE(11) SHEEP_FIN_WAVE(12) SHEEP_FIN_WAVE(13)
 #undef SHEEP_FIN_CASE
+#undef SHEEP_FIN_WAVE
+#undef SHEEP_FIN_LANES
+#undef SHEEP_FIN_HEAVY
         default: throw Error(SHEEP_ERR_ARG, "etree: bad finishing block size");
       }
       if (g_debug_etree) {
@@ -1109,7 +1130,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
       group_edges_by_lo(c, edges, m, lg, pst, r0, seg, counted);
     }
     TimedRegion tr(c, "etree", 8 * m);
-    etree_from_edges(c, r0, m, n, parent, seg, FIN_MAP, 0);
+    etree_from_edges(c, r0, m, n, parent, seg, FIN_MAP);
   } else {
     fill_u32(c, parent, n, INVALID);
   }
@@ -1119,49 +1140,102 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   }
 }
 
-void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n, sheep_jnode *out) {
-  if (n == 0) return;
-  uint32_t *pst = c.get_as<uint32_t>("mg_pst", n);
-  uint32_t *parent = c.get_as<uint32_t>("mg_parent", n);
-  uint64_t *edges = c.get_as<uint64_t>("mg_edges", 2 * n);
+// The merge's edges: every node's distinct parents over the K trees, compacted in node
+// (= lo) order, and their first-activity group bounds (group s = the lo range whose
+// spread has its highest zero bit at s).  Returns the edge count; pst = the summed weights.
+static uint64_t merge_edges(Ctx &c, const TreeSet &ts, uint32_t K, uint64_t n, uint32_t *pst, uint64_t **edges_out,
+                            uint64_t **seg_out, int *L_out) {
+  int L;
+  uint32_t clo;
+  spread_params(n, &L, &clo);
+  uint32_t *off = c.get_as<uint32_t>("mg_off", n + 1);
   unsigned long long *d = (unsigned long long *)c.d_scalars + 10;
   HIP_CHECK(hipMemsetAsync(d + 1, 0, sizeof(uint64_t), c.stream));
-  hipLaunchKernelGGL(k_tree_edges, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, a, b, n, edges, pst, d + 1);
+  const unsigned g = grid_for(n);
+#define SHEEP_KM(KM) hipLaunchKernelGGL(k_tree_count<KM>, dim3(g), dim3(BLOCK), 0, c.stream, ts, K, n, off, pst, d + 1)
+  if (K <= 2) SHEEP_KM(2); else if (K <= 4) SHEEP_KM(4); else if (K <= 8) SHEEP_KM(8);
+  else if (K <= 16) SHEEP_KM(16); else if (K <= 32) SHEEP_KM(32); else SHEEP_KM(64);
+#undef SHEEP_KM
   LAUNCH_CHECK();
+  scan_exclusive_u32(c, off, off, n, off + n);
+  c.h_scalars[12] = 0;   // the u32 total lands in the low half
   HIP_CHECK(hipMemcpyAsync(c.h_scalars + 11, d + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 12, off + n, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
   if (c.h_scalars[11]) throw Error(SHEEP_ERR_ARG, "merge: a parent is not a later node of the tree");
-  {
-    TimedRegion tr(c, "merge", 16 * n);
-    etree_from_edges(c, edges, 2 * n, n, parent, nullptr, FIN_MERGE, 2);
+  const uint64_t m = c.h_scalars[12];
+  uint64_t *edges = c.get_as<uint64_t>("mg_edges", m ? m : 1);
+#define SHEEP_KM(KM) hipLaunchKernelGGL(k_tree_write<KM>, dim3(g), dim3(BLOCK), 0, c.stream, ts, K, n, (const uint32_t *)off, edges)
+  if (K <= 2) SHEEP_KM(2); else if (K <= 4) SHEEP_KM(4); else if (K <= 8) SHEEP_KM(8);
+  else if (K <= 16) SHEEP_KM(16); else if (K <= 32) SHEEP_KM(32); else SHEEP_KM(64);
+#undef SHEEP_KM
+  LAUNCH_CHECK();
+  // group b = lo with spread(lo) in [2^L - 2^(b+1), 2^L - 2^b)
+  auto first_lo = [&](uint64_t y) {   // min lo with spread(lo) >= y
+    uint64_t a = 0, z = n;
+    while (a < z) {
+      const uint64_t x = (a + z) / 2;
+      if (x + ((x * (uint64_t)clo) >> 32) >= y) z = x; else a = x + 1;
+    }
+    return a;
+  };
+  SegNodes sn{};
+  for (int b = 0; b < L; ++b) {
+    sn.node[b] = (uint32_t)first_lo((1ull << L) - (2ull << b));
+    sn.node[L + b] = (uint32_t)first_lo((1ull << L) - (1ull << b));
+  }
+  uint64_t *seg = c.get_as<uint64_t>("mg_seg", 2 * (uint64_t)L);
+  hipLaunchKernelGGL(k_seg_at, dim3(1), dim3(64), 0, c.stream, (const uint32_t *)off, sn, 2 * L, seg);
+  LAUNCH_CHECK();
+  *edges_out = edges;
+  *seg_out = seg;
+  *L_out = L;
+  return m;
+}
+
+// The elimination tree of the union of the K trees' parent-edge sets (JNodeTable::merge,
+// jnode.cpp:174-201, for K = 2; for K > 2 the same tree as K - 1 pairwise merges in any
+// order — merge is associative and commutative — i.e. mpi_merge's whole reduction,
+// jnode.cpp:203-250, in one pass).
+static void merge_set(Ctx &c, const TreeSet &ts, uint32_t K, uint64_t n, sheep_jnode *out) {
+  if ((uint64_t)K * n >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "merge: too many parent edges for one pass");
+  uint32_t *pst = c.get_as<uint32_t>("mg_pst", n);
+  uint32_t *parent = c.get_as<uint32_t>("mg_parent", n);
+  uint64_t *edges = nullptr, *seg = nullptr;
+  int L = 0;
+  if (n < 2) {
+    // one node: no edges; the weights still add up
+    merge_edges(c, ts, K, n, pst, &edges, &seg, &L);
+    fill_u32(c, parent, n, INVALID);
+  } else {
+    TimedRegion tr(c, "merge", 8 * (uint64_t)K * n);   // the K trees
+    const uint64_t m = merge_edges(c, ts, K, n, pst, &edges, &seg, &L);
+    etree_from_edges(c, edges, m, n, parent, seg, FIN_MERGE);
   }
   hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);
   LAUNCH_CHECK();
 }
 
-// K trees at once: the elimination tree of the union of all K parent-edge sets, the same
-// tree as K - 1 pairwise merges in any order (merge is associative and commutative) —
-// the whole of mpi_merge's reduction (jnode.cpp:203-250) in one pass.
+void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n, sheep_jnode *out) {
+  if (n == 0) return;
+  merge_set(c, TreeSet{a, b, 0}, 2, n, out);
+}
+
 void merge_trees_many(Ctx &c, const sheep_jnode *trees, uint32_t K, uint64_t n, sheep_jnode *out) {
   if (n == 0) return;
   if (K == 0) throw Error(SHEEP_ERR_ARG, "merge: no trees");
-  if ((uint64_t)K * n >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "merge: too many parent edges for one pass");
-  uint32_t *pst = c.get_as<uint32_t>("mg_pst", n);
-  uint32_t *parent = c.get_as<uint32_t>("mg_parent", n);
-  uint64_t *edges = c.get_as<uint64_t>("mg_edges", (uint64_t)K * n);
-  unsigned long long *d = (unsigned long long *)c.d_scalars + 10;
-  HIP_CHECK(hipMemsetAsync(d + 1, 0, sizeof(uint64_t), c.stream));
-  hipLaunchKernelGGL(k_tree_edges_many, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, trees, K, n, edges, pst, d + 1);
-  LAUNCH_CHECK();
-  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 11, d + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-  c.sync();
-  if (c.h_scalars[11]) throw Error(SHEEP_ERR_ARG, "merge: a parent is not a later node of the tree");
-  {
-    TimedRegion tr(c, "merge", 8 * (uint64_t)K * n);
-    etree_from_edges(c, edges, (uint64_t)K * n, n, parent, nullptr, FIN_MERGE, K);
+  if (K == 1) {
+    HIP_CHECK(hipMemcpyAsync(out, trees, n * sizeof(sheep_jnode), hipMemcpyDeviceToDevice, c.stream));
+    return;
   }
-  hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);
-  LAUNCH_CHECK();
+  // MERGE_KMAX trees per pass; later passes merge the running result with the next ones
+  uint32_t done = K < MERGE_KMAX ? K : MERGE_KMAX;
+  merge_set(c, TreeSet{trees, trees + n, n}, done, n, out);
+  while (done < K) {
+    const uint32_t k = K - done < MERGE_KMAX - 1 ? K - done : MERGE_KMAX - 1;
+    merge_set(c, TreeSet{out, trees + (uint64_t)done * n, n}, k + 1, n, out);
+    done += k;
+  }
 }
 
 }  // namespace sheep

@@ -80,7 +80,8 @@ __global__ __launch_bounds__(CB) void k_hist_count(Src src, uint64_t n, uint32_t
   extern __shared__ uint32_t lds[];
   for (uint32_t b = threadIdx.x; b < nb; b += CB) lds[b] = 0;
   __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x << TLOG;
+  const uint32_t tile = xcd_tile();
+  const uint64_t base = (uint64_t)tile << TLOG;
   for (uint32_t step = 0; step < TKEYS; step += CB * CPT) {
     uint32_t k[CPT];
 #pragma unroll
@@ -93,7 +94,7 @@ __global__ __launch_bounds__(CB) void k_hist_count(Src src, uint64_t n, uint32_t
       if (k[j] != NO_KEY) atomicAdd(&lds[k[j] >> WBITS], 1u);
   }
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nb; b += CB) tile_hist[(uint64_t)b * ntiles + blockIdx.x] = lds[b];
+  for (uint32_t b = threadIdx.x; b < nb; b += CB) tile_hist[(uint64_t)b * ntiles + tile] = lds[b];
 }
 
 // Block-wide exclusive scan of a[0, nb) in LDS (nb <= 8 * HB), in place; returns total.
@@ -142,7 +143,8 @@ __global__ __launch_bounds__(HB) void k_hist_scatter(Src src, uint64_t n, uint32
   uint32_t *stage = lds + 2 * nb + HB / WAVE;
   for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
   __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x << TLOG;
+  const uint32_t tile = xcd_tile();
+  const uint64_t base = (uint64_t)tile << TLOG;
   uint32_t k[KPT];
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
@@ -165,7 +167,7 @@ __global__ __launch_bounds__(HB) void k_hist_scatter(Src src, uint64_t n, uint32
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < total; j += HB) {
     const uint32_t x = stage[j], b = x >> 16;
-    out[offsets[(uint64_t)b * ntiles + blockIdx.x] + (j - start[b])] = (uint16_t)(x & 0xFFFF);
+    out[offsets[(uint64_t)b * ntiles + tile] + (j - start[b])] = (uint16_t)(x & 0xFFFF);
   }
 }
 
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(HB) void k_hist_scatter_staged(Src src, uint64_t n,
   extern __shared__ uint32_t lds[];
   uint32_t *cur = lds, *gb = lds + nb, *wsum = lds + 2 * nb;
   uint32_t *stage = lds + 2 * nb + HB / WAVE;
-  const uint64_t tile = blockIdx.x;
+  const uint64_t tile = xcd_tile();
   for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] = offsets[(uint64_t)b * ntiles + tile];
   const uint64_t base = tile << TLOG;
   for (uint32_t s0 = 0; s0 < TKEYS; s0 += SUB) {
@@ -228,7 +230,7 @@ __global__ __launch_bounds__(HB) void k_lo_scatter_staged(EdgeLoPadded src, uint
   extern __shared__ uint32_t lds[];
   uint32_t *cur = lds, *gb = lds + nb, *wsum = lds + 2 * nb;
   uint64_t *stage = (uint64_t *)(lds + ((2 * nb + HB / WAVE + 1) & ~1u));
-  const uint64_t tile = blockIdx.x;
+  const uint64_t tile = xcd_tile();
   for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] = offsets[(uint64_t)b * ntiles + tile];
   const uint64_t base = tile << TLOG;
   for (uint32_t s0 = 0; s0 < TKEYS; s0 += SUB) {
@@ -419,7 +421,8 @@ __global__ __launch_bounds__(CB) void k_degree_fused(const sheep_xs1 *__restrict
   extern __shared__ uint32_t lds[];
   for (uint32_t b = threadIdx.x; b < nb; b += CB) lds[b] = 0;
   __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x << TLOG;
+  const uint32_t tile = xcd_tile();
+  const uint64_t base = (uint64_t)tile << TLOG;
   uint32_t lmax = 0;
   bool bad = false;
   for (uint32_t step = 0; step < TKEYS; step += CB * CPT) {
@@ -451,9 +454,8 @@ __global__ __launch_bounds__(CB) void k_degree_fused(const sheep_xs1 *__restrict
     }
   }
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nb; b += CB) tile_hist[(uint64_t)b * ntiles + blockIdx.x] = lds[b];
-  lmax = wave_max(lmax);
-  if ((threadIdx.x & 63) == 0 && lmax) atomicMax(d_max, (unsigned long long)lmax);
+  for (uint32_t b = threadIdx.x; b < nb; b += CB) tile_hist[(uint64_t)b * ntiles + tile] = lds[b];
+  block_atomic_max(d_max, lmax);
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(d_err, 1ull);
 }
 
@@ -495,7 +497,7 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
   extern __shared__ uint32_t lds[];
   uint32_t *cur = lds, *gb = lds + nb, *end = lds + 2 * nb, *wsum = lds + 3 * nb;
   uint64_t *stage = (uint64_t *)(lds + ((3 * nb + HB / WAVE + 1) & ~1u));
-  const uint64_t tile = blockIdx.x;
+  const uint64_t tile = xcd_tile();
   for (uint32_t b = threadIdx.x; b < nb; b += HB) {
     const uint64_t o = (uint64_t)b * ntiles + tile;
     gb[b] = offsets[o];

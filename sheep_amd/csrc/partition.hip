@@ -23,6 +23,8 @@
 //      the assigned nodes' Euler-tour intervals (laminar), then re-indexes jnid -> vid.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <vector>
 
@@ -311,6 +313,23 @@ struct EvView {
   }
 };
 
+// Tables of up to EV_ARG events travel as a kernel argument (device-side kernarg memory):
+// reading the mapped host copy cost each event launch a PCIe round trip (2.7 us).
+constexpr uint32_t EV_ARG = 128;
+struct EvArg {
+  uint32_t m;
+  uint32_t pos[EV_ARG];
+  uint64_t pre[EV_ARG + 1];
+};
+__device__ __forceinline__ EvView load_arg(const EvArg &arg, uint32_t *spos, uint64_t *spre) {
+  for (uint32_t i = threadIdx.x; i <= arg.m; i += blockDim.x) {
+    if (i < arg.m) spos[i] = arg.pos[i];
+    spre[i] = arg.pre[i];
+  }
+  __syncthreads();
+  return EvView{spos, spre, arg.m};
+}
+
 // loads the table into LDS when it fits (every thread of the block must call it)
 __device__ __forceinline__ EvView load_table(const uint32_t *gpos, const uint64_t *gpre, uint32_t m, uint32_t *spos,
                                              uint64_t *spre) {
@@ -361,12 +380,14 @@ __global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hi
                                                  const uint32_t *__restrict__ tD, const uint32_t *__restrict__ tU,
                                                  const uint32_t *__restrict__ rst, const uint32_t *__restrict__ ren,
                                                  uint32_t *__restrict__ hdr, uint32_t *__restrict__ kid_out,
-                                                 uint64_t *__restrict__ r_out, uint32_t seq) {
+                                                 uint64_t *__restrict__ r_out, uint32_t seq, const EvArg arg) {
   __shared__ uint32_t spos[EV_LDS];
   __shared__ uint64_t spre[EV_LDS + 1];
   __shared__ unsigned long long s_best[BLOCK / WAVE];
   __shared__ bool last;
-  const EvView ev = load_table(epos, epre, m, spos, spre);
+  uint64_t t_start = wall_clock64();
+  const EvView ev = epos ? load_table(epos, epre, m, spos, spre) : load_arg(arg, spos, spre);
+  uint64_t t_table = wall_clock64();
   const uint64_t prev = *evprev;
   const uint64_t start = prev == ~0ull ? 0 : (uint32_t)prev;
   const uint32_t vlast = prev == ~0ull ? INVALID : (uint32_t)(prev >> 32);
@@ -376,13 +397,25 @@ __global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hi
     const unsigned long long f = __hip_atomic_load(found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (f != ~0ull && (uint32_t)f < base) break;   // a hit below this chunk is known
     unsigned long long best = ~0ull;
+    // every candidate's four words loaded before any is decoded (a load behind the id
+    // check of the same candidate serialised two latencies per candidate: 24 us a scan)
+    uint32_t ca[EVI], cs[EVI], ce[EVI];
+    uint64_t cr[EVI];
 #pragma unroll
     for (int j = 0; j < EVI; ++j) {
       const uint64_t h = base + (uint64_t)j * BLOCK + threadIdx.x;
-      if (h >= nh) continue;
-      const uint32_t a = hids[h];
-      if (vlast != INVALID && a <= vlast) continue;
-      const uint64_t r = SH[h] - ev.removed(hst[h], hen[h]);
+      const bool in = h < nh;
+      ca[j] = in ? hids[h] : INVALID;
+      cr[j] = in ? SH[h] : 0;
+      cs[j] = in ? hst[h] : INVALID;
+      ce[j] = in ? hen[h] : INVALID;
+    }
+#pragma unroll
+    for (int j = 0; j < EVI; ++j) {
+      const uint64_t h = base + (uint64_t)j * BLOCK + threadIdx.x;
+      const uint32_t a = ca[j];
+      if (a == INVALID || (vlast != INVALID && a <= vlast)) continue;
+      const uint64_t r = cr[j] - ev.removed(cs[j], ce[j]);
       if (r > maxc) {
         const unsigned long long key = ((unsigned long long)a << 32) | h;
         best = key < best ? key : best;
@@ -404,6 +437,7 @@ __global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hi
   if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
+  const uint64_t t_search = wall_clock64();
   const unsigned long long e = __hip_atomic_load(found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t v = e == ~0ull ? INVALID : (uint32_t)(e >> 32);
   if (v != INVALID) {
@@ -427,6 +461,10 @@ __global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hi
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    const uint64_t t_stage = wall_clock64();
+    hdr[8] = (uint32_t)(t_table - t_start);
+    hdr[9] = (uint32_t)(t_search - t_table);
+    hdr[10] = (uint32_t)(t_stage - t_search);
     *found = ~0ull;   // the next event's search starts clean
     *done = 0;
     __threadfence_system();
@@ -732,6 +770,8 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   HIP_CHECK(hipMemsetAsync(evprev, 0xFF, sizeof(uint64_t), c.stream));
   HIP_CHECK(hipMemsetAsync(done_ctr, 0, sizeof(uint64_t), c.stream));
   HIP_CHECK(hipMemsetAsync(found, 0xFF, sizeof(uint64_t), c.stream));   // k_event resets it after each event
+  static const bool dbg = getenv("SHEEP_DEBUG_PART") != nullptr;
+  double dbg_tab = 0, dbg_search = 0, dbg_stage = 0, dbg_wait = 0, dbg_host = 0;
   uint8_t *stage = (uint8_t *)c.get_pinned("pt_event", 64 + (size_t)EV_STAGE * 12);
   volatile uint32_t *hdr = (volatile uint32_t *)stage;
   uint32_t *st_kids = (uint32_t *)(stage + 64);
@@ -754,8 +794,17 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   const uint32_t *t_pos = (const uint32_t *)d_ev_stage;   // the table the next launch reads
   const uint64_t *t_pre = (const uint64_t *)(d_ev_stage + 8);
   *(uint64_t *)(ev_stage + 8) = 0;   // empty table: pre[0] = 0
+  EvArg evarg;
+  evarg.m = 0;
+  evarg.pre[0] = 0;
   auto write_table = [&](bool to_device) {
     m_ev = (uint32_t)evs.size();
+    if (m_ev <= EV_ARG) {
+      uint64_t run = 0;
+      for (uint32_t i = 0; i < m_ev; ++i) { evarg.pos[i] = evs[i].first; evarg.pre[i] = run; run += evs[i].second; }
+      evarg.pre[m_ev] = run;
+      evarg.m = m_ev;
+    }
     const size_t pre_off = ((size_t)m_ev * 4 + 15) & ~(size_t)7;
     uint32_t *hp = (uint32_t *)ev_stage;
     uint64_t *hs = (uint64_t *)(ev_stage + pre_off);
@@ -787,7 +836,7 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   std::vector<uint32_t> seg, order, sorted, upl_pos, upl_ids;
   std::vector<uint64_t> segR, scb;
   std::vector<char> done;
-  const unsigned gev = nh ? (unsigned)std::min<uint64_t>((nh + EV_CH - 1) / EV_CH, 128) : 1;
+  const unsigned gev = nh ? (unsigned)std::min<uint64_t>((nh + EV_CH - 1) / EV_CH, 512) : 1;
   auto stage_kids_of = [&](uint32_t beg_j, uint32_t cap, uint32_t *o_kids, uint64_t *o_r) {
     ++seq_no;
     hipLaunchKernelGGL(k_event_kids, dim3(256), dim3(BLOCK), 0, c.stream, (const uint64_t *)evprev, t_pos, t_pre, m_ev,
@@ -802,13 +851,23 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
     hdr[7] = 0;
     for (;;) {
       ++seq_no;
+      const bool by_arg = m_ev <= EV_ARG;
       hipLaunchKernelGGL(k_event, dim3(gev), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh, (const uint64_t *)SH,
-                         (const uint32_t *)hst, (const uint32_t *)hen, t_pos, t_pre, m_ev, max_component, evprev, found,
+                         (const uint32_t *)hst, (const uint32_t *)hen, by_arg ? nullptr : t_pos, by_arg ? nullptr : t_pre, m_ev, max_component, evprev, found,
                          done_ctr, (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
                          (const uint32_t *)core.parent, (const uint32_t *)core.koff, (const uint32_t *)t.tD,
-                         (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren, d_hdr, d_kids, d_r, seq_no);
+                         (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren, d_hdr, d_kids, d_r, seq_no,
+                         evarg);
       LAUNCH_CHECK();
+      const auto h0 = std::chrono::steady_clock::now();
       wait_stage(seq_no);
+      const auto h1 = std::chrono::steady_clock::now();
+      if (dbg) {
+        dbg_tab += hdr[8] / 100.0;   // wall_clock64: 100 MHz
+        dbg_search += hdr[9] / 100.0;
+        dbg_stage += hdr[10] / 100.0;
+        dbg_wait += std::chrono::duration<double, std::micro>(h1 - h0).count();
+      }
       const uint32_t v = hdr[0];
       if (v == INVALID) break;
       info->packing_nodes++;
@@ -868,8 +927,12 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
       else
         root_own.push_back({v, cb0 - cb});
       write_table(false);   // (no kernel reads the table now: the last one has finished)
+      if (dbg) dbg_host += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h1).count();
     }
   }
+  if (dbg)
+    fprintf(stderr, "partition events %u (us total): table %.1f search %.1f stage %.1f | host wait %.1f host pack %.1f\n",
+            (unsigned)info->packing_nodes, dbg_tab, dbg_search, dbg_stage, dbg_wait, dbg_host);
   write_table(true);   // the device copy k_roots_r reads
   if (!upl_pos.empty()) {   // persist the sorted kid orders (forwardPartition mutates kids, :104-106)
     const uint64_t mu = upl_pos.size();

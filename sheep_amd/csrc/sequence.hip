@@ -64,10 +64,10 @@ __global__ __launch_bounds__(BLOCK) void k_compact_count(const uint32_t *__restr
     if (i < vs) { uint32_t d = deg[i]; cnt += d != 0; mx = d > mx ? d : mx; }
   }
   cnt = wave_sum(cnt);
-  mx = wave_max(mx);
-  if ((threadIdx.x & 63) == 0) { s[threadIdx.x >> 6] = cnt; if (mx) atomicMax(d_maxdeg, (unsigned long long)mx); }
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = cnt;
   __syncthreads();
   if (threadIdx.x == 0) block_cnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+  block_atomic_max(d_maxdeg, mx);
 }
 
 // Order-preserving compaction: (key = degree, value = vid) for every non-zero slot.

@@ -54,10 +54,10 @@ __global__ void k_rk_count(const uint32_t *__restrict__ parent, const uint32_t *
     if (i < n) { c += root_with_kids(parent, koff, i); r += parent[i] == INVALID; }
   }
   c = wave_sum(c);
-  r = wave_sum(r);
-  if ((threadIdx.x & 63) == 0) { s[threadIdx.x >> 6] = c; if (r) atomicAdd(nroots, (unsigned long long)r); }
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
   __syncthreads();
   if (threadIdx.x == 0) bcnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+  block_atomic_add(nroots, r);
 }
 __global__ void k_rk_write(const uint32_t *__restrict__ parent, const uint32_t *__restrict__ koff, uint64_t n,
                            const uint32_t *__restrict__ boff, uint32_t *__restrict__ rk) {

@@ -166,9 +166,10 @@ def test_merge_many_golden_halves(gpu_ctx, name):
     assert np.array_equal(p, gp) and np.array_equal(w, gw)
 
 
-@pytest.mark.parametrize("k", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 8, 70])
 def test_merge_many_shards_to_whole_tree(gpu_ctx, k):
-    """k contiguous shards merged in ONE pass == the whole tree == pairwise merges."""
+    """k contiguous shards merged in ONE pass == the whole tree == pairwise merges (k = 70:
+    more trees than one merge pass takes, so a second pass merges the first's result)."""
     import sheep_amd
     import torch
     d = sheep_amd.rmat(17, 16, 7)
