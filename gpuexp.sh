@@ -1,6 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out && export HSA_ENABLE_IPC_MODE_LEGACY=0 && export TMPDIR=/tmp
 T="timeout -k 10"
-$T 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "partition or oracle or c2 or c3 or cli or group" > gpurun_out/e1.log 2>&1 || exit 1
-SHEEP_DEBUG_PART=1 $T 300 python -u bench.py --steps 3 --no-cpu-baseline --eval-reps 0 > gpurun_out/b1.log 2> gpurun_out/b1.err || exit 1
-SHEEP_DEBUG_PART=1 $T 300 python -u bench.py --graph powerlaw --k 128 --steps 2 --no-cpu-baseline --eval-reps 0 > gpurun_out/b4.log 2> gpurun_out/b4.err || exit 1
+for G in 16 32 64 128 256; do SHEEP_EV_WG=$G SHEEP_DEBUG_PART=1 $T 200 python -u bench.py --steps 2 --no-cpu-baseline --eval-reps 0 > gpurun_out/bg$G.log 2> gpurun_out/bg$G.err || exit 1; done

@@ -836,7 +836,10 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   std::vector<uint32_t> seg, order, sorted, upl_pos, upl_ids;
   std::vector<uint64_t> segR, scb;
   std::vector<char> done;
-  const unsigned gev = nh ? (unsigned)std::min<uint64_t>((nh + EV_CH - 1) / EV_CH, 512) : 1;
+  // 64 workgroups: an event's scan usually ends within its first round of chunks, and every
+  // extra workgroup adds to the last-workgroup hand-off (RMAT-26 k=64, us per event:
+  // 16 WGs 26.5, 32 19.4, 64 16.5, 128 18.1, 256 27.3, 512 48)
+  const unsigned gev = nh ? (unsigned)std::min<uint64_t>((nh + EV_CH - 1) / EV_CH, 64) : 1;
   auto stage_kids_of = [&](uint32_t beg_j, uint32_t cap, uint32_t *o_kids, uint64_t *o_r) {
     ++seq_no;
     hipLaunchKernelGGL(k_event_kids, dim3(256), dim3(BLOCK), 0, c.stream, (const uint64_t *)evprev, t_pos, t_pre, m_ev,
