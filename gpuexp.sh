@@ -1,4 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out && export HSA_ENABLE_IPC_MODE_LEGACY=0 && export TMPDIR=/tmp
 T="timeout -k 10"
-for G in 16 32 64 128 256; do SHEEP_EV_WG=$G SHEEP_DEBUG_PART=1 $T 200 python -u bench.py --steps 2 --no-cpu-baseline --eval-reps 0 > gpurun_out/bg$G.log 2> gpurun_out/bg$G.err || exit 1; done
+P="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+$T 500 $P tests/test_gpu_parity.py tests/test_scale_parity.py -m gpu -k "degree or c2 or shuffled or cli" > gpurun_out/e2.log 2>&1 || exit 1
+$T 300 python -u bench.py --shuffle --steps 3 --no-cpu-baseline --eval-reps 0 > gpurun_out/bs.log 2> gpurun_out/bs.err || exit 1
+$T 300 python -u bench.py --steps 3 --no-cpu-baseline --eval-reps 0 > gpurun_out/b1.log 2> gpurun_out/b1.err || exit 1

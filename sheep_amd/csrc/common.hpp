@@ -321,6 +321,8 @@ void radix_sort_keys_u64(Ctx &c, uint64_t *keys, uint64_t n, int end_bit, uint64
 // hist.hip — cnt[key] += occurrences, keys bucketed through LDS (no scattered atomics)
 void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt,
                      bool counted = false);
+// both endpoints (every tail, and the heads as above) for records in no particular order
+void histogram_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt);
 // the degree pass fused with the heads' bucket counts; false (nothing launched) when the
 // capacity does not fit the bucket layout
 bool degree_fused(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap,

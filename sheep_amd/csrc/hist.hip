@@ -41,6 +41,17 @@ struct HeadKeys {
     return (llama && r.tail == r.head) ? NO_KEY : r.head;
   }
 };
+// Both endpoints: keys [0, n) are the tails, [n, 2n) the heads (HeadKeys' rule).
+struct EndpointKeys {
+  const sheep_xs1 *rec;
+  uint64_t n;
+  int llama;
+  __device__ __forceinline__ uint32_t operator()(uint64_t i) const {
+    if (i < n) return rec[i].tail;
+    const sheep_xs1 r = rec[i - n];
+    return (llama && r.tail == r.head) ? NO_KEY : r.head;
+  }
+};
 // lo = low 32 bits of a (hi << 32 | lo) tree edge; DEAD edges carry no key.
 struct EdgeLoKeys {
   const uint64_t *edges;
@@ -347,6 +358,7 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
     }
   }
   for (const void *f : {(const void *)k_hist_scatter<HeadKeys>, (const void *)k_hist_scatter<EdgeLoKeys>,
+                        (const void *)k_hist_scatter<EndpointKeys>, (const void *)k_hist_scatter_staged<EndpointKeys, 16>,
                         (const void *)k_hist_scatter_staged<HeadKeys, 16>,
                         (const void *)k_hist_scatter_staged<EdgeLoKeys, 16>, (const void *)k_hist_final,
                         (const void *)k_lo_scatter_staged<16>, (const void *)k_lo_scatter_staged<8>})
@@ -652,6 +664,12 @@ void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uin
   hl.nrec = nrec;
   hl.K = K;
   hl.valid = hl.bstart.size() == nb + 1;
+}
+
+void histogram_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt) {
+  c.head_layout.valid = false;   // the relabel counts its own head layout
+  c.head_layout.bstart.clear();
+  histogram_add(c, EndpointKeys{rec, nrec, llama}, 2 * nrec, K, cnt);
 }
 
 uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,

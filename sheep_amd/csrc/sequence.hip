@@ -16,10 +16,13 @@
 namespace sheep {
 namespace {
 
+// tails: add the tails here (run-combined atomics: records stored tail-sorted); otherwise
+// the tails go through the LDS-bucketed histogram with the heads and only the FILE_DAT
+// last record's extra tail count is added here.
 __global__ __launch_bounds__(BLOCK) void k_degree(const sheep_xs1 *__restrict__ rec, uint64_t nrec, int mode,
                                                   uint32_t *__restrict__ deg, uint64_t cap,
                                                   unsigned long long *__restrict__ d_max,
-                                                  unsigned long long *__restrict__ d_err) {
+                                                  unsigned long long *__restrict__ d_err, bool tails) {
   uint32_t lmax = 0;
   bool bad = false;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
@@ -42,12 +45,21 @@ __global__ __launch_bounds__(BLOCK) void k_degree(const sheep_xs1 *__restrict__ 
     }
     // tails here (runs: records are usually stored sorted by tail); heads go through
     // the LDS-bucketed histogram (hist.hip), except the FILE_DAT last record's extra
-    run_add(deg, kt, inc);
+    if (tails) run_add(deg, kt, inc);
+    else if (inc == 2) atomicAdd(&deg[kt], 1u);
     if (inc == 2 && kh != INVALID) atomicAdd(&deg[kh], 1u);
   }
-  lmax = wave_max(lmax);
-  if ((threadIdx.x & 63) == 0 && lmax) atomicMax(d_max, (unsigned long long)lmax);
+  block_atomic_max(d_max, lmax);
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(d_err, 1ull);
+}
+
+// Sortedness probe: descents tail[i + 1] < tail[i] at `samples` evenly spaced i.
+__global__ __launch_bounds__(BLOCK) void k_tail_descents(const sheep_xs1 *__restrict__ rec, uint64_t nrec, uint64_t step,
+                                                         uint64_t samples, unsigned long long *__restrict__ cnt) {
+  const uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const uint64_t i = j * step;
+  const bool d = j < samples && i + 1 < nrec && rec[i + 1].tail < rec[i].tail;
+  block_atomic_add(cnt, d ? 1 : 0);
 }
 
 constexpr int C_ITEMS = 8;
@@ -125,17 +137,36 @@ void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v) {
   LAUNCH_CHECK();
 }
 
+// Records stored sorted by tail (as generated, as hep-th and most edge lists are) put a
+// tail's records in one run, so the degree pass adds each run with one atomic.  In a
+// generic order every record's tail is its own scattered atomic (RMAT-26 shuffled: 44 ms),
+// so then the tails are bucketed in LDS together with the heads instead.
+static bool tails_sorted(Ctx &c, const sheep_xs1 *rec, uint64_t nrec) {
+  constexpr uint64_t SAMPLES = 1 << 16;
+  if (nrec < 2 * SAMPLES) return true;   // small inputs: the atomics cost nothing
+  unsigned long long *d = (unsigned long long *)c.d_scalars + 2;
+  HIP_CHECK(hipMemsetAsync(d, 0, sizeof(uint64_t), c.stream));
+  hipLaunchKernelGGL(k_tail_descents, dim3((unsigned)(SAMPLES / BLOCK)), dim3(BLOCK), 0, c.stream, rec, nrec,
+                     (nrec - 1) / SAMPLES, SAMPLES, d);
+  LAUNCH_CHECK();
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 2, d, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  return c.h_scalars[2] * 50 < SAMPLES;   // fewer than 2% descents
+}
+
 void degree_count(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap,
                   uint64_t *max_slot) {
   if (mode < 0 || mode > 2) throw Error(SHEEP_ERR_ARG, "bad degree mode");
   unsigned long long *d = (unsigned long long *)c.d_scalars;
+  const bool sorted = !nrec || nrec >= (1ull << 31) || tails_sorted(c, rec, nrec);
   HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
   bool counted = false;   // heads' (bucket, tile) counts made by the same pass (hist.hip)
   if (nrec) {
     TimedRegion tr(c, "degree", 12 * nrec);   // one read of the 12-B records
-    counted = degree_fused(c, rec, nrec, mode, deg, cap, d, d + 1);
+    if (sorted) counted = degree_fused(c, rec, nrec, mode, deg, cap, d, d + 1);
     if (!counted) {
-      hipLaunchKernelGGL(k_degree, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, mode, deg, cap, d, d + 1);
+      hipLaunchKernelGGL(k_degree, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, mode, deg, cap, d, d + 1,
+                         sorted);
       LAUNCH_CHECK();
     }
   }
@@ -145,7 +176,8 @@ void degree_count(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_
   *max_slot = c.h_scalars[0];
   if (nrec) {
     TimedRegion tr(c, "degree_heads", 12 * nrec);
-    histogram_heads(c, rec, nrec, mode == SHEEP_DEGREE_LLAMA, *max_slot, deg, counted);
+    if (sorted) histogram_heads(c, rec, nrec, mode == SHEEP_DEGREE_LLAMA, *max_slot, deg, counted);
+    else histogram_endpoints(c, rec, nrec, mode == SHEEP_DEGREE_LLAMA, *max_slot, deg);
   }
 }
 

@@ -22,7 +22,7 @@ __global__ void k_max_u32(const uint32_t *__restrict__ x, uint64_t n, unsigned l
 
 __global__ void k_kid_keys(const sheep_jnode *__restrict__ tree, uint64_t n, uint32_t *__restrict__ keys,
                            uint32_t *__restrict__ vals, uint32_t *__restrict__ parent,
-                           uint32_t *__restrict__ cnt, unsigned long long *__restrict__ err) {
+                           unsigned long long *__restrict__ err) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
     uint32_t p = tree[i].parent;
@@ -30,7 +30,19 @@ __global__ void k_kid_keys(const sheep_jnode *__restrict__ tree, uint64_t n, uin
     parent[i] = p;
     keys[i] = p == INVALID ? (uint32_t)n : p;
     vals[i] = (uint32_t)i;
-    if (p != INVALID) atomicAdd(&cnt[p], 1u);
+  }
+}
+
+// Kid counts from the parent-sorted keys: a parent's kids are one run, so run_add adds
+// each run with one atomic per wave it spans (a scattered atomic per node before the
+// sort cost 1.4 ms at RMAT-26).
+__global__ void k_kid_counts(const uint32_t *__restrict__ keys, uint64_t n, uint32_t *__restrict__ cnt) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const uint64_t iters = (n + stride - 1) / stride;
+  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (uint64_t it = 0; it < iters; ++it, i += stride) {   // wave-uniform trip count (run_add)
+    const uint32_t k = i < n ? keys[i] : (uint32_t)n;
+    run_add(cnt, k < n ? k : INVALID, 1u);
   }
 }
 
@@ -225,16 +237,17 @@ void build_kids(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_kids *k) {
   HIP_CHECK(hipMemsetAsync(k->koff, 0, (n + 1) * sizeof(uint32_t), c.stream));
   unsigned long long *d = (unsigned long long *)c.d_scalars + 16;
   HIP_CHECK(hipMemsetAsync(d, 0, 3 * sizeof(uint64_t), c.stream));
-  hipLaunchKernelGGL(k_kid_keys, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, tree, n, keys, vals, k->parent,
-                     k->koff, d);
+  hipLaunchKernelGGL(k_kid_keys, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, tree, n, keys, vals, k->parent, d);
+  LAUNCH_CHECK();
+  int bits = 0;
+  while (bits < 32 && (n >> bits)) ++bits;
+  radix_sort_pairs_u32(c, keys, vals, n, bits, kalt, valt);   // stable: kids ascending per parent
+  hipLaunchKernelGGL(k_kid_counts, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)keys, n, k->koff);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_max_u32, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->koff, n, d + 2);
   LAUNCH_CHECK();   // the largest kid count (the partition's packed rake state needs it < 2^24)
   // counts -> offsets; total = number of kids
   scan_exclusive_u32(c, k->koff, k->koff, n + 1, (uint32_t *)(d + 1));
-  int bits = 0;
-  while (bits < 32 && (n >> bits)) ++bits;
-  radix_sort_pairs_u32(c, keys, vals, n, bits, kalt, valt);   // stable: kids ascending per parent
   HIP_CHECK(hipMemcpyAsync(k->kids, vals, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
   HIP_CHECK(hipMemcpyAsync(c.h_scalars + 16, d, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();

@@ -43,6 +43,21 @@ def test_degree_sequence(gpu_ctx, name, mode, kind):
     assert np.count_nonzero(pos != 0xFFFFFFFF) == len(seq)
 
 
+@pytest.mark.parametrize("mode", ["llama", "dat"])
+def test_degree_sequence_unsorted_records(gpu_ctx, mode):
+    """Records in no particular order (tails bucketed with the heads instead of run-added)
+    give the oracle's sequence in both degree modes, the FILE_DAT last record included."""
+    import sheep_amd
+    import torch
+    d = sheep_amd.rmat(15, 16, 15)
+    g = torch.Generator(device=d.device)
+    g.manual_seed(5)
+    d = d[torch.randperm(d.shape[0], device=d.device, generator=g)].contiguous()
+    h = sheep_amd.to_numpy_u32(d).reshape(-1, 3)
+    s = sheep_amd.degree_sequence(d, mode=mode)
+    assert np.array_equal(s.numpy(), oracle.sequence(h[:, 0], h[:, 1], mode))
+
+
 @pytest.mark.parametrize("name", GRAPHS)
 def test_tree(gpu_ctx, name):
     import sheep_amd
