@@ -36,6 +36,7 @@ def per_kernel(path):
 
 
 def base(name):
+    name = name.replace("(anonymous namespace)::", "")   # its "(" is not the argument list
     head = name.split("(")[0]
     return head.split("<")[0].split("::")[-1].replace("void ", "").strip()
 
