@@ -72,8 +72,10 @@ def parse():
                     help="gloo stages the exchanges through host memory (rehearsal)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on cuda:0 (rehearse N ranks on a 1-GPU box; needs gloo)")
-    ap.add_argument("--reduce", default="kway", choices=("kway", "binomial"),
-                    help="kway: gather the partial trees to rank 0 and merge them in one pass; "
+    ap.add_argument("--reduce", default="split", choices=("split", "kway", "binomial"),
+                    help="split: ranks 0 and 1 receive every partial tree and each merges one half of the "
+                         "position range (rank 0 the heavier upper half), rank 1 sends its half's parents; "
+                         "kway: gather the partial trees to rank 0 and merge them in one pass; "
                          "binomial: ceil(log2 N) send/recv hops with a pairwise merge each")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 also builds the whole-graph tree and checks the merged one against it")
@@ -119,6 +121,7 @@ def main():
     if a.shards > 1 and world > 1:
         raise SystemExit("--shards is the one-GPU form of the edge-shard path")
 
+    reduce = a.reduce
     ctx = sheep_amd.Context(local)
     if a.graph == "rmat":                                       # whole graph, identical on every rank
         rec = sheep_amd.rmat(a.scale, a.ef, seed, ctx=ctx)
@@ -156,7 +159,10 @@ def main():
             tree = sheep_amd.merge_trees_many(stack[0], ctx=ctx)
         else:
             tree = sheep_amd.build_tree(shard, s, ctx=ctx)
-        if world > 1 and a.reduce == "kway":                    # reduce to rank 0 (jnode.cpp:241) in one pass
+        if world > 1 and reduce == "split":                     # the K-way merge split over the ranks
+            tree = sdist.reduce_trees_split(tree, lambda st, p, q: sheep_amd.merge_trees_part(st, p, q, ctx=ctx),
+                                            rank, world)
+        elif world > 1 and reduce == "kway":                    # reduce to rank 0 (jnode.cpp:241) in one pass
             tree = sdist.reduce_trees_kway(tree, lambda t: sheep_amd.merge_trees_many(t, ctx=ctx), rank, world)
         elif world > 1:                                         # binomial reduce to rank 0 (jnode.cpp:241)
             tree = sdist.reduce_trees(tree, lambda x, y: sheep_amd.merge_trees(x, y, ctx=ctx), rank, world)
@@ -256,7 +262,7 @@ def main():
             "config": {"workload": workload, "records": R, "vertex_slots": s.pos_size,
                        "tree_nodes": n, "k": a.k, "created": res.created, "packing_nodes": res.packing_nodes,
                        "heavy_nodes": res.heavy_nodes, "seed": seed, "shuffled": a.shuffle, "shards": a.shards,
-                       "parallelism": f"edge-shards x{world}" + (f", {a.reduce} reduce" if world > 1 else "")
+                       "parallelism": f"edge-shards x{world}" + (f", {reduce} reduce" if world > 1 else "")
                        + ("" if a.dist_backend == "nccl" else f" ({a.dist_backend}"
                           + (", one device" if a.same_device else "") + ")")},
             "roofline": roof,

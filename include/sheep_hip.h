@@ -159,6 +159,14 @@ int sheep_merge_trees(sheep_ctx *ctx, const sheep_jnode *a_dev, const sheep_jnod
  * parent-edge sets, pst summed.  Equal to any order of k - 1 sheep_merge_trees calls. */
 int sheep_merge_trees_many(sheep_ctx *ctx, const sheep_jnode *trees_dev, uint32_t k,
                            uint64_t n, sheep_jnode *out_dev);
+/* The same merge split over nparts = 2^l GPUs (the log-depth reduce of mpi_merge,
+ * jnode.cpp:203-250, without its serial tail): every part runs the first l levels of the
+ * merge over all k trees, then only its own subproblem.  out_dev holds every node's pst
+ * and a correct parent for every node in [*v_lo, *v_hi); the nparts ranges tile [0, n),
+ * so the parts' slices together are sheep_merge_trees_many's tree.  k <= 64. */
+int sheep_merge_trees_part(sheep_ctx *ctx, const sheep_jnode *trees_dev, uint32_t k,
+                           uint64_t n, uint32_t part, uint32_t nparts, sheep_jnode *out_dev,
+                           uint64_t *v_lo, uint64_t *v_hi);
 
 /* ---- partition ------------------------------------------------------------------ */
 int sheep_kids_create(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n,

@@ -94,6 +94,8 @@ def lib() -> ctypes.CDLL:
         "sheep_build_tree": ([P, P, U64, P, U64, U64, P], I32),
         "sheep_merge_trees": ([P, P, P, U64, P], I32),
         "sheep_merge_trees_many": ([P, P, ctypes.c_uint32, U64, P], I32),
+        "sheep_merge_trees_part": ([P, P, ctypes.c_uint32, U64, ctypes.c_uint32, ctypes.c_uint32, P,
+                                    ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], I32),
         "sheep_kids_create": ([P, P, U64, ctypes.POINTER(P)], I32),
         "sheep_kids_destroy": ([P], I32),
         "sheep_partition": ([P, P, U64, P, U64, U64, P, I16, D, I32, I32, P, ctypes.POINTER(_PartInfo)], I32),
@@ -321,6 +323,20 @@ def merge_trees_many(trees, ctx: Context | None = None):
     out = t.empty((max(n, 1), 2), dtype=t.int32, device=_dev(ctx))
     _check(lib().sheep_merge_trees_many(ctx.handle, _ptr(trees), k, n, _ptr(out)))
     return out[:n]
+
+
+def merge_trees_part(trees, part: int, nparts: int, ctx: Context | None = None):
+    """One part of a split K-way merge (sheep_merge_trees_part): returns (tree, lo, hi) —
+    every node's pst and the parents of nodes [lo, hi) are the merged tree's."""
+    ctx = ctx or default_context()
+    t = _torch()
+    k, n = trees.shape[0], trees.shape[1]
+    trees = trees.contiguous()
+    out = t.empty((max(n, 1), 2), dtype=t.int32, device=_dev(ctx))
+    lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().sheep_merge_trees_part(ctx.handle, _ptr(trees), k, n, part, nparts, _ptr(out), ctypes.byref(lo),
+                                        ctypes.byref(hi)))
+    return out[:n], lo.value, hi.value
 
 
 def tree_to_device(parent: np.ndarray, pst: np.ndarray):

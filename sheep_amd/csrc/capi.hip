@@ -18,6 +18,8 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
                       sheep_jnode *tree);
 void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n, sheep_jnode *out);
 void merge_trees_many(Ctx &c, const sheep_jnode *trees, uint32_t k, uint64_t n, sheep_jnode *out);
+void merge_trees_part(Ctx &c, const sheep_jnode *trees, uint32_t k, uint64_t n, uint32_t part, uint32_t nparts,
+                      sheep_jnode *out, uint64_t *v_lo, uint64_t *v_hi);
 void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t *seq, uint64_t seq_n, uint64_t pos_size,
                     sheep_kids *k, int16_t np, double balance, int vtx, int pstw, int16_t *parts_vid,
                     sheep_partition_info *info);
@@ -252,6 +254,16 @@ int sheep_merge_trees_many(sheep_ctx *ctx, const sheep_jnode *trees, uint32_t k,
   NEED(ctx && ((trees && out) || !n), "null argument");
   NEED(k >= 1, "merge: no trees");
   sheep::merge_trees_many(ctx->c, trees, k, n, out);
+  API_END
+}
+
+int sheep_merge_trees_part(sheep_ctx *ctx, const sheep_jnode *trees, uint32_t k, uint64_t n, uint32_t part,
+                           uint32_t nparts, sheep_jnode *out, uint64_t *v_lo, uint64_t *v_hi) {
+  API_BEGIN
+  DeviceGuard dg(ctx);
+  NEED(ctx && v_lo && v_hi && ((trees && out) || !n), "null argument");
+  NEED(k >= 1, "merge: no trees");
+  sheep::merge_trees_part(ctx->c, trees, k, n, part, nparts, out, v_lo, v_hi);
   API_END
 }
 

@@ -351,8 +351,10 @@ void histogram_edge_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t K, ui
 void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGroup &g, uint32_t *pst, uint64_t *r0,
                        uint64_t *seg, bool counted);
 // etree.hip
+// filt_lvl >= 0: at that level only entries with spread(lo) in [ylo, yhi) are kept (one
+// subproblem of a split merge; the caller cuts the later groups to it)
 void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
-                      int fin_bits);
+                      int fin_bits, int filt_lvl = -1, uint32_t ylo = 0, uint32_t yhi = 0);
 void spread_params(uint64_t n, int *L, uint32_t *clo);
 // append.hip — sharded appends: counters (NSHARD * SHARD_STRIDE u64, zeroed).  The pack
 // step moves the shard regions of a producer that streamed *n_in items together in dst

@@ -484,9 +484,16 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restric
 //   light  same half, bit s of yb == 0  -> the light list, and it stays in the list
 //   right  same half, bit s of yb == 1  -> stays in the list
 // DEAD entries (contractions that died) are dropped.
-__device__ __forceinline__ uint32_t classify(uint64_t e, int s, uint32_t clo) {
+// A range-restricted run (one part of a split merge, below) keeps, at the level where the
+// subproblems become that fine, only the entries of its own subproblem: ya in [lo, hi).
+struct YRange {
+  uint32_t lo, hi;
+  bool on;
+};
+__device__ __forceinline__ uint32_t classify(uint64_t e, int s, uint32_t clo, YRange yr) {
   if (e == DEAD) return 0;
   const uint32_t ya = spread((uint32_t)e, clo), yb = spread((uint32_t)(e >> 32), clo);
+  if (yr.on && (ya < yr.lo || ya >= yr.hi)) return 0;
   const uint32_t d = (ya ^ yb) >> s;
   if (d == 1) return 4;                          // cross
   return ((yb >> s) & 1) == 0 ? 3 : 1;           // light (bit 1: light, bit 0: stays) / right
@@ -514,7 +521,7 @@ __device__ __forceinline__ uint64_t pack3(uint32_t c) {
 }
 
 __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
-                                                       uint64_t *__restrict__ st, int s, uint32_t clo,
+                                                       uint64_t *__restrict__ st, int s, uint32_t clo, YRange yr,
                                                        const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
                                                        int L, uint64_t *__restrict__ cnt, uint64_t cstride) {
   const SplitIn in(list, prev, r0, seg, s, L);
@@ -530,7 +537,7 @@ __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restric
     for (int j = 0; j < TILE_ITEMS; ++j) ev[j] = in[tile * TILE + (uint64_t)j * BLOCK + threadIdx.x];
     uint64_t c3 = 0;
 #pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) c3 += pack3(classify(ev[j], s, clo));
+    for (int j = 0; j < TILE_ITEMS; ++j) c3 += pack3(classify(ev[j], s, clo, yr));
     c3 = wave_sum(c3);
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c3;
     __syncthreads();
@@ -548,7 +555,7 @@ __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restric
 // run of the tile is first placed in LDS at its thread-major rank, then copied out by
 // consecutive lanes (per-thread stores to the same positions: 16.6 against 12.2 ms).
 __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
-                                                       uint64_t *__restrict__ st, int s, uint32_t clo,
+                                                       uint64_t *__restrict__ st, int s, uint32_t clo, YRange yr,
                                                        const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
                                                        int L, const uint64_t *__restrict__ cnt, uint64_t cstride,
                                                        uint64_t *__restrict__ next, uint64_t *__restrict__ lbuf,
@@ -571,7 +578,7 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
     for (int j = 0; j < TILE_ITEMS; ++j) ev[j] = in[tile * TILE + (uint64_t)j * BLOCK + threadIdx.x];
 #pragma unroll
     for (int j = 0; j < TILE_ITEMS; ++j) {
-      cl[j] = classify(ev[j], s, clo);
+      cl[j] = classify(ev[j], s, clo, yr);
       c3 += pack3(cl[j]);
     }
     // thread-major ranks inside the tile: exclusive scan of the packed counters
@@ -905,7 +912,7 @@ static uint64_t list_capacity(uint64_t m) { return 2 * m + TILE; }
 // One pass of launches per level, no host synchronisation inside the loop (see the
 // stats row above); the stats come back once at the end for the timers / debug log.
 void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
-                      int fin_bits) {
+                      int fin_bits, int filt_lvl, uint32_t ylo, uint32_t yhi) {
   fill_u32(c, parent, n, INVALID);
   if (n < 2 || m == 0) return;
   if (m >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "too many edges for one shard");
@@ -949,14 +956,15 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     const uint64_t *prev = lvl ? st - ST_ROW : nullptr;
     const Tg g = make_tag(lvl, tagged);
     uint64_t *cur = lists[lvl & 1], *next = lists[(lvl + 1) & 1];
+    const YRange yr{ylo, yhi, lvl == filt_lvl};
     {
       TimedRegion tr(c, "etree_split");
       HIP_CHECK(hipMemsetAsync(tcnt, 0, (3 * cstride + 1) * sizeof(uint64_t), c.stream));
-      hipLaunchKernelGGL(k_split_count, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo,
+      hipLaunchKernelGGL(k_split_count, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo, yr,
                          (const uint64_t *)r0, (const uint64_t *)seg, L, tcnt, cstride);
       LAUNCH_CHECK();
       scan_exclusive_u64(c, tcnt, tcnt, 3 * cstride + 1, nullptr);
-      hipLaunchKernelGGL(k_split_write, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo,
+      hipLaunchKernelGGL(k_split_write, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo, yr,
                          (const uint64_t *)r0, (const uint64_t *)seg, L, (const uint64_t *)tcnt, cstride, next, lbuf, xbuf);
       LAUNCH_CHECK();
     }
@@ -1143,8 +1151,10 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
 // The merge's edges: every node's distinct parents over the K trees, compacted in node
 // (= lo) order, and their first-activity group bounds (group s = the lo range whose
 // spread has its highest zero bit at s).  Returns the edge count; pst = the summed weights.
+// Groups b < bmax (activated at the levels a part of a split merge runs alone) are cut to
+// the part's node range [v_lo, v_hi).
 static uint64_t merge_edges(Ctx &c, const TreeSet &ts, uint32_t K, uint64_t n, uint32_t *pst, uint64_t **edges_out,
-                            uint64_t **seg_out, int *L_out) {
+                            uint64_t **seg_out, int *L_out, int bmax = 0, uint64_t v_lo = 0, uint64_t v_hi = 0) {
   int L;
   uint32_t clo;
   spread_params(n, &L, &clo);
@@ -1181,8 +1191,13 @@ static uint64_t merge_edges(Ctx &c, const TreeSet &ts, uint32_t K, uint64_t n, u
   };
   SegNodes sn{};
   for (int b = 0; b < L; ++b) {
-    sn.node[b] = (uint32_t)first_lo((1ull << L) - (2ull << b));
-    sn.node[L + b] = (uint32_t)first_lo((1ull << L) - (1ull << b));
+    uint64_t g0 = first_lo((1ull << L) - (2ull << b)), g1 = first_lo((1ull << L) - (1ull << b));
+    if (b < bmax) {   // the part's share of the group: a node range, so a range of the edges
+      g0 = std::min(std::max(g0, v_lo), v_hi);
+      g1 = std::max(std::min(g1, v_hi), g0);
+    }
+    sn.node[b] = (uint32_t)g0;
+    sn.node[L + b] = (uint32_t)g1;
   }
   uint64_t *seg = c.get_as<uint64_t>("mg_seg", 2 * (uint64_t)L);
   hipLaunchKernelGGL(k_seg_at, dim3(1), dim3(64), 0, c.stream, (const uint32_t *)off, sn, 2 * L, seg);
@@ -1193,27 +1208,75 @@ static uint64_t merge_edges(Ctx &c, const TreeSet &ts, uint32_t K, uint64_t n, u
   return m;
 }
 
+// min node x with spread(x) >= y
+static uint64_t first_node(uint64_t n, uint32_t clo, uint64_t y) {
+  uint64_t a = 0, z = n;
+  while (a < z) {
+    const uint64_t x = (a + z) / 2;
+    if (x + ((x * (uint64_t)clo) >> 32) >= y) z = x; else a = x + 1;
+  }
+  return a;
+}
+
 // The elimination tree of the union of the K trees' parent-edge sets (JNodeTable::merge,
 // jnode.cpp:174-201, for K = 2; for K > 2 the same tree as K - 1 pairwise merges in any
 // order — merge is associative and commutative — i.e. mpi_merge's whole reduction,
 // jnode.cpp:203-250, in one pass).
-static void merge_set(Ctx &c, const TreeSet &ts, uint32_t K, uint64_t n, sheep_jnode *out) {
+//
+// Split merge (nparts = 2^l > 1): after the first l levels every live edge lies inside one
+// of nparts subproblems, and each is finished independently; this call runs the first l
+// levels in full and then only subproblem `part` (its share of the list, of the later
+// groups and of the per-block finish).  Every node's pst and the parent of every node
+// assigned in the first l levels are the full merge's; below them only the nodes of the
+// part's range [*v_lo, *v_hi) are (the others keep INVALID where a later level would
+// have linked them).  nparts GPUs that each run one part together hold the whole tree.
+static void merge_set(Ctx &c, const TreeSet &ts, uint32_t K, uint64_t n, sheep_jnode *out, uint32_t part = 0,
+                      uint32_t nparts = 1, uint64_t *v_lo = nullptr, uint64_t *v_hi = nullptr) {
   if ((uint64_t)K * n >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "merge: too many parent edges for one pass");
   uint32_t *pst = c.get_as<uint32_t>("mg_pst", n);
   uint32_t *parent = c.get_as<uint32_t>("mg_parent", n);
   uint64_t *edges = nullptr, *seg = nullptr;
-  int L = 0;
+  int L = 0, l = 0;
+  uint32_t clo = 0;
+  while ((1u << l) < nparts) ++l;
+  if (nparts == 0 || (1u << l) != nparts || part >= nparts) throw Error(SHEEP_ERR_ARG, "merge: parts must be a power of two");
+  uint64_t lo = 0, hi = n;
+  if (n >= 2) spread_params(n, &L, &clo);
+  // only as many parts as global levels (below them the per-block finish runs whole)
+  const int nglobal = L > FIN_MERGE ? L - FIN_MERGE : 0;
+  if (nparts > 1 && (l >= nglobal || L > 31)) l = 0;   // too small a tree to split: every part runs it all
+  uint32_t ylo = 0, yhi = 0;
+  if (l > 0) {
+    ylo = (uint32_t)((uint64_t)part << (L - l));
+    yhi = (uint32_t)((uint64_t)(part + 1) << (L - l));
+    lo = first_node(n, clo, ylo);
+    hi = first_node(n, clo, yhi);
+  }
+  if (v_lo) *v_lo = lo;
+  if (v_hi) *v_hi = hi;
   if (n < 2) {
     // one node: no edges; the weights still add up
     merge_edges(c, ts, K, n, pst, &edges, &seg, &L);
     fill_u32(c, parent, n, INVALID);
   } else {
     TimedRegion tr(c, "merge", 8 * (uint64_t)K * n);   // the K trees
-    const uint64_t m = merge_edges(c, ts, K, n, pst, &edges, &seg, &L);
-    etree_from_edges(c, edges, m, n, parent, seg, FIN_MERGE);
+    // groups activated at levels >= l are b < L - l
+    const uint64_t m = merge_edges(c, ts, K, n, pst, &edges, &seg, &L, l > 0 ? L - l : 0, lo, hi);
+    etree_from_edges(c, edges, m, n, parent, seg, FIN_MERGE, l > 0 ? l : -1, ylo, yhi);
   }
   hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);
   LAUNCH_CHECK();
+}
+
+void merge_trees_part(Ctx &c, const sheep_jnode *trees, uint32_t K, uint64_t n, uint32_t part, uint32_t nparts,
+                      sheep_jnode *out, uint64_t *v_lo, uint64_t *v_hi) {
+  if (K == 0) throw Error(SHEEP_ERR_ARG, "merge: no trees");
+  if (K > MERGE_KMAX) throw Error(SHEEP_ERR_ARG, "split merge: more trees than one pass takes");
+  if (n == 0) {
+    *v_lo = *v_hi = 0;
+    return;
+  }
+  merge_set(c, TreeSet{trees, trees + n, n}, K, n, out, part, nparts, v_lo, v_hi);
 }
 
 void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n, sheep_jnode *out) {

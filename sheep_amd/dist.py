@@ -17,7 +17,11 @@ path (graph2tree.cpp:161-216).
                         (sheep_merge_trees_many): every rank sends its tree straight to
                         rank 0 (each over its own xGMI link, all at once), and the merge
                         runs once over all K parent-edge sets instead of ceil(log2 K)
-                        merges in sequence on rank 0's critical path.
+                        merges in sequence on rank 0's critical path;
+  * reduce_trees_split— the K-way merge split over two ranks (sheep_merge_trees_part):
+                        ranks 0 and 1 receive every tree, each runs the merge's top level
+                        in full and then one half of the position range, and rank 1 sends
+                        its half's parents to rank 0 (see the function for why two parts).
 
 One process per GPU.  With the "nccl" backend (RCCL over xGMI) device tensors are sent
 as they are.  With "gloo" they are staged through host memory, which lets the schedule
@@ -113,6 +117,69 @@ def reduce_trees_kway(tree: torch.Tensor, merge_many, rank: int, world: int):
     None elsewhere."""
     stacked = gather_trees(tree, rank, world)
     return None if stacked is None else merge_many(stacked)
+
+
+def gather_trees_to(tree: torch.Tensor, rank: int, world: int, receivers) -> torch.Tensor | None:
+    """Every rank's (n, 2) tree stacked as (world, n, 2) on each rank in `receivers`
+    (None elsewhere): one batch of point-to-point transfers, each sender's copies on
+    different xGMI links."""
+    recv_here = rank in receivers
+    staged = _host_staged() and tree.is_cuda
+    src = tree.cpu().contiguous() if staged else tree.contiguous()
+    out = None
+    ops = []
+    if recv_here:
+        out = torch.empty((world,) + tuple(tree.shape), dtype=tree.dtype, device="cpu" if staged else tree.device)
+        out[rank].copy_(src)
+        ops += [dist.P2POp(dist.irecv, out[r], r) for r in range(world) if r != rank]
+    ops += [dist.P2POp(dist.isend, src, q) for q in receivers if q != rank]
+    if ops:
+        if _host_staged():
+            reqs = [op.op(op.tensor, op.peer) for op in ops]
+        else:
+            reqs = dist.batch_isend_irecv(ops)
+        for q in reqs:
+            q.wait()
+    if out is not None and staged:
+        out = out.to(tree.device)
+    return out
+
+
+def reduce_trees_split(tree: torch.Tensor, merge_part, rank: int, world: int, nparts: int = 2):
+    """The K-way merge split over `nparts` ranks (a power of two <= world): ranks
+    0..nparts-1 receive every tree, each runs one part (merge_part(stacked, part, nparts)
+    -> (tree, lo, hi): every pst and the parents of nodes [lo, hi) are the merged tree's)
+    and ranks 1..nparts-1 send their parent slices to rank 0.  Rank 0 takes the LAST part:
+    contractions move every level's work into right halves, so the part of the highest
+    positions is by far the largest (RMAT-26, 8 trees: parts of a 2-way split 3.1 and
+    12.6 ms against 17.9 for the whole merge; an 8-way split's last part alone 16.1 ms).
+    Returns the merged tree on rank 0, None elsewhere."""
+    nparts = max(1, min(nparts, world))
+    if nparts & (nparts - 1):
+        raise ValueError("split reduce needs a power-of-two number of parts")
+    stacked = gather_trees_to(tree, rank, world, range(nparts))
+    if rank >= nparts:
+        return None
+    part_id = nparts - 1 if rank == 0 else rank - 1
+    part, lo, hi = merge_part(stacked, part_id, nparts)
+    del stacked
+    staged = _host_staged() and part.is_cuda
+    if rank != 0:
+        rng = torch.tensor([lo, hi], dtype=torch.int64, device="cpu" if _host_staged() else part.device)
+        sl = part[lo:hi, 0].contiguous()
+        _send(rng, 0)
+        if hi > lo:
+            _send(sl, 0)
+        return None
+    for r in range(1, nparts):
+        rng = torch.empty(2, dtype=torch.int64, device="cpu" if _host_staged() else part.device)
+        dist.recv(rng, r)
+        a, b = int(rng[0]), int(rng[1])
+        if b > a:
+            buf = torch.empty(b - a, dtype=part.dtype, device="cpu" if staged else part.device)
+            dist.recv(buf, r)
+            part[a:b, 0] = buf.to(part.device)
+    return part
 
 
 def reduce_eval(ev, rank: int, world: int):

@@ -37,7 +37,7 @@ def _oracle_merge_many(stacked):
     return acc
 
 
-def _rank_main(rank, world, port, name, out_path, reduce="binomial"):
+def _rank_main(rank, world, port, name, out_path, reduce="binomial", split_parts=2):
     import oracle
     from sheep_amd import dist as sdist
 
@@ -60,7 +60,18 @@ def _rank_main(rank, world, port, name, out_path, reduce="binomial"):
         p, w = oracle.build_tree(tail, head, seq)
         tree = torch.from_numpy(np.stack([p, w], axis=1).view(np.int32))
 
-        if reduce == "kway":
+        if reduce == "split":
+            def merge_part(stacked, part, nparts):
+                # the split merge's contract: every pst, and parents only in the part's
+                # range (the rest scrambled, so rank 0 must take them from their owners)
+                full = _oracle_merge_many(stacked).clone()
+                n = full.shape[0]
+                lo, hi = part * n // nparts, (part + 1) * n // nparts
+                full[:lo, 0] = -7
+                full[hi:, 0] = -7
+                return full, lo, hi
+            tree = sdist.reduce_trees_split(tree, merge_part, rank, world, nparts=split_parts)
+        elif reduce == "kway":
             stacked = sdist.gather_trees(tree, rank, world)
             if rank == 0:   # the gather itself is exact: row r is rank r's own tree
                 assert stacked.shape == (world,) + tuple(tree.shape)
@@ -103,6 +114,18 @@ def test_kway_schedule_matches_serial(tmp_path, world):
     """Gather to rank 0 + one K-way reduction (bench.py's default --reduce kway)."""
     out = str(tmp_path / "rank0.json")
     mp.spawn(_rank_main, args=(world, _free_port(), "rmat10", out, "kway"), nprocs=world, join=True)
+    got = json.load(open(out))
+    parent, pst = golden_tree("rmat10")
+    assert np.array_equal(np.array(got["parent"], np.uint32), parent)
+    assert np.array_equal(np.array(got["pst"], np.uint32), pst)
+
+
+@pytest.mark.parametrize("world,nparts", [(2, 2), (3, 2), (4, 2), (4, 4)])
+def test_split_schedule_matches_serial(tmp_path, world, nparts):
+    """Every tree to the part ranks + one part of the split merge each + the parts' node
+    ranges gathered to rank 0 (bench.py's --reduce split)."""
+    out = str(tmp_path / "rank0.json")
+    mp.spawn(_rank_main, args=(world, _free_port(), "rmat10", out, "split", nparts), nprocs=world, join=True)
     got = json.load(open(out))
     parent, pst = golden_tree("rmat10")
     assert np.array_equal(np.array(got["parent"], np.uint32), parent)

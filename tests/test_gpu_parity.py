@@ -201,6 +201,34 @@ def test_merge_many_shards_to_whole_tree(gpu_ctx, k):
     assert np.array_equal(p2, whole[0]) and np.array_equal(w2, whole[1])
 
 
+@pytest.mark.parametrize("scale,k", [(17, 8), (17, 4), (17, 2), (12, 8)])
+def test_split_merge_parts_tile_whole_tree(gpu_ctx, scale, k):
+    """sheep_merge_trees_part: each part's node range of parents (plus every pst) is the
+    merged tree's, the k ranges tile [0, n) and together they are the whole-graph tree
+    (RMAT-12: too few levels to split, every part runs the whole merge)."""
+    import sheep_amd
+    import torch
+    d = sheep_amd.rmat(scale, 16, 9)
+    s = sheep_amd.degree_sequence(d)
+    whole = sheep_amd.build_tree(d, s)
+    R = d.shape[0]
+    stacked = torch.stack([sheep_amd.build_tree(d[i * R // k:(i + 1) * R // k], s) for i in range(k)])
+    asm, covered = None, 0
+    for p in range(k):
+        part, lo, hi = sheep_amd.merge_trees_part(stacked, p, k)
+        assert torch.equal(part[:, 1], whole[:, 1])
+        assert torch.equal(part[lo:hi, 0], whole[lo:hi, 0])
+        if asm is None:
+            asm = part.clone()
+        asm[lo:hi, 0] = part[lo:hi, 0]
+        covered += hi - lo
+        assert lo <= hi
+    assert covered == whole.shape[0] or covered == k * whole.shape[0]   # a tiling, or every part whole
+    assert torch.equal(asm, whole)
+    with pytest.raises(ValueError):
+        sheep_amd.merge_trees_part(stacked, 0, 3)   # parts must be a power of two
+
+
 def test_merge_many_rejects_bad_parent(gpu_ctx):
     import sheep_amd
     import torch

@@ -1,12 +1,15 @@
 #!/usr/bin/env python3
 """Time the reduce step alone on one GPU: K shard trees of RMAT-<scale> reduced to one.
 
-    python tools/merge_probe.py [scale] [reps] [K]
+    python tools/merge_probe.py [scale] [reps] [K] [nparts]
 
-Two schedules are timed: the binomial pairwise schedule's critical path (the
+Three schedules are timed: the binomial pairwise schedule's critical path (the
 ceil(log2 K) merges rank 0 performs; the other ranks' merges are precomputed,
-untimed, as they would run on their own GPUs) and one K-way merge
-(sheep_merge_trees_many).  Both results are checked against the whole-graph tree.
+untimed, as they would run on their own GPUs), one K-way merge
+(sheep_merge_trees_many), and the split K-way merge (sheep_merge_trees_part over nparts,
+a power of two, default 2): each part is timed on its own (as nparts GPUs would run them
+side by side) and the slowest part is the critical path.  Every result is checked against the
+whole-graph tree.
 Prints wall time per reduction and the per-region device times (HIP events)."""
 import os
 import sys
@@ -21,6 +24,7 @@ def main():
     scale = int(sys.argv[1]) if len(sys.argv) > 1 else 24
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     K = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+    NP = int(sys.argv[4]) if len(sys.argv) > 4 else 2
     ctx = sheep_amd.Context(0)
     rec = sheep_amd.rmat(scale, 16, scale, ctx=ctx)
     s = sheep_amd.degree_sequence(rec, ctx=ctx)
@@ -46,6 +50,23 @@ def main():
     m = sheep_amd.merge_trees_many(stacked, ctx=ctx)
     assert torch.equal(m, whole), "K-way merge differs from the whole-graph tree"
     print(f"RMAT-{scale}: n={s.n} K={K} hops={len(inputs)}")
+    if NP & (NP - 1) == 0:
+        asm = None
+        worst = 0.0
+        for p in range(NP):
+            for rep in range(reps + 1):                      # the first run warms the workspaces
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                part, lo, hi = sheep_amd.merge_trees_part(stacked, p, NP, ctx=ctx)
+                torch.cuda.synchronize()
+                dt = time.perf_counter() - t0
+            worst = max(worst, dt)
+            print(f"  split part {p}: nodes [{lo}, {hi}) {1e3 * dt:.2f} ms")
+            if asm is None:
+                asm = part.clone()
+            asm[lo:hi, 0] = part[lo:hi, 0]
+        assert torch.equal(asm, whole), "split merge differs from the whole-graph tree"
+        print(f"split K-way merge over {NP} parts: {1e3 * worst:.2f} ms critical path (slowest part)")
     for label, fn in (("pairwise critical path", None), ("one K-way merge", None)):
         torch.cuda.synchronize()
         ctx.timing(True)
