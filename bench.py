@@ -72,10 +72,10 @@ def parse():
                     help="gloo stages the exchanges through host memory (rehearsal)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on cuda:0 (rehearse N ranks on a 1-GPU box; needs gloo)")
-    ap.add_argument("--reduce", default="split", choices=("split", "kway", "binomial"),
-                    help="split: ranks 0 and 1 receive every partial tree and each merges one half of the "
+    ap.add_argument("--reduce", default="kway", choices=("kway", "split", "binomial"),
+                    help="kway: gather the partial trees to rank 0 and merge them in one pass; "
+                         "split: ranks 0 and 1 receive every partial tree and each merges one half of the "
                          "position range (rank 0 the heavier upper half), rank 1 sends its half's parents; "
-                         "kway: gather the partial trees to rank 0 and merge them in one pass; "
                          "binomial: ceil(log2 N) send/recv hops with a pairwise merge each")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 also builds the whole-graph tree and checks the merged one against it")

@@ -18,10 +18,10 @@ path (graph2tree.cpp:161-216).
                         rank 0 (each over its own xGMI link, all at once), and the merge
                         runs once over all K parent-edge sets instead of ceil(log2 K)
                         merges in sequence on rank 0's critical path;
-  * reduce_trees_split— the K-way merge split over two ranks (sheep_merge_trees_part):
-                        ranks 0 and 1 receive every tree, each runs the merge's top level
-                        in full and then one half of the position range, and rank 1 sends
-                        its half's parents to rank 0 (see the function for why two parts).
+  * reduce_trees_split— the K-way merge split over nparts ranks (sheep_merge_trees_part):
+                        the part ranks receive every tree, each runs the merge's top levels
+                        in full and then one subproblem, and they send their node ranges'
+                        parents to rank 0 (measured: little gain, see the function).
 
 One process per GPU.  With the "nccl" backend (RCCL over xGMI) device tensors are sent
 as they are.  With "gloo" they are staged through host memory, which lets the schedule
@@ -151,8 +151,9 @@ def reduce_trees_split(tree: torch.Tensor, merge_part, rank: int, world: int, np
     -> (tree, lo, hi): every pst and the parents of nodes [lo, hi) are the merged tree's)
     and ranks 1..nparts-1 send their parent slices to rank 0.  Rank 0 takes the LAST part:
     contractions move every level's work into right halves, so the part of the highest
-    positions is by far the largest (RMAT-26, 8 trees: parts of a 2-way split 3.1 and
-    12.6 ms against 17.9 for the whole merge; an 8-way split's last part alone 16.1 ms).
+    positions is by far the largest — which is also why the split gains little (RMAT-26,
+    8 trees: 2 parts 4.1 / 17.3 ms, 8 parts 7.4 ... 16.1 ms, against 17.8 ms for the
+    whole merge on one GPU), so bench.py keeps the K-way gather by default.
     Returns the merged tree on rank 0, None elsewhere."""
     nparts = max(1, min(nparts, world))
     if nparts & (nparts - 1):
