@@ -179,20 +179,17 @@ __global__ void k_walk(const uint32_t *__restrict__ rulers, uint64_t nr, const u
 }
 
 // Wyllie pointer jumping on the ruler list: suffix sums of lengths.
+// (The round count is fixed on the host: ceil(log2 nr).  A per-wave "still active"
+// atomic on one word cost each round ~30 us for 4K waves.)
 __global__ void k_jump(const uint32_t *__restrict__ nxt_in, const uint32_t *__restrict__ suf_in, uint64_t nr,
-                       uint32_t *__restrict__ nxt_out, uint32_t *__restrict__ suf_out,
-                       unsigned long long *__restrict__ active) {
+                       uint32_t *__restrict__ nxt_out, uint32_t *__restrict__ suf_out) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  bool any = false;
   for (uint64_t r = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; r < nr; r += stride) {
     uint32_t nx = nxt_in[r];
     if (nx == INVALID) { nxt_out[r] = INVALID; suf_out[r] = suf_in[r]; continue; }
     suf_out[r] = suf_in[r] + suf_in[nx];
-    uint32_t nn = nxt_in[nx];
-    nxt_out[r] = nn;
-    any |= nn != INVALID;
+    nxt_out[r] = nxt_in[nx];
   }
-  if (__any(any) && (threadIdx.x & 63) == 0) atomicAdd(active, 1ull);
 }
 
 __global__ void k_tpos(const uint32_t *__restrict__ parent, uint64_t n, const uint32_t *__restrict__ owner,
@@ -329,7 +326,7 @@ void build_tour(Ctx &c, sheep_kids *k, Tour &t) {
   int rounds = 0;
   while ((1ull << rounds) < nr) ++rounds;
   for (int it = 0; it < rounds; ++it) {
-    hipLaunchKernelGGL(k_jump, dim3(grid_for(nr)), dim3(BLOCK), 0, c.stream, na, sa, nr, nb2, sb, d + 3);
+    hipLaunchKernelGGL(k_jump, dim3(grid_for(nr)), dim3(BLOCK), 0, c.stream, na, sa, nr, nb2, sb);
     LAUNCH_CHECK();
     std::swap(sa, sb);
     std::swap(na, nb2);
