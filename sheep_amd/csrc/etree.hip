@@ -273,7 +273,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_clean(const uint64_t *__restric
   }
 }
 
-constexpr int XK = 4;   // items per thread in the gather kernels (independent chains in flight)
+constexpr int XK = 8;   // items per thread in the gather kernels (independent chains in flight)
 
 // top[root] = the component's largest id.  Every vertex of a non-singleton light
 // component is an endpoint of a light edge and its maximum is the hi end of one, so a
