@@ -1,5 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out && export HSA_ENABLE_IPC_MODE_LEGACY=0 && export TMPDIR=/tmp
 T="timeout -k 10"
+P="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+$T 500 $P tests/test_gpu_parity.py tests/test_scale_parity.py -m gpu -k "degree or c2 or relabel or tree or wide or unsequenced" > gpurun_out/e2.log 2>&1 || exit 1
 $T 300 python -u bench.py --steps 3 --no-cpu-baseline --eval-reps 0 > gpurun_out/b1.log 2> gpurun_out/b1.err || exit 1
-$T 300 python -u bench.py --graph powerlaw --k 128 --steps 2 --no-cpu-baseline --eval-reps 0 > gpurun_out/b4.log 2> gpurun_out/b4.err || exit 1

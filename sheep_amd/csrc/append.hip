@@ -33,7 +33,7 @@ __global__ __launch_bounds__(BLOCK) void k_pack(const T *__restrict__ src, T *__
     }
   }
   if (zero_after && blockIdx.x == 0 && threadIdx.x < NSHARD) zero_after[(uint64_t)threadIdx.x * SHARD_STRIDE] = 0;
-  __syncthreads();
+  lds_barrier();
   const uint64_t cnt = s_count, per = (cnt + PACK_SLICES - 1) / PACK_SLICES;
   const uint64_t beg = (uint64_t)slice * per, end = beg + per < cnt ? beg + per : cnt;
   const T *s = src + shard_base(ntiles, k, 1);

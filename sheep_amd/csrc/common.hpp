@@ -159,6 +159,18 @@ struct TimedRegion {
 // ---------------------------------------------------------------------------------
 __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
 
+// Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup release/acquire
+// over all of memory, so it first waits for every global load and store the wave has in
+// flight (vmcnt(0)): a streaming kernel's prefetches and write-backs drain at each of its
+// barriers.  For kernels whose threads exchange data through LDS only (the bucket sorts,
+// scans, the level splits); a kernel that reads global memory another thread of its
+// workgroup wrote keeps __syncthreads().
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
   unsigned l = __lane_id();
   return l == 0 ? 0ull : (~0ull >> (64 - l));
@@ -209,11 +221,11 @@ __device__ __forceinline__ uint64_t block_reduce_u64(uint64_t v, bool is_max) {
   __shared__ uint64_t s_red[16];
   v = is_max ? wave_max(v) : wave_sum(v);
   if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
-  __syncthreads();
+  lds_barrier();
   uint64_t r = 0;
   if (threadIdx.x == 0)
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) r = is_max ? (s_red[w] > r ? s_red[w] : r) : r + s_red[w];
-  __syncthreads();   // s_red is reused by the next call
+  lds_barrier();   // s_red is reused by the next call
   return r;          // meaningful in thread 0
 }
 __device__ __forceinline__ void block_atomic_max(unsigned long long *dst, uint64_t v) {
@@ -251,7 +263,7 @@ __device__ __forceinline__ uint64_t block_reserve(uint32_t cnt, unsigned long lo
     if (lane >= o) inc += u;
   }
   if (lane == 63) s_w[wave] = inc;
-  __syncthreads();
+  lds_barrier();
   uint32_t woff = 0, tot = 0;
 #pragma unroll
   for (int w = 0; w < BLOCK / WAVE; ++w) {
@@ -260,9 +272,9 @@ __device__ __forceinline__ uint64_t block_reserve(uint32_t cnt, unsigned long lo
     tot += x;
   }
   if (threadIdx.x == 0) s_base = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
-  __syncthreads();
+  lds_barrier();
   const uint64_t first = s_base + woff + inc - cnt;
-  __syncthreads();   // s_w / s_base are reused by the next call
+  lds_barrier();   // s_w / s_base are reused by the next call
   return first;
 }
 

@@ -540,13 +540,13 @@ __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restric
     for (int j = 0; j < TILE_ITEMS; ++j) c3 += pack3(classify(ev[j], s, clo, yr));
     c3 = wave_sum(c3);
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c3;
-    __syncthreads();
+    lds_barrier();
     if (threadIdx.x < 3) {
       uint64_t t = 0;
       for (int w = 0; w < BLOCK / WAVE; ++w) t += s_w[w];
       cnt[threadIdx.x * cstride + tile] = (t >> (16 * threadIdx.x)) & 0xFFFF;
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -589,7 +589,7 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
       if (lane >= o) inc += u;
     }
     if (lane == 63) s_w[wave] = inc;
-    __syncthreads();
+    lds_barrier();
     uint64_t off = 0;
     for (int w = 0; w < wave; ++w) off += s_w[w];
     const uint64_t ex = off + inc - c3;
@@ -603,11 +603,11 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
 #pragma unroll
       for (int j = 0; j < TILE_ITEMS; ++j)
         if ((cl[j] >> k) & 1) stg[r++] = ev[j];
-      __syncthreads();
+      lds_barrier();
       const uint32_t n_k = (uint32_t)((tot >> (16 * k)) & 0xFFFF);
       uint64_t *const o = outs[k] + (cnt[k * cstride + tile] - cnt[k * cstride]);
       for (uint32_t i = threadIdx.x; i < n_k; i += BLOCK) o[i] = stg[i];
-      __syncthreads();   // stg (and, after the last class, s_w) is rewritten next
+      lds_barrier();   // stg (and, after the last class, s_w) is rewritten next
     }
   }
 }
@@ -759,13 +759,13 @@ __global__ __launch_bounds__(WAVE) void k_fin_heavy(const uint64_t *__restrict__
     const uint32_t b = heavy[h];
     const uint32_t v0 = vb[b], cnt = vb[b + 1] - v0;
     const uint64_t e0 = eb[b], e1 = eb[b + 1];
-    __syncthreads();   // the previous block is done with uf and stage
+    lds_barrier();   // the previous block is done with uf and stage
     for (uint32_t i = lane; i < cnt; i += WAVE) uf[i] = (U)i;
     for (uint64_t base = e0; base < e1; base += FIN_STAGE) {
       const uint32_t len = (uint32_t)(e1 - base < FIN_STAGE ? e1 - base : FIN_STAGE);
-      __syncthreads();
+      lds_barrier();
       for (uint32_t i = lane; i < len; i += WAVE) stage[i] = fin[base + i];
-      __syncthreads();
+      lds_barrier();
       for (uint32_t p = 0; p < len;) {
         const uint32_t v = (uint32_t)stage[p];
         const uint32_t idx = p + lane;
@@ -780,7 +780,7 @@ __global__ __launch_bounds__(WAVE) void k_fin_heavy(const uint64_t *__restrict__
             uf[r] = (U)vv;
           }
         }
-        __syncthreads();   // this v's links before the next v's finds
+        lds_barrier();   // this v's links before the next v's finds
         p += __popcll(mask);   // v's entries are a prefix of the window (sorted by hi)
       }
     }

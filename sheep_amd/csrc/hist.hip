@@ -90,7 +90,7 @@ __global__ __launch_bounds__(CB) void k_hist_count(Src src, uint64_t n, uint32_t
                                                    uint64_t ntiles) {
   extern __shared__ uint32_t lds[];
   for (uint32_t b = threadIdx.x; b < nb; b += CB) lds[b] = 0;
-  __syncthreads();
+  lds_barrier();
   const uint32_t tile = xcd_tile();
   const uint64_t base = (uint64_t)tile << TLOG;
   for (uint32_t step = 0; step < TKEYS; step += CB * CPT) {
@@ -104,7 +104,7 @@ __global__ __launch_bounds__(CB) void k_hist_count(Src src, uint64_t n, uint32_t
     for (int j = 0; j < CPT; ++j)
       if (k[j] != NO_KEY) atomicAdd(&lds[k[j] >> WBITS], 1u);
   }
-  __syncthreads();
+  lds_barrier();
   for (uint32_t b = threadIdx.x; b < nb; b += CB) tile_hist[(uint64_t)b * ntiles + tile] = lds[b];
 }
 
@@ -126,7 +126,7 @@ __device__ uint32_t lds_exclusive_scan(uint32_t *a, uint32_t nb, uint32_t *wsum)
     if (lane >= o) inc += u;
   }
   if (lane == 63) wsum[wave] = inc;
-  __syncthreads();
+  lds_barrier();
   uint32_t off = 0, tot = 0;
   for (int w = 0; w < HB / WAVE; ++w) {
     const uint32_t x = wsum[w];
@@ -137,23 +137,25 @@ __device__ uint32_t lds_exclusive_scan(uint32_t *a, uint32_t nb, uint32_t *wsum)
 #pragma unroll
   for (int q = 0; q < 8; ++q)
     if (q < (int)per && b0 + q < nb) { a[b0 + q] = run; run += v[q]; }
-  __syncthreads();
+  lds_barrier();
   return tot;
 }
 
 // Tile keys are held in registers (one source read); counting sort of (bucket, local)
 // in LDS; runs written with consecutive lanes.  stage[] carries bucket << 16 | local.
+// gb[b] = the bucket's output position for this tile minus its local start, read from the
+// scanned offsets once per bucket (not once per written key).
 template <typename Src>
 __global__ __launch_bounds__(HB) void k_hist_scatter(Src src, uint64_t n, uint32_t nb,
                                                      const uint32_t *__restrict__ offsets, uint64_t ntiles,
                                                      uint16_t *__restrict__ out) {
   extern __shared__ uint32_t lds[];
   uint32_t *cur = lds;              // nb: counts -> starts -> running cursors
-  uint32_t *start = lds + nb;       // nb: bucket starts inside the staged tile
+  uint32_t *gb = lds + nb;          // nb: output base of each bucket's run (global - local start)
   uint32_t *wsum = lds + 2 * nb;    // HB / WAVE
   uint32_t *stage = lds + 2 * nb + HB / WAVE;
   for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
-  __syncthreads();
+  lds_barrier();
   const uint32_t tile = xcd_tile();
   const uint64_t base = (uint64_t)tile << TLOG;
   uint32_t k[KPT];
@@ -165,20 +167,20 @@ __global__ __launch_bounds__(HB) void k_hist_scatter(Src src, uint64_t n, uint32
 #pragma unroll
   for (int j = 0; j < KPT; ++j)
     if (k[j] != NO_KEY) atomicAdd(&cur[k[j] >> WBITS], 1u);
-  __syncthreads();
+  lds_barrier();
   const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
-  for (uint32_t b = threadIdx.x; b < nb; b += HB) start[b] = cur[b];
-  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] = offsets[(uint64_t)b * ntiles + tile] - cur[b];
+  lds_barrier();
 #pragma unroll
   for (int j = 0; j < KPT; ++j)
     if (k[j] != NO_KEY) {
       const uint32_t b = k[j] >> WBITS;
       stage[atomicAdd(&cur[b], 1u)] = (b << 16) | (k[j] & (W - 1));
     }
-  __syncthreads();
+  lds_barrier();
   for (uint32_t j = threadIdx.x; j < total; j += HB) {
-    const uint32_t x = stage[j], b = x >> 16;
-    out[offsets[(uint64_t)b * ntiles + tile] + (j - start[b])] = (uint16_t)(x & 0xFFFF);
+    const uint32_t x = stage[j];
+    out[gb[x >> 16] + j] = (uint16_t)(x & 0xFFFF);
   }
 }
 
@@ -199,7 +201,7 @@ __global__ __launch_bounds__(HB) void k_hist_scatter_staged(Src src, uint64_t n,
   const uint64_t base = tile << TLOG;
   for (uint32_t s0 = 0; s0 < TKEYS; s0 += SUB) {
     for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
-    __syncthreads();
+    lds_barrier();
     uint32_t k[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
@@ -209,21 +211,21 @@ __global__ __launch_bounds__(HB) void k_hist_scatter_staged(Src src, uint64_t n,
 #pragma unroll
     for (int j = 0; j < PER; ++j)
       if (k[j] != NO_KEY) atomicAdd(&cur[k[j] >> WBITS], 1u);
-    __syncthreads();
+    lds_barrier();
     const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
     for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] -= cur[b];
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int j = 0; j < PER; ++j)
       if (k[j] != NO_KEY) stage[atomicAdd(&cur[k[j] >> WBITS], 1u)] = k[j];
-    __syncthreads();
+    lds_barrier();
     for (uint32_t j = threadIdx.x; j < total; j += HB) {
       const uint32_t key = stage[j];
       out[gb[key >> WBITS] + j] = (uint16_t)(key & (W - 1));
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += cur[b];
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -246,7 +248,7 @@ __global__ __launch_bounds__(HB) void k_lo_scatter_staged(EdgeLoPadded src, uint
   const uint64_t base = tile << TLOG;
   for (uint32_t s0 = 0; s0 < TKEYS; s0 += SUB) {
     for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
-    __syncthreads();
+    lds_barrier();
     uint64_t e[PER];
     uint32_t k[PER];
 #pragma unroll
@@ -259,23 +261,23 @@ __global__ __launch_bounds__(HB) void k_lo_scatter_staged(EdgeLoPadded src, uint
       k[j] = src.key(e[j]);
       if (k[j] != NO_KEY) atomicAdd(&cur[k[j] >> WBITS], 1u);
     }
-    __syncthreads();
+    lds_barrier();
     const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
     for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] -= cur[b];
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int j = 0; j < PER; ++j)
       if (k[j] != NO_KEY) stage[atomicAdd(&cur[k[j] >> WBITS], 1u)] = e[j];
-    __syncthreads();
+    lds_barrier();
     for (uint32_t j = threadIdx.x; j < total; j += HB) {
       const uint64_t v = stage[j];
       const uint32_t key = src.key(v), dst = gb[key >> WBITS] + j;
       grouped[dst] = v;
       out[dst] = (uint16_t)(key & (W - 1));
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += cur[b];
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -296,7 +298,7 @@ __global__ __launch_bounds__(HB) void k_hist_final(const uint16_t *__restrict__ 
   extern __shared__ uint32_t lds[];
   const Chunk ch = chunks[blockIdx.x];
   for (uint32_t i = threadIdx.x; i < W; i += HB) lds[i] = 0;
-  __syncthreads();
+  lds_barrier();
   for (uint64_t i0 = ch.beg; i0 < ch.end; i0 += 8 * HB) {
     uint32_t k[8];
 #pragma unroll
@@ -308,7 +310,7 @@ __global__ __launch_bounds__(HB) void k_hist_final(const uint16_t *__restrict__ 
     for (int j = 0; j < 8; ++j)
       if (k[j] != NO_KEY) atomicAdd(&lds[k[j]], 1u);
   }
-  __syncthreads();
+  lds_barrier();
   // counter index of the bucket's first key (padded keys: the range's own lo offset)
   const uint64_t k0 = kbase ? kbase[ch.bucket] : (uint64_t)ch.bucket << WBITS;
   for (uint32_t i = threadIdx.x; i < W; i += HB) {
@@ -432,7 +434,7 @@ __global__ __launch_bounds__(CB) void k_degree_fused(const sheep_xs1 *__restrict
                                                      unsigned long long *__restrict__ d_err) {
   extern __shared__ uint32_t lds[];
   for (uint32_t b = threadIdx.x; b < nb; b += CB) lds[b] = 0;
-  __syncthreads();
+  lds_barrier();
   const uint32_t tile = xcd_tile();
   const uint64_t base = (uint64_t)tile << TLOG;
   uint32_t lmax = 0;
@@ -465,7 +467,7 @@ __global__ __launch_bounds__(CB) void k_degree_fused(const sheep_xs1 *__restrict
       if (kh != INVALID) atomicAdd(&lds[kh >> WBITS], 1u);
     }
   }
-  __syncthreads();
+  lds_barrier();
   for (uint32_t b = threadIdx.x; b < nb; b += CB) tile_hist[(uint64_t)b * ntiles + tile] = lds[b];
   block_atomic_max(d_max, lmax);
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(d_err, 1ull);
@@ -519,7 +521,7 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
   const uint64_t base = tile << TLOG;
   for (uint32_t s0 = 0; s0 < TKEYS; s0 += SUB) {
     for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
-    __syncthreads();
+    lds_barrier();
     uint64_t x[PER];
     uint32_t pt[PER], hd[PER];
 #pragma unroll
@@ -545,23 +547,23 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
       x[j] = ((uint64_t)ptm << 32) | h;
       atomicAdd(&cur[h >> WBITS], 1u);
     }
-    __syncthreads();
+    lds_barrier();
     const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
     for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] -= cur[b];   // region cursor - local start
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int j = 0; j < PER; ++j)
       if (x[j] != NO_PAIR) stage[atomicAdd(&cur[(uint32_t)x[j] >> WBITS], 1u)] = x[j];
-    __syncthreads();
+    lds_barrier();
     for (uint32_t j = threadIdx.x; j < total; j += HB) {
       const uint64_t v = stage[j];
       const uint32_t b = (uint32_t)v >> WBITS, dst = gb[b] + j;
       if (dst < end[b]) out[dst] = v;
       else lost = true;
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += cur[b];   // past this sub-tile's run
-    __syncthreads();
+    lds_barrier();
   }
   for (uint32_t b = threadIdx.x; b < nb; b += HB)
     if (gb[b] != end[b]) lost = true;
@@ -593,7 +595,7 @@ __global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restric
     const uint64_t s1 = t1 < ch.end ? t1 : ch.end;
     if (COUNT)
       for (uint32_t b = threadIdx.x; b < lnb; b += HB) lcnt[b] = 0;
-    __syncthreads();
+    lds_barrier();
     for (uint64_t i0 = t0; i0 < s1; i0 += 8 * HB) {
       uint64_t x[8];
 #pragma unroll
@@ -619,11 +621,11 @@ __global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restric
       }
     }
     if (COUNT) {
-      __syncthreads();
+      lds_barrier();
       const uint64_t tile = t0 >> TLOG;
       for (uint32_t b = threadIdx.x; b < lnb; b += HB)
         if (lcnt[b]) atomicAdd(&tile_hist[(uint64_t)b * ntiles + tile], lcnt[b]);
-      __syncthreads();   // lcnt is cleared for the next tile
+      lds_barrier();   // lcnt is cleared for the next tile
     }
     t0 = s1;
   }

@@ -31,7 +31,7 @@ __global__ __launch_bounds__(BLOCK) void k_hist(const K *__restrict__ keys, uint
                                                 uint32_t ntiles, uint32_t *__restrict__ hist) {
   __shared__ uint32_t h[RADIX];
   h[threadIdx.x] = 0;
-  __syncthreads();
+  lds_barrier();
   uint64_t base = (uint64_t)blockIdx.x * R_TILE;
   for (int j = 0; j < R_ITEMS; ++j) {
     uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
@@ -40,7 +40,7 @@ __global__ __launch_bounds__(BLOCK) void k_hist(const K *__restrict__ keys, uint
     uint64_t peers = digit_peers(valid, d);
     if (valid && (peers & lanemask_lt()) == 0) atomicAdd(&h[d], (uint32_t)__popcll(peers));
   }
-  __syncthreads();
+  lds_barrier();
   hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const K *__restrict__ kin, co
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   run[t] = 0;
   for (int w = 0; w < BLOCK / WAVE; ++w) wcnt[w][t] = 0;
-  __syncthreads();
+  lds_barrier();
 
   const uint64_t base = (uint64_t)blockIdx.x * R_TILE;
   K key[R_ITEMS];
@@ -74,17 +74,17 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const K *__restrict__ kin, co
     uint64_t peers = digit_peers(valid, d);
     uint32_t lrank = (uint32_t)__popcll(peers & lanemask_lt());
     if (valid && lrank == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
-    __syncthreads();
+    lds_barrier();
     if (valid) {
       uint32_t before = run[d];
       for (int w = 0; w < wave; ++w) before += wcnt[w][d];
       rank[j] = before + lrank;
     }
-    __syncthreads();
+    lds_barrier();
     uint32_t add = 0;
     for (int w = 0; w < BLOCK / WAVE; ++w) { add += wcnt[w][t]; wcnt[w][t] = 0; }
     run[t] += add;
-    __syncthreads();
+    lds_barrier();
   }
   // tile-local digit starts (exclusive scan of run[] over the 256 digits)
   uint32_t v = run[t], inc = v;
@@ -93,11 +93,11 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const K *__restrict__ kin, co
     if (lane >= o) inc += u;
   }
   if (lane == 63) wtot[wave] = inc;
-  __syncthreads();
+  lds_barrier();
   uint32_t woff = 0;
   for (int w = 0; w < wave; ++w) woff += wtot[w];
   dstart[t] = woff + inc - v;
-  __syncthreads();
+  lds_barrier();
   for (int j = 0; j < R_ITEMS; ++j) {
     uint64_t i = base + (uint64_t)j * BLOCK + t;
     if (i < n) {
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const K *__restrict__ kin, co
       if (VALS) svals[lp] = val[j];
     }
   }
-  __syncthreads();
+  lds_barrier();
   uint32_t cnt = (uint32_t)((n - base) < (uint64_t)R_TILE ? (n - base) : (uint64_t)R_TILE);
   for (uint32_t idx = t; idx < cnt; idx += BLOCK) {
     K k = skeys[idx];

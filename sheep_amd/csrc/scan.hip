@@ -18,7 +18,7 @@ template <typename T> __device__ __forceinline__ T block_exclusive_scan(T v, T *
     if (lane >= o) inc += u;
   }
   if (lane == 63) lds_wave[wave] = inc;
-  __syncthreads();
+  lds_barrier();
   T wave_off = 0, tot = 0;
 #pragma unroll
   for (int w = 0; w < BLOCK / WAVE; ++w) {
@@ -42,7 +42,7 @@ __global__ __launch_bounds__(BLOCK) void k_reduce(const T *__restrict__ in, uint
   }
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = s;
-  __syncthreads();
+  lds_barrier();
   if (threadIdx.x == 0) {
     T t = 0;
     for (int w = 0; w < BLOCK / WAVE; ++w) t += lds[w];
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(BLOCK) void k_apply(const T *__restrict__ in, T *__
     uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
     tile[j * BLOCK + threadIdx.x] = i < n ? in[i] : T(0);
   }
-  __syncthreads();
+  lds_barrier();
   T local[SCAN_ITEMS];
   T s = 0;
 #pragma unroll
@@ -70,10 +70,10 @@ __global__ __launch_bounds__(BLOCK) void k_apply(const T *__restrict__ in, T *__
   T ex = block_exclusive_scan(s, lds_wave, block_total);
   T off = block_off ? block_off[blockIdx.x] : T(0);
   ex += off;
-  __syncthreads();
+  lds_barrier();
 #pragma unroll
   for (int j = 0; j < SCAN_ITEMS; ++j) { tile[threadIdx.x * SCAN_ITEMS + j] = ex; ex += local[j]; }
-  __syncthreads();
+  lds_barrier();
 #pragma unroll
   for (int j = 0; j < SCAN_ITEMS; ++j) {
     uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
