@@ -356,9 +356,10 @@ void lo_group_prepare(Ctx &c, uint64_t n, int L, uint32_t clo, LoGroup &g);
 // UINT64_MAX when the key range / record count does not fit the bucket layout.  With lg,
 // the gather also writes the edges' (padded-lo bucket, tile) counts for the grouping
 // (*counted = true), so group_edges_by_lo skips its count pass.
+// n_tree = the sequence's length (pst entries).
 uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
-                          uint32_t *pst, uint64_t *edges, unsigned long long *err, const LoGroup *lg = nullptr,
-                          bool *counted = nullptr);
+                          uint64_t n_tree, uint32_t *pst, uint64_t *edges, unsigned long long *err,
+                          const LoGroup *lg = nullptr, bool *counted = nullptr);
 void histogram_edge_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t K, uint32_t *cnt);
 void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGroup &g, uint32_t *pst, uint64_t *r0,
                        uint64_t *seg, bool counted);

@@ -1118,7 +1118,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
     TimedRegion tr(c, "relabel", 20 * nrec);   // record + 2 pos gathers
     // head-bucketed relabel (hist.hip) when the key range fits its LDS buckets; it also
     // counts the edges for the grouping below
-    m = relabel_bucketed(c, rec, nrec, pos, pos_size, pst, edges, d + 1, n >= 2 ? &lg : nullptr, &counted);
+    m = relabel_bucketed(c, rec, nrec, pos, pos_size, n, pst, edges, d + 1, n >= 2 ? &lg : nullptr, &counted);
     if (m == UINT64_MAX) {
       m = nrec;
       hipLaunchKernelGGL(k_relabel, dim3(grid_tiles(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos, pos_size, pst,

@@ -583,7 +583,8 @@ __global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restric
                                                        const uint32_t *__restrict__ pos, uint64_t pos_size,
                                                        uint32_t *__restrict__ pst, uint64_t *__restrict__ edges,
                                                        unsigned long long *__restrict__ flags, EdgeLoPadded lk,
-                                                       uint32_t lnb, uint32_t *__restrict__ tile_hist, uint64_t ntiles) {
+                                                       uint32_t lnb, uint32_t *__restrict__ tile_hist, uint64_t ntiles,
+                                                       uint64_t n_tree) {
   extern __shared__ uint32_t lds[];
   uint32_t *const lcnt = lds + W;
   const Chunk ch = chunks[blockIdx.x];
@@ -609,11 +610,13 @@ __global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restric
         if (i >= s1) continue;
         const uint32_t ptm = (uint32_t)(x[j] >> 32), ph = lds[(uint32_t)x[j] & (W - 1)];
         uint64_t e = ~0ull;   // DEAD
+        // (ptm is a position < n_tree, INVALID or PT_OOR; anything else is a stale region
+        // of a run the host discards, kept in bounds)
         if (ph != INVALID) {
           if (ptm == PT_OOR) bad = true;                       // index.at(tail) throws
-          else if (ptm != INVALID) e = ptm < ph ? ((uint64_t)ph << 32) | ptm : ((uint64_t)ptm << 32) | ph;
-          else atomicAdd(&pst[ph], 1u);
-        } else if (ptm < PT_OOR) {
+          else if (ptm < n_tree) e = ptm < ph ? ((uint64_t)ph << 32) | ptm : ((uint64_t)ptm << 32) | ph;
+          else if (ptm == INVALID) atomicAdd(&pst[ph], 1u);
+        } else if (ptm < n_tree) {
           atomicAdd(&pst[ptm], 1u);
         }
         edges[i] = e;
@@ -675,7 +678,8 @@ void histogram_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama,
 }
 
 uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
-                          uint32_t *pst, uint64_t *edges, unsigned long long *err, const LoGroup *lg, bool *counted) {
+                          uint64_t n_tree, uint32_t *pst, uint64_t *edges, unsigned long long *err, const LoGroup *lg,
+                          bool *counted) {
   if (counted) *counted = false;
   const uint64_t nb = (pos_size + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
   if (nrec == 0 || nb == 0 || nb > 8192 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return UINT64_MAX;
@@ -723,53 +727,62 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
     LAUNCH_CHECK();
     HIP_CHECK(hipMemcpyAsync(c.h_scalars + 12, flags, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   };
-  // chunk list of pass B from the bucket starts (host), built while pass A runs
-  std::vector<Chunk> chunks;
-  auto make_chunks = [&]() {
-    chunks.clear();
+  // Pass B is launched right behind pass A on the layout's chunk list (pinned host memory,
+  // built from the bucket starts), and ONE sync then checks pass A's flags: a stale layout
+  // (the same record buffer refilled) is recounted and both passes run again; the first
+  // run's writes stay in bounds (the gather checks every tail position against n) and its
+  // pst / error counts are cleared.
+  const uint64_t ntiles_e_max = (total + TKEYS - 1) >> TLOG;
+  auto gather = [&]() -> bool {
+    const uint64_t m = hl.bstart[nb];
+    uint64_t nch = 0;
+    for (uint32_t b = 0; b < nb; ++b) nch += (hl.bstart[b + 1] - hl.bstart[b] + CHUNK - 1) / CHUNK;
+    // the grouping's count pass fused in when its bucket counters fit beside the pos slice
+    const uint64_t ntiles_e = (m + TKEYS - 1) >> TLOG;
+    const bool count = lg && m && lg->nb && ((size_t)W + lg->nb) * 4 <= 160 * 1024 &&
+                       ntiles_e * lg->nb + 1 < (1ull << 32) && m < (1ull << 32);
+    uint32_t *tile_hist = nullptr;
+    if (count) {
+      tile_hist = c.get_as<uint32_t>("hist_tiles", std::max(ntiles_e, ntiles_e_max) * lg->nb + 1);
+      HIP_CHECK(hipMemsetAsync(tile_hist, 0, ntiles_e * lg->nb * sizeof(uint32_t), c.stream));
+    }
+    if (!nch) return count;
+    Chunk *hch = (Chunk *)c.get_pinned("rl_chunks_host", nch * sizeof(Chunk));
+    uint64_t j = 0;
     for (uint32_t b = 0; b < nb; ++b) {
       const uint64_t beg = hl.bstart[b], end = hl.bstart[b + 1];
-      for (uint64_t x = beg; x < end; x += CHUNK) chunks.push_back({x, x + CHUNK < end ? x + CHUNK : end, b, 0});
+      for (uint64_t x = beg; x < end; x += CHUNK) hch[j++] = {x, x + CHUNK < end ? x + CHUNK : end, b, 0};
     }
+    Chunk *dch = c.get_as<Chunk>("rl_chunks", nch);
+    HIP_CHECK(hipMemcpyAsync(dch, hch, nch * sizeof(Chunk), hipMemcpyHostToDevice, c.stream));
+    const EdgeLoPadded lk{edges, lg ? lg->d_pad : nullptr, lg ? lg->clo : 0, lg ? lg->mask : 0};
+    if (count)
+      hipLaunchKernelGGL(k_relabel_gather<true>, dim3((unsigned)nch), dim3(HB), (W + lg->nb) * 4, c.stream,
+                         (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err, lk, lg->nb,
+                         tile_hist, ntiles_e, n_tree);
+    else
+      hipLaunchKernelGGL(k_relabel_gather<false>, dim3((unsigned)nch), dim3(HB), W * 4, c.stream,
+                         (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err, lk, 0u,
+                         (uint32_t *)nullptr, (uint64_t)0, n_tree);
+    LAUNCH_CHECK();
+    return count;
   };
   scatter();
-  make_chunks();
+  bool count = gather();
   c.sync();
-  if (c.h_scalars[13]) {   // offsets did not match these records: recount, scatter again
+  if (c.h_scalars[13]) {   // offsets did not match these records: recount, run both passes again
     if (!cached) throw Error(SHEEP_ERR_HIP, "relabel: bucket layout inconsistent with its own count");
+    HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned long long), c.stream));
+    if (n_tree) HIP_CHECK(hipMemsetAsync(pst, 0, n_tree * sizeof(uint32_t), c.stream));
     off = recount();
     if (hl.bstart[nb] > total) pairs = c.get_as<uint64_t>("rl_pairs", hl.bstart[nb]);
     scatter();
-    make_chunks();
+    count = gather();
     c.sync();
     if (c.h_scalars[13]) throw Error(SHEEP_ERR_HIP, "relabel: bucket layout inconsistent with its own count");
   }
   const uint64_t m = hl.bstart[nb];
   if (c.h_scalars[12]) HIP_CHECK(hipMemsetAsync(err, 0xFF, 1, c.stream));   // range error (reported by the caller)
-  // the grouping's count pass fused in when its bucket counters fit beside the pos slice
-  const uint64_t ntiles_e = (m + TKEYS - 1) >> TLOG;
-  const bool count = lg && m && lg->nb && ((size_t)W + lg->nb) * 4 <= 160 * 1024 && ntiles_e * lg->nb + 1 < (1ull << 32) &&
-                     m < (1ull << 32);
-  uint32_t *tile_hist = nullptr;
-  if (count) {
-    tile_hist = c.get_as<uint32_t>("hist_tiles", ntiles_e * lg->nb + 1);
-    HIP_CHECK(hipMemsetAsync(tile_hist, 0, ntiles_e * lg->nb * sizeof(uint32_t), c.stream));
-  }
-  if (!chunks.empty()) {
-    Chunk *dch = c.get_as<Chunk>("rl_chunks", chunks.size());
-    HIP_CHECK(hipMemcpyAsync(dch, chunks.data(), chunks.size() * sizeof(Chunk), hipMemcpyHostToDevice, c.stream));
-    const EdgeLoPadded lk{edges, lg ? lg->d_pad : nullptr, lg ? lg->clo : 0, lg ? lg->mask : 0};
-    if (count)
-      hipLaunchKernelGGL(k_relabel_gather<true>, dim3((unsigned)chunks.size()), dim3(HB), (W + lg->nb) * 4, c.stream,
-                         (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err, lk, lg->nb,
-                         tile_hist, ntiles_e);
-    else
-      hipLaunchKernelGGL(k_relabel_gather<false>, dim3((unsigned)chunks.size()), dim3(HB), W * 4, c.stream,
-                         (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err, lk, 0u,
-                         (uint32_t *)nullptr, (uint64_t)0);
-    LAUNCH_CHECK();
-    c.sync();   // `chunks` is a pageable host buffer
-  }
   if (counted) *counted = count;
   return m;
 }
