@@ -72,6 +72,9 @@ struct Ctx {
   // it sees the same records and key range (and verifies every region's count in-kernel).
   struct HeadLayout { const void *rec = nullptr; uint64_t nrec = 0, K = 0; std::vector<uint32_t> bstart; bool valid = false; };
   HeadLayout head_layout;
+  // the degree pass's sortedness probe of the last record buffer (sequence.hip)
+  struct SortedProbe { const void *rec = nullptr; uint64_t nrec = 0; bool sorted = true; };
+  SortedProbe sorted_probe;
 
   bool timing = false;
   struct Timer { std::vector<std::pair<hipEvent_t, hipEvent_t>> pending; double ms = 0; uint64_t launches = 0; uint64_t bytes = 0; };

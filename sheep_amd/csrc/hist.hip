@@ -393,31 +393,36 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
                        nb, (const uint32_t *)tile_hist, ntiles, keys);
   }
   LAUNCH_CHECK();
-  // bucket starts (column 0 of the bucket-major offsets) -> chunk list
-  std::vector<uint32_t> bstart(nb + 1);
-  HIP_CHECK(hipMemcpy2DAsync(bstart.data(), sizeof(uint32_t), tile_hist, ntiles * sizeof(uint32_t), sizeof(uint32_t),
+  // bucket starts (column 0 of the bucket-major offsets) -> chunk list.  Host buffers are
+  // pinned, so the chunk list's copy needs no sync of its own (the next call's first sync
+  // comes before it rewrites them).
+  uint32_t *bstart = (uint32_t *)c.get_pinned("hist_bstart_host", (nb + 1) * sizeof(uint32_t));
+  HIP_CHECK(hipMemcpy2DAsync(bstart, sizeof(uint32_t), tile_hist, ntiles * sizeof(uint32_t), sizeof(uint32_t),
                              nb, hipMemcpyDeviceToHost, c.stream));
   HIP_CHECK(hipMemcpyAsync(&bstart[nb], total, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
-  if (save_bstart) *save_bstart = bstart;
-  if (bstart_out) HIP_CHECK(hipMemcpyAsync(bstart_out, bstart.data(), (nb + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
-  std::vector<Chunk> chunks;
+  if (save_bstart) save_bstart->assign(bstart, bstart + nb + 1);
+  uint64_t nch = 0;
+  for (uint32_t b = 0; b < nb; ++b) nch += (bstart[b + 1] - bstart[b] + CHUNK - 1) / CHUNK;
+  if (bstart_out) {
+    uint32_t *bs = (uint32_t *)c.get_pinned("hist_bstart_copy", (nb + 1) * sizeof(uint32_t));
+    std::copy(bstart, bstart + nb + 1, bs);
+    HIP_CHECK(hipMemcpyAsync(bstart_out, bs, (nb + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
+  }
+  if (!nch) return;
+  Chunk *chunks = (Chunk *)c.get_pinned("hist_chunks_host", nch * sizeof(Chunk));
+  uint64_t j = 0;
   for (uint32_t b = 0; b < nb; ++b) {
     const uint64_t beg = bstart[b], end = bstart[b + 1];
     if (beg == end) continue;
     const uint32_t shared = end - beg > CHUNK;
-    for (uint64_t x = beg; x < end; x += CHUNK) chunks.push_back({x, x + CHUNK < end ? x + CHUNK : end, b, shared});
+    for (uint64_t x = beg; x < end; x += CHUNK) chunks[j++] = {x, x + CHUNK < end ? x + CHUNK : end, b, shared};
   }
-  if (chunks.empty()) {
-    c.sync();   // bstart is a pageable host buffer
-    return;
-  }
-  Chunk *dch = c.get_as<Chunk>("hist_chunks", chunks.size());
-  HIP_CHECK(hipMemcpyAsync(dch, chunks.data(), chunks.size() * sizeof(Chunk), hipMemcpyHostToDevice, c.stream));
-  hipLaunchKernelGGL(k_hist_final, dim3((unsigned)chunks.size()), dim3(HB), W * 4, c.stream, (const uint16_t *)keys,
+  Chunk *dch = c.get_as<Chunk>("hist_chunks", nch);
+  HIP_CHECK(hipMemcpyAsync(dch, chunks, nch * sizeof(Chunk), hipMemcpyHostToDevice, c.stream));
+  hipLaunchKernelGGL(k_hist_final, dim3((unsigned)nch), dim3(HB), W * 4, c.stream, (const uint16_t *)keys,
                      (const Chunk *)dch, K, kbase, cnt);
   LAUNCH_CHECK();
-  c.sync();   // `chunks` is a pageable host buffer
 }
 
 
@@ -839,14 +844,14 @@ void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGroup 
   HIP_CHECK(hipMemsetAsync(d_bstart, 0, (g.nb + 1) * sizeof(uint32_t), c.stream));
   histogram_add(c, EdgeLoPadded{edges, g.d_pad, g.clo, g.mask}, m, g.K, pst, r0, g.d_kbase, d_bstart, nullptr, nullptr,
                 counted);
-  std::vector<uint64_t> hseg(2 * (size_t)L);
+  // (pinned: no sync for the copy; histogram_add's sync above ordered any earlier use)
+  uint64_t *hseg = (uint64_t *)c.get_pinned("grp_segb_host", 2 * (size_t)L * sizeof(uint64_t));
   for (int s = 0; s < L; ++s) { hseg[s] = g.pstart[s] / W; hseg[L + s] = (g.pstart[s] + g.plen[s]) / W; }
   uint64_t *d_sb = c.get_as<uint64_t>("grp_segb", 2 * (size_t)L);
-  HIP_CHECK(hipMemcpyAsync(d_sb, hseg.data(), 2 * (size_t)L * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+  HIP_CHECK(hipMemcpyAsync(d_sb, hseg, 2 * (size_t)L * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
   hipLaunchKernelGGL(k_seg_from_buckets, dim3(1), dim3(64), 0, c.stream, (const uint32_t *)d_bstart,
                      (const uint64_t *)d_sb, L, seg);
   LAUNCH_CHECK();
-  c.sync();   // the host vector above is pageable
 }
 
 }  // namespace sheep

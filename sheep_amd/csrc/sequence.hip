@@ -144,6 +144,9 @@ void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v) {
 static bool tails_sorted(Ctx &c, const sheep_xs1 *rec, uint64_t nrec) {
   constexpr uint64_t SAMPLES = 1 << 16;
   if (nrec < 2 * SAMPLES) return true;   // small inputs: the atomics cost nothing
+  // the answer is kept per record buffer: either path counts correctly, so a buffer
+  // refilled in another order only costs speed, and a repeated call skips the probe's sync
+  if (c.sorted_probe.rec == rec && c.sorted_probe.nrec == nrec) return c.sorted_probe.sorted;
   unsigned long long *d = (unsigned long long *)c.d_scalars + 2;
   HIP_CHECK(hipMemsetAsync(d, 0, sizeof(uint64_t), c.stream));
   hipLaunchKernelGGL(k_tail_descents, dim3((unsigned)(SAMPLES / BLOCK)), dim3(BLOCK), 0, c.stream, rec, nrec,
@@ -151,7 +154,8 @@ static bool tails_sorted(Ctx &c, const sheep_xs1 *rec, uint64_t nrec) {
   LAUNCH_CHECK();
   HIP_CHECK(hipMemcpyAsync(c.h_scalars + 2, d, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
-  return c.h_scalars[2] * 50 < SAMPLES;   // fewer than 2% descents
+  c.sorted_probe = {rec, nrec, c.h_scalars[2] * 50 < SAMPLES};   // fewer than 2% descents
+  return c.sorted_probe.sorted;
 }
 
 void degree_count(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap,
