@@ -328,6 +328,8 @@ void set_error(const char *msg);
 // scan.hip
 void scan_exclusive_u32(Ctx &c, const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total_dev);
 void scan_exclusive_u64(Ctx &c, const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *total_dev);
+// the first *n_dev (<= n_max) entries, the length read on the device (launch sized for n_max)
+void scan_exclusive_u64_dev(Ctx &c, const uint64_t *in, uint64_t *out, uint64_t n_max, const uint64_t *n_dev);
 // radix.hip — stable LSD sort of (key, value) pairs on bits [0, end_bit); results end
 // in (keys, vals); alt buffers are scratch of the same size.
 void radix_sort_pairs_u32(Ctx &c, uint32_t *keys, uint32_t *vals, uint64_t n, int end_bit,

@@ -195,7 +195,8 @@ __global__ __launch_bounds__(BLOCK) void k_relabel(const sheep_xs1 *__restrict__
 // [2] cross edges, [3] entries that stayed, [4] contractions that survived, [5..7]
 // unresolved light edges after hooking round 0..2, [10] edges activated from the
 // level's bucket.
-constexpr int ST_ROW = 16, ST_LIVE = 0, ST_NL = 1, ST_NX = 2, ST_KEPT = 3, ST_CONTR = 4, ST_HOOK = 5, ST_R0 = 10;
+constexpr int ST_ROW = 16, ST_LIVE = 0, ST_NL = 1, ST_NX = 2, ST_KEPT = 3, ST_CONTR = 4, ST_HOOK = 5, ST_R0 = 10,
+              ST_SCANN = 11;
 constexpr int HOOK_ROUNDS = 3;
 // counter sets zeroed at every level: hook rounds and the contractions (sharded appends)
 constexpr int CSET_HOOK = 0, CSET_APPLY = CSET_HOOK + HOOK_ROUNDS, NCSET = CSET_APPLY + 1;
@@ -523,12 +524,16 @@ __device__ __forceinline__ uint64_t pack3(uint32_t c) {
 __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
                                                        uint64_t *__restrict__ st, int s, uint32_t clo, YRange yr,
                                                        const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
-                                                       int L, uint64_t *__restrict__ cnt, uint64_t cstride) {
+                                                       int L, uint64_t *__restrict__ cnt) {
+  // the three count rows at stride ntiles (this level's), then one 0: scanned as one
+  // exclusive scan of 3 ntiles + 1 entries (the length in st, read by the scan)
   const SplitIn in(list, prev, r0, seg, s, L);
-  const uint64_t ntiles = (in.m + TILE - 1) / TILE;
+  const uint64_t ntiles = (in.m + TILE - 1) / TILE, cstride = ntiles;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st[ST_LIVE] = in.len;
     st[ST_R0] = in.m - in.len;
+    st[ST_SCANN] = 3 * ntiles + 1;
+    cnt[3 * ntiles] = 0;
   }
   __shared__ uint64_t s_w[BLOCK / WAVE];
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -550,18 +555,18 @@ __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restric
   }
 }
 
-// cnt: the three rows (stride cstride, zero-padded) scanned as ONE exclusive scan, so a
+// cnt: the three rows (stride ntiles, then a 0) scanned as ONE exclusive scan, so a
 // row's offsets are relative to its first entry; the row totals go to st.  Each class's
 // run of the tile is first placed in LDS at its thread-major rank, then copied out by
 // consecutive lanes (per-thread stores to the same positions: 16.6 against 12.2 ms).
 __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
                                                        uint64_t *__restrict__ st, int s, uint32_t clo, YRange yr,
                                                        const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
-                                                       int L, const uint64_t *__restrict__ cnt, uint64_t cstride,
+                                                       int L, const uint64_t *__restrict__ cnt,
                                                        uint64_t *__restrict__ next, uint64_t *__restrict__ lbuf,
                                                        uint64_t *__restrict__ xbuf) {
   const SplitIn in(list, prev, r0, seg, s, L);
-  const uint64_t ntiles = (in.m + TILE - 1) / TILE;
+  const uint64_t ntiles = (in.m + TILE - 1) / TILE, cstride = ntiles;
   const uint64_t b0 = cnt[0], b1 = cnt[cstride], b2 = cnt[2 * cstride], b3 = cnt[3 * cstride];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st[ST_KEPT] = b1 - b0;
@@ -959,13 +964,12 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     const YRange yr{ylo, yhi, lvl == filt_lvl};
     {
       TimedRegion tr(c, "etree_split");
-      HIP_CHECK(hipMemsetAsync(tcnt, 0, (3 * cstride + 1) * sizeof(uint64_t), c.stream));
       hipLaunchKernelGGL(k_split_count, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo, yr,
-                         (const uint64_t *)r0, (const uint64_t *)seg, L, tcnt, cstride);
+                         (const uint64_t *)r0, (const uint64_t *)seg, L, tcnt);
       LAUNCH_CHECK();
-      scan_exclusive_u64(c, tcnt, tcnt, 3 * cstride + 1, nullptr);
+      scan_exclusive_u64_dev(c, tcnt, tcnt, 3 * cstride + 1, st + ST_SCANN);
       hipLaunchKernelGGL(k_split_write, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo, yr,
-                         (const uint64_t *)r0, (const uint64_t *)seg, L, (const uint64_t *)tcnt, cstride, next, lbuf, xbuf);
+                         (const uint64_t *)r0, (const uint64_t *)seg, L, (const uint64_t *)tcnt, next, lbuf, xbuf);
       LAUNCH_CHECK();
     }
     {

@@ -30,9 +30,12 @@ template <typename T> __device__ __forceinline__ T block_exclusive_scan(T v, T *
   return wave_off + inc - v;
 }
 
+// n_dev (optional): the length is read on the device (at most n; the grid is sized for n)
 template <typename T>
-__global__ __launch_bounds__(BLOCK) void k_reduce(const T *__restrict__ in, uint64_t n, T *__restrict__ sums) {
+__global__ __launch_bounds__(BLOCK) void k_reduce(const T *__restrict__ in, uint64_t n, T *__restrict__ sums,
+                                                  const uint64_t *__restrict__ n_dev) {
   __shared__ T lds[BLOCK / WAVE];
+  if (n_dev && *n_dev < n) n = *n_dev;
   uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
   T s = 0;
 #pragma unroll
@@ -52,8 +55,10 @@ __global__ __launch_bounds__(BLOCK) void k_reduce(const T *__restrict__ in, uint
 
 template <typename T>
 __global__ __launch_bounds__(BLOCK) void k_apply(const T *__restrict__ in, T *__restrict__ out, uint64_t n,
-                                                 const T *__restrict__ block_off, T *__restrict__ total) {
+                                                 const T *__restrict__ block_off, T *__restrict__ total,
+                                                 const uint64_t *__restrict__ n_dev) {
   __shared__ T tile[SCAN_TILE];
+  if (n_dev && *n_dev < n) n = *n_dev;   // blocks past it see zeros; the last still writes the total
   __shared__ T lds_wave[BLOCK / WAVE];
   uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
 #pragma unroll
@@ -83,7 +88,7 @@ __global__ __launch_bounds__(BLOCK) void k_apply(const T *__restrict__ in, T *__
 }
 
 template <typename T>
-void scan_rec(Ctx &c, const T *in, T *out, uint64_t n, T *total_dev, int depth) {
+void scan_rec(Ctx &c, const T *in, T *out, uint64_t n, T *total_dev, int depth, const uint64_t *n_dev = nullptr) {
   if (n == 0) {
     if (total_dev) HIP_CHECK(hipMemsetAsync(total_dev, 0, sizeof(T), c.stream));
     return;
@@ -93,12 +98,12 @@ void scan_rec(Ctx &c, const T *in, T *out, uint64_t n, T *total_dev, int depth) 
   T *sums = nullptr;
   if (nb > 1) {
     sums = c.get_as<T>("scan_sums_" + std::to_string(depth) + (sizeof(T) == 8 ? "_64" : "_32"), nb);
-    hipLaunchKernelGGL(k_reduce<T>, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, in, n, sums);
+    hipLaunchKernelGGL(k_reduce<T>, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, in, n, sums, n_dev);
     LAUNCH_CHECK();
     scan_rec<T>(c, sums, sums, nb, nullptr, depth + 1);
   }
   hipLaunchKernelGGL(k_apply<T>, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, in, out, n,
-                     (const T *)sums, total_dev);
+                     (const T *)sums, total_dev, n_dev);
   LAUNCH_CHECK();
 }
 
@@ -109,6 +114,9 @@ void scan_exclusive_u32(Ctx &c, const uint32_t *in, uint32_t *out, uint64_t n, u
 }
 void scan_exclusive_u64(Ctx &c, const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *total_dev) {
   scan_rec<uint64_t>(c, in, out, n, total_dev, 0);
+}
+void scan_exclusive_u64_dev(Ctx &c, const uint64_t *in, uint64_t *out, uint64_t n_max, const uint64_t *n_dev) {
+  scan_rec<uint64_t>(c, in, out, n_max, nullptr, 0, n_dev);
 }
 
 }  // namespace sheep
