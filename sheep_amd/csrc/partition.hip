@@ -42,8 +42,7 @@ __global__ void k_weights(const sheep_jnode *__restrict__ tree, uint64_t n, int 
     w[i] = x;
     s += x;
   }
-  s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0 && s) atomicAdd(total, (unsigned long long)s);
+  block_atomic_add(total, s);
 }
 
 // tour-order value array for a sum channel: val[tU[c]] = up(c), val[tD[c]] = down(c)
@@ -192,14 +191,9 @@ __global__ void k_parts_to_vid(const uint32_t *__restrict__ seq, uint64_t seq_n,
     c1 += p == 1;
     mx = (uint64_t)(p + 1) > mx ? (uint64_t)(p + 1) : mx;
   }
-  c0 = wave_sum(c0);
-  c1 = wave_sum(c1);
-  mx = wave_max(mx);
-  if ((threadIdx.x & 63) == 0) {
-    if (c0) atomicAdd(&cnt[0], (unsigned long long)c0);
-    if (c1) atomicAdd(&cnt[1], (unsigned long long)c1);
-    if (mx) atomicMax(&cnt[2], (unsigned long long)mx);
-  }
+  block_atomic_add(&cnt[0], c0);
+  block_atomic_add(&cnt[1], c1);
+  block_atomic_max(&cnt[2], mx);
 }
 
 // ---- raking: exact subtree sums of the light fringe -------------------------------

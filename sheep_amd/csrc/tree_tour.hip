@@ -16,8 +16,7 @@ __global__ void k_max_u32(const uint32_t *__restrict__ x, uint64_t n, unsigned l
   uint32_t m = 0;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) m = x[i] > m ? x[i] : m;
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0 && m) atomicMax(out, (unsigned long long)m);
+  block_atomic_max(out, m);
 }
 
 __global__ void k_kid_keys(const sheep_jnode *__restrict__ tree, uint64_t n, uint32_t *__restrict__ keys,
@@ -57,19 +56,18 @@ __device__ __forceinline__ bool root_with_kids(const uint32_t *parent, const uin
   return parent[i] == INVALID && koff[i] < koff[i + 1];
 }
 __global__ void k_rk_count(const uint32_t *__restrict__ parent, const uint32_t *__restrict__ koff, uint64_t n,
-                           uint32_t *__restrict__ bcnt, unsigned long long *__restrict__ nroots) {
+                           uint32_t *__restrict__ bcnt) {
   __shared__ uint32_t s[BLOCK / WAVE];
   uint64_t base = (uint64_t)blockIdx.x * RK_TILE;
-  uint32_t c = 0, r = 0;
+  uint32_t c = 0;
   for (int j = 0; j < RK_ITEMS; ++j) {
     uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
-    if (i < n) { c += root_with_kids(parent, koff, i); r += parent[i] == INVALID; }
+    if (i < n) c += root_with_kids(parent, koff, i);
   }
   c = wave_sum(c);
   if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
   __syncthreads();
   if (threadIdx.x == 0) bcnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
-  block_atomic_add(nroots, r);
 }
 __global__ void k_rk_write(const uint32_t *__restrict__ parent, const uint32_t *__restrict__ koff, uint64_t n,
                            const uint32_t *__restrict__ boff, uint32_t *__restrict__ rk) {
@@ -266,7 +264,7 @@ void build_tour(Ctx &c, sheep_kids *k, Tour &t) {
   uint32_t *bcnt = c.get_as<uint32_t>("tour_bcnt", nb);
   unsigned long long *d = (unsigned long long *)c.d_scalars + 20;
   HIP_CHECK(hipMemsetAsync(d, 0, 4 * sizeof(uint64_t), c.stream));
-  hipLaunchKernelGGL(k_rk_count, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, k->parent, k->koff, n, bcnt, d);
+  hipLaunchKernelGGL(k_rk_count, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, k->parent, k->koff, n, bcnt);
   LAUNCH_CHECK();
   scan_exclusive_u32(c, bcnt, bcnt, nb, (uint32_t *)(d + 1));
   uint32_t *rk = c.get_as<uint32_t>("tour_rk", n);
@@ -274,7 +272,7 @@ void build_tour(Ctx &c, sheep_kids *k, Tour &t) {
   LAUNCH_CHECK();
   HIP_CHECK(hipMemcpyAsync(c.h_scalars + 20, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
-  t.nroots = c.h_scalars[20];
+  t.nroots = n - k->nkids;   // every non-root is one kid
   t.nrk = (uint32_t)c.h_scalars[21];
   t.rk = rk;
   t.A = 2 * (n - t.nroots);
