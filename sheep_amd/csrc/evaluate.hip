@@ -165,14 +165,9 @@ __global__ __launch_bounds__(BLOCK) void k_eval_records(const sheep_xs1 *__restr
       }
     }
   }
-  cut = wave_sum(cut);
-  bad = wave_sum(bad);
-  loops = wave_sum(loops);
-  if ((threadIdx.x & 63) == 0) {
-    if (cut) atomicAdd(&acc[AC_CUT], (unsigned long long)cut);
-    if (bad) atomicAdd(&acc[AC_BAD], (unsigned long long)bad);
-    if (loops) atomicAdd(&acc[AC_LOOPS], (unsigned long long)loops);
-  }
+  block_atomic_add(&acc[AC_CUT], cut);
+  block_atomic_add(&acc[AC_BAD], bad);
+  block_atomic_add(&acc[AC_LOOPS], loops);
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&acc[AC_RECS], (unsigned long long)nrec);
   __syncthreads();
   if (lds)
@@ -233,14 +228,8 @@ __global__ __launch_bounds__(BLOCK) void k_eval_nodes(uint64_t vs, const int16_t
     }
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) s[q] = wave_sum(s[q]);
-  nodes = wave_sum(nodes);
-  if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (s[q]) atomicAdd(&out[q], (unsigned long long)s[q]);
-    if (nodes) atomicAdd(&out[4], (unsigned long long)nodes);
-  }
+  for (int q = 0; q < 4; ++q) block_atomic_add(&out[q], s[q]);
+  block_atomic_add(&out[4], nodes);
   __syncthreads();
   if (lds)
     for (int x = threadIdx.x; x < nparts; x += BLOCK)
