@@ -197,7 +197,11 @@ __global__ __launch_bounds__(BLOCK) void k_relabel(const sheep_xs1 *__restrict__
 // level's bucket.
 constexpr int ST_ROW = 16, ST_LIVE = 0, ST_NL = 1, ST_NX = 2, ST_KEPT = 3, ST_CONTR = 4, ST_HOOK = 5, ST_R0 = 10,
               ST_SCANN = 11;
-constexpr int HOOK_ROUNDS = 3;
+// One deferred round, then the in-place finish (swept: 0 / 1 / 2 / 3 rounds = union 8.4 /
+// 6.3 / 6.6 / 6.7 ms at RMAT-26; 1 also best on the Chung-Lu graph, RMAT-28 and merges):
+// the first round clears the pile-up on a forming giant component's root, and what is
+// left is too little to pay for more launches and packs.
+constexpr int HOOK_ROUNDS = 1;
 // counter sets zeroed at every level: hook rounds and the contractions (sharded appends)
 constexpr int CSET_HOOK = 0, CSET_APPLY = CSET_HOOK + HOOK_ROUNDS, NCSET = CSET_APPLY + 1;
 constexpr uint64_t CSET_WORDS = (uint64_t)NSHARD * SHARD_STRIDE;
