@@ -3,10 +3,12 @@
 //
 // The trees are extremely tall (twitter vheight ~1e7), so nothing here is level
 // synchronous.  The tour is a linked list of 2(n - roots) arcs; it is ranked with a
-// sparse ruling set: ~1/64 of the arcs (hash-selected) walk to the next ruler
+// sparse ruling set: ~1/32 of the arcs (hash-selected) walk to the next ruler
 // (independent short pointer chases, all in flight at once), the ruler list is ranked
 // by pointer jumping, and every arc gets ruler prefix + local offset.  Subtree sums,
 // depths and path sums then become ordinary prefix sums over tour order.
+#include <cstdlib>
+
 #include "tree_tour.hpp"
 
 namespace sheep {
@@ -119,17 +121,17 @@ __global__ void k_head(const uint32_t *__restrict__ rk, const uint32_t *__restri
   if (threadIdx.x == 0) head[0] = kids[koff[rk[0]]];
 }
 
-__device__ __forceinline__ bool hash_ruler(uint32_t a) {
+__device__ __forceinline__ bool hash_ruler(uint32_t a, uint32_t mask) {
   uint32_t h = a * 0x9E3779B1u;
   h ^= h >> 15;
   h *= 0x85EBCA77u;
   h ^= h >> 13;
-  return (h & 63u) == 0;
+  return (h & mask) == 0;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_pick_rulers(const uint32_t *__restrict__ parent, uint64_t n, uint32_t head,
                                                        uint32_t *__restrict__ rid, uint32_t *__restrict__ rulers,
-                                                       uint64_t cap, unsigned long long *__restrict__ counter) {
+                                                       uint64_t cap, unsigned long long *__restrict__ counter, uint32_t rmask) {
   const uint64_t total = 2 * n;
   const uint64_t ntiles = (total + TILE - 1) / TILE;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -139,7 +141,7 @@ __global__ __launch_bounds__(BLOCK) void k_pick_rulers(const uint32_t *__restric
       const uint64_t a = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
       if (a < total) {
         const uint32_t node = (uint32_t)(a < n ? a : a - n);
-        if (parent[node] != INVALID && (a == head || hash_ruler((uint32_t)a))) flags |= 1u << j;
+        if (parent[node] != INVALID && (a == head || hash_ruler((uint32_t)a, rmask))) flags |= 1u << j;
       }
     }
     uint64_t slot = block_reserve((uint32_t)__popc(flags), counter);
@@ -158,17 +160,17 @@ __global__ __launch_bounds__(BLOCK) void k_pick_rulers(const uint32_t *__restric
 
 __global__ void k_walk(const uint32_t *__restrict__ rulers, uint64_t nr, const uint32_t *__restrict__ succ,
                        const uint32_t *__restrict__ rid, uint32_t *__restrict__ owner, uint32_t *__restrict__ loff,
-                       uint32_t *__restrict__ rlen, uint32_t *__restrict__ rnext) {
+                       uint32_t *__restrict__ rlen, uint32_t *__restrict__ rnext, uint32_t rmask, uint64_t arcs) {
   // launched with 64-thread workgroups (one wave: the walks are long dependent chains)
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nr; r += stride) {
     uint32_t cur = rulers[r], local = 0, nx;
-    const uint32_t cap = (uint32_t)(2 * (nr + 1) * 64 + 2);   // > any list length: guards a corrupt list
+    const uint32_t cap = (uint32_t)(arcs + 2);   // > any list length: guards a corrupt list
     while (local < cap) {
       owner[cur] = (uint32_t)r;
       loff[cur] = local++;
       nx = succ[cur];
-      if (nx == INVALID || hash_ruler(nx)) break;
+      if (nx == INVALID || hash_ruler(nx, rmask)) break;
       cur = nx;
     }
     rlen[r] = local;
@@ -300,11 +302,14 @@ void build_tour(Ctx &c, sheep_kids *k, Tour &t) {
   const uint32_t head = (uint32_t)c.h_scalars[24];
 
   uint32_t *rid = c.get_as<uint32_t>("tour_rid", 2 * n);
-  const uint64_t rcap = 2 * n / 16 + 1024;   // expected 2n/64 hash-picked rulers
+  // one arc in 32 is a ruler (1/32, 1/64, 1/128 measured 8.54 / 8.71 / 8.81 ms of partition
+  // at RMAT-26: shorter walks against more pointer-jumping work)
+  constexpr uint32_t rmask = 31u;
+  const uint64_t rcap = 2 * n * 4 / (rmask + 1) + 1024;   // expected 2n/(rmask + 1) hash-picked rulers
   uint32_t *rulers = c.get_as<uint32_t>("tour_rulers", rcap);
   HIP_CHECK(hipMemsetAsync(d + 2, 0, sizeof(uint64_t), c.stream));
   hipLaunchKernelGGL(k_pick_rulers, dim3(grid_tiles(2 * n)), dim3(BLOCK), 0, c.stream, k->parent, n, head, rid,
-                     rulers, rcap, d + 2);
+                     rulers, rcap, d + 2, rmask);
   LAUNCH_CHECK();
   HIP_CHECK(hipMemcpyAsync(c.h_scalars + 22, d + 2, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
@@ -316,7 +321,7 @@ void build_tour(Ctx &c, sheep_kids *k, Tour &t) {
   {
     TimedRegion tr(c, "tour_walk");
     hipLaunchKernelGGL(k_walk, dim3(grid_for(nr, 64)), dim3(64), 0, c.stream, rulers, nr, succ, rid, owner, loff, rlen,
-                       rnext);
+                       rnext, rmask, 2 * n);
     LAUNCH_CHECK();
   }
   uint32_t *sa = rlen, *na = rnext, *sb = rlen2, *nb2 = rnext2;
