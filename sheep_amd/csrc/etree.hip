@@ -520,6 +520,12 @@ struct SplitIn {
   }
 };
 
+// The split streams SPLIT_TILE-entry tiles (its own tiling: only its count rows depend on
+// it): 16 entries per thread measured 7.2 against 7.9 ms at RMAT-26 (the kernels whose
+// appends pack_shards moves stay at TILE, whose 16-item form slowed k_cross_apply).
+constexpr int SPLIT_ITEMS = 16;
+constexpr int SPLIT_TILE = BLOCK * SPLIT_ITEMS;
+
 // the three class bits as three 16-bit counters
 __device__ __forceinline__ uint64_t pack3(uint32_t c) {
   return (uint64_t)(c & 1) | ((uint64_t)((c >> 1) & 1) << 16) | ((uint64_t)(c >> 2) << 32);
@@ -532,7 +538,7 @@ __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restric
   // the three count rows at stride ntiles (this level's), then one 0: scanned as one
   // exclusive scan of 3 ntiles + 1 entries (the length in st, read by the scan)
   const SplitIn in(list, prev, r0, seg, s, L);
-  const uint64_t ntiles = (in.m + TILE - 1) / TILE, cstride = ntiles;
+  const uint64_t ntiles = (in.m + SPLIT_TILE - 1) / SPLIT_TILE, cstride = ntiles;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st[ST_LIVE] = in.len;
     st[ST_R0] = in.m - in.len;
@@ -541,12 +547,12 @@ __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restric
   }
   __shared__ uint64_t s_w[BLOCK / WAVE];
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    uint64_t ev[TILE_ITEMS];
+    uint64_t ev[SPLIT_ITEMS];
 #pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) ev[j] = in[tile * TILE + (uint64_t)j * BLOCK + threadIdx.x];
+    for (int j = 0; j < SPLIT_ITEMS; ++j) ev[j] = in[tile * SPLIT_TILE + (uint64_t)j * BLOCK + threadIdx.x];
     uint64_t c3 = 0;
 #pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) c3 += pack3(classify(ev[j], s, clo, yr));
+    for (int j = 0; j < SPLIT_ITEMS; ++j) c3 += pack3(classify(ev[j], s, clo, yr));
     c3 = wave_sum(c3);
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c3;
     lds_barrier();
@@ -570,7 +576,7 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
                                                        uint64_t *__restrict__ next, uint64_t *__restrict__ lbuf,
                                                        uint64_t *__restrict__ xbuf) {
   const SplitIn in(list, prev, r0, seg, s, L);
-  const uint64_t ntiles = (in.m + TILE - 1) / TILE, cstride = ntiles;
+  const uint64_t ntiles = (in.m + SPLIT_TILE - 1) / SPLIT_TILE, cstride = ntiles;
   const uint64_t b0 = cnt[0], b1 = cnt[cstride], b2 = cnt[2 * cstride], b3 = cnt[3 * cstride];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st[ST_KEPT] = b1 - b0;
@@ -580,13 +586,13 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
   __shared__ uint64_t s_w[BLOCK / WAVE];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    uint64_t ev[TILE_ITEMS];
-    uint32_t cl[TILE_ITEMS];
+    uint64_t ev[SPLIT_ITEMS];
+    uint32_t cl[SPLIT_ITEMS];
     uint64_t c3 = 0;
 #pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) ev[j] = in[tile * TILE + (uint64_t)j * BLOCK + threadIdx.x];
+    for (int j = 0; j < SPLIT_ITEMS; ++j) ev[j] = in[tile * SPLIT_TILE + (uint64_t)j * BLOCK + threadIdx.x];
 #pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) {
+    for (int j = 0; j < SPLIT_ITEMS; ++j) {
       cl[j] = classify(ev[j], s, clo, yr);
       c3 += pack3(cl[j]);
     }
@@ -602,7 +608,7 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
     uint64_t off = 0;
     for (int w = 0; w < wave; ++w) off += s_w[w];
     const uint64_t ex = off + inc - c3;
-    __shared__ uint64_t stg[TILE];
+    __shared__ uint64_t stg[SPLIT_TILE];
     uint64_t tot = 0;
     for (int w = 0; w < BLOCK / WAVE; ++w) tot += s_w[w];
     uint64_t *const outs[3] = {next, lbuf, xbuf};
@@ -610,7 +616,7 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
     for (int k = 0; k < 3; ++k) {
       uint32_t r = (uint32_t)((ex >> (16 * k)) & 0xFFFF);
 #pragma unroll
-      for (int j = 0; j < TILE_ITEMS; ++j)
+      for (int j = 0; j < SPLIT_ITEMS; ++j)
         if ((cl[j] >> k) & 1) stg[r++] = ev[j];
       lds_barrier();
       const uint32_t n_k = (uint32_t)((tot >> (16 * k)) & 0xFFFF);
@@ -942,7 +948,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   uint64_t *lists[2] = {c.get_as<uint64_t>("et_list1", lcap), c.get_as<uint64_t>("et_list2", lcap)};
   const uint64_t *r0 = edges;
   // a split reads at most the list plus a bucket: (lcap + m) entries, in TILE tiles
-  const uint64_t cstride = (lcap + m + TILE - 1) / TILE + 1;
+  const uint64_t cstride = (lcap + m + SPLIT_TILE - 1) / SPLIT_TILE + 1;
   uint64_t *tcnt = c.get_as<uint64_t>("et_tilecnt", 3 * cstride + 1);
   uint64_t *lbuf = c.get_as<uint64_t>("et_light", mcap);  // must outlive the hook rounds (k_level_clean)
   uint64_t *alt = c.get_as<uint64_t>("et_alt", mcap);     // shard scratch of the hook rounds
@@ -951,7 +957,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   uint64_t *stats = c.get_as<uint64_t>("et_stats", (uint64_t)(L + 1) * ST_ROW);
   HIP_CHECK(hipMemsetAsync(stats, 0, (uint64_t)(L + 1) * ST_ROW * sizeof(uint64_t), c.stream));
   auto cset = [&](int k) { return csets + (uint64_t)k * CSET_WORDS; };
-  const unsigned gt = grid_tiles(m), gt2 = grid_tiles(lcap + m), gf = grid_for(m, BLOCK * XK), gn = grid_for(n);
+  const unsigned gt = grid_tiles(m), gt2 = grid_for(lcap + m, SPLIT_TILE), gf = grid_for(m, BLOCK * XK), gn = grid_for(n);
   const int FINB = fin_bits < 0 ? 0 : fin_bits > FIN_BITS_MAX ? FIN_BITS_MAX : fin_bits;   // levels s < FINB: Liu per block (0: none)
   const int nglobal = L > FINB ? L - FINB : 0;
   // the per-level state starts clean; tagged words need no restore between levels,
