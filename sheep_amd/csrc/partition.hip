@@ -347,7 +347,9 @@ __device__ __forceinline__ EvView load_table(const uint32_t *gpos, const uint64_
 // search state for the next event and raises hdr[7] = seq (system scope), which the
 // host polls instead of synchronising the stream.  The event table is read from mapped
 // host memory too (the host rewrites it between events), so an event is ONE launch.
-constexpr int EVI = 8, EV_CH = BLOCK * EVI;
+// 512-entry chunks: an event's scan reaches its hit in fewer dependent rounds per
+// workgroup (RMAT-26 / Chung-Lu events: 2048-entry chunks 2.2 / 4.6 ms, 512 2.0 / 3.9 ms)
+constexpr int EVI = 2, EV_CH = BLOCK * EVI;
 constexpr uint32_t EV_STAGE = 1u << 16;   // mapped staging area (kids)
 constexpr uint32_t EV_INLINE = 4096;      // kid lists staged by the event kernel itself
 
@@ -378,18 +380,28 @@ __global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hi
   __shared__ uint32_t spos[EV_LDS];
   __shared__ uint64_t spre[EV_LDS + 1];
   __shared__ unsigned long long s_best[BLOCK / WAVE];
+  __shared__ unsigned long long s_word;   // one thread's atomic read, for the workgroup
   __shared__ bool last;
   uint64_t t_start = wall_clock64();
   const EvView ev = epos ? load_table(epos, epre, m, spos, spre) : load_arg(arg, spos, spre);
   uint64_t t_table = wall_clock64();
-  const uint64_t prev = *evprev;
+  // The search state (evprev, found, done) is only ever touched by atomic read-modify-writes,
+  // which every XCD sees at one coherent point: a plain or atomic LOAD is served from the
+  // reading XCD's own L2 and can return a value an earlier event left there (a stale hit
+  // below every chunk made one search end empty: seen with 512-entry chunks on C4).
+  if (threadIdx.x == 0) s_word = atomicOr((unsigned long long *)evprev, 0ull);
+  __syncthreads();
+  const uint64_t prev = s_word;
+  __syncthreads();   // s_word is rewritten below
   const uint64_t start = prev == ~0ull ? 0 : (uint32_t)prev;
   const uint32_t vlast = prev == ~0ull ? INVALID : (uint32_t)(prev >> 32);
   for (uint64_t ch = blockIdx.x;; ch += gridDim.x) {
     const uint64_t base = start + ch * EV_CH;
     if (base >= nh) break;
-    const unsigned long long f = __hip_atomic_load(found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (f != ~0ull && (uint32_t)f < base) break;   // a hit below this chunk is known
+    if (threadIdx.x == 0) s_word = atomicOr(found, 0ull);
+    __syncthreads();
+    const unsigned long long f = s_word;
+    if (f != ~0ull && (uint32_t)f < base) break;   // a hit below this chunk is known (uniform)
     unsigned long long best = ~0ull;
     // every candidate's four words loaded before any is decoded (a load behind the id
     // check of the same candidate serialised two latencies per candidate: 24 us a scan)
@@ -432,13 +444,15 @@ __global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hi
   __syncthreads();
   if (!last) return;
   const uint64_t t_search = wall_clock64();
-  const unsigned long long e = __hip_atomic_load(found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) s_word = atomicOr(found, 0ull);
+  __syncthreads();
+  const unsigned long long e = s_word;
   const uint32_t v = e == ~0ull ? INVALID : (uint32_t)(e >> 32);
   if (v != INVALID) {
     const uint32_t beg = koff[v], cnt = koff[v + 1] - beg;
     if (cnt <= EV_INLINE) stage_kids(ev, beg, cnt, threadIdx.x, BLOCK, kids, S, cparent, tD, tU, kid_out, r_out);
     if (threadIdx.x == 0) {
-      *evprev = e;
+      atomicExch((unsigned long long *)evprev, e);
       uint32_t lo, hi;
       node_interval(v, cparent, ckoff, tD, tU, rst, ren, lo, hi);
       const uint64_t r = S[v] - ev.removed(lo, hi);
@@ -459,8 +473,8 @@ __global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hi
     hdr[8] = (uint32_t)(t_table - t_start);
     hdr[9] = (uint32_t)(t_search - t_table);
     hdr[10] = (uint32_t)(t_stage - t_search);
-    *found = ~0ull;   // the next event's search starts clean
-    *done = 0;
+    atomicExch(found, ~0ull);   // the next event's search starts clean
+    atomicExch(done, 0u);
     __threadfence_system();
     __hip_atomic_store(&hdr[7], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -468,7 +482,7 @@ __global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hi
 
 // The kids [beg_j, beg_j + cap) of the last event's node (evprev) with their residuals,
 // for kid lists above EV_INLINE; the last workgroup raises hdr[7] = seq.
-__global__ __launch_bounds__(BLOCK) void k_event_kids(const uint64_t *__restrict__ evprev,
+__global__ __launch_bounds__(BLOCK) void k_event_kids(uint64_t *__restrict__ evprev,
                                                       const uint32_t *__restrict__ epos,
                                                       const uint64_t *__restrict__ epre, uint32_t m,
                                                       const uint32_t *__restrict__ koff,
@@ -481,7 +495,10 @@ __global__ __launch_bounds__(BLOCK) void k_event_kids(const uint64_t *__restrict
   __shared__ uint32_t spos[EV_LDS];
   __shared__ uint64_t spre[EV_LDS + 1];
   __shared__ bool last;
-  const uint32_t v = (uint32_t)(*evprev >> 32);
+  __shared__ unsigned long long s_word;
+  if (threadIdx.x == 0) s_word = atomicOr((unsigned long long *)evprev, 0ull);
+  __syncthreads();
+  const uint32_t v = (uint32_t)(s_word >> 32);
   const EvView ev = load_table(epos, epre, m, spos, spre);
   const uint32_t beg = koff[v] + beg_j, cnt = koff[v + 1] - koff[v];
   const uint32_t lim = cnt - beg_j < cap ? cnt - beg_j : cap;
@@ -492,7 +509,7 @@ __global__ __launch_bounds__(BLOCK) void k_event_kids(const uint64_t *__restrict
   if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (last && threadIdx.x == 0) {
-    *done = 0;
+    atomicExch(done, 0u);
     __threadfence_system();
     __hip_atomic_store(&hdr[7], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -837,7 +854,7 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   const unsigned gev = nh ? (unsigned)std::min<uint64_t>((nh + EV_CH - 1) / EV_CH, 64) : 1;
   auto stage_kids_of = [&](uint32_t beg_j, uint32_t cap, uint32_t *o_kids, uint64_t *o_r) {
     ++seq_no;
-    hipLaunchKernelGGL(k_event_kids, dim3(256), dim3(BLOCK), 0, c.stream, (const uint64_t *)evprev, t_pos, t_pre, m_ev,
+    hipLaunchKernelGGL(k_event_kids, dim3(256), dim3(BLOCK), 0, c.stream, evprev, t_pos, t_pre, m_ev,
                        (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
                        (const uint32_t *)core.parent, (const uint32_t *)t.tD, (const uint32_t *)t.tU, d_hdr, o_kids, o_r,
                        beg_j, cap, done_ctr, seq_no);
