@@ -104,6 +104,7 @@ int sheep_ctx_destroy(sheep_ctx *ctx) {
   HIP_CHECK(hipSetDevice(c.device));
   HIP_CHECK(hipStreamSynchronize(c.stream));
   for (auto &kv : c.ws) if (kv.second.p) hipFree(kv.second.p);
+  if (c.kid_spare.parent) { hipFree(c.kid_spare.parent); hipFree(c.kid_spare.koff); hipFree(c.kid_spare.kids); }
   for (auto &kv : c.pinned) if (kv.second.p) hipHostFree(kv.second.p);
   for (auto &kv : c.timers) for (auto &p : kv.second.pending) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
   for (hipEvent_t e : c.event_pool) hipEventDestroy(e);
@@ -289,10 +290,19 @@ int sheep_kids_destroy(sheep_kids *k) {
   int prev = -1;
   if (k->ctx && hipGetDevice(&prev) == hipSuccess && prev != k->ctx->device) HIP_CHECK(hipSetDevice(k->ctx->device));
   else prev = -1;
-  if (k->ctx) k->ctx->sync();
-  hipFree(k->parent);
-  hipFree(k->koff);
-  hipFree(k->kids);
+  sheep::Ctx::KidBufs *sp = k->ctx ? &k->ctx->kid_spare : nullptr;
+  if (sp && k->parent && k->koff && k->kids && (!sp->parent || sp->cap < k->cap)) {
+    if (sp->parent) {   // keep the larger table's buffers
+      k->ctx->sync();
+      hipFree(sp->parent); hipFree(sp->koff); hipFree(sp->kids);
+    }
+    *sp = {k->parent, k->koff, k->kids, k->cap};
+  } else {
+    if (k->ctx) k->ctx->sync();
+    hipFree(k->parent);
+    hipFree(k->koff);
+    hipFree(k->kids);
+  }
   delete k;
   if (prev >= 0) HIP_CHECK(hipSetDevice(prev));
   API_END

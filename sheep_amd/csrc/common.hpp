@@ -75,6 +75,11 @@ struct Ctx {
   // the degree pass's sortedness probe of the last record buffer (sequence.hip)
   struct SortedProbe { const void *rec = nullptr; uint64_t nrec = 0; bool sorted = true; };
   SortedProbe sorted_probe;
+  // The last destroyed kid table's buffers, taken by the next sheep_kids_create: a
+  // partition per tree would otherwise pay three hipMalloc / hipFree pairs of n words
+  // (hipFree waits for the device), ~1 ms of idle GPU per step at RMAT-26.
+  struct KidBufs { uint32_t *parent = nullptr, *koff = nullptr, *kids = nullptr; uint64_t cap = 0; };
+  KidBufs kid_spare;
 
   bool timing = false;
   struct Timer { std::vector<std::pair<hipEvent_t, hipEvent_t>> pending; double ms = 0; uint64_t launches = 0; uint64_t bytes = 0; };

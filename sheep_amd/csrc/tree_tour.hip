@@ -224,9 +224,16 @@ void gather_u32(Ctx &c, const uint32_t *src, const uint32_t *idx, uint64_t m, ui
 void build_kids(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_kids *k) {
   k->ctx = &c;
   k->n = n;
-  HIP_CHECK(hipMalloc(&k->parent, (n + 1) * sizeof(uint32_t)));
-  HIP_CHECK(hipMalloc(&k->koff, (n + 2) * sizeof(uint32_t)));
-  HIP_CHECK(hipMalloc(&k->kids, (n + 1) * sizeof(uint32_t)));
+  Ctx::KidBufs &sp = c.kid_spare;
+  if (sp.parent && sp.cap >= n) {   // stream-ordered reuse: the old table's work is queued before ours
+    k->parent = sp.parent; k->koff = sp.koff; k->kids = sp.kids; k->cap = sp.cap;
+    sp = Ctx::KidBufs();
+  } else {
+    HIP_CHECK(hipMalloc(&k->parent, (n + 1) * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&k->koff, (n + 2) * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&k->kids, (n + 1) * sizeof(uint32_t)));
+    k->cap = n;
+  }
   if (n == 0) { HIP_CHECK(hipMemsetAsync(k->koff, 0, sizeof(uint32_t), c.stream)); return; }
   TimedRegion tr(c, "kids", 8 * n + 12 * n);   // tree read; parent copy, offsets, kid ids written
   uint32_t *keys = c.get_as<uint32_t>("kid_keys", n), *vals = c.get_as<uint32_t>("kid_vals", n);

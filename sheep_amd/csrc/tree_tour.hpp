@@ -11,6 +11,7 @@ struct sheep_kids {
                                // FFD sorts segments in place (persistent, partition.cpp:104-106)
   uint64_t nkids = 0;
   uint64_t max_kids = 0;       // the largest kid count
+  uint64_t cap = 0;            // the buffers hold cap + 2 / cap + 1 words
 };
 
 namespace sheep {
