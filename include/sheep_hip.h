@@ -171,6 +171,9 @@ int sheep_merge_trees_part(sheep_ctx *ctx, const sheep_jnode *trees_dev, uint32_
 /* ---- partition ------------------------------------------------------------------ */
 int sheep_kids_create(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n,
                       sheep_kids **out);
+/* The context keeps a destroyed table's device buffers (3 x 4 B x n) for the next
+   sheep_kids_create on it, or frees them in sheep_ctx_destroy; the context must outlive
+   its kid tables. */
 int sheep_kids_destroy(sheep_kids *kids);
 /* parts_vid_dev[0, pos_size) (pos_size = max(seq)+1) receives the vid-indexed parts
  * (SHEEP_INVALID_PART for unsequenced slots): parts of jnids 0 .. seq_n-1 go to
