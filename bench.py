@@ -65,21 +65,36 @@ def parse():
     ap.add_argument("--shuffle", action="store_true",
                     help="records in a random order, half with tail/head swapped (a generic edge list)")
     ap.add_argument("--eval-reps", type=int, default=3, help="timed evaluator runs (0: skip)")
-    ap.add_argument("--cpu-scale", type=int, default=22, help="RMAT scale of the CPU-baseline sample")
-    ap.add_argument("--cpu-ranks", type=int, default=16, help="MPI ranks of the reference CPU baseline")
+    ap.add_argument("--cpu-scale", type=int, default=None,
+                    help="RMAT scale of the CPU-baseline sample (default: the bench's own RMAT scale up to 26, else 22)")
+    ap.add_argument("--cpu-ranks", type=int, nargs="+", default=[16, 32, 64],
+                    help="MPI rank counts of the reference CPU baseline (capped by the host cores this process may "
+                         "use, os.sched_getaffinity); the best is reported")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
-                    help="gloo stages the exchanges through host memory (rehearsal)")
     ap.add_argument("--same-device", action="store_true",
-                    help="every rank on cuda:0 (rehearse N ranks on a 1-GPU box; needs gloo)")
-    ap.add_argument("--reduce", default="kway", choices=("kway", "split", "binomial"),
+                    help="every rank on cuda:0: rehearse N ranks on a 1-GPU box (the world's host link over TCP "
+                         "carries the exchanges instead of RCCL)")
+    ap.add_argument("--reduce", default="kway", choices=("kway", "binomial"),
                     help="kway: gather the partial trees to rank 0 and merge them in one pass; "
-                         "split: ranks 0 and 1 receive every partial tree and each merges one half of the "
-                         "position range (rank 0 the heavier upper half), rank 1 sends its half's parents; "
-                         "binomial: ceil(log2 N) send/recv hops with a pairwise merge each")
-    ap.add_argument("--verify", action="store_true",
-                    help="rank 0 also builds the whole-graph tree and checks the merged one against it")
+                         "binomial: ceil(log2 N) send/recv hops with a pairwise merge each (mpi_merge's schedule)")
+    ap.add_argument("--no-verify", dest="verify", action="store_false",
+                    help="skip the after-timing check of the merged tree (N > 1: against the whole-graph tree; "
+                         "--shards: against the binomial pairwise merges of the same shard trees)")
     return ap.parse_args()
+
+
+def make_records(a, seed, ctx):
+    """The workload's records in HBM: (records, vertex-slot capacity, workload name)."""
+    import sheep_amd
+    if a.graph == "rmat":
+        rec = sheep_amd.rmat(a.scale, a.ef, seed, ctx=ctx)
+        vs_cap, workload = 1 << a.scale, f"RMAT-{a.scale} ef{a.ef}, k={a.k}"
+    else:
+        rec = sheep_amd.powerlaw(sheep_amd.TWITTER_VERTICES, a.draws, 1.9, seed, ctx=ctx)
+        vs_cap, workload = sheep_amd.TWITTER_VERTICES, f"Chung-Lu power law (twitter-2010 scale), k={a.k}"
+    if a.shuffle:
+        rec = shuffled(rec, 1000 + seed)
+    return rec, vs_cap, workload
 
 
 def shuffled(d, seed):
@@ -95,95 +110,105 @@ def shuffled(d, seed):
     return out
 
 
+def spawn_ranks(a):
+    """`--gpus N` without a torch.distributed launcher: start one rank per GPU with
+    torch.distributed.run as a CHILD process (nothing here has touched the GPU: device
+    counting does not initialise it) and exit with its status.  Fewer than N visible
+    devices is an error, never a silent one-GPU run."""
+    import socket
+    import subprocess
+    import torch
+    have = torch.cuda.device_count()
+    if have < a.gpus and not a.same_device:
+        print(f"bench: --gpus {a.gpus} but only {have} HIP device(s) visible", file=sys.stderr, flush=True)
+        sys.exit(2)
+    with socket.socket() as sk:                                   # a free rendezvous port
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        spawn_ranks(a)
     import torch
-    import torch.distributed as dist
     import sheep_amd
     from sheep_amd import dist as sdist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus and world > 1:
+    local = 0 if a.same_device else int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
-    if a.same_device:
-        if a.dist_backend != "gloo":
-            raise SystemExit("--same-device needs --dist-backend gloo (RCCL wants one rank per GPU)")
-        local = 0
-    torch.cuda.set_device(local)
-    if world > 1:
-        if a.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
-    seed = (a.scale if a.graph == "rmat" else 2010) if a.seed is None else a.seed
     if a.shards > 1 and world > 1:
         raise SystemExit("--shards is the one-GPU form of the edge-shard path")
-
-    reduce = a.reduce
-    ctx = sheep_amd.Context(local)
-    if a.graph == "rmat":                                       # whole graph, identical on every rank
-        rec = sheep_amd.rmat(a.scale, a.ef, seed, ctx=ctx)
-        vs_cap, workload = 1 << a.scale, f"RMAT-{a.scale} ef{a.ef}, k={a.k}"
+    torch.cuda.set_device(local)
+    seed = (a.scale if a.graph == "rmat" else 2010) if a.seed is None else a.seed
+    group = None
+    if world > 1:
+        # torch.distributed (gloo, host) is the control plane only: the rendezvous port,
+        # barriers and the max over ranks of the wall time.  The data path is the world of
+        # include/sheep_hip.h (sheep_group_join, group.hip): RCCL over xGMI between the
+        # ranks' GPUs, the same code graph2tree -i -r runs under mpiexec.
+        sdist.init_control()
+        group = sheep_amd.Group.join(local, rank, world, "127.0.0.1", sdist.shared_port(),
+                                     link="host" if a.same_device else "rccl")
+        ctx = group.ctx[0]
     else:
-        rec = sheep_amd.powerlaw(sheep_amd.TWITTER_VERTICES, a.draws, 1.9, seed, ctx=ctx)
-        vs_cap, workload = sheep_amd.TWITTER_VERTICES, f"Chung-Lu power law (twitter-2010 scale), k={a.k}"
+        ctx = sheep_amd.Context(local)
+    rec, vs_cap, workload = make_records(a, seed, ctx)          # whole graph, identical on every rank
     if a.shards > 1:
         workload += f", {a.shards} shards on 1 GPU"
-    if a.shuffle:
-        rec = shuffled(rec, 1000 + seed)
     R = rec.shape[0]
     beg, end = sdist.shard_bounds(R, rank, world)               # contiguous edge shard (graph2tree -l)
     shard = rec[beg:end].contiguous() if world > 1 else rec
     del rec
     torch.cuda.empty_cache()
-    deg = torch.zeros(vs_cap, dtype=torch.int32, device=f"cuda:{local}")
+    dev = f"cuda:{local}"
+    deg = torch.zeros(vs_cap, dtype=torch.int32, device=dev)
     subs = [shard[i * shard.shape[0] // a.shards:(i + 1) * shard.shape[0] // a.shards] for i in range(a.shards)]
     stack = [None]
+    bufs = {}
 
     def step():
         deg.zero_()
-        vs = 0
-        for sub in subs:                                        # shards accumulate into one histogram
-            _, max_slot = sheep_amd.degree_count(sub, mode="llama", deg=deg, ctx=ctx)
-            vs = max(vs, max_slot)
-        if world > 1:                                           # sequence.h:72,78 MPI_Allreduce
-            vs = sdist.allreduce_degrees(deg, vs)
-        s = sheep_amd.sequence_from_degrees(deg, vs, ctx=ctx)
-        if a.shards > 1:                                        # map per shard, then ONE K-way merge
-            if stack[0] is None or stack[0].shape[1] != s.n:
-                stack[0] = torch.empty((a.shards, s.n, 2), dtype=torch.int32, device=f"cuda:{local}")
-            for i, sub in enumerate(subs):
-                sheep_amd.build_tree(sub, s, ctx=ctx, out=stack[0][i])
-            tree = sheep_amd.merge_trees_many(stack[0], ctx=ctx)
+        if group is not None:                                   # graph2tree -i -r over the world
+            if "seq" not in bufs:
+                bufs["seq"] = torch.empty(vs_cap, dtype=torch.int32, device=dev)
+                bufs["pos"] = torch.empty(vs_cap, dtype=torch.int32, device=dev)
+            s = group.sequence([shard], vs_cap, deg=[deg], seq=[bufs["seq"]], pos=[bufs["pos"]])[0]
+            if "tree" not in bufs or bufs["tree"].shape[0] < s.n:
+                bufs["tree"] = torch.empty((max(s.n, 1), 2), dtype=torch.int32, device=dev)
+            tree = group.build_tree([shard], [s], a.reduce, trees=[bufs["tree"]])[0]
         else:
-            tree = sheep_amd.build_tree(shard, s, ctx=ctx)
-        if world > 1 and reduce == "split":                     # the K-way merge split over the ranks
-            tree = sdist.reduce_trees_split(tree, lambda st, p, q: sheep_amd.merge_trees_part(st, p, q, ctx=ctx),
-                                            rank, world)
-        elif world > 1 and reduce == "kway":                    # reduce to rank 0 (jnode.cpp:241) in one pass
-            tree = sdist.reduce_trees_kway(tree, lambda t: sheep_amd.merge_trees_many(t, ctx=ctx), rank, world)
-        elif world > 1:                                         # binomial reduce to rank 0 (jnode.cpp:241)
-            tree = sdist.reduce_trees(tree, lambda x, y: sheep_amd.merge_trees(x, y, ctx=ctx), rank, world)
+            vs = 0
+            for sub in subs:                                    # shards accumulate into one histogram
+                _, max_slot = sheep_amd.degree_count(sub, mode="llama", deg=deg, ctx=ctx)
+                vs = max(vs, max_slot)
+            s = sheep_amd.sequence_from_degrees(deg, vs, ctx=ctx)
+            if a.shards > 1:                                    # map per shard, then ONE K-way merge
+                if stack[0] is None or stack[0].shape[1] != s.n:
+                    stack[0] = torch.empty((a.shards, s.n, 2), dtype=torch.int32, device=dev)
+                for i, sub in enumerate(subs):
+                    sheep_amd.build_tree(sub, s, ctx=ctx, out=stack[0][i])
+                tree = sheep_amd.merge_trees_many(stack[0], ctx=ctx)
+            else:
+                tree = sheep_amd.build_tree(shard, s, ctx=ctx)
         res = None
-        if rank == 0:
+        if rank == 0:                                           # graph2tree.cpp:203-208
             kids = sheep_amd.KidTable(tree, ctx)
             res = sheep_amd.partition(s, tree, a.k, kids=kids, ctx=ctx)
             kids.close()
         return s, tree, res
 
     def barrier():
-        if world > 1:
-            dist.barrier()
         torch.cuda.synchronize()
-
-    def max_over_ranks(t):
+        ctx.sync()
         if world > 1:
-            tt = torch.tensor([t], dtype=torch.float64, device=f"cuda:{local}" if a.dist_backend == "nccl" else "cpu")
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            t = float(tt.item())
-        return t
+            sdist.barrier()
 
     for _ in range(a.warmup):
         step()
@@ -195,7 +220,7 @@ def main():
     for _ in range(a.steps):
         s, tree, res = step()
     barrier()
-    t = max_over_ranks(time.perf_counter() - t0)
+    t = sdist.max_over_ranks(time.perf_counter() - t0) if world > 1 else time.perf_counter() - t0
 
     # per-region device timings (HIP events on the context stream), timed steps only
     phases = {}
@@ -206,22 +231,17 @@ def main():
 
     evaluator = None
     if a.eval_reps > 0:
-        evaluator = time_evaluator(a, ctx, shard, subs, s, res, rank, world, local, barrier, max_over_ranks)
+        evaluator = time_evaluator(a, ctx, group, shard, subs, s, res, rank, world, dev, barrier)
     ctx.timing(False)
 
     verified = None
-    if a.verify and rank == 0:                                  # merged tree == whole-graph tree
-        if world == 1 and a.shards == 1:
-            verified = True
-        elif world == 1:
-            verified = bool(torch.equal(sheep_amd.build_tree(shard, s, ctx=ctx), tree)) if R < (1 << 32) else None
-        else:
-            whole = sheep_amd.build_tree(sheep_amd.rmat(a.scale, a.ef, seed, ctx=ctx) if not a.shuffle else
-                                         shuffled(sheep_amd.rmat(a.scale, a.ef, seed, ctx=ctx), 1000 + seed), s, ctx=ctx)
-            verified = bool(torch.equal(whole, tree))
-            del whole
-        if not verified:
-            print("bench: merged tree differs from the whole-graph tree", file=sys.stderr, flush=True)
+    if a.verify and (world > 1 or a.shards > 1):
+        if rank == 0:
+            verified = verify_tree(a, seed, ctx, shard, subs, s, tree, stack[0], world)
+            if not verified:
+                print("bench: merged tree differs from its cross-check", file=sys.stderr, flush=True)
+        if world > 1:
+            sdist.barrier()
 
     out = None
     if rank == 0:
@@ -239,6 +259,8 @@ def main():
             roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                     "alg_bytes_per_launch": int(b_launch), "ms_per_launch": round(ms_launch, 4)}
+            if world > 1:
+                roof["note"] = "rank 0's leaf regions (rank 0 also runs the merge, kids and partition)"
             roof.update(pmc_region(a, world, dom, p["launches"] / a.steps))
         path = {"alg_bytes": b_alg, "achieved_GBs": round(b_alg * a.steps / t / 1e9, 2),
                 "frac": round(b_alg * a.steps / t / 1e9 / (HBM_PEAK_GBS * world), 4)}
@@ -262,57 +284,85 @@ def main():
             "config": {"workload": workload, "records": R, "vertex_slots": s.pos_size,
                        "tree_nodes": n, "k": a.k, "created": res.created, "packing_nodes": res.packing_nodes,
                        "heavy_nodes": res.heavy_nodes, "seed": seed, "shuffled": a.shuffle, "shards": a.shards,
-                       "parallelism": f"edge-shards x{world}" + (f", {reduce} reduce" if world > 1 else "")
-                       + ("" if a.dist_backend == "nccl" else f" ({a.dist_backend}"
-                          + (", one device" if a.same_device else "") + ")")},
+                       "parallelism": f"edge-shards x{world}" + (
+                           f", {a.reduce} reduce, sheep_group over {'RCCL' if group.rccl else 'host TCP (one device)'}"
+                           if world > 1 else "")},
             "roofline": roof,
             "path_roofline": path,
             "evaluator": evaluator,
             "phases": phases,
         }
         if verified is not None:
-            out["verified_vs_whole_graph"] = verified
+            out["verified_vs_whole_graph" if world > 1 or R < (1 << 32) else "verified_vs_pairwise_merges"] = verified
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a, ctx)
     del shard
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    if group is not None:
+        sdist.barrier()
+        group.close()
+        sdist.shutdown()
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if verified is False:
+        sys.exit(1)
 
 
-def time_evaluator(a, ctx, shard, subs, s, res, rank, world, local, barrier, max_over_ranks):
+def verify_tree(a, seed, ctx, shard, subs, s, tree, stacked, world):
+    """After the timed steps, rank 0 checks the reduced tree.  N ranks: against the
+    whole graph's tree built on rank 0 alone.  One GPU with --shards: against the whole
+    graph's tree when it holds fewer than 2^32 records, and always against the binomial
+    pairwise merges (mpi_merge's schedule, jnode.cpp:203-250) of the same shard trees."""
+    import torch
+    import sheep_amd
+    if world > 1:
+        rec, _, _ = make_records(a, seed, ctx)
+        whole = sheep_amd.build_tree(rec, s, ctx=ctx)
+        del rec
+        ok = bool(torch.equal(whole, tree))
+        del whole
+        torch.cuda.empty_cache()
+        return ok
+    ok = True
+    if shard.shape[0] < (1 << 32):
+        ok = bool(torch.equal(sheep_amd.build_tree(shard, s, ctx=ctx), tree))
+    cur = [stacked[i] for i in range(len(subs))]
+    d = 1
+    while d < len(cur):
+        for i in range(0, len(cur), 2 * d):
+            if i + d < len(cur):
+                cur[i] = sheep_amd.merge_trees(cur[i], cur[i + d], ctx=ctx)
+        d *= 2
+    return ok and bool(torch.equal(cur[0], tree))
+
+
+def time_evaluator(a, ctx, group, shard, subs, s, res, rank, world, dev, barrier):
     """ECV(down) + balance (evaluate(graph, seq), partition.cpp:475-521), timed on its own:
-    one GPU — sheep_evaluate over all records; N GPUs — parts broadcast, per-shard
-    bitsets, binomial OR-reduction to rank 0, node pass there.  B_eval per SURVEY §8(d)."""
+    one GPU — sheep_evaluate over all records (or the shards' bitsets with --shards); N
+    GPUs — rank 0's parts broadcast (Partition::mpi_sync), per-shard bitsets, the binomial
+    OR-reduction to rank 0 and the node pass there (sheep_group_broadcast_parts +
+    sheep_group_evaluate).  B_eval per SURVEY §8(d)."""
     import torch
     import sheep_amd
     from sheep_amd import dist as sdist
     R_total = shard.shape[0] * world if world > 1 else shard.shape[0]
     times, ev = [], None
-    parts0 = res.parts if rank == 0 else None
     for _ in range(a.eval_reps):
         barrier()
         t0 = time.perf_counter()
         if world == 1 and a.shards == 1:
-            ev = sheep_amd.evaluate(shard, s, parts0, what=sheep_amd.EVAL_DOWN, ctx=ctx)
+            ev = sheep_amd.evaluate(shard, s, res.parts, what=sheep_amd.EVAL_DOWN, ctx=ctx)
         elif world == 1:                                         # the shards' bitsets, then one node pass
-            e = sheep_amd.ShardedEvaluator(s, parts0, sheep_amd.EVAL_DOWN, ctx=ctx)
+            e = sheep_amd.ShardedEvaluator(s, res.parts, sheep_amd.EVAL_DOWN, ctx=ctx)
             for sub in subs:
                 e.add(sub)
             ev = e.finish()
         else:
-            parts = sdist.sync_parts(parts0, s.pos_size, torch.device("cuda", local))
-            nparts = torch.tensor([0 if rank else sheep_amd.ShardedEvaluator.num_parts(parts, s, ctx)],
-                                  dtype=torch.int64, device=f"cuda:{local}" if a.dist_backend == "nccl" else "cpu")
-            dist_broadcast(nparts)
-            e = sheep_amd.ShardedEvaluator(s, parts, sheep_amd.EVAL_DOWN, nparts=int(nparts.item()), ctx=ctx)
-            e.add(shard)
-            e = sdist.reduce_eval(e, rank, world)
-            ev = e.finish() if rank == 0 else None
+            parts = res.parts.clone() if rank == 0 else torch.empty(s.pos_size, dtype=torch.int16, device=dev)
+            parts = group.broadcast_parts([parts], s.pos_size)[0]
+            ev = group.evaluate([shard], [s], [parts], what=sheep_amd.EVAL_DOWN)
         barrier()
-        times.append(max_over_ranks(time.perf_counter() - t0))
+        dt = time.perf_counter() - t0
+        times.append(sdist.max_over_ranks(dt) if world > 1 else dt)
     if rank != 0:
         return None
     k = res.created
@@ -329,17 +379,6 @@ def time_evaluator(a, ctx, shard, subs, s, res, rank, world, local, barrier, max
             out["device_ms"] = round(ms / launches, 3)
     out.update(pmc_region(a, world, "evaluate", 1))
     return out
-
-
-def dist_broadcast(t):
-    import torch.distributed as dist
-    from sheep_amd import dist as sdist
-    if sdist._host_staged() and t.is_cuda:
-        h = t.cpu()
-        dist.broadcast(h, 0)
-        t.copy_(h)
-    else:
-        dist.broadcast(t, 0)
 
 
 def _pmc(a, world):
@@ -394,11 +433,15 @@ def cpu_info():
                 break
     except OSError:
         pass
-    return model, os.cpu_count()
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count()
+    return model, os.cpu_count(), usable
 
 
 def cpu_baseline(a, ctx):
-    """CPU baseline on a bounded sample: RMAT-<cpu-scale> from the same generator.
+    """The reference CPU path on the same workload (RMAT-26 by default), on this host.
 
     kind "reference": the reference's own lib/ code, compiled from /root/reference into
     oracle/_ref/ref_harness by oracle/ref/Makefile, run as the graph2tree `-r -p k` flow
@@ -406,44 +449,55 @@ def cpu_baseline(a, ctx):
     (graph2tree -l semantics, untimed), then mpiSequence's degree all-reduce with
     degreeSequence's sort, JTree on the shard (map), JNodeTable::mpi_merge (the custom-op
     MPI_Reduce), makeKids + Partition(k) + mpi_sync on rank 0.  The timed region starts at
-    a barrier after the load.  Test infrastructure timed as a baseline; never the
-    measured path."""
+    a barrier after the load.  P runs over --cpu-ranks, capped by the cores this process
+    may run on (os.sched_getaffinity); the fastest P is the value.  The literal `-ir` is
+    not used: its sort copies the whole degree vector per comparison (sequence.h:85,
+    BASELINE.md §2).  Test infrastructure timed as a baseline; never the measured path."""
     import shutil
     import subprocess
     import tempfile
-    import numpy as np
     import sheep_amd
-    sc = a.cpu_scale
-    d = sheep_amd.rmat(sc, a.ef, sc, ctx=ctx)
-    h = sheep_amd.to_numpy_u32(d).reshape(-1, 3)
-    del d
-    R = len(h)
-    model, ncpu = cpu_info()
+    sc = a.cpu_scale if a.cpu_scale is not None else (min(a.scale, 26) if a.graph == "rmat" else 22)
+    model, ncpu, usable = cpu_info()
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     mpiexec = shutil.which("mpiexec", path="/opt/conda/bin") or shutil.which("mpiexec")
     if not os.path.exists(harness) or not mpiexec:
         return {"value": None, "unit": "edges/s", "cores": 0, "kind": "reference",
                 "sample": "oracle/_ref/ref_harness or mpiexec missing on this host"}
-    ranks = max(1, min(a.cpu_ranks, ncpu or 1))
-    with tempfile.TemporaryDirectory() as td:
+    ranks = sorted({max(1, min(p, usable or 1)) for p in a.cpu_ranks})
+    runs = []
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
         path = os.path.join(td, f"rmat{sc}.dat")
-        h.tofile(path)
-        del h
+        d = sheep_amd.rmat(sc, a.ef, sc, ctx=ctx)
+        R = d.shape[0]
+        with open(path, "wb") as f:                               # XS1 records, streamed in chunks
+            step = 1 << 26
+            for b in range(0, R, step):
+                f.write(sheep_amd.to_numpy_u32(d[b:b + step]).tobytes())
+        del d
+        ctx.sync()
         env = dict(os.environ, OMP_NUM_THREADS="1")
-        r = subprocess.run([mpiexec, "-n", str(ranks), harness, "mpi", path, str(a.k)], capture_output=True,
-                           text=True, timeout=900, env=env)
-    if r.returncode != 0:
-        return {"value": None, "unit": "edges/s", "cores": ranks, "kind": "reference",
-                "sample": f"mpiexec failed: {r.stderr.strip()[-300:]}"}
-    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-    sec = res["seconds"]
-    return {"value": round(R / sec, 1), "unit": "edges/s", "cores": ranks, "kind": "reference",
-            "cpu_model": model, "host_cpus": ncpu,
+        for p in ranks:
+            r = subprocess.run([mpiexec, "-n", str(p), harness, "mpi", path, str(a.k)], capture_output=True,
+                               text=True, timeout=900, env=env)
+            if r.returncode != 0:
+                runs.append({"ranks": p, "error": r.stderr.strip()[-300:]})
+                continue
+            res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+            runs.append({"ranks": p, "seconds": round(res["seconds"], 3), "edges_per_s": round(R / res["seconds"], 1),
+                         "phases_s": {k: round(v, 3) for k, v in res.get("phases", {}).items()}})
+            print(f"cpu_baseline: {p} ranks {res['seconds']:.2f} s", file=sys.stderr, flush=True)
+    ok = [x for x in runs if "seconds" in x]
+    if not ok:
+        return {"value": None, "unit": "edges/s", "cores": 0, "kind": "reference", "sample": f"failed: {runs}"}
+    best = min(ok, key=lambda x: x["seconds"])
+    return {"value": best["edges_per_s"], "unit": "edges/s", "cores": best["ranks"], "kind": "reference",
+            "cpu_model": model, "host_cpus": ncpu, "usable_cpus": usable,
             "sample": f"RMAT-{sc} ef{a.ef} seed {sc} ({R} records), k={a.k}: reference lib/ graph2tree -r -p flow "
                       f"(mpiSequence all-reduce + degreeSequence sort, JTree per shard, JNodeTable::mpi_merge, "
-                      f"makeKids + Partition + mpi_sync) on {ranks} MPI ranks x 1 thread, shards loaded untimed, "
-                      f"{sec:.2f} s",
-            "phases_s": {k: round(v, 3) for k, v in res.get("phases", {}).items()}}
+                      f"makeKids + Partition + mpi_sync) on P MPI ranks x 1 thread, P in {ranks} (best P="
+                      f"{best['ranks']}, {best['seconds']:.2f} s), shards loaded untimed",
+            "phases_s": best["phases_s"], "sweep": runs}
 
 
 if __name__ == "__main__":

@@ -105,6 +105,10 @@ const char *sheep_last_error(void);
 #define SHEEP_OWN_STREAM ((void *)(intptr_t)-1)
 int sheep_ctx_create(int device, void *hip_stream, sheep_ctx **out);
 int sheep_ctx_destroy(sheep_ctx *ctx);
+/* Frees the context's device workspace (the scratch arrays kernels keep between calls,
+ * sized by the largest graph seen, and the spare kid-table buffers); the next call
+ * allocates again.  Synchronises the context's stream. */
+int sheep_ctx_trim(sheep_ctx *ctx);
 int sheep_ctx_sync(sheep_ctx *ctx);
 void *sheep_ctx_stream(sheep_ctx *ctx);
 int sheep_malloc(sheep_ctx *ctx, size_t bytes, void **dev_out);
@@ -228,31 +232,54 @@ int sheep_eval_finish(sheep_ctx *ctx, const uint64_t *bits_dev, const uint64_t *
 int sheep_edge_parts(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec, const uint32_t *pos_dev,
                      uint64_t pos_size, const int16_t *parts_vid_dev, int16_t *edge_part_dev);
 
-/* ---- several GPUs of one node (graph2tree -i / -r without MPI) ----------------------
- * One process drives `ndev` ranks, rank r on devices[r] with a context of its own.  Distinct
- * devices exchange over RCCL (one communicator clique, xGMI); a device listed more than
- * once (several edge shards rehearsed on one GPU) exchanges by device-to-device copies.
- * Per-rank arrays (rec_dev[r], deg_dev[r], ...) live on rank r's device.  The ranks run on
- * streams of their own: inputs written on other streams must be complete before a call
- * (synchronise them first); every call is complete (all ranks synchronised) on return.  Replaces (chan150/sheep):
+/* ---- several GPUs of one node: the MPI world of graph2tree -i / -r -------------------
+ * A world of `world` ranks; rank r holds edge shard r on one device.  Two ways to form it:
+ *   sheep_group_create  ONE process drives every rank: rank r on devices[r], a context of its
+ *                       own each (graph2tree -i / -r without mpiexec, SHEEP_DEVICES);
+ *   sheep_group_join    ONE PROCESS PER RANK (replaces MPI_Init / MPI_Comm_rank / _size,
+ *                       graph2tree.cpp:134-143): every rank calls it with its device, rank and
+ *                       the world size; they meet over TCP at host:port (rank 0 listens there).
+ *                       This is how `mpiexec -n W graph2tree ... -ir` and bench.py's
+ *                       torch.distributed ranks run.
+ * Data moves by RCCL when every rank has a device of its own (ncclCommInitAll, or
+ * ncclCommInitRank with rank 0's id sent over the TCP links; xGMI), by device copies when
+ * one process lists a device twice, and through host memory over the TCP links when
+ * processes share a device (a one-GPU rehearsal).  `link` forces the choice for a joined
+ * world (SHEEP_LINK_RCCL fails when two ranks share a device).
+ * Per-rank array arguments (rec_dev[i], deg_dev[i], ...) are indexed by the LOCAL ranks of
+ * the calling process (sheep_group_local_count of them; local i is global rank
+ * sheep_group_rank(g, i)) and live on that rank's device.  Every call is collective: all
+ * processes of a joined world make it, with the same scalars.  The ranks run on streams of
+ * their own: inputs written on other streams must be complete before a call (synchronise
+ * them first); every call is complete on return.  Replaces (chan150/sheep):
  *   sheep_group_sequence        mpiSequence (sequence.h:65-93): per-shard LLAMA degrees
- *                               into deg_dev[r] (zeroed by the caller, capacity cap), the
+ *                               into deg_dev[i] (zeroed by the caller, capacity cap), the
  *                               MPI_Allreduce(MAX) of max_slot and MPI_Allreduce(SUM) of the
  *                               degrees, then the same seq/pos on every rank
  *   sheep_group_build_tree      JTree per shard (graph2tree.cpp:185-189) + mpi_merge
- *                               (jnode.cpp:203-250): reduce 0 = partial trees only (tree_dev[r]
- *                               = rank r's tree), 1 = gather + one K-way merge on rank 0,
- *                               2 = binomial rounds of pairwise merges on disjoint device pairs;
- *                               with 1 / 2 the merged tree is in tree_dev[0]
+ *                               (jnode.cpp:203-250): reduce 0 = partial trees only (tree_dev[i]
+ *                               = the local rank's tree), 1 = gather + one K-way merge on
+ *                               rank 0, 2 = binomial rounds of pairwise merges on disjoint rank
+ *                               pairs; with 1 / 2 the merged tree is rank 0's tree_dev
  *   sheep_group_broadcast_parts Partition::mpi_sync (partition.cpp:69-79): rank 0's parts
  *   sheep_group_evaluate        Partition::evaluate over the shards: per-rank part bitsets,
- *                               binomial OR-reduction, the node pass on rank 0 */
+ *                               binomial OR-reduction, the node pass on rank 0 (*out is
+ *                               zero on the other ranks)
+ *   sheep_group_barrier / sheep_group_allreduce_max_u64   MPI_Barrier / MPI_Allreduce(MAX) */
 typedef struct sheep_group sheep_group;
+#define SHEEP_LINK_AUTO 0
+#define SHEEP_LINK_RCCL 1
+#define SHEEP_LINK_HOST 2
 int sheep_group_create(const int *devices, int ndev, sheep_group **out);
+int sheep_group_join(int device, int rank, int world, const char *host, int port, int link, sheep_group **out);
 int sheep_group_destroy(sheep_group *g);
-int sheep_group_size(const sheep_group *g);
-sheep_ctx *sheep_group_ctx(sheep_group *g, int rank);
+int sheep_group_size(const sheep_group *g);                /* world size */
+int sheep_group_local_count(const sheep_group *g);         /* ranks held by this process */
+int sheep_group_rank(const sheep_group *g, int local);     /* global rank of local rank i */
+sheep_ctx *sheep_group_ctx(sheep_group *g, int local);
 int sheep_group_uses_rccl(const sheep_group *g);
+int sheep_group_barrier(sheep_group *g);
+int sheep_group_allreduce_max_u64(sheep_group *g, uint64_t *value);
 int sheep_group_sequence(sheep_group *g, const sheep_xs1 *const *rec_dev, const uint64_t *nrec,
                          uint32_t *const *deg_dev, uint64_t cap, uint32_t *const *seq_dev,
                          uint32_t *const *pos_dev, uint64_t *n_out, uint64_t *vs_out);
@@ -266,6 +293,12 @@ int sheep_device_count(int *out);
 int sheep_group_evaluate(sheep_group *g, const sheep_xs1 *const *rec_dev, const uint64_t *nrec,
                          const uint32_t *const *pos_dev, uint64_t pos_size,
                          const int16_t *const *parts_vid_dev, int what, sheep_eval *out);
+/* Host-only self-test of a joined world's TCP links (no device touched): rank 0's bytes to
+ * every rank, a ring shift, a gather to rank 0, all-reduce max / sum.  *checksum_out = the
+ * world's sum of FNV-1a hashes of every received buffer, *max_out = the max of the ranks'
+ * own buffer hashes (tests/test_dist.py checks both on CPUs). */
+int sheep_mesh_selftest(int rank, int world, const char *host, int port, uint64_t bytes, uint64_t *checksum_out,
+                        uint64_t *max_out);
 
 /* ---- tree facts (TREEFAQS) -------------------------------------------------------- */
 int sheep_facts(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n, sheep_facts_t *out);

@@ -25,6 +25,7 @@ def lib():
         L.or_last_error.restype = ctypes.c_char_p
         L.or_sequence.argtypes = [P, P, U64, I32, P, U64, ctypes.POINTER(U64)]
         L.or_build_tree.argtypes = [P, P, U64, U64, U64, P, U64, P, P]
+        L.or_build_tree_mr.argtypes = [P, P, U64, P, U64, U64, P, P]
         L.or_merge.argtypes = [P, P, P, P, U64, P, P]
         L.or_facts.argtypes = [P, P, U64, P]
         L.or_kids_create.argtypes = [P, U64]
@@ -75,6 +76,17 @@ def build_tree(tail, head, seq, part=0, num_parts=0):
     n = len(seq)
     parent, pst = np.empty(n, np.uint32), np.empty(n, np.uint32)
     _chk(lib().or_build_tree(_p(tail), _p(head), len(tail), part, num_parts, _p(seq), n, _p(parent), _p(pst)))
+    return parent, pst
+
+
+def build_tree_mr(tail, head, seq, shards=16):
+    """The same tree in graph2tree -r's map/reduce form: `shards` contiguous record
+    shards' partial trees (OpenMP threads) merged in binomial rounds (mpi_merge).  Linear
+    memory in the records, for the BASELINE-size checks (C3-C5)."""
+    tail, head, seq = _u32(tail), _u32(head), _u32(seq)
+    n = len(seq)
+    parent, pst = np.empty(n, np.uint32), np.empty(n, np.uint32)
+    _chk(lib().or_build_tree_mr(_p(tail), _p(head), len(tail), _p(seq), n, int(shards), _p(parent), _p(pst)))
     return parent, pst
 
 

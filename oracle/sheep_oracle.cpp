@@ -112,12 +112,26 @@ struct LlamaGraph {
 // so any correct sort gives the same vector.
 static std::vector<uint32_t> sort_by_degree(const std::vector<uint64_t> &degree) {
   std::vector<uint32_t> seq;
+  uint64_t maxdeg = 0;
   for (uint32_t x = 0; x < degree.size(); ++x)
-    if (degree[x] != 0) seq.push_back(x);
-  std::sort(seq.begin(), seq.end(), [&degree](uint32_t a, uint32_t b) {
-    return degree[a] != degree[b] ? degree[a] < degree[b] : a < b;
-  });
-  return seq;
+    if (degree[x] != 0) {
+      seq.push_back(x);
+      maxdeg = std::max(maxdeg, degree[x]);
+    }
+  if (maxdeg > 4 * (uint64_t)degree.size() + 1024) {
+    std::sort(seq.begin(), seq.end(), [&degree](uint32_t a, uint32_t b) {
+      return degree[a] != degree[b] ? degree[a] < degree[b] : a < b;
+    });
+    return seq;
+  }
+  // The same total order by a counting sort over the degree (vids stay ascending within
+  // one degree): linear time for the BASELINE-size sequences (C3-C5).
+  std::vector<uint64_t> at(maxdeg + 2, 0);
+  for (uint32_t x : seq) ++at[degree[x] + 1];
+  for (uint64_t d = 0; d <= maxdeg; ++d) at[d + 1] += at[d];
+  std::vector<uint32_t> out(seq.size());
+  for (uint32_t x : seq) out[at[degree[x]]++] = x;
+  return out;
 }
 
 std::vector<uint32_t> degreeSequence(const LlamaGraph &g) {
@@ -228,6 +242,178 @@ Tree buildTree(const LlamaGraph &g, const std::vector<uint32_t> &seq) {
     }
     index.at(X) = cur;                              // jtree.h:165-168
   }
+  return t;
+}
+
+// -------------------------------------------------------------------------------------
+// Map/reduce form of the same tree, for the BASELINE-size checks (C3-C5):
+// graph2tree -r (graph2tree.cpp:185-196) — every MPI rank builds JTree over its
+// contiguous edge shard (`-l part/num_parts`, graph_wrapper.h:47-49) and
+// JNodeTable::mpi_merge reduces the partial trees pairwise in binomial rounds
+// (jnode.cpp:203-250; merge :174-201).  Here the ranks are OpenMP threads.
+//
+// A partial tree is Liu's algorithm written per record instead of per adjacency list: a
+// record (u, v) with positions p(u) != p(v) is, in JTree::insert (jtree.cpp:72-91), a
+// PREORDER entry of the later endpoint (adopt the earlier one's component top) and a
+// POSTORDER entry of the earlier one (++pst).  The adopts are grouped by the later
+// position (the reference's outer loop over seq); their order inside one group does not
+// change the tree.  The union-find is Liu's ancestor forest with path compression (a
+// find re-points the visited path at the current node), the textbook form of the
+// union-find sweep in unionfind.h:46-102: the elimination tree is unique given (edge
+// multiset, order), so either gives the reference's tree.
+// pst adds under merge (jnode.cpp:193), so the whole graph's pst is counted once.
+//
+// Both forms are pinned against each other and the golden trees in
+// tests/test_oracle_golden.py.
+// -------------------------------------------------------------------------------------
+
+// Liu over adopt edges grouped by the later position: lo[off[k] .. off[k+1]) are the
+// earlier endpoints of node k's PREORDER entries.  parent[] must be INVALID-filled.
+// Union-find as unionfind.h:46-102 (union by rank, the set's newest node kept at its
+// root as the representative), with path halving.
+static void liuGrouped(uint64_t n, const uint64_t *off, const uint32_t *lo, uint32_t *parent) {
+  struct Slot { uint32_t up, rep; };
+  std::vector<Slot> uf(n);
+  std::vector<uint8_t> rank(n, 0);
+  Slot *u = uf.data();
+  for (uint64_t i = 0; i < n; ++i) u[i] = Slot{(uint32_t)i, (uint32_t)i};
+  auto find = [u](uint32_t x) {
+    while (u[x].up != x) {
+      const uint32_t g = u[u[x].up].up;
+      u[x].up = g;
+      x = g;
+    }
+    return x;
+  };
+  for (uint64_t k = 0; k < n; ++k) {
+    uint32_t rk = find((uint32_t)k);
+    const uint64_t e = off[k + 1];
+    for (uint64_t j = off[k]; j < e; ++j) {
+      if (j + 16 < e) __builtin_prefetch(&u[lo[j + 16]]);
+      const uint32_t r = find(lo[j]);
+      if (r == rk) continue;
+      parent[u[r].rep] = (uint32_t)k;           // adopt (jnode.h:158-162)
+      if (rank[r] > rank[rk]) { u[rk].up = r; rk = r; }
+      else { u[r].up = rk; if (rank[r] == rank[rk]) ++rank[rk]; }
+      u[rk].rep = (uint32_t)k;
+    }
+  }
+}
+
+// Counting sort of adopt edges (lo, hi) by hi over items [0, N): `emit(f, a, b)` calls
+// f(lo, hi) for the edges of items [a, b).  Outside a parallel region the two passes run
+// on all threads (atomic counts and cursors: the order inside one group is free).
+template <class Emit>
+static void groupByHi(uint64_t n, uint64_t N, Emit emit, std::vector<uint64_t> &off, std::vector<uint32_t> &lo) {
+  off.assign(n + 1, 0);
+  uint64_t *o = off.data();
+  const bool par = !omp_in_parallel() && omp_get_max_threads() > 1;
+  if (par) {
+#pragma omp parallel for schedule(static)
+    for (uint64_t c = 0; c < (N + 65535) / 65536; ++c)
+      emit([&](uint32_t, uint32_t h) { __atomic_fetch_add(&o[(uint64_t)h + 1], 1, __ATOMIC_RELAXED); },
+           c * 65536, std::min(N, (c + 1) * 65536));
+  } else {
+    emit([&](uint32_t, uint32_t h) { ++o[(uint64_t)h + 1]; }, 0, N);
+  }
+  for (uint64_t k = 0; k < n; ++k) o[k + 1] += o[k];
+  lo.resize(o[n]);
+  std::vector<uint64_t> cur(off.begin(), off.end() - 1);
+  uint64_t *c = cur.data();
+  uint32_t *l = lo.data();
+  if (par) {
+#pragma omp parallel for schedule(static)
+    for (uint64_t b = 0; b < (N + 65535) / 65536; ++b)
+      emit([&](uint32_t x, uint32_t h) { l[__atomic_fetch_add(&c[h], 1, __ATOMIC_RELAXED)] = x; },
+           b * 65536, std::min(N, (b + 1) * 65536));
+  } else {
+    emit([&](uint32_t x, uint32_t h) { l[c[h]++] = x; }, 0, N);
+  }
+}
+
+// One shard's partial tree (parent only): records [beg, end).
+static void shardTree(const uint32_t *tail, const uint32_t *head, uint64_t beg, uint64_t end,
+                      const std::vector<uint32_t> &pos, uint64_t n, uint32_t *parent) {
+  std::fill(parent, parent + n, INVALID);
+  const uint32_t *p = pos.data();
+  const uint64_t ps = pos.size();
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> lo;
+  groupByHi(n, end - beg, [&](auto f, uint64_t a, uint64_t b) {
+    for (uint64_t i = beg + a; i < beg + b; ++i) {
+      const uint32_t u = tail[i], v = head[i];
+      if (u >= ps || v >= ps) continue;   // range errors are reported by the caller
+      const uint32_t pu = p[u], pv = p[v];
+      if (pu == INVALID || pv == INVALID || pu == pv) continue;
+      f(std::min(pu, pv), std::max(pu, pv));
+    }
+  }, off, lo);
+  liuGrouped(n, off.data(), lo.data(), parent);
+}
+
+// JNodeTable::merge (jnode.cpp:174-201) on parent arrays: Liu over the union of both
+// trees' parent edges (kid, parent).  `out` may alias `a`.
+static void mergeParents(const uint32_t *a, const uint32_t *b, uint64_t n, uint32_t *out) {
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> lo;
+  groupByHi(n, n, [&](auto f, uint64_t lo_id, uint64_t hi_id) {
+    for (uint64_t id = lo_id; id < hi_id; ++id) {
+      if (a[id] != INVALID) f((uint32_t)id, a[id]);
+      if (b[id] != INVALID) f((uint32_t)id, b[id]);
+    }
+  }, off, lo);
+  std::fill(out, out + n, INVALID);
+  liuGrouped(n, off.data(), lo.data(), out);
+}
+
+// graph2tree -r over `shards` contiguous record shards + the binomial mpi_merge.
+Tree buildTreeMapReduce(const uint32_t *tail, const uint32_t *head, uint64_t R,
+                        const std::vector<uint32_t> &seq, uint64_t shards) {
+  Tree t;
+  const uint64_t n = seq.size();
+  t.parent.assign(n, INVALID);
+  t.pst.assign(n, 0);
+  if (n == 0) return t;
+  if (shards < 1) shards = 1;
+  std::vector<uint32_t> pos((size_t)*std::max_element(seq.begin(), seq.end()) + 1, INVALID);
+  for (uint64_t i = 0; i < n; ++i) pos[seq[i]] = (uint32_t)i;
+  const uint64_t ps = pos.size();
+  // index.at(nbr) (jtree.cpp:75) throws when a sequenced vertex has a neighbour beyond
+  // max(seq); pst counts POSTORDER entries (jtree.cpp:84-90), unsequenced neighbours
+  // included (their index is INVALID); self-loops count nowhere.
+  bool oor = false;
+  uint32_t *w = t.pst.data();
+#pragma omp parallel for schedule(static) reduction(|| : oor)
+  for (uint64_t i = 0; i < R; ++i) {
+    const uint32_t u = tail[i], v = head[i];
+    const uint32_t pu = u < ps ? pos[u] : INVALID, pv = v < ps ? pos[v] : INVALID;
+    if ((pu != INVALID && v >= ps) || (pv != INVALID && u >= ps)) { oor = true; continue; }
+    if (u == v) continue;
+    if (pu != INVALID && (pv == INVALID || pu < pv)) __atomic_fetch_add(&w[pu], 1, __ATOMIC_RELAXED);
+    else if (pv != INVALID) __atomic_fetch_add(&w[pv], 1, __ATOMIC_RELAXED);
+  }
+  if (oor) throw std::out_of_range("vector::_M_range_check: index.at()");
+  std::vector<std::vector<uint32_t>> part(shards);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (uint64_t s = 0; s < shards; ++s) {
+    part[s].resize(n);
+    shardTree(tail, head, s * R / shards, (s + 1) * R / shards, pos, n, part[s].data());
+  }
+  for (uint64_t d = 1; d < shards; d *= 2) {   // MPI_Reduce's binomial rounds
+    std::vector<uint64_t> pairs;
+    for (uint64_t i = 0; i + d < shards; i += 2 * d) pairs.push_back(i);
+    auto merge = [&](uint64_t i) {
+      mergeParents(part[i].data(), part[i + d].data(), n, part[i].data());
+      std::vector<uint32_t>().swap(part[i + d]);
+    };
+    if (pairs.size() == 1) {
+      merge(pairs[0]);   // the last round groups its edges on every thread
+    } else {
+#pragma omp parallel for schedule(dynamic, 1)
+      for (uint64_t j = 0; j < pairs.size(); ++j) merge(pairs[j]);
+    }
+  }
+  t.parent.swap(part[0]);
   return t;
 }
 
@@ -578,6 +764,17 @@ int or_build_tree(const uint32_t *tail, const uint32_t *head, uint64_t R, uint64
   OR_TRY({
     LlamaGraph g(tail, head, R, part, num_parts);
     Tree t = buildTree(g, std::vector<uint32_t>(seq, seq + n));
+    std::copy(t.parent.begin(), t.parent.end(), parent);
+    std::copy(t.pst.begin(), t.pst.end(), pst);
+  })
+}
+
+// graph2tree -r form (shard trees on OpenMP threads + binomial merges); parent/pst of
+// length n.
+int or_build_tree_mr(const uint32_t *tail, const uint32_t *head, uint64_t R, const uint32_t *seq, uint64_t n,
+                     uint64_t shards, uint32_t *parent, uint32_t *pst) {
+  OR_TRY({
+    Tree t = buildTreeMapReduce(tail, head, R, std::vector<uint32_t>(seq, seq + n), shards);
     std::copy(t.parent.begin(), t.parent.end(), parent);
     std::copy(t.pst.begin(), t.pst.end(), pst);
   })

@@ -78,6 +78,7 @@ def lib() -> ctypes.CDLL:
         "sheep_last_error": ([], ctypes.c_char_p),
         "sheep_ctx_create": ([I32, P, ctypes.POINTER(P)], I32),
         "sheep_ctx_destroy": ([P], I32),
+        "sheep_ctx_trim": ([P], I32),
         "sheep_ctx_sync": ([P], I32),
         "sheep_ctx_stream": ([P], P),
         "sheep_malloc": ([P, ctypes.c_size_t, ctypes.POINTER(P)], I32),
@@ -108,10 +109,16 @@ def lib() -> ctypes.CDLL:
         "sheep_eval_finish": ([P, P, P, U64, P, I32, I32, ctypes.POINTER(_Eval)], I32),
         "sheep_edge_parts": ([P, P, U64, P, U64, P, P], I32),
         "sheep_group_create": ([P, I32, ctypes.POINTER(P)], I32),
+        "sheep_group_join": ([I32, I32, I32, ctypes.c_char_p, I32, I32, ctypes.POINTER(P)], I32),
         "sheep_group_destroy": ([P], I32),
         "sheep_group_size": ([P], I32),
+        "sheep_group_local_count": ([P], I32),
+        "sheep_group_rank": ([P, I32], I32),
         "sheep_group_ctx": ([P, I32], P),
         "sheep_group_uses_rccl": ([P], I32),
+        "sheep_group_barrier": ([P], I32),
+        "sheep_group_allreduce_max_u64": ([P, ctypes.POINTER(U64)], I32),
+        "sheep_group_reduce_trees": ([P, P, U64, I32], I32),
         "sheep_group_sequence": ([P, P, P, P, U64, P, P, ctypes.POINTER(U64), ctypes.POINTER(U64)], I32),
         "sheep_group_build_tree": ([P, P, P, P, U64, U64, P, I32], I32),
         "sheep_group_broadcast_parts": ([P, P, U64], I32),
@@ -167,6 +174,10 @@ class Context:
 
     def sync(self):
         _check(lib().sheep_ctx_sync(self.handle))
+
+    def trim(self):
+        """Free the context's device workspace (sheep_ctx_trim)."""
+        _check(lib().sheep_ctx_trim(self.handle))
 
     # device-side kernel timers (HIP events on the context stream)
     def timing(self, on: bool = True):
@@ -562,20 +573,43 @@ class _BorrowedContext(Context):
 
 
 class Group:
-    """One process driving several devices as the ranks of graph2tree's MPI world
-    (sheep_group_* in include/sheep_hip.h): RCCL between distinct devices, device copies
-    when a device is listed more than once (a rehearsal of several shards on one GPU)."""
+    """The ranks of graph2tree's MPI world (sheep_group_* in include/sheep_hip.h).
+
+    ``Group(devices)`` — this process drives every rank (rank r on devices[r]): RCCL
+    between distinct devices, device copies when a device is listed more than once.
+    ``Group.join(device, rank, world, host, port)`` — one process per rank (mpiexec /
+    torch.distributed ranks): this process holds one rank; RCCL when every rank has a
+    device of its own, host memory over TCP when ranks share one (``link``).
+
+    Per-rank arguments and results are lists over the ranks THIS process holds
+    (``self.local`` of them, global ranks ``self.ranks``)."""
 
     REDUCE = {"none": 0, "kway": 1, "binomial": 2}
+    LINK = {"auto": 0, "rccl": 1, "host": 2}
 
-    def __init__(self, devices):
-        self.devices = list(devices)
-        arr = (ctypes.c_int * len(self.devices))(*self.devices)
-        h = ctypes.c_void_p()
-        _check(lib().sheep_group_create(arr, len(self.devices), ctypes.byref(h)))
+    def __init__(self, devices=None, _handle=None):
+        if _handle is None:
+            self.devices = list(devices)
+            arr = (ctypes.c_int * len(self.devices))(*self.devices)
+            h = ctypes.c_void_p()
+            _check(lib().sheep_group_create(arr, len(self.devices), ctypes.byref(h)))
+        else:
+            h = _handle
+            self.devices = list(devices)
         self.handle = h
-        self.ctx = [_BorrowedContext(d, ctypes.c_void_p(lib().sheep_group_ctx(h, r)))
-                    for r, d in enumerate(self.devices)]
+        self.size = lib().sheep_group_size(h)
+        self.local = lib().sheep_group_local_count(h)
+        self.ranks = [lib().sheep_group_rank(h, i) for i in range(self.local)]
+        self.ctx = [_BorrowedContext(d, ctypes.c_void_p(lib().sheep_group_ctx(h, i)))
+                    for i, d in enumerate(self.devices)]
+
+    @classmethod
+    def join(cls, device: int, rank: int, world: int, host: str = "127.0.0.1", port: int = 29650,
+             link: str = "auto") -> "Group":
+        h = ctypes.c_void_p()
+        _check(lib().sheep_group_join(int(device), int(rank), int(world), host.encode(), int(port), cls.LINK[link],
+                                      ctypes.byref(h)))
+        return cls([device], _handle=h)
 
     @property
     def rccl(self) -> bool:
@@ -592,8 +626,8 @@ class Group:
         except Exception:
             pass
 
-    def _dev(self, r):
-        return f"cuda:{self.devices[r]}"
+    def _dev(self, i):
+        return f"cuda:{self.devices[i]}"
 
     def _ready(self):
         """The ranks run on streams of their own: finish torch's work on every device
@@ -602,45 +636,59 @@ class Group:
         for d in sorted(set(self.devices)):
             t.cuda.synchronize(d)
 
-    def sequence(self, shards, vs_cap: int):
-        """mpiSequence over the ranks' record shards: a Sequence per rank (all equal)."""
+    def barrier(self):
+        _check(lib().sheep_group_barrier(self.handle))
+
+    def allreduce_max(self, v: int) -> int:
+        x = ctypes.c_uint64(int(v))
+        _check(lib().sheep_group_allreduce_max_u64(self.handle, ctypes.byref(x)))
+        return x.value
+
+    def sequence(self, shards, vs_cap: int, deg=None, seq=None, pos=None):
+        """mpiSequence over the ranks' record shards: a Sequence per local rank (all
+        equal).  deg / seq / pos: optional per-rank buffers (deg zeroed) to reuse."""
         t = _torch()
-        P = len(self.devices)
-        deg = [t.zeros(max(vs_cap, 1), dtype=t.int32, device=self._dev(r)) for r in range(P)]
-        seq = [t.empty(max(vs_cap, 1), dtype=t.int32, device=self._dev(r)) for r in range(P)]
-        pos = [t.empty(max(vs_cap, 1), dtype=t.int32, device=self._dev(r)) for r in range(P)]
-        nrec = (ctypes.c_uint64 * P)(*[s.shape[0] for s in shards])
+        L = self.local
+        deg = deg or [t.zeros(max(vs_cap, 1), dtype=t.int32, device=self._dev(i)) for i in range(L)]
+        seq = seq or [t.empty(max(vs_cap, 1), dtype=t.int32, device=self._dev(i)) for i in range(L)]
+        pos = pos or [t.empty(max(vs_cap, 1), dtype=t.int32, device=self._dev(i)) for i in range(L)]
+        nrec = (ctypes.c_uint64 * L)(*[s.shape[0] for s in shards])
         n, vs = ctypes.c_uint64(), ctypes.c_uint64()
         self._ready()
         _check(lib().sheep_group_sequence(self.handle, _ptr_array(shards), nrec, _ptr_array(deg), vs_cap,
                                           _ptr_array(seq), _ptr_array(pos), ctypes.byref(n), ctypes.byref(vs)))
-        return [Sequence(seq[r], pos[r], n.value, vs.value) for r in range(P)]
+        return [Sequence(seq[i], pos[i], n.value, vs.value) for i in range(L)]
 
-    def build_tree(self, shards, seqs, reduce: str = "kway"):
-        """JTree per shard + mpi_merge: the merged tree (rank 0's device) for kway/binomial,
-        every rank's partial tree for "none"."""
+    def build_tree(self, shards, seqs, reduce: str = "kway", trees=None):
+        """JTree per shard + mpi_merge: per local rank its tree — rank 0's is the merged
+        tree for kway / binomial, every tree is the rank's partial tree for "none"."""
         t = _torch()
-        P = len(self.devices)
+        L = self.local
         n = seqs[0].n
-        trees = [t.empty((max(n, 1), 2), dtype=t.int32, device=self._dev(r)) for r in range(P)]
-        nrec = (ctypes.c_uint64 * P)(*[s.shape[0] for s in shards])
+        trees = trees or [t.empty((max(n, 1), 2), dtype=t.int32, device=self._dev(i)) for i in range(L)]
+        nrec = (ctypes.c_uint64 * L)(*[s.shape[0] for s in shards])
         self._ready()
         _check(lib().sheep_group_build_tree(self.handle, _ptr_array(shards), nrec, _ptr_array([s.pos for s in seqs]),
                                             seqs[0].pos_size, n, _ptr_array(trees), self.REDUCE[reduce]))
-        return [x[:n] for x in trees] if reduce == "none" else trees[0][:n]
+        return [x[:n] for x in trees]
 
-    def broadcast_parts(self, parts0, pos_size: int):
-        """Partition::mpi_sync: rank 0's parts on every rank."""
-        t = _torch()
-        P = len(self.devices)
-        parts = [parts0] + [t.empty(max(pos_size, 1), dtype=t.int16, device=self._dev(r)) for r in range(1, P)]
+    def reduce_trees(self, trees, reduce: str = "kway"):
+        """The reduction step alone over the local ranks' partial trees (in place)."""
+        self._ready()
+        _check(lib().sheep_group_reduce_trees(self.handle, _ptr_array(trees), trees[0].shape[0], self.REDUCE[reduce]))
+        return trees
+
+    def broadcast_parts(self, parts, pos_size: int):
+        """Partition::mpi_sync: rank 0's parts to every rank.  `parts` lists one int16
+        tensor (pos_size entries) per local rank; rank 0's holds the parts."""
         self._ready()
         _check(lib().sheep_group_broadcast_parts(self.handle, _ptr_array(parts), pos_size))
         return [p[:pos_size] for p in parts]
 
     def evaluate(self, shards, seqs, parts, what: int = 0) -> "EvalResult":
-        P = len(self.devices)
-        nrec = (ctypes.c_uint64 * P)(*[s.shape[0] for s in shards])
+        """The evaluator over the shards; the counts are rank 0's (zero elsewhere)."""
+        L = self.local
+        nrec = (ctypes.c_uint64 * L)(*[s.shape[0] for s in shards])
         out = _Eval()
         self._ready()
         _check(lib().sheep_group_evaluate(self.handle, _ptr_array(shards), nrec, _ptr_array([s.pos for s in seqs]),

@@ -5,11 +5,11 @@
 //
 // Phases (graph2tree.cpp:161-218): load the records into HBM, degree sequence (or -s
 // read), map (JTree on the GPU), [reduce], [partition], [TREEFAQS].  -i / -r select the
-// reference's MPI sort / reduce: here ONE process plays the MPI world, rank r on device r
-// of SHEEP_DEVICES (default: every visible GPU; a device listed twice rehearses two
-// shards on it) — edge shards, an RCCL all-reduce of the degrees, per-GPU partial trees,
-// the merge on rank 0, the parts broadcast and per-rank partition files, with the
-// reference's file names (sheep/world.hpp, include/sheep_hip.h sheep_group_*).  With one
+// reference's MPI sort / reduce over a world of GPUs (sheep/world.hpp): one process per
+// rank under `mpiexec -n W` (or torchrun), exactly the reference's launch, or one process
+// driving the ranks of SHEEP_DEVICES — edge shards, an RCCL all-reduce of the degrees,
+// per-GPU partial trees, the merge on rank 0, the parts broadcast and per-rank partition
+// files, with the reference's file names (include/sheep_hip.h sheep_group_*).  With one
 // rank the single-GPU path runs.  Flags of the junction-tree experiments (-e -j -m -w -x)
 // and -t are rejected with a message.
 #include <unistd.h>
@@ -37,63 +37,62 @@ static bool tree_valid(const std::vector<sheep_jnode> &nodes, uint64_t n, uint64
   return ok;
 }
 
-// The -i / -r MPI world over several GPUs (graph2tree.cpp:134-216).
-static int run_world(const std::vector<int> &devs, const char *graph_filename, bool use_mpi_sort, bool use_mpi_reduce,
+// The -i / -r MPI world over several GPUs (graph2tree.cpp:134-216).  This process holds
+// w.local() of the w.size() ranks (all of them without a launcher, one under mpiexec).
+static int run_world(World &w, const char *graph_filename, bool use_mpi_sort, bool use_mpi_reduce,
                      size_t partitions, const char *sequence_filename, const char *output_filename, bool verbose,
                      bool do_faqs, bool do_validate, std::chrono::steady_clock::time_point start_point) {
-  World w(devs);
-  const int P = w.size();
-  if (partitions != 0 && !use_mpi_reduce) {
-    printf("graph2tree: -p with -i needs -r (the ranks' partial trees are merged before partitioning).\n");
-    return 1;
-  }
+  const int P = w.size(), L = w.local();
   if (!use_mpi_sort && strcmp(sequence_filename, "") == 0) {
     printf("graph2tree: -r needs -i or -s SEQ (every rank must use the same sequence).\n");
     return 1;
   }
+  const bool leader_here = w.rank(0) == 0;   // rank 0 prints (graph2tree.cpp:158-159)
   if (verbose) printf("Loading %s...\n", graph_filename);
   std::vector<sheep_xs1> all;
   if (is_dat(graph_filename)) {
     all = readRecords(graph_filename);
-  } else {   // SNAP text, parsed on rank 0's GPU
+  } else {   // SNAP text, parsed on the first local rank's GPU
     uint64_t nr = 0;
     DeviceArray<sheep_xs1> d = parseNet(graph_filename, true, &nr, w.ctx(0));
     all.resize(nr);
     if (nr) d.download(all.data(), nr);
   }
   const uint64_t R = all.size();
-  std::vector<RankState> rk(P);
-  uint64_t cap = 1;
-  for (int r = 0; r < P; ++r) {   // rank r loads part r+1 of P (graph2tree.cpp:137-143, 162)
+  uint64_t cap = 1;   // the degree array's capacity: the same on every rank
+  for (const sheep_xs1 &x : all) cap = std::max<uint64_t>(cap, (uint64_t)std::max(x.tail, x.head) + 1);
+  std::vector<RankState> rk(L);
+  for (int i = 0; i < L; ++i) {   // rank r loads part r+1 of P (graph2tree.cpp:137-143, 162)
+    const int r = w.rank(i);
     const uint64_t beg = (uint64_t)r * R / P, end = (uint64_t)(r + 1) * R / P;
-    rk[r].host.assign(all.begin() + beg, all.begin() + end);
-    rk[r].rec = DeviceArray<sheep_xs1>(end - beg, w.ctx(r));
-    if (end > beg) rk[r].rec.upload(rk[r].host.data(), end - beg);
-    for (const sheep_xs1 &x : rk[r].host)
-      rk[r].max_vid = std::max<uint64_t>(rk[r].max_vid, (uint64_t)std::max(x.tail, x.head) + 1);
-    cap = std::max(cap, rk[r].max_vid);
+    rk[i].rank = r;
+    rk[i].host.assign(all.begin() + beg, all.begin() + end);
+    rk[i].rec = DeviceArray<sheep_xs1>(end - beg, w.ctx(i));
+    if (end > beg) rk[i].rec.upload(rk[i].host.data(), end - beg);
+    for (const sheep_xs1 &x : rk[i].host)
+      rk[i].max_vid = std::max<uint64_t>(rk[i].max_vid, (uint64_t)std::max(x.tail, x.head) + 1);
   }
-  const bool is_leader = true;   // rank 0 prints (graph2tree.cpp:158-159)
+  std::vector<sheep_xs1>().swap(all);
   const double load_s = seconds_since(start_point);
-  if (is_leader) printf("Loaded graph in: %f seconds\n", load_s);
+  if (leader_here) printf("Loaded graph in: %f seconds\n", load_s);
 
-  std::vector<const sheep_xs1 *> recp(P);
-  std::vector<uint64_t> nrec(P);
-  std::vector<uint32_t *> seqp(P), posp(P), degp(P);
-  for (int r = 0; r < P; ++r) { recp[r] = rk[r].rec.get(); nrec[r] = rk[r].host.size(); }
+  std::vector<const sheep_xs1 *> recp(L);
+  std::vector<uint64_t> nrec(L);
+  std::vector<uint32_t *> seqp(L), posp(L), degp(L);
+  for (int i = 0; i < L; ++i) { recp[i] = rk[i].rec.get(); nrec[i] = rk[i].host.size(); }
   uint64_t n = 0, pos_size = 0;
   if (use_mpi_sort) {   // mpiSequence (sequence.h:65-93)
     const std::vector<uint32_t> zero(cap, 0);
-    for (int r = 0; r < P; ++r) {
-      rk[r].deg = DeviceArray<uint32_t>(cap, w.ctx(r));
-      rk[r].deg.upload(zero.data(), cap);
-      rk[r].seq = DeviceArray<uint32_t>(cap, w.ctx(r));
-      rk[r].pos = DeviceArray<uint32_t>(cap, w.ctx(r));
-      degp[r] = rk[r].deg.get(); seqp[r] = rk[r].seq.get(); posp[r] = rk[r].pos.get();
+    for (int i = 0; i < L; ++i) {
+      rk[i].deg = DeviceArray<uint32_t>(cap, w.ctx(i));
+      rk[i].deg.upload(zero.data(), cap);
+      rk[i].seq = DeviceArray<uint32_t>(cap, w.ctx(i));
+      rk[i].pos = DeviceArray<uint32_t>(cap, w.ctx(i));
+      degp[i] = rk[i].deg.get(); seqp[i] = rk[i].seq.get(); posp[i] = rk[i].pos.get();
     }
     check(sheep_group_sequence(w.handle(), recp.data(), nrec.data(), degp.data(), cap, seqp.data(), posp.data(), &n,
                                &pos_size));
-    if (strcmp(sequence_filename, "") != 0) {   // rank 0 writes it (graph2tree.cpp:177-178)
+    if (leader_here && strcmp(sequence_filename, "") != 0) {   // rank 0 writes it (graph2tree.cpp:177-178)
       std::vector<vid_t> h(n);
       if (n) rk[0].seq.download(h.data(), n);
       writeSequence(h, sequence_filename);
@@ -102,74 +101,85 @@ static int run_world(const std::vector<int> &devs, const char *graph_filename, b
     const std::vector<vid_t> h = readSequence(sequence_filename);
     n = h.size();
     pos_size = h.empty() ? 0 : (uint64_t)*std::max_element(h.begin(), h.end()) + 1;
-    for (int r = 0; r < P; ++r) {
-      rk[r].seq = DeviceArray<uint32_t>(n, w.ctx(r));
-      if (n) rk[r].seq.upload(h.data(), n);
-      rk[r].pos = DeviceArray<uint32_t>(pos_size, w.ctx(r));
-      check(sheep_positions(w.ctx(r), rk[r].seq.get(), n, rk[r].pos.get(), pos_size));
-      posp[r] = rk[r].pos.get();
+    for (int i = 0; i < L; ++i) {
+      rk[i].seq = DeviceArray<uint32_t>(n, w.ctx(i));
+      if (n) rk[i].seq.upload(h.data(), n);
+      rk[i].pos = DeviceArray<uint32_t>(pos_size, w.ctx(i));
+      check(sheep_positions(w.ctx(i), rk[i].seq.get(), n, rk[i].pos.get(), pos_size));
+      posp[i] = rk[i].pos.get();
     }
   }
   const double sort_s = seconds_since(start_point) - load_s;
-  if (is_leader && (use_mpi_sort || strcmp(sequence_filename, "") == 0)) printf("Sorted in: %f seconds\n", sort_s);
+  if (leader_here && (use_mpi_sort || strcmp(sequence_filename, "") == 0)) printf("Sorted in: %f seconds\n", sort_s);
 
-  std::vector<sheep_jnode *> treep(P);
-  for (int r = 0; r < P; ++r) { rk[r].tree = DeviceArray<sheep_jnode>(n, w.ctx(r)); treep[r] = rk[r].tree.get(); }
+  std::vector<sheep_jnode *> treep(L);
+  for (int i = 0; i < L; ++i) { rk[i].tree = DeviceArray<sheep_jnode>(n, w.ctx(i)); treep[i] = rk[i].tree.get(); }
   std::vector<const uint32_t *> cposp(posp.begin(), posp.end());
   check(sheep_group_build_tree(w.handle(), recp.data(), nrec.data(), cposp.data(), pos_size, n, treep.data(), 0));
   const double map_s = seconds_since(start_point) - sort_s - load_s;
-  if (is_leader) printf("Mapped in: %f seconds\n", map_s);
+  if (leader_here) printf("Mapped in: %f seconds\n", map_s);
   if (use_mpi_reduce) {   // mpi_merge (jnode.cpp:213-250): gather + one K-way merge on rank 0
     check(sheep_group_reduce_trees(w.handle(), treep.data(), n, 1));
     const double reduce_s = seconds_since(start_point) - map_s - sort_s - load_s;
-    if (is_leader) printf("Reduced in: %f seconds\n", reduce_s);
+    if (leader_here) printf("Reduced in: %f seconds\n", reduce_s);
   }
 
+  // graph2tree.cpp:144-156: -i alone maps rank r into OUTPUTrr r0.tre (its partition files
+  // too), -r -p writes PREFIX-wRRRR-pPPPP
+  auto rank_output = [&](int r) {
+    char buf[4096];
+    if (!use_mpi_reduce) snprintf(buf, sizeof buf, "%s%02dr0.tre", output_filename, r);
+    else if (partitions != 0) snprintf(buf, sizeof buf, "%s-w%04d-p", output_filename, r);
+    else snprintf(buf, sizeof buf, "%s", output_filename);
+    return std::string(buf);
+  };
   if (partitions != 0) {   // graph2tree.cpp:203-213
-    sheep_kids *kids = nullptr;
-    check(sheep_kids_create(w.ctx(0), rk[0].tree.get(), n, &kids));
-    std::vector<int16_t *> partp(P);
-    for (int r = 0; r < P; ++r) { rk[r].parts = DeviceArray<int16_t>(pos_size, w.ctx(r)); partp[r] = rk[r].parts.get(); }
+    std::vector<int16_t *> partp(L);
+    for (int i = 0; i < L; ++i) { rk[i].parts = DeviceArray<int16_t>(pos_size, w.ctx(i)); partp[i] = rk[i].parts.get(); }
     sheep_partition_info info{};
-    const int rc = sheep_partition(w.ctx(0), rk[0].tree.get(), n, rk[0].seq.get(), n, pos_size, kids, (int16_t)partitions,
-                                   1.03, 0, 1, rk[0].parts.get(), &info);
-    sheep_kids_destroy(kids);
-    check(rc);
-    check(sheep_group_broadcast_parts(w.handle(), partp.data(), pos_size));   // p.mpi_sync()
-    if (strcmp(output_filename, "") != 0) {   // every rank writes its shard: PREFIX-wRRRR-pPPPP
-      std::vector<int16_t> pv(pos_size);
-      if (pos_size) rk[0].parts.download(pv.data(), pos_size);
-      part_t max_part = -1;
-      for (part_t x : pv) max_part = std::max(max_part, x);
-      for (int r = 0; r < P; ++r) {
-        DeviceArray<int16_t> ep(nrec[r], w.ctx(r));
-        check(sheep_edge_parts(w.ctx(r), rk[r].rec.get(), nrec[r], rk[r].pos.get(), pos_size, rk[r].parts.get(), ep.get()));
-        std::vector<int16_t> eh(nrec[r]);
-        if (nrec[r]) ep.download(eh.data(), nrec[r]);
-        char prefix[4096];
-        snprintf(prefix, sizeof prefix, "%s-w%04d-p", output_filename, r);   // graph2tree.cpp:151-156
-        write_partition_files(rk[r].host, eh, max_part, rk[r].max_vid, prefix, false, false);
+    // with -r rank 0 partitions the merged tree and mpi_sync broadcasts it; without, every
+    // rank partitions its own partial tree
+    for (int i = 0; i < L; ++i) {
+      if (use_mpi_reduce && rk[i].rank != 0) continue;
+      sheep_kids *kids = nullptr;
+      check(sheep_kids_create(w.ctx(i), rk[i].tree.get(), n, &kids));
+      sheep_partition_info inf{};
+      const int rc = sheep_partition(w.ctx(i), rk[i].tree.get(), n, rk[i].seq.get(), n, pos_size, kids,
+                                     (int16_t)partitions, 1.03, 0, 1, rk[i].parts.get(), &inf);
+      sheep_kids_destroy(kids);
+      check(rc);
+      if (rk[i].rank == 0) info = inf;
+    }
+    if (use_mpi_reduce) check(sheep_group_broadcast_parts(w.handle(), partp.data(), pos_size));   // p.mpi_sync()
+    if (strcmp(output_filename, "") != 0) {   // every rank writes its shard's files
+      for (int i = 0; i < L; ++i) {
+        std::vector<int16_t> pv(pos_size);
+        if (pos_size) rk[i].parts.download(pv.data(), pos_size);
+        part_t max_part = -1;
+        for (part_t x : pv) max_part = std::max(max_part, x);
+        DeviceArray<int16_t> ep(nrec[i], w.ctx(i));
+        check(sheep_edge_parts(w.ctx(i), rk[i].rec.get(), nrec[i], rk[i].pos.get(), pos_size, rk[i].parts.get(),
+                               ep.get()));
+        std::vector<int16_t> eh(nrec[i]);
+        if (nrec[i]) ep.download(eh.data(), nrec[i]);
+        write_partition_files(rk[i].host, eh, max_part, rk[i].max_vid, rank_output(rk[i].rank).c_str(), false, false);
       }
-    } else if (is_leader) {
+    } else if (leader_here) {
       printf("Actually created %d partitions.\n", (int)info.created);
       printf("First two partition sizes: %zu and %zu\n", (size_t)info.first_size, (size_t)info.second_size);
     }
   } else if (strcmp(output_filename, "") != 0) {
-    if (use_mpi_reduce) {   // rank 0 saves the merged tree (graph2tree.cpp:217-218)
+    for (int i = 0; i < L; ++i) {
+      if (use_mpi_reduce && rk[i].rank != 0) continue;   // rank 0 saves the merged tree (:217-218)
       JNodeTable t;
-      t.assign_from_device(rk[0].tree, (jnid_t)n, (jnid_t)n);
-      t.save(output_filename);
-    } else {   // -i alone: every rank maps its shard into OUTPUTrrr0.tre (graph2tree.cpp:144-149)
-      for (int r = 0; r < P; ++r) {
-        char name[4096];
-        snprintf(name, sizeof name, "%s%02dr0.tre", output_filename, r);
-        JNodeTable t;
-        t.assign_from_device(rk[r].tree, (jnid_t)n, (jnid_t)n);
-        t.save(name);
-      }
+      t.assign_from_device(rk[i].tree, (jnid_t)n, (jnid_t)n);
+      t.save(rank_output(rk[i].rank).c_str());
     }
   }
+  w.barrier();   // MPI_Finalize
   if (verbose) printf("Built in: %f seconds\n", seconds_since(start_point));
+  // every rank prints its own tree's facts (rank 0's is the merged one); a process holding
+  // several ranks prints its first one's
   if (do_faqs || do_validate) {
     Facts f;
     check(sheep_facts(w.ctx(0), rk[0].tree.get(), n, &f.f));
@@ -232,9 +242,9 @@ int main(int argc, char *argv[]) {
 
   if (use_mpi_sort || use_mpi_reduce) {
     try {
-      const std::vector<int> devs = world_devices();
-      if (devs.size() > 1)
-        return run_world(devs, graph_filename, use_mpi_sort, use_mpi_reduce, partitions, sequence_filename,
+      std::unique_ptr<World> w = World::from_env();
+      if (w->size() > 1)
+        return run_world(*w, graph_filename, use_mpi_sort, use_mpi_reduce, partitions, sequence_filename,
                          output_filename, verbose, do_faqs, do_validate, start_point);
     } catch (const std::out_of_range &e) {
       fprintf(stderr, "terminate called after throwing an instance of 'std::out_of_range'\n  what():  %s\n", e.what());

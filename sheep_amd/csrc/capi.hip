@@ -96,6 +96,21 @@ int sheep_ctx_create(int device, void *hip_stream, sheep_ctx **out) {
   API_END
 }
 
+int sheep_ctx_trim(sheep_ctx *ctx) {
+  API_BEGIN
+  DeviceGuard dg(ctx);
+  NEED(ctx, "null context");
+  sheep::Ctx &c = ctx->c;
+  HIP_CHECK(hipSetDevice(c.device));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  for (auto &kv : c.ws) if (kv.second.p) HIP_CHECK(hipFree(kv.second.p));
+  c.ws.clear();
+  c.head_layout = sheep::Ctx::HeadLayout();   // its offsets lived in the workspace
+  if (c.kid_spare.parent) { hipFree(c.kid_spare.parent); hipFree(c.kid_spare.koff); hipFree(c.kid_spare.kids); }
+  c.kid_spare = sheep::Ctx::KidBufs();
+  API_END
+}
+
 int sheep_ctx_destroy(sheep_ctx *ctx) {
   API_BEGIN
   DeviceGuard dg(ctx);
@@ -290,19 +305,7 @@ int sheep_kids_destroy(sheep_kids *k) {
   int prev = -1;
   if (k->ctx && hipGetDevice(&prev) == hipSuccess && prev != k->ctx->device) HIP_CHECK(hipSetDevice(k->ctx->device));
   else prev = -1;
-  sheep::Ctx::KidBufs *sp = k->ctx ? &k->ctx->kid_spare : nullptr;
-  if (sp && k->parent && k->koff && k->kids && (!sp->parent || sp->cap < k->cap)) {
-    if (sp->parent) {   // keep the larger table's buffers
-      k->ctx->sync();
-      hipFree(sp->parent); hipFree(sp->koff); hipFree(sp->kids);
-    }
-    *sp = {k->parent, k->koff, k->kids, k->cap};
-  } else {
-    if (k->ctx) k->ctx->sync();
-    hipFree(k->parent);
-    hipFree(k->koff);
-    hipFree(k->kids);
-  }
+  sheep::release_kids(k->ctx, k);
   delete k;
   if (prev >= 0) HIP_CHECK(hipSetDevice(prev));
   API_END

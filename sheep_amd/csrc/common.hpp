@@ -223,8 +223,8 @@ template <typename T> __device__ __forceinline__ T wave_min(T v) {
 // One atomic per workgroup for a value every thread contributes (every thread of the
 // workgroup calls; blockDim.x a multiple of 64, <= 1024).  Per-wave atomics on one word
 // serialise a launch of ~1e5 workgroups (k_compact_count: 1.5 ms for 1.3e5 of them).
-// The max skips its atomic when a plain read already shows a value >= v (the word only
-// grows; a stale read is smaller, so nothing is lost).
+// Both always issue their one atomic: a load-before-atomic check could be served a stale
+// line from another XCD's L2 (coherence across XCDs).
 __device__ __forceinline__ uint64_t block_reduce_u64(uint64_t v, bool is_max) {
   __shared__ uint64_t s_red[16];
   v = is_max ? wave_max(v) : wave_sum(v);
@@ -238,8 +238,7 @@ __device__ __forceinline__ uint64_t block_reduce_u64(uint64_t v, bool is_max) {
 }
 __device__ __forceinline__ void block_atomic_max(unsigned long long *dst, uint64_t v) {
   const uint64_t m = block_reduce_u64(v, true);
-  if (threadIdx.x == 0 && m && m > __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-    atomicMax(dst, (unsigned long long)m);
+  if (threadIdx.x == 0 && m) atomicMax(dst, (unsigned long long)m);
 }
 __device__ __forceinline__ void block_atomic_add(unsigned long long *dst, uint64_t v) {
   const uint64_t m = block_reduce_u64(v, false);

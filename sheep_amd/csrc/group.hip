@@ -1,35 +1,53 @@
 // group.hip — several GPUs of one node as one Sheep "world": the MI355X replacement of
 // graph2tree's MPI -i / -r path (graph2tree.cpp:134-216).
 //
-// One process drives every device (one context and stream per rank, one host thread
-// per rank for the per-shard compute).  Exchanges between distinct devices go over RCCL
-// (one communicator clique from ncclCommInitAll, xGMI); a device listed more than once
-// (several shards rehearsed on one GPU) exchanges by device-to-device copies instead.
+// A world has `world` ranks; rank r owns edge shard r on one device.  Two ways to run it:
+//   * one process drives every rank (sheep_group_create): a context and stream per rank,
+//     one host thread per rank for the per-shard compute;
+//   * one process per rank (sheep_group_join): `mpiexec -n W graph2tree ... -ir`, or one
+//     rank per torch.distributed process in bench.py.  The processes meet over TCP
+//     (mesh.hpp), which carries the RCCL bootstrap, barriers and host scalars.
+// The algorithm is written once, over the ranks this process holds ("local" ranks):
+// every exchange below names global ranks and does only its local side.
+//
+// Transports (the same for both ways, chosen when the world is formed):
+//   RCCL   — every rank on a distinct device: ncclSend/ncclRecv, ncclAllReduce and
+//            ncclBroadcast over xGMI (ncclCommInitAll in one process, ncclCommInitRank
+//            with rank 0's unique id across processes);
+//   copy   — one process, a device listed more than once: device-to-device copies;
+//   host   — one process per rank, devices repeated (a one-GPU rehearsal of W ranks):
+//            device -> host -> TCP -> host -> device.
 //
 //   reference (MPI)                               here
-//   MPI_Allreduce(MAX / SUM) in mpiSequence       sheep_group_sequence: ncclAllReduce of the
-//     (sequence.h:72,78)                          degree histograms, host max of max_slot
+//   MPI_Allreduce(MAX / SUM) in mpiSequence       sheep_group_sequence: all-reduce of the
+//     (sequence.h:72,78)                          degree histograms, max of max_slot
 //   MPI_Reduce(mpi_merge_reduction)               sheep_group_build_tree: a gather of the
 //     (jnode.cpp:203-250)                         partial trees + ONE K-way merge on rank 0,
 //                                                 or binomial rounds of pairwise merges on
-//                                                 disjoint device pairs (ncclSend/ncclRecv)
-//   Partition::mpi_sync (partition.cpp:69-79)     sheep_group_broadcast_parts: ncclBroadcast
+//                                                 disjoint rank pairs
+//   Partition::mpi_sync (partition.cpp:69-79)     sheep_group_broadcast_parts
 //   (evaluate on one rank)                        sheep_group_evaluate: per-shard bitsets,
 //                                                 binomial OR-reduction, node pass on rank 0
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <functional>
+#include <memory>
 #include <thread>
 #include <vector>
 
 #include "common.hpp"
+#include "mesh.hpp"
 
 struct sheep_group {
-  std::vector<sheep_ctx *> ctx;
-  std::vector<int> dev;
-  std::vector<ncclComm_t> comm;   // empty: copy transport
+  std::vector<sheep_ctx *> ctx;   // the local ranks' contexts
+  std::vector<int> dev;           // their devices
+  std::vector<int> rank;          // their global ranks
+  int world = 0;
+  std::vector<ncclComm_t> comm;   // per local rank when RCCL carries the data
+  std::unique_ptr<sheep::Mesh> mesh;   // one process per rank
 };
 
 namespace sheep {
@@ -62,27 +80,33 @@ __global__ void k_add_u32(uint32_t *__restrict__ dst, const uint32_t *__restrict
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) dst[i] += src[i];
 }
 
-Ctx &C(sheep_group *g, int r) { return g->ctx[r]->c; }
-int size(const sheep_group *g) { return (int)g->ctx.size(); }
+Ctx &C(sheep_group *g, int li) { return g->ctx[li]->c; }
+int nlocal(const sheep_group *g) { return (int)g->ctx.size(); }
+// local index of global rank r, -1 when another process holds it
+int local_of(const sheep_group *g, int r) {
+  if (!g->mesh) return r;
+  return r == g->rank[0] ? 0 : -1;
+}
+bool host_transport(const sheep_group *g) { return g->mesh && g->comm.empty(); }
 
-// Runs f(rank) on one host thread per rank (each on its rank's device) and rethrows the
-// first failure.
+// Runs f(local index) on one host thread per local rank (each on its rank's device) and
+// rethrows the first failure.
 void per_rank(sheep_group *g, const std::function<void(int)> &f) {
-  const int P = size(g);
-  if (P == 1) {
+  const int L = nlocal(g);
+  if (L == 1) {
     HIP_CHECK(hipSetDevice(g->dev[0]));
     f(0);
     return;
   }
-  std::vector<std::exception_ptr> err(P);
+  std::vector<std::exception_ptr> err(L);
   std::vector<std::thread> th;
-  for (int r = 0; r < P; ++r)
-    th.emplace_back([&, r]() {
+  for (int i = 0; i < L; ++i)
+    th.emplace_back([&, i]() {
       try {
-        HIP_CHECK(hipSetDevice(g->dev[r]));
-        f(r);
+        HIP_CHECK(hipSetDevice(g->dev[i]));
+        f(i);
       } catch (...) {
-        err[r] = std::current_exception();
+        err[i] = std::current_exception();
       }
     });
   for (auto &t : th) t.join();
@@ -91,30 +115,82 @@ void per_rank(sheep_group *g, const std::function<void(int)> &f) {
 }
 
 void sync_all(sheep_group *g) {
-  for (int r = 0; r < size(g); ++r) {
-    HIP_CHECK(hipSetDevice(g->dev[r]));
-    C(g, r).sync();
+  for (int i = 0; i < nlocal(g); ++i) {
+    HIP_CHECK(hipSetDevice(g->dev[i]));
+    C(g, i).sync();
   }
 }
 
-// bytes from rank `from` (src on its device) to rank `to` (dst on its device)
+// bytes from rank `from` to rank `to` (global ranks): `src` is meaningful where `from` is
+// local, `dst` where `to` is local.
 struct Xfer { int from, to; const void *src; void *dst; size_t bytes; };
 
+// Host transport: device -> host -> socket; sends on a helper thread, receives here.
+void host_transfer(sheep_group *g, const std::vector<Xfer> &xs) {
+  const int me = g->rank[0];
+  std::vector<const Xfer *> out, in;
+  for (const Xfer &x : xs) {
+    if (x.from == me && x.to != me) out.push_back(&x);
+    if (x.to == me && x.from != me) in.push_back(&x);
+  }
+  Ctx &c = C(g, 0);
+  HIP_CHECK(hipSetDevice(g->dev[0]));
+  c.sync();
+  std::exception_ptr serr;
+  std::thread sender([&]() {
+    try {
+      HIP_CHECK(hipSetDevice(g->dev[0]));
+      std::vector<char> buf;
+      for (const Xfer *x : out) {
+        buf.resize(x->bytes);
+        HIP_CHECK(hipMemcpy(buf.data(), x->src, x->bytes, hipMemcpyDeviceToHost));
+        g->mesh->send(x->to, buf.data(), x->bytes);
+      }
+    } catch (...) {
+      serr = std::current_exception();
+    }
+  });
+  std::exception_ptr rerr;
+  try {
+    std::vector<char> buf;
+    for (const Xfer *x : in) {
+      buf.resize(x->bytes);
+      g->mesh->recv(x->from, buf.data(), x->bytes);
+      HIP_CHECK(hipMemcpy(x->dst, buf.data(), x->bytes, hipMemcpyHostToDevice));
+    }
+  } catch (...) {
+    rerr = std::current_exception();
+  }
+  sender.join();
+  for (const Xfer &x : xs)   // a transfer within this process (never issued today)
+    if (x.from == me && x.to == me)
+      HIP_CHECK(hipMemcpyAsync(x.dst, x.src, x.bytes, hipMemcpyDeviceToDevice, c.stream));
+  if (serr) std::rethrow_exception(serr);
+  if (rerr) std::rethrow_exception(rerr);
+  c.sync();
+}
+
 // A set of point-to-point transfers issued together (one RCCL group: every pair on its
-// own xGMI link), complete on return.
+// own xGMI link), complete on return.  Every rank calls it with the same list.
 void transfer(sheep_group *g, const std::vector<Xfer> &xs) {
   if (xs.empty()) return;
   if (!g->comm.empty()) {
+    sync_all(g);   // the sources are complete (they may come from other streams)
     NCCL_CHECK(ncclGroupStart());
     for (const Xfer &x : xs) {
-      NCCL_CHECK(ncclSend(x.src, x.bytes, ncclUint8, x.to, g->comm[x.from], C(g, x.from).stream));
-      NCCL_CHECK(ncclRecv(x.dst, x.bytes, ncclUint8, x.from, g->comm[x.to], C(g, x.to).stream));
+      const int lf = local_of(g, x.from), lt = local_of(g, x.to);
+      if (lf >= 0) NCCL_CHECK(ncclSend(x.src, x.bytes, ncclUint8, x.to, g->comm[lf], C(g, lf).stream));
+      if (lt >= 0) NCCL_CHECK(ncclRecv(x.dst, x.bytes, ncclUint8, x.from, g->comm[lt], C(g, lt).stream));
     }
     NCCL_CHECK(ncclGroupEnd());
     sync_all(g);
     return;
   }
-  sync_all(g);   // the sources are complete before another stream copies them
+  if (host_transport(g)) {
+    host_transfer(g, xs);
+    return;
+  }
+  sync_all(g);   // copy transport: the sources are complete before another stream copies them
   for (const Xfer &x : xs) {
     HIP_CHECK(hipSetDevice(g->dev[x.to]));
     if (g->dev[x.from] == g->dev[x.to])
@@ -125,46 +201,76 @@ void transfer(sheep_group *g, const std::vector<Xfer> &xs) {
   sync_all(g);
 }
 
-// In-place sum of one u32 array per rank (the degree all-reduce).
+// In-place sum of one u32 array per rank (the degree all-reduce); buf[li] per local rank.
 void allreduce_sum_u32(sheep_group *g, uint32_t *const *buf, uint64_t count) {
-  const int P = size(g);
+  const int P = g->world;
   if (P == 1 || count == 0) return;
   if (!g->comm.empty()) {
+    sync_all(g);
     NCCL_CHECK(ncclGroupStart());
-    for (int r = 0; r < P; ++r)
-      NCCL_CHECK(ncclAllReduce(buf[r], buf[r], count, ncclUint32, ncclSum, g->comm[r], C(g, r).stream));
+    for (int i = 0; i < nlocal(g); ++i)
+      NCCL_CHECK(ncclAllReduce(buf[i], buf[i], count, ncclUint32, ncclSum, g->comm[i], C(g, i).stream));
     NCCL_CHECK(ncclGroupEnd());
     sync_all(g);
     return;
   }
-  HIP_CHECK(hipSetDevice(g->dev[0]));
-  uint32_t *tmp = C(g, 0).get_as<uint32_t>("grp_reduce_tmp", count);
+  // reduce to rank 0, one rank at a time into a scratch array, then broadcast
+  const int l0 = local_of(g, 0);
+  uint32_t *tmp = nullptr;
+  if (l0 >= 0) {
+    HIP_CHECK(hipSetDevice(g->dev[l0]));
+    tmp = C(g, l0).get_as<uint32_t>("grp_reduce_tmp", count);
+  }
   for (int r = 1; r < P; ++r) {
-    transfer(g, {Xfer{r, 0, buf[r], tmp, count * sizeof(uint32_t)}});
-    HIP_CHECK(hipSetDevice(g->dev[0]));
-    hipLaunchKernelGGL(k_add_u32, dim3(grid_for(count)), dim3(BLOCK), 0, C(g, 0).stream, buf[0], (const uint32_t *)tmp,
-                       count);
-    LAUNCH_CHECK();
+    const int lr = local_of(g, r);
+    transfer(g, {Xfer{r, 0, lr >= 0 ? buf[lr] : nullptr, tmp, count * sizeof(uint32_t)}});
+    if (l0 >= 0) {
+      HIP_CHECK(hipSetDevice(g->dev[l0]));
+      hipLaunchKernelGGL(k_add_u32, dim3(grid_for(count)), dim3(BLOCK), 0, C(g, l0).stream, buf[l0],
+                         (const uint32_t *)tmp, count);
+      LAUNCH_CHECK();
+    }
   }
   std::vector<Xfer> xs;
-  for (int r = 1; r < P; ++r) xs.push_back(Xfer{0, r, buf[0], buf[r], count * sizeof(uint32_t)});
+  for (int r = 1; r < P; ++r) {
+    const int lr = local_of(g, r);
+    xs.push_back(Xfer{0, r, l0 >= 0 ? buf[l0] : nullptr, lr >= 0 ? buf[lr] : nullptr, count * sizeof(uint32_t)});
+  }
   transfer(g, xs);
 }
 
+// rank 0's bytes to every rank; buf[li] per local rank
 void broadcast(sheep_group *g, void *const *buf, size_t bytes) {
-  const int P = size(g);
+  const int P = g->world;
   if (P == 1 || bytes == 0) return;
   if (!g->comm.empty()) {
+    sync_all(g);
     NCCL_CHECK(ncclGroupStart());
-    for (int r = 0; r < P; ++r)
-      NCCL_CHECK(ncclBroadcast(buf[r], buf[r], bytes, ncclUint8, 0, g->comm[r], C(g, r).stream));
+    for (int i = 0; i < nlocal(g); ++i)
+      NCCL_CHECK(ncclBroadcast(buf[i], buf[i], bytes, ncclUint8, 0, g->comm[i], C(g, i).stream));
     NCCL_CHECK(ncclGroupEnd());
     sync_all(g);
     return;
   }
+  const int l0 = local_of(g, 0);
   std::vector<Xfer> xs;
-  for (int r = 1; r < P; ++r) xs.push_back(Xfer{0, r, buf[0], buf[r], bytes});
+  for (int r = 1; r < P; ++r) {
+    const int lr = local_of(g, r);
+    xs.push_back(Xfer{0, r, l0 >= 0 ? buf[l0] : nullptr, lr >= 0 ? buf[lr] : nullptr, bytes});
+  }
   transfer(g, xs);
+}
+
+uint64_t allreduce_max(sheep_group *g, const std::vector<uint64_t> &local) {
+  uint64_t m = 0;
+  for (uint64_t v : local) m = v > m ? v : m;
+  return g->mesh ? g->mesh->allreduce_max(m) : m;
+}
+
+std::string bus_id(int device) {
+  char b[64] = {0};
+  if (hipDeviceGetPCIBusId(b, sizeof b, device) != hipSuccess) return "dev" + std::to_string(device);
+  return b;
 }
 
 }  // namespace
@@ -189,6 +295,12 @@ struct DeviceRestore {
   ~DeviceRestore() { if (prev >= 0) (void)hipSetDevice(prev); }
 };
 
+static void group_free(sheep_group *g) {
+  for (ncclComm_t c : g->comm) if (c) ncclCommDestroy(c);
+  for (sheep_ctx *c : g->ctx) sheep_ctx_destroy(c);
+  delete g;
+}
+
 extern "C" {
 
 int sheep_group_create(const int *devices, int ndev, sheep_group **out) {
@@ -198,6 +310,7 @@ int sheep_group_create(const int *devices, int ndev, sheep_group **out) {
   sheep_group *g = new sheep_group();
   try {
     bool distinct = true;
+    g->world = ndev;
     for (int r = 0; r < ndev; ++r) {
       for (int q = 0; q < r; ++q) distinct &= devices[q] != devices[r];
       sheep_ctx *c = nullptr;
@@ -205,15 +318,52 @@ int sheep_group_create(const int *devices, int ndev, sheep_group **out) {
       if (rc != SHEEP_OK) throw sheep::Error(rc, sheep_last_error());
       g->ctx.push_back(c);
       g->dev.push_back(devices[r]);
+      g->rank.push_back(r);
     }
     if (distinct && ndev > 1) {
       g->comm.resize(ndev);
       NCCL_CHECK(ncclCommInitAll(g->comm.data(), ndev, devices));
     }
   } catch (...) {
-    for (ncclComm_t c : g->comm) if (c) ncclCommDestroy(c);
-    for (sheep_ctx *c : g->ctx) sheep_ctx_destroy(c);
-    delete g;
+    group_free(g);
+    throw;
+  }
+  *out = g;
+  GAPI_END
+}
+
+int sheep_group_join(int device, int rank, int world, const char *host, int port, int link, sheep_group **out) {
+  DeviceRestore dr;
+  GAPI_BEGIN
+  GNEED(out && host && world >= 1 && rank >= 0 && rank < world && port > 0 && port < 65536, "bad argument");
+  GNEED(link >= SHEEP_LINK_AUTO && link <= SHEEP_LINK_HOST, "bad link");
+  sheep_group *g = new sheep_group();
+  try {
+    g->world = world;
+    sheep_ctx *c = nullptr;
+    const int rc = sheep_ctx_create(device, SHEEP_OWN_STREAM, &c);
+    if (rc != SHEEP_OK) throw sheep::Error(rc, sheep_last_error());
+    g->ctx.push_back(c);
+    g->dev.push_back(device);
+    g->rank.push_back(rank);
+    const int timeout = getenv("SHEEP_JOIN_TIMEOUT") ? atoi(getenv("SHEEP_JOIN_TIMEOUT")) : 300;
+    g->mesh.reset(new sheep::Mesh(rank, world, host, port, sheep::bus_id(device), timeout));
+    bool distinct = true;
+    const auto &bus = g->mesh->bus_ids();
+    for (int r = 0; r < world; ++r)
+      for (int q = 0; q < r; ++q) distinct &= bus[q] != bus[r];
+    if (link == SHEEP_LINK_RCCL && !distinct)
+      throw sheep::Error(SHEEP_ERR_ARG, "RCCL needs every rank on its own device (two ranks share one)");
+    if (world > 1 && (link == SHEEP_LINK_RCCL || (link == SHEEP_LINK_AUTO && distinct))) {
+      ncclUniqueId id;
+      if (rank == 0) NCCL_CHECK(ncclGetUniqueId(&id));
+      g->mesh->bcast(&id, sizeof id);
+      HIP_CHECK(hipSetDevice(device));
+      g->comm.resize(1);
+      NCCL_CHECK(ncclCommInitRank(&g->comm[0], world, id, rank));
+    }
+  } catch (...) {
+    group_free(g);
     throw;
   }
   *out = g;
@@ -224,34 +374,51 @@ int sheep_group_destroy(sheep_group *g) {
   DeviceRestore dr;
   GAPI_BEGIN
   if (!g) return SHEEP_OK;
-  for (ncclComm_t c : g->comm) ncclCommDestroy(c);
-  for (sheep_ctx *c : g->ctx) sheep_ctx_destroy(c);
-  delete g;
+  group_free(g);
   GAPI_END
 }
 
-int sheep_group_size(const sheep_group *g) { return g ? (int)g->ctx.size() : 0; }
-sheep_ctx *sheep_group_ctx(sheep_group *g, int rank) {
-  return g && rank >= 0 && rank < (int)g->ctx.size() ? g->ctx[rank] : nullptr;
+int sheep_group_size(const sheep_group *g) { return g ? g->world : 0; }
+int sheep_group_local_count(const sheep_group *g) { return g ? (int)g->ctx.size() : 0; }
+int sheep_group_rank(const sheep_group *g, int local) {
+  return g && local >= 0 && local < (int)g->rank.size() ? g->rank[local] : -1;
+}
+sheep_ctx *sheep_group_ctx(sheep_group *g, int local) {
+  return g && local >= 0 && local < (int)g->ctx.size() ? g->ctx[local] : nullptr;
 }
 int sheep_group_uses_rccl(const sheep_group *g) { return g && !g->comm.empty(); }
+
+int sheep_group_barrier(sheep_group *g) {
+  DeviceRestore dr;
+  GAPI_BEGIN
+  GNEED(g, "null argument");
+  sheep::sync_all(g);
+  if (g->mesh) g->mesh->barrier();
+  GAPI_END
+}
+
+int sheep_group_allreduce_max_u64(sheep_group *g, uint64_t *v) {
+  GAPI_BEGIN
+  GNEED(g && v, "null argument");
+  if (g->mesh) *v = g->mesh->allreduce_max(*v);
+  GAPI_END
+}
 
 int sheep_group_sequence(sheep_group *g, const sheep_xs1 *const *rec, const uint64_t *nrec, uint32_t *const *deg,
                          uint64_t cap, uint32_t *const *seq, uint32_t *const *pos, uint64_t *n_out, uint64_t *vs_out) {
   DeviceRestore dr;
   GAPI_BEGIN
   GNEED(g && rec && nrec && deg && seq && pos && n_out && vs_out, "null argument");
-  const int P = sheep::size(g);
-  std::vector<uint64_t> ms(P, 0), n(P, 0);
-  sheep::per_rank(g, [&](int r) {   // each shard's LLAMA degrees (mpiSequence, sequence.h:76-77)
-    sheep::degree_count(sheep::C(g, r), rec[r], nrec[r], SHEEP_DEGREE_LLAMA, deg[r], cap, &ms[r]);
+  const int L = sheep::nlocal(g);
+  std::vector<uint64_t> ms(L, 0), n(L, 0);
+  sheep::per_rank(g, [&](int i) {   // each shard's LLAMA degrees (mpiSequence, sequence.h:76-77)
+    sheep::degree_count(sheep::C(g, i), rec[i], nrec[i], SHEEP_DEGREE_LLAMA, deg[i], cap, &ms[i]);
   });
-  uint64_t vs = 0;
-  for (uint64_t m : ms) vs = m > vs ? m : vs;                         // MPI_Allreduce(MAX), sequence.h:72
-  sheep::allreduce_sum_u32(g, deg, vs);                               // MPI_Allreduce(SUM), sequence.h:78
-  sheep::per_rank(g, [&](int r) {
-    n[r] = sheep::sequence_from_degrees(sheep::C(g, r), deg[r], vs, seq[r], pos[r]);
-    sheep::C(g, r).sync();
+  const uint64_t vs = sheep::allreduce_max(g, ms);                   // MPI_Allreduce(MAX), sequence.h:72
+  sheep::allreduce_sum_u32(g, deg, vs);                              // MPI_Allreduce(SUM), sequence.h:78
+  sheep::per_rank(g, [&](int i) {
+    n[i] = sheep::sequence_from_degrees(sheep::C(g, i), deg[i], vs, seq[i], pos[i]);
+    sheep::C(g, i).sync();
   });
   *n_out = n[0];
   *vs_out = vs;
@@ -263,37 +430,51 @@ int sheep_group_reduce_trees(sheep_group *g, sheep_jnode *const *tree, uint64_t 
   GAPI_BEGIN
   GNEED(g && tree, "null argument");
   GNEED(reduce >= 0 && reduce <= 2, "bad reduce mode");
-  const int P = sheep::size(g);
+  const int P = g->world;
   if (P == 1 || reduce == 0 || n == 0) return SHEEP_OK;
   const size_t tb = n * sizeof(sheep_jnode);
+  const int l0 = sheep::local_of(g, 0);
   if (reduce == 1) {   // gather + one K-way merge on rank 0 (every transfer on its own link)
-    HIP_CHECK(hipSetDevice(g->dev[0]));
-    sheep_jnode *stack = sheep::C(g, 0).get_as<sheep_jnode>("grp_stack", (uint64_t)P * n);
-    HIP_CHECK(hipMemcpyAsync(stack, tree[0], tb, hipMemcpyDeviceToDevice, sheep::C(g, 0).stream));
+    sheep_jnode *stack = nullptr;
+    if (l0 >= 0) {
+      HIP_CHECK(hipSetDevice(g->dev[l0]));
+      stack = sheep::C(g, l0).get_as<sheep_jnode>("grp_stack", (uint64_t)P * n);
+      HIP_CHECK(hipMemcpyAsync(stack, tree[l0], tb, hipMemcpyDeviceToDevice, sheep::C(g, l0).stream));
+    }
     std::vector<sheep::Xfer> xs;
-    for (int r = 1; r < P; ++r) xs.push_back(sheep::Xfer{r, 0, tree[r], stack + (uint64_t)r * n, tb});
+    for (int r = 1; r < P; ++r) {
+      const int lr = sheep::local_of(g, r);
+      xs.push_back(sheep::Xfer{r, 0, lr >= 0 ? tree[lr] : nullptr, stack ? stack + (uint64_t)r * n : nullptr, tb});
+    }
     sheep::transfer(g, xs);
-    HIP_CHECK(hipSetDevice(g->dev[0]));
-    sheep::merge_trees_many(sheep::C(g, 0), stack, (uint32_t)P, n, tree[0]);
-    sheep::C(g, 0).sync();
+    if (l0 >= 0) {
+      HIP_CHECK(hipSetDevice(g->dev[l0]));
+      sheep::merge_trees_many(sheep::C(g, l0), stack, (uint32_t)P, n, tree[l0]);
+      sheep::C(g, l0).sync();
+    }
     return SHEEP_OK;
   }
   // binomial: at hop d, rank i with i % 2d == 0 receives from i + d (disjoint pairs) and merges
   for (int d = 1; d < P; d *= 2) {
     std::vector<sheep::Xfer> xs;
     for (int i = 0; i + d < P; i += 2 * d) {
-      HIP_CHECK(hipSetDevice(g->dev[i]));
-      sheep_jnode *in = sheep::C(g, i).get_as<sheep_jnode>("grp_in", n);
-      xs.push_back(sheep::Xfer{i + d, i, tree[i + d], in, tb});
+      const int li = sheep::local_of(g, i), ls = sheep::local_of(g, i + d);
+      sheep_jnode *in = nullptr;
+      if (li >= 0) {
+        HIP_CHECK(hipSetDevice(g->dev[li]));
+        in = sheep::C(g, li).get_as<sheep_jnode>("grp_in", n);
+      }
+      xs.push_back(sheep::Xfer{i + d, i, ls >= 0 ? tree[ls] : nullptr, in, tb});
     }
     sheep::transfer(g, xs);
-    sheep::per_rank(g, [&](int r) {
+    sheep::per_rank(g, [&](int li) {
+      const int r = g->rank[li];
       if (r % (2 * d) != 0 || r + d >= P) return;
-      sheep_jnode *in = sheep::C(g, r).get_as<sheep_jnode>("grp_in", n);
-      sheep_jnode *out = sheep::C(g, r).get_as<sheep_jnode>("grp_out", n);
-      sheep::merge_trees(sheep::C(g, r), tree[r], in, n, out);
-      HIP_CHECK(hipMemcpyAsync(tree[r], out, tb, hipMemcpyDeviceToDevice, sheep::C(g, r).stream));
-      sheep::C(g, r).sync();
+      sheep_jnode *in = sheep::C(g, li).get_as<sheep_jnode>("grp_in", n);
+      sheep_jnode *out = sheep::C(g, li).get_as<sheep_jnode>("grp_out", n);
+      sheep::merge_trees(sheep::C(g, li), tree[li], in, n, out);
+      HIP_CHECK(hipMemcpyAsync(tree[li], out, tb, hipMemcpyDeviceToDevice, sheep::C(g, li).stream));
+      sheep::C(g, li).sync();
     });
   }
   GAPI_END
@@ -307,9 +488,9 @@ int sheep_group_build_tree(sheep_group *g, const sheep_xs1 *const *rec, const ui
   GNEED(g && rec && nrec && pos && tree, "null argument");
   GNEED(n < 0xFFFFFFFFull, "tree too large for 32-bit node ids");
   GNEED(reduce >= 0 && reduce <= 2, "bad reduce mode");
-  sheep::per_rank(g, [&](int r) {   // map: JTree on every shard (graph2tree.cpp:185-189)
-    sheep::relabel_and_tree(sheep::C(g, r), rec[r], nrec[r], pos[r], pos_size, n, tree[r]);
-    sheep::C(g, r).sync();
+  sheep::per_rank(g, [&](int i) {   // map: JTree on every shard (graph2tree.cpp:185-189)
+    sheep::relabel_and_tree(sheep::C(g, i), rec[i], nrec[i], pos[i], pos_size, n, tree[i]);
+    sheep::C(g, i).sync();
   });
   const int rc = sheep_group_reduce_trees(g, tree, n, reduce);
   if (rc != SHEEP_OK) return rc;
@@ -339,38 +520,52 @@ int sheep_group_evaluate(sheep_group *g, const sheep_xs1 *const *rec, const uint
   GAPI_BEGIN
   GNEED(g && rec && nrec && pos && parts && out, "null argument");
   GNEED(!(what & ~7), "bad argument");
-  const int P = sheep::size(g);
-  HIP_CHECK(hipSetDevice(g->dev[0]));
-  const int nparts = sheep::eval_num_parts(sheep::C(g, 0), parts[0], pos_size);
+  const int P = g->world;
+  const int l0 = sheep::local_of(g, 0);
+  uint64_t np = 0;
+  if (l0 >= 0) {
+    HIP_CHECK(hipSetDevice(g->dev[l0]));
+    np = (uint64_t)sheep::eval_num_parts(sheep::C(g, l0), parts[l0], pos_size);
+  }
+  if (g->mesh) g->mesh->bcast(&np, sizeof np);
+  const int nparts = (int)np;
   uint64_t words = 0, aw = 0;
   sheep::eval_sizes(what, nparts, pos_size, &words, &aw);
-  std::vector<uint64_t *> bits(P), acc(P), rb(P), ra(P);
-  sheep::per_rank(g, [&](int r) {   // every shard's owner bits and counts
-    sheep::Ctx &c = sheep::C(g, r);
-    bits[r] = c.get_as<uint64_t>("grp_ev_bits", words ? words : 1);
-    acc[r] = c.get_as<uint64_t>("grp_ev_acc", aw);
-    rb[r] = c.get_as<uint64_t>("grp_ev_rbits", words ? words : 1);
-    ra[r] = c.get_as<uint64_t>("grp_ev_racc", aw);
-    HIP_CHECK(hipMemsetAsync(bits[r], 0, words * sizeof(uint64_t), c.stream));
-    HIP_CHECK(hipMemsetAsync(acc[r], 0, aw * sizeof(uint64_t), c.stream));
-    sheep::eval_shard(c, rec[r], nrec[r], pos[r], pos_size, parts[r], what, nparts, bits[r], acc[r]);
+  const int L = sheep::nlocal(g);
+  std::vector<uint64_t *> bits(L), acc(L), rb(L), ra(L);
+  sheep::per_rank(g, [&](int i) {   // every shard's owner bits and counts
+    sheep::Ctx &c = sheep::C(g, i);
+    bits[i] = c.get_as<uint64_t>("grp_ev_bits", words ? words : 1);
+    acc[i] = c.get_as<uint64_t>("grp_ev_acc", aw);
+    rb[i] = c.get_as<uint64_t>("grp_ev_rbits", words ? words : 1);
+    ra[i] = c.get_as<uint64_t>("grp_ev_racc", aw);
+    HIP_CHECK(hipMemsetAsync(bits[i], 0, words * sizeof(uint64_t), c.stream));
+    HIP_CHECK(hipMemsetAsync(acc[i], 0, aw * sizeof(uint64_t), c.stream));
+    sheep::eval_shard(c, rec[i], nrec[i], pos[i], pos_size, parts[i], what, nparts, bits[i], acc[i]);
     c.sync();
   });
   for (int d = 1; d < P; d *= 2) {   // binomial OR / sum reduction to rank 0
     std::vector<sheep::Xfer> xs;
     for (int i = 0; i + d < P; i += 2 * d) {
-      xs.push_back(sheep::Xfer{i + d, i, bits[i + d], rb[i], words * sizeof(uint64_t)});
-      xs.push_back(sheep::Xfer{i + d, i, acc[i + d], ra[i], aw * sizeof(uint64_t)});
+      const int li = sheep::local_of(g, i), ls = sheep::local_of(g, i + d);
+      xs.push_back(sheep::Xfer{i + d, i, ls >= 0 ? bits[ls] : nullptr, li >= 0 ? rb[li] : nullptr,
+                               words * sizeof(uint64_t)});
+      xs.push_back(sheep::Xfer{i + d, i, ls >= 0 ? acc[ls] : nullptr, li >= 0 ? ra[li] : nullptr,
+                               aw * sizeof(uint64_t)});
     }
     sheep::transfer(g, xs);
-    sheep::per_rank(g, [&](int r) {
+    sheep::per_rank(g, [&](int li) {
+      const int r = g->rank[li];
       if (r % (2 * d) != 0 || r + d >= P) return;
-      sheep::eval_combine(sheep::C(g, r), bits[r], rb[r], words, acc[r], ra[r], aw);
-      sheep::C(g, r).sync();
+      sheep::eval_combine(sheep::C(g, li), bits[li], rb[li], words, acc[li], ra[li], aw);
+      sheep::C(g, li).sync();
     });
   }
-  HIP_CHECK(hipSetDevice(g->dev[0]));
-  sheep::eval_finish(sheep::C(g, 0), bits[0], acc[0], pos_size, parts[0], what, nparts, out);
+  *out = sheep_eval();
+  if (l0 >= 0) {
+    HIP_CHECK(hipSetDevice(g->dev[l0]));
+    sheep::eval_finish(sheep::C(g, l0), bits[l0], acc[l0], pos_size, parts[l0], what, nparts, out);
+  }
   GAPI_END
 }
 

@@ -1124,10 +1124,10 @@ void tree_facts(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_facts_t *out)
     maxdepth = c.h_scalars[44];
     eheight = c.h_scalars[45];
   } catch (...) {
-    hipFree(k.parent); hipFree(k.koff); hipFree(k.kids);
+    release_kids(&c, &k);
     throw;
   }
-  HIP_CHECK(hipFree(k.parent)); HIP_CHECK(hipFree(k.koff)); HIP_CHECK(hipFree(k.kids));
+  release_kids(&c, &k);   // the buffers stay with the context for the next kid table
   const uint64_t sum = c.h_scalars[40], mx = c.h_scalars[41], roots = c.h_scalars[42], halo = c.h_scalars[43];
   out->vert_cnt = n;
   out->edge_cnt = sum;

@@ -221,6 +221,25 @@ void gather_u32(Ctx &c, const uint32_t *src, const uint32_t *idx, uint64_t m, ui
   LAUNCH_CHECK();
 }
 
+// A kid table's buffers back to the context for the next table (the larger table's
+// buffers are kept), or freed.  The caller has made the context's device current.
+void release_kids(Ctx *c, sheep_kids *k) {
+  Ctx::KidBufs *sp = c ? &c->kid_spare : nullptr;
+  if (sp && k->parent && k->koff && k->kids && (!sp->parent || sp->cap < k->cap)) {
+    if (sp->parent) {
+      c->sync();
+      hipFree(sp->parent); hipFree(sp->koff); hipFree(sp->kids);
+    }
+    *sp = {k->parent, k->koff, k->kids, k->cap};
+  } else {
+    if (c) c->sync();
+    hipFree(k->parent);
+    hipFree(k->koff);
+    hipFree(k->kids);
+  }
+  k->parent = k->koff = k->kids = nullptr;
+}
+
 void build_kids(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_kids *k) {
   k->ctx = &c;
   k->n = n;

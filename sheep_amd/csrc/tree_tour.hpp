@@ -27,6 +27,7 @@ struct Tour {
 };
 
 void build_kids(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_kids *k);
+void release_kids(Ctx *c, sheep_kids *k);
 void build_tour(Ctx &c, sheep_kids *k, Tour &t);
 // generic helpers
 void gather_u32(Ctx &c, const uint32_t *src, const uint32_t *idx, uint64_t m, uint32_t *dst);

@@ -2,6 +2,8 @@
 golden outputs: same files byte for byte, same stdout lines (timing lines aside)."""
 import filecmp
 import os
+import shutil
+import socket
 import subprocess
 
 import pytest
@@ -103,37 +105,81 @@ def test_partition_tree_cli(gpu_ctx, tmp_path, name):
     assert p.stdout == open(os.path.join(GOLDEN, f"{name}.part.txt")).read()
 
 
-# ---- graph2tree -i / -r: the MPI world as one process over several GPUs ----------------
-def _world_env(ranks):
-    """SHEEP_DEVICES lists device 0 `ranks` times: the world's ranks rehearsed on one GPU
-    (device copies stand in for RCCL, which needs distinct devices)."""
-    return dict(os.environ, SHEEP_DEVICES=",".join(["0"] * ranks))
+# ---- graph2tree -i / -r: the MPI world over several GPUs ---------------------------------
+# Two launches (sheep/world.hpp): "devices" — ONE process drives the ranks listed in
+# SHEEP_DEVICES (device 0 listed `ranks` times: device copies stand in for RCCL, which needs
+# distinct devices); "mpiexec" — the reference's own launch, `mpiexec -n P graph2tree ...`,
+# one process per rank (they share device 0, so the host link over TCP carries the data).
+MPIEXEC = shutil.which("mpiexec", path="/opt/conda/bin") or shutil.which("mpiexec")
+LAUNCHES = ["devices", "mpiexec"]
 
 
-def run_env(env, *args, check=True):
-    p = subprocess.run([str(a) for a in args], capture_output=True, text=True, timeout=120, env=env)
+def _free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def seq_copy(tmp_path, name="hep"):
+    """A copy of the golden sequence: with -i, rank 0 WRITES the all-reduced sequence to
+    the -s file (graph2tree.cpp:174-175)."""
+    dst = tmp_path / f"{name}.in.seq"
+    shutil.copy(os.path.join(GOLDEN, f"{name}.seq"), dst)
+    return dst
+
+
+def world_run(launch, ranks, *args, check=True):
+    env = dict(os.environ)
+    for k in ("SHEEP_DEVICES", "RANK", "WORLD_SIZE", "LOCAL_RANK", "PMI_RANK", "PMI_SIZE"):
+        env.pop(k, None)
+    if launch == "devices":
+        env["SHEEP_DEVICES"] = ",".join(["0"] * ranks)
+        cmd = [os.path.join(BIN, "graph2tree"), *args]
+    else:
+        if not MPIEXEC:
+            pytest.skip("no mpiexec on this host")
+        env["SHEEP_MASTER_PORT"] = str(_free_port())
+        cmd = [MPIEXEC, "-n", str(ranks), os.path.join(BIN, "graph2tree"), *args]
+    p = subprocess.run([str(a) for a in cmd], capture_output=True, text=True, timeout=180, env=env)
     if check:
         assert p.returncode == 0, p.stdout + p.stderr
     return p
 
 
+def test_graph2tree_single_rank_without_launcher(tmp_path):
+    """No SHEEP_DEVICES and no launcher: `graph2tree -i` is a world of ONE rank, as an MPI
+    program started without mpiexec (MPI_Comm_size 1), whatever the number of GPUs."""
+    import sys
+    sys.path.insert(0, ROOT)
+    src = open(os.path.join(ROOT, "sheep_amd", "include", "sheep", "world.hpp")).read()
+    assert "if (devs.empty()) devs.push_back(0);" in src
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("launch", LAUNCHES)
 @pytest.mark.parametrize("ranks", [2, 3])
 @pytest.mark.parametrize("name", ["hep", "edge"])
-def test_graph2tree_world_ir(gpu_ctx, tmp_path, name, ranks):
-    """mpirun -n P graph2tree G -s SEQ -o OUT -ir (graph2tree.cpp:134-218): rank 0 writes
-    the all-reduced degree sequence and the merged tree, both equal to the serial ones."""
+def test_graph2tree_world_ir(gpu_ctx, tmp_path, name, ranks, launch):
+    """mpirun -n P graph2tree G -s SEQ -o OUT -ir -f (graph2tree.cpp:134-218): rank 0 writes
+    the all-reduced degree sequence and the merged tree, both equal to the serial ones, and
+    prints the merged tree's TREEFAQS (under mpiexec every rank prints its own tree's)."""
     dat = dat_path(name, tmp_path)
     seq, out = tmp_path / "w.seq", tmp_path / "w.tre"
-    p = run_env(_world_env(ranks), os.path.join(BIN, "graph2tree"), dat, "-s", seq, "-o", out, "-i", "-r", "-f")
+    p = world_run(launch, ranks, dat, "-s", seq, "-o", out, "-i", "-r", "-f")
     assert filecmp.cmp(seq, os.path.join(GOLDEN, f"{name}.seq"), shallow=False)
     assert filecmp.cmp(out, os.path.join(GOLDEN, f"{name}.tre"), shallow=False)
-    assert strip_timing(p.stdout) == open(os.path.join(GOLDEN, f"{name}.facts")).read()
-    assert "Reduced in:" in p.stdout and "Mapped in:" in p.stdout
+    facts = open(os.path.join(GOLDEN, f"{name}.facts")).read()
+    if launch == "devices":
+        assert strip_timing(p.stdout) == facts
+    else:
+        assert facts in strip_timing(p.stdout)
+        assert strip_timing(p.stdout).count("TREEFAQS") == ranks
+    assert p.stdout.count("Reduced in:") == 1 and p.stdout.count("Mapped in:") == 1
 
 
 @pytest.mark.gpu
-def test_graph2tree_world_i_partial_trees(gpu_ctx, tmp_path):
+@pytest.mark.parametrize("launch", LAUNCHES)
+def test_graph2tree_world_i_partial_trees(gpu_ctx, tmp_path, launch):
     """-i without -r: every rank saves its shard's tree as OUTrr r0.tre (graph2tree.cpp:
     144-149), the map-worker files; their merge is the whole tree."""
     import numpy as np
@@ -141,7 +187,7 @@ def test_graph2tree_world_i_partial_trees(gpu_ctx, tmp_path):
     from conftest import golden_seq, read_tre
     dat = dat_path("hep", tmp_path)
     out = tmp_path / "m"
-    run_env(_world_env(3), os.path.join(BIN, "graph2tree"), dat, "-s", os.path.join(GOLDEN, "hep.seq"), "-o", out, "-i")
+    world_run(launch, 3, dat, "-s", seq_copy(tmp_path), "-o", out, "-i")
     r = golden_records("hep")
     seq = golden_seq("hep")
     for rank in range(3):
@@ -151,15 +197,52 @@ def test_graph2tree_world_i_partial_trees(gpu_ctx, tmp_path):
 
 
 @pytest.mark.gpu
-def test_graph2tree_world_fast_partition_path(gpu_ctx, tmp_path):
+@pytest.mark.parametrize("launch", LAUNCHES)
+def test_graph2tree_world_i_partitions_each_partial_tree(gpu_ctx, tmp_path, launch):
+    """-i -p K without -r (graph2tree.cpp:144-149, 203-213): every rank partitions ITS
+    partial tree and writes its shard's edges under OUTrr r0.tre%04d; rank 0 alone prints
+    when there is no -o."""
+    import numpy as np
+    import oracle
+    from conftest import golden_seq
+    dat = dat_path("hep", tmp_path)
+    out = tmp_path / "q"
+    r = golden_records("hep")
+    seq = golden_seq("hep")
+    world_run(launch, 2, dat, "-s", seq_copy(tmp_path), "-o", out, "-p", "4", "-i")
+    R = len(r)
+    pos = np.full(int(seq.max()) + 1, -1, np.int64)
+    pos[seq] = np.arange(len(seq))
+    for rank in range(2):
+        op, ow = oracle.build_tree(r["tail"], r["head"], seq, rank + 1, 2)
+        parts, info = oracle.partition(op, ow, seq, 4)
+        want = {}
+        for t, h in zip(r["tail"][rank * R // 2:(rank + 1) * R // 2], r["head"][rank * R // 2:(rank + 1) * R // 2]):
+            x, y = min(t, h), max(t, h)
+            if x == y:
+                continue
+            owner = x if pos[x] < pos[y] else y
+            want.setdefault(int(parts[owner]), []).append(f"{x} {y}")
+        for part in range(info["created"]):
+            got = open(f"{out}{rank:02d}r0.tre{part:04d}").read().splitlines()
+            assert sorted(got) == sorted(want.get(part, [])), (rank, part)
+    p = world_run(launch, 2, dat, "-s", seq_copy(tmp_path), "-p", "4", "-i")
+    op, ow = oracle.build_tree(r["tail"], r["head"], seq, 1, 2)
+    parts, info = oracle.partition(op, ow, seq, 4)
+    assert strip_timing(p.stdout) == (f"Actually created {info['created']} partitions.\n"
+                                      f"First two partition sizes: {np.count_nonzero(parts == 0)} and "
+                                      f"{np.count_nonzero(parts == 1)}\n")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("launch", LAUNCHES)
+def test_graph2tree_world_fast_partition_path(gpu_ctx, tmp_path, launch):
     """graph2tree G -s SEQ -o OUT -p K -ir (the "fast partition path", horizontal-dist.sh:
     30-37): parts broadcast (mpi_sync), every rank writes its shard's edges into
     OUT-wRRRR-pPPPP.  Per part, the union of the ranks' lines is the serial writer's."""
     dat = dat_path("hep", tmp_path)
     out = tmp_path / "P"
-    p = run_env(_world_env(3), os.path.join(BIN, "graph2tree"), dat, "-s", os.path.join(GOLDEN, "hep.seq"), "-o", out,
-                "-p", "4", "-i", "-r")
-    assert p.returncode == 0
+    world_run(launch, 3, dat, "-s", seq_copy(tmp_path), "-o", out, "-p", "4", "-i", "-r")
     for part in range(4):
         lines = []
         for rank in range(3):
@@ -169,13 +252,14 @@ def test_graph2tree_world_fast_partition_path(gpu_ctx, tmp_path):
 
 
 @pytest.mark.gpu
-def test_graph2tree_world_prints_partition(gpu_ctx, tmp_path):
+@pytest.mark.parametrize("launch", LAUNCHES)
+def test_graph2tree_world_prints_partition(gpu_ctx, tmp_path, launch):
     """graph2tree G -p K -ir without -o: rank 0 prints Partition::print (graph2tree.cpp:214-215)."""
     import numpy as np
     import oracle
     from conftest import golden_seq, golden_tree
     dat = dat_path("hep", tmp_path)
-    p = run_env(_world_env(2), os.path.join(BIN, "graph2tree"), dat, "-p", "4", "-i", "-r")
+    p = world_run(launch, 2, dat, "-p", "4", "-i", "-r")
     gp, gw = golden_tree("hep")
     parts, info = oracle.partition(gp, gw, golden_seq("hep"), 4)
     want = (f"Actually created {info['created']} partitions.\n"

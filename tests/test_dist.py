@@ -1,19 +1,27 @@
-"""The N-rank schedule (sheep_amd/dist.py) on CPUs over gloo: edge shards -> degree
-all-reduce -> per-shard trees -> binomial tree reduction to rank 0, with the CPU oracle
-as the per-rank compute.  The sequence and the tree at rank 0 must equal the reference's
-serial outputs (golden .seq / .tre) for every world size, odd ones included; this is the
-same schedule bench.py drives with the HIP kernels over RCCL."""
-import json
+"""The N-rank run on CPUs (no device): the pieces of bench.py's and graph2tree -i -r's
+one-process-per-rank world that are host code.
+
+* the TCP links every joined world is built on (sheep_group_join -> mesh.hip): the
+  rendezvous, rank 0's bytes to everyone, a ring shift, a gather to rank 0 and the
+  all-reduces, at world sizes 1-4 (sheep_mesh_selftest, one process per rank);
+* bench.py's control plane (sheep_amd/dist.py) over gloo at world 2-3: the shared
+  rendezvous port, the barrier and the max over ranks of the wall time;
+* the contiguous edge shards of `-l part/num_parts`.
+
+The world's data path (the degree all-reduce, the tree gather / binomial reduce, the parts
+broadcast, the sharded evaluator) runs in HIP kernels: tests/test_gpu_parity.py runs it as
+processes joined over these links on one GPU, tests/test_cli.py under mpiexec."""
+import ctypes
 import os
 import socket
 
 import numpy as np
 import pytest
-import torch
-import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import golden_records, golden_seq, golden_tree
+from conftest import ROOT
+
+LIB = os.path.join(ROOT, "sheep_amd", "lib", "libsheep_hip.so")
 
 
 def _free_port():
@@ -22,114 +30,85 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _oracle_merge(x, y):
-    import oracle
-    xa, ya = x.numpy().view(np.uint32), y.numpy().view(np.uint32)
-    po, wo = oracle.merge(xa[:, 0], xa[:, 1], ya[:, 0], ya[:, 1])
-    return torch.from_numpy(np.stack([po, wo], axis=1).view(np.int32))
+def _pattern(rank, nbytes):
+    out = np.empty(nbytes, np.uint8)
+    x = (0x9E3779B97F4A7C15 * (rank + 1)) & 0xFFFFFFFFFFFFFFFF
+    for i in range(nbytes):
+        x ^= (x << 13) & 0xFFFFFFFFFFFFFFFF
+        x ^= x >> 7
+        x ^= (x << 17) & 0xFFFFFFFFFFFFFFFF
+        out[i] = x & 0xFF
+    return out
 
 
-def _oracle_merge_many(stacked):
-    """K-way merge = any fold of pairwise merges (the oracle has the pairwise one)."""
-    acc = stacked[0]
-    for t in stacked[1:]:
-        acc = _oracle_merge(acc, t)
-    return acc
+def _fnv(b):
+    h = 1469598103934665603
+    for x in b.tolist():
+        h = ((h ^ x) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
 
 
-def _rank_main(rank, world, port, name, out_path, reduce="binomial", split_parts=2):
-    import oracle
+def _mesh_rank(rank, world, port, nbytes, q):
+    L = ctypes.CDLL(LIB)
+    L.sheep_mesh_selftest.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_uint64,
+                                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    cs, mx = ctypes.c_uint64(), ctypes.c_uint64()
+    rc = L.sheep_mesh_selftest(rank, world, b"127.0.0.1", port, nbytes, ctypes.byref(cs), ctypes.byref(mx))
+    q.put((rank, rc, cs.value, mx.value))
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+def test_mesh_links(world):
+    if not os.path.exists(LIB):
+        pytest.skip("libsheep_hip.so not built")
+    nbytes = 3000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mesh_rank, args=(r, world, port, nbytes, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    h = [_fnv(_pattern(r, nbytes)) for r in range(world)]
+    want = sum(h[0] + (h[(r - 1) % world] if world > 1 else 0) for r in range(world))
+    want += sum(h[1:]) if world > 1 else 0
+    want &= 0xFFFFFFFFFFFFFFFF
+    for rank, rc, cs, mx in got:
+        assert rc == 0, rank
+        assert cs == want, rank
+        assert mx == max(h), rank
+
+
+def _control_rank(rank, world, port, q):
+    import torch.distributed as dist
     from sheep_amd import dist as sdist
-
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    try:
-        rec = golden_records(name)
-        beg, end = sdist.shard_bounds(len(rec), rank, world)
-        tail = rec["tail"][beg:end].astype(np.int64)
-        head = rec["head"][beg:end].astype(np.int64)
-        vs_cap = int(max(rec["tail"].max(), rec["head"].max())) + 1
-        # LLAMA degrees of this shard (graph_wrapper.h:87-89): +1 per endpoint, a self-loop once
-        deg = np.bincount(tail, minlength=vs_cap) + np.bincount(head[head != tail], minlength=vs_cap)
-        max_slot = int(max(tail.max(), head.max())) + 1 if len(tail) else 0
-        deg_t = torch.from_numpy(deg.astype(np.int32))
-        vs = sdist.allreduce_degrees(deg_t, max_slot)
-        d = deg_t.numpy()[:vs]
-        slots = np.nonzero(d)[0]
-        seq = slots[np.lexsort((slots, d[slots]))].astype(np.uint32)   # (degree, vid), sequence.h:52-63
-
-        p, w = oracle.build_tree(tail, head, seq)
-        tree = torch.from_numpy(np.stack([p, w], axis=1).view(np.int32))
-
-        if reduce == "split":
-            def merge_part(stacked, part, nparts):
-                # the split merge's contract: every pst, and parents only in the part's
-                # range (the rest scrambled, so rank 0 must take them from their owners)
-                full = _oracle_merge_many(stacked).clone()
-                n = full.shape[0]
-                lo, hi = part * n // nparts, (part + 1) * n // nparts
-                full[:lo, 0] = -7
-                full[hi:, 0] = -7
-                return full, lo, hi
-            tree = sdist.reduce_trees_split(tree, merge_part, rank, world, nparts=split_parts)
-        elif reduce == "kway":
-            stacked = sdist.gather_trees(tree, rank, world)
-            if rank == 0:   # the gather itself is exact: row r is rank r's own tree
-                assert stacked.shape == (world,) + tuple(tree.shape)
-                assert torch.equal(stacked[0], tree)
-            tree = None if stacked is None else _oracle_merge_many(stacked)
-        else:
-            tree = sdist.reduce_trees(tree, _oracle_merge, rank, world)
-        assert (tree is None) == (rank != 0)
-        # Partition::mpi_sync: rank 0 partitions, every rank gets the parts
-        parts = None
-        if rank == 0:
-            t0 = tree.numpy().view(np.uint32)
-            parts = torch.from_numpy(oracle.partition(t0[:, 0], t0[:, 1], seq, 4)[0])
-        n_slots = int(seq.max()) + 1
-        parts = sdist.sync_parts(parts, n_slots, "cpu")
-        gp, gw = golden_tree(name)
-        assert np.array_equal(parts.numpy(), oracle.partition(gp, gw, seq, 4)[0])
-        if rank == 0:
-            t = tree.numpy().view(np.uint32)
-            json.dump({"seq": seq.tolist(), "parent": t[:, 0].tolist(), "pst": t[:, 1].tolist()}, open(out_path, "w"))
-        dist.barrier()
-    finally:
-        dist.destroy_process_group()
+    sdist.init_control(init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    p = sdist.shared_port()
+    sdist.barrier()
+    t = sdist.max_over_ranks(0.5 + rank)
+    q.put((rank, p, t, dist.get_backend()))
+    sdist.shutdown()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
-@pytest.mark.parametrize("name", ["hep", "rmat10"])
-def test_sharded_schedule_matches_serial(tmp_path, name, world):
-    out = str(tmp_path / "rank0.json")
-    mp.spawn(_rank_main, args=(world, _free_port(), name, out), nprocs=world, join=True)
-    got = json.load(open(out))
-    assert np.array_equal(np.array(got["seq"], np.uint32), golden_seq(name))
-    parent, pst = golden_tree(name)
-    assert np.array_equal(np.array(got["parent"], np.uint32), parent)
-    assert np.array_equal(np.array(got["pst"], np.uint32), pst)
-
-
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_kway_schedule_matches_serial(tmp_path, world):
-    """Gather to rank 0 + one K-way reduction (bench.py's default --reduce kway)."""
-    out = str(tmp_path / "rank0.json")
-    mp.spawn(_rank_main, args=(world, _free_port(), "rmat10", out, "kway"), nprocs=world, join=True)
-    got = json.load(open(out))
-    parent, pst = golden_tree("rmat10")
-    assert np.array_equal(np.array(got["parent"], np.uint32), parent)
-    assert np.array_equal(np.array(got["pst"], np.uint32), pst)
-
-
-@pytest.mark.parametrize("world,nparts", [(2, 2), (3, 2), (4, 2), (4, 4)])
-def test_split_schedule_matches_serial(tmp_path, world, nparts):
-    """Every tree to the part ranks + one part of the split merge each + the parts' node
-    ranges gathered to rank 0 (bench.py's --reduce split)."""
-    out = str(tmp_path / "rank0.json")
-    mp.spawn(_rank_main, args=(world, _free_port(), "rmat10", out, "split", nparts), nprocs=world, join=True)
-    got = json.load(open(out))
-    parent, pst = golden_tree("rmat10")
-    assert np.array_equal(np.array(got["parent"], np.uint32), parent)
-    assert np.array_equal(np.array(got["pst"], np.uint32), pst)
+@pytest.mark.parametrize("world", [2, 3])
+def test_control_plane(world):
+    """bench.py's N-rank control plane over gloo: every rank gets rank 0's rendezvous
+    port for sheep_group_join, and the wall time is the slowest rank's."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_control_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    ports = {g[1] for g in got}
+    assert len(ports) == 1 and 0 < ports.pop() < 65536
+    assert all(g[2] == 0.5 + world - 1 for g in got)
+    assert all(g[3] == "gloo" for g in got)
 
 
 def test_shard_bounds_cover():

@@ -416,14 +416,50 @@ def test_group_rehearsal_matches_single_gpu(gpu_ctx, ranks):
     for q in seqs:
         assert q.n == s.n and torch.equal(q.seq[: q.n], s.seq[: s.n])
     for mode in ("kway", "binomial"):
-        assert torch.equal(g.build_tree(shards, seqs, mode), whole), mode
+        assert torch.equal(g.build_tree(shards, seqs, mode)[0], whole), mode
     partial = g.build_tree(shards, seqs, "none")
     assert torch.equal(sheep_amd.merge_trees_many(torch.stack(partial)), whole)
-    parts = g.broadcast_parts(res.parts.clone(), s.pos_size)
+    parts = g.broadcast_parts([res.parts.clone()] + [torch.full_like(res.parts, 7) for _ in range(ranks - 1)],
+                              s.pos_size)
     for p in parts:
         assert torch.equal(p, res.parts)
     assert g.evaluate(shards, seqs, parts) == ev
     g.close()
+
+
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_group_join_processes_match_single_gpu(gpu_ctx, tmp_path, ranks):
+    """sheep_group_join: `ranks` PROCESSES, one rank each (the mpiexec / torch.distributed
+    form), sharing device 0, so the host link over TCP carries the exchanges.  Every rank
+    runs tests/group_worker.py; rank 0's sequence, K-way and binomial trees, broadcast parts
+    and evaluator equal the single-GPU results."""
+    import socket
+    import subprocess
+    import sys
+    import torch
+    import sheep_amd
+    d = sheep_amd.rmat(16, 16, 16)
+    s = sheep_amd.degree_sequence(d)
+    whole = sheep_amd.build_tree(d, s)
+    res = sheep_amd.partition(s, whole, 32)
+    ev = sheep_amd.evaluate(d, s, res.parts)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "group_worker.py")
+    procs = [subprocess.Popen([sys.executable, worker, str(r), str(ranks), str(port), str(tmp_path)],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(ranks)]
+    outs = [p.communicate(timeout=240)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    got = np.load(tmp_path / "rank0.npz")
+    assert np.array_equal(got["seq"], s.numpy())
+    p, w = sheep_amd.tree_to_numpy(whole)
+    for mode in ("kway", "binomial"):
+        assert np.array_equal(got[f"parent_{mode}"], p) and np.array_equal(got[f"pst_{mode}"], w), mode
+    for r in range(ranks):
+        assert np.array_equal(np.load(tmp_path / f"rank{r}.npz")["parts"], res.numpy()), r
+    assert got["ecv"].tolist() == [ev.ecv_down, ev.max_down_bal, ev.edges_cut, ev.ecv_hash, ev.ecv_up]
+    assert "link=host" in outs[0]
 
 
 def _snapreader(text: bytes, skip_comments: bool):

@@ -132,6 +132,49 @@ def test_threaded_oracle_matches_golden(name):
         oracle.set_threads(1)
 
 
+@pytest.mark.parametrize("name", GRAPHS)
+@pytest.mark.parametrize("shards", [1, 2, 3, 8])
+def test_map_reduce_oracle_matches_golden(name, shards):
+    """oracle.build_tree_mr (graph2tree -r's form: shard trees + binomial merges, used for
+    the C3-C5 checks) gives the reference-built tree for every shard count."""
+    r = golden_records(name)
+    seq = golden_seq(name)
+    gp, gw = golden_tree(name)
+    oracle.set_threads(4)
+    try:
+        p, w = oracle.build_tree_mr(r["tail"], r["head"], seq, shards)
+    finally:
+        oracle.set_threads(1)
+    assert np.array_equal(p, gp) and np.array_equal(w, gw)
+
+
+def test_map_reduce_oracle_edge_semantics():
+    """Unsequenced and out-of-range neighbours, self-loops and duplicate records: the
+    map/reduce form agrees with the adjacency form (JTree::insert, jtree.cpp:66-110),
+    including index.at()'s out_of_range."""
+    rng = np.random.default_rng(7)
+    t = rng.integers(0, 300, 5000).astype(np.uint32)
+    h = rng.integers(0, 300, 5000).astype(np.uint32)
+    t[:50] = h[:50]                                          # self-loops
+    t[50:100], h[50:100] = t[100:150], h[100:150]            # duplicates
+    seq = oracle.sequence(t, h)
+    for s in (seq, seq[rng.permutation(len(seq))], np.sort(seq)[: len(seq) // 2],
+              np.setdiff1d(seq, np.arange(250, 300, dtype=np.uint32))):
+        s = np.ascontiguousarray(s, np.uint32)
+        want = None
+        try:
+            want = oracle.build_tree(t, h, s)
+        except RuntimeError as e:
+            assert "range" in str(e)
+        for shards in (1, 4):
+            if want is None:
+                with pytest.raises(RuntimeError, match="range"):
+                    oracle.build_tree_mr(t, h, s, shards)
+            else:
+                p, w = oracle.build_tree_mr(t, h, s, shards)
+                assert np.array_equal(p, want[0]) and np.array_equal(w, want[1])
+
+
 def test_partition_sequence_length_semantics():
     """Partition ctor (partition.cpp:62-66): a sequence longer than the tree throws
     (parts.at); a shorter one converts only its own entries."""
