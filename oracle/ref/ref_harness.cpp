@@ -142,13 +142,20 @@ static int usage() {
           "ref_harness write G SEQ|- TREE k PREFIX        Partition + graph-based writePartitionedGraph\n"
           "ref_harness writefile G SEQ|- TREE k PREFIX    Partition + file-based writePartitionedGraph\n"
           "ref_harness time G k                           seconds for degreeSequence + JTree + Partition(k)\n"
-          "mpiexec -n P ref_harness mpi G k              graph2tree -r -p k over P MPI ranks (timed)\n");
+          "mpiexec -n P ref_harness mpi G k              graph2tree -r -p k over P MPI ranks (timed)\n"
+          "ref_harness snap FILE                          SNAPReader::read pairs, one \"X Y\" per line\n");
   return 1;
 }
 
 int main(int argc, char **argv) {
   if (argc < 2) return usage();
   std::string cmd = argv[1];
+  if (cmd == "snap" && argc == 3) {   // readerwriter.h:78-90, the text reader of .net files
+    SNAPReader r(argv[2]);
+    vid_t X, Y;
+    while (r.read(X, Y)) printf("%u %u\n", (unsigned)X, (unsigned)Y);
+    return 0;
+  }
   if (cmd == "seq" && argc == 4) {
     HarnessGraph g(argv[2]);
     writeSequence(degreeSequence(g), argv[3]);

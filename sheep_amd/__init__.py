@@ -754,23 +754,3 @@ XS1 = np.dtype([("tail", "<u4"), ("head", "<u4"), ("weight", "<f4")])
 
 def read_dat(path: str) -> np.ndarray:
     return np.fromfile(path, dtype=XS1)
-
-
-def read_net(path: str) -> np.ndarray:
-    """SNAPReader (readerwriter.h:166-178): whitespace-separated pairs, stop at the first
-    incomplete pair."""
-    toks = open(path).read().split()
-    vals = []
-    for tok in toks:
-        try:
-            vals.append(int(tok))
-        except ValueError:
-            break
-    if len(vals) % 2:
-        vals = vals[:-1]
-    a = np.array(vals, dtype=np.uint64).reshape(-1, 2)
-    rec = np.zeros(len(a), dtype=XS1)
-    rec["tail"] = a[:, 0]
-    rec["head"] = a[:, 1]
-    rec["weight"] = 1.0
-    return rec

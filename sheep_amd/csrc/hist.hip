@@ -428,20 +428,36 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
 
 
 // ---- degree pass fused with the heads' bucket counts (sequence.h:65-107) --------------
-// k_degree's work (tails with run-combined atomics, the FILE_DAT last record's extra head,
-// max slot, range check) and k_hist_count's per-tile head bucket counts in one read of the
-// records.  Buckets are laid out for the capacity (nb_cap rows); the rows beyond the max
-// slot's stay zero, so the same offsets serve the true key range.
+// k_degree's work (tails, the FILE_DAT last record's extra head, max slot, range check)
+// and k_hist_count's per-tile head bucket counts in one read of the records.  Buckets are
+// laid out for the capacity (nb_cap rows); the rows beyond the max slot's stay zero, so
+// the same offsets serve the true key range.
+// Tails: the records come tail-sorted, so a tile's tails lie in [first tail, last tail]
+// (about 2K slots at RMAT-26).  When that span fits TSPAN LDS counters, each wave adds
+// its tail RUNS there (one LDS atomic per run) and the tile flushes the counters with
+// full-wave atomics: ~span/64 global atomic instructions per tile instead of one per
+// wave-load of records (run_add), whose issue rate bound the pass (4.5 ms at RMAT-26:
+// one atomic wave-instruction per ~50 ns per CU, MI355X_MICROARCH.md).  A tail outside
+// the span (an unsorted stretch) takes a global atomic of its own.
+constexpr uint32_t TSPAN = 4096;
+
 __global__ __launch_bounds__(CB) void k_degree_fused(const sheep_xs1 *__restrict__ rec, uint64_t n, int mode,
                                                      uint32_t *__restrict__ deg, uint64_t cap, uint32_t nb,
                                                      uint32_t *__restrict__ tile_hist, uint64_t ntiles,
                                                      unsigned long long *__restrict__ d_max,
                                                      unsigned long long *__restrict__ d_err) {
   extern __shared__ uint32_t lds[];
-  for (uint32_t b = threadIdx.x; b < nb; b += CB) lds[b] = 0;
-  lds_barrier();
+  uint32_t *tcnt = lds + nb;   // TSPAN tail counters after the nb head buckets
   const uint32_t tile = xcd_tile();
   const uint64_t base = (uint64_t)tile << TLOG;
+  const uint64_t last = (base + TKEYS < n ? base + TKEYS : n) - 1;
+  const uint32_t t0 = rec[base].tail, t1 = rec[last].tail;
+  const bool span = t1 >= t0 && t1 - t0 < TSPAN;   // uniform over the workgroup
+  for (uint32_t b = threadIdx.x; b < nb; b += CB) lds[b] = 0;
+  if (span)
+    for (uint32_t b = threadIdx.x; b <= t1 - t0; b += CB) tcnt[b] = 0;
+  lds_barrier();
+  const int lane = (int)__lane_id();
   uint32_t lmax = 0;
   bool bad = false;
   for (uint32_t step = 0; step < TKEYS; step += CB * CPT) {
@@ -467,13 +483,35 @@ __global__ __launch_bounds__(CB) void k_degree_fused(const sheep_xs1 *__restrict
           lmax = m > lmax ? m : lmax;
         }
       }
-      run_add(deg, kt, inc);   // every lane of the wave takes part (uniform loop)
+      if (span) {
+        // runs of equal tails among the wave's consecutive lanes: the run's first lane adds
+        // its length (the FILE_DAT last record's second count goes to the global counter)
+        const uint32_t prev = __shfl_up(kt, 1, 64);
+        const bool start = kt != INVALID && (lane == 0 || prev != kt);
+        const uint64_t starts = __ballot(start);
+        const uint64_t valid = __ballot(kt != INVALID);
+        if (start) {
+          const uint64_t above = lane == 63 ? 0ull : (starts & ~((2ull << lane) - 1));
+          const uint64_t vend = lane == 63 ? 0ull : (~valid & ~((2ull << lane) - 1));
+          const uint64_t stop = above | vend;
+          const int next = stop ? __ffsll((long long)stop) - 1 : 64;
+          const uint32_t len = (uint32_t)(next - lane);
+          if (kt >= t0 && kt <= t1) atomicAdd(&tcnt[kt - t0], len);   // the tile's zeroed counters
+          else atomicAdd(&deg[kt], len);
+        }
+        if (inc == 2) atomicAdd(&deg[kt], 1u);
+      } else {
+        run_add(deg, kt, inc);   // every lane of the wave takes part (uniform loop)
+      }
       if (inc == 2 && kh != INVALID) atomicAdd(&deg[kh], 1u);
       if (kh != INVALID) atomicAdd(&lds[kh >> WBITS], 1u);
     }
   }
   lds_barrier();
   for (uint32_t b = threadIdx.x; b < nb; b += CB) tile_hist[(uint64_t)b * ntiles + tile] = lds[b];
+  if (span)
+    for (uint32_t b = threadIdx.x; b <= t1 - t0; b += CB)
+      if (tcnt[b]) atomicAdd(&deg[t0 + b], tcnt[b]);
   block_atomic_max(d_max, lmax);
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(d_err, 1ull);
 }
@@ -653,7 +691,7 @@ bool degree_fused(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_
   const uint64_t nb = (cap + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
   if (nrec == 0 || nb == 0 || nb > 8192 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return false;
   uint32_t *tile_hist = c.get_as<uint32_t>("hist_tiles", ntiles * nb + 1);
-  hipLaunchKernelGGL(k_degree_fused, dim3((unsigned)ntiles), dim3(CB), nb * 4, c.stream, rec, nrec, mode, deg, cap,
+  hipLaunchKernelGGL(k_degree_fused, dim3((unsigned)ntiles), dim3(CB), (nb + TSPAN) * 4, c.stream, rec, nrec, mode, deg, cap,
                      (uint32_t)nb, tile_hist, ntiles, d_max, d_err);
   LAUNCH_CHECK();
   return true;

@@ -7,14 +7,16 @@
 // parsed in parallel, byte-bound:
 //   1. token starts (a non-blank byte after a blank one) counted per 4 KiB tile, scanned;
 //   2. token start offsets written in order;
-//   3. every token parsed: an unsigned decimal that fits 32 bits, or "bad"; whether a
+//   3. every token parsed the way istream >> reads an unsigned int, or "bad"; whether a
 //      newline precedes it (a line's first token); whether it opens a comment line;
 //   4. with skip_comments (the graph loader) tokens on '#' / '%' lines are dropped (line
 //      ids by a scan of the line-start flags); the first bad token left ends the input,
 //      as SNAPReader's failed >> does, and the valid tokens before it pair up into
 //      records {tail, head, 1.0f} (an incomplete last pair is dropped).
-// Unsigned decimal tokens only: istream >> accepts forms such as "+5" or "-5" (wrapped)
-// that no edge list uses; they count as "bad" here.
+// Tokens are read as istream >> reads an unsigned int (signs, wrap-around, leading zeros,
+// a number followed by other characters: k_tok_parse); pinned by the reference's own
+// SNAPReader on tests/golden/snap_cases.json.  Not followed: a token that holds two
+// numbers glued by a sign ("4-5": istream reads 4 and then -5) ends the input after 4.
 #include "common.hpp"
 
 namespace sheep {
@@ -69,8 +71,12 @@ __global__ __launch_bounds__(BLOCK) void k_tok_write(const char *__restrict__ te
 }
 
 // value; flags: 1 = a newline precedes the token (or it is the first), 2 = it opens a
-// comment line ('#' or '%' first on its line), 4 = not an unsigned 32-bit decimal
-// (4294967295 is a valid value, so validity is a flag, not a sentinel)
+// comment line ('#' or '%' first on its line), 4 = `>>` fails on it, 8 = `>>` reads a
+// number from its start but stops inside it (the next `>>` fails there).
+// The token as istream >> into an unsigned int reads it (num_get): an optional sign, at
+// least one digit, the magnitude at most 2^32 - 1 (else failbit), a '-' wraps modulo 2^32;
+// reading stops at the first non-digit.  (4294967295 is a valid value, so validity is a
+// flag, not a sentinel.)
 __global__ __launch_bounds__(BLOCK) void k_tok_parse(const char *__restrict__ text, uint64_t bytes,
                                                      const uint64_t *__restrict__ tpos, uint64_t ntok,
                                                      uint32_t *__restrict__ val, uint32_t *__restrict__ linestart,
@@ -81,20 +87,22 @@ __global__ __launch_bounds__(BLOCK) void k_tok_parse(const char *__restrict__ te
     bool nl = p == 0 || t == 0;
     for (uint64_t q = p; q > 0 && blank(text[q - 1]); --q)
       if (text[q - 1] == '\n') { nl = true; break; }
+    uint64_t q = p;
+    const bool neg = text[q] == '-';
+    if (text[q] == '+' || text[q] == '-') ++q;
     uint64_t v = 0;
     int digits = 0;
-    bool ok = true;
-    uint64_t q = p;
-    for (; q < bytes && !blank(text[q]); ++q) {
-      const char ch = text[q];
-      if (ch < '0' || ch > '9' || digits >= 10) { ok = false; }
-      else { v = v * 10 + (uint32_t)(ch - '0'); ++digits; }
+    for (; q < bytes && text[q] >= '0' && text[q] <= '9'; ++q) {
+      v = v * 10 + (uint32_t)(text[q] - '0');
+      if (v > 0xFFFFFFFFull) v = 0x100000000ull;   // saturated: overflow stays overflow
+      ++digits;
     }
-    ok = ok && digits > 0 && v <= 0xFFFFFFFFull;
-    val[t] = (uint32_t)v;
+    const bool ok = digits > 0 && v <= 0xFFFFFFFFull;
+    const bool rest = ok && q < bytes && !blank(text[q]);
+    val[t] = neg ? 0u - (uint32_t)v : (uint32_t)v;
     const char c0 = text[p];
     linestart[t] = nl ? 1u : 0u;
-    flags[t] = (nl ? 1 : 0) | (nl && (c0 == '#' || c0 == '%') ? 2 : 0) | (ok ? 0 : 4);
+    flags[t] = (nl ? 1 : 0) | (nl && (c0 == '#' || c0 == '%') ? 2 : 0) | (ok ? 0 : 4) | (rest ? 8 : 0);
   }
 }
 
@@ -110,6 +118,7 @@ __global__ __launch_bounds__(BLOCK) void k_tok_keep(const uint32_t *__restrict__
     const bool dropped = skip_comments && comment[lineid[t] - 1];
     keep[t] = dropped ? 0u : 1u;
     if (!dropped && (flags[t] & 4) && t < fb) fb = t;
+    if (!dropped && (flags[t] & 8) && t + 1 < fb) fb = t + 1;   // the input ends right after it
   }
   fb = wave_min(fb);
   if ((threadIdx.x & 63) == 0 && fb != ~0ull) atomicMin(first_bad, (unsigned long long)fb);

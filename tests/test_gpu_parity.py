@@ -2,6 +2,8 @@
 reference's golden fixtures (tests/golden, produced by oracle/_ref) and, at sizes the
 golden files do not cover, against the CPU oracle.  Bit-exact throughout (integer /
 index work)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -462,43 +464,51 @@ def test_group_join_processes_match_single_gpu(gpu_ctx, tmp_path, ranks):
     assert "link=host" in outs[0]
 
 
-def _snapreader(text: bytes, skip_comments: bool):
-    """SNAPReader (readerwriter.h:78-90) restated on the host: `>> X` then `>> Y` until one
-    fails; with skip_comments, lines whose first token starts with '#'/'%' are dropped first."""
-    toks = []
-    for line in text.decode().splitlines():
-        parts = line.split()
-        if skip_comments and parts and parts[0][0] in "#%":
-            continue
-        toks += parts
-    vals = []
-    for tok in toks:
-        if not tok.isdigit() or int(tok) > 0xFFFFFFFF:
-            break
-        vals.append(int(tok))
-    vals = vals[: len(vals) // 2 * 2]
-    return np.array(vals, dtype=np.uint64).reshape(-1, 2)
+def _skip_comment_lines(text: bytes) -> bytes:
+    """The graph loader's SNAP header handling (LLAMA's, un-vendored: parity unpinned):
+    lines whose first token starts with '#' or '%' are dropped before reading."""
+    keep = [ln for ln in text.split(b"\n") if not (ln.split() and ln.split()[0][:1] in (b"#", b"%"))]
+    return b"\n".join(keep)
 
 
-@pytest.mark.parametrize("skip", [False, True])
-@pytest.mark.parametrize("text", [
-    b"1 2\n3 4\n5 6\n",
-    b"1 2\n3 4\n5",                                   # incomplete last pair
-    b"  10\t20\r\n30    40\r\n\n\n50 60",             # tabs, CRLF, blank lines
-    b"# header\n% more\n1 2\n3 4\n",                  # comment header
-    b"1 2\n# mid comment 7 8\n3 4\n",                 # comment line inside
-    b"1 2\n3 x\n5 6\n",                               # garbage stops the input
-    b"1 2\n4294967295 0\n4294967296 1\n7 8\n",        # u32 overflow stops it
-    b"",
-    b"\n \n",
-])
-def test_parse_net(gpu_ctx, text, skip):
+def _snap_cases():
+    import json
+    from conftest import GOLDEN
+    return json.load(open(os.path.join(GOLDEN, "snap_cases.json")))
+
+
+@pytest.mark.parametrize("case", range(len(_snap_cases())))
+def test_parse_net_vs_reference_snapreader(gpu_ctx, case):
+    """sheep_parse_net against the reference's own SNAPReader (readerwriter.h:78-90,
+    compiled from /root/reference: tests/golden/make_snap_golden.py): signs, wrap-around,
+    leading zeros, overflow, a number with trailing characters, '#' as a bad token."""
     import sheep_amd
-    want = _snapreader(text, skip)
-    got = sheep_amd.to_numpy_u32(sheep_amd.parse_net(text, skip)).reshape(-1, 3)
-    assert got.shape[0] == want.shape[0]
+    c = _snap_cases()[case]
+    text = c["text"].encode()
+    want = np.array(c["pairs"], dtype=np.uint64).reshape(-1, 2)
+    got = sheep_amd.to_numpy_u32(sheep_amd.parse_net(text, False)).reshape(-1, 3)
     assert np.array_equal(got[:, :2].astype(np.uint64), want)
     assert np.all(got[:, 2].view(np.float32) == 1.0)
+
+
+@pytest.mark.parametrize("case", range(len(_snap_cases())))
+def test_parse_net_skip_comments(gpu_ctx, case):
+    """skip_comments = the same reading after the comment lines are dropped."""
+    import sheep_amd
+    c = _snap_cases()[case]
+    text = c["text"].encode()
+    stripped = sheep_amd.to_numpy_u32(sheep_amd.parse_net(_skip_comment_lines(text), False)).reshape(-1, 3)
+    got = sheep_amd.to_numpy_u32(sheep_amd.parse_net(text, True)).reshape(-1, 3)
+    assert np.array_equal(got, stripped)
+
+
+@pytest.mark.parametrize("text", [b"# header\n% more\n1 2\n3 4\n", b"1 2\n# mid comment 7 8\n3 4\n"])
+def test_parse_net_comment_lines(gpu_ctx, text):
+    import sheep_amd
+    got = sheep_amd.to_numpy_u32(sheep_amd.parse_net(text, True)).reshape(-1, 3)
+    assert got[:, :2].tolist() == [[1, 2], [3, 4]]
+    raw = sheep_amd.to_numpy_u32(sheep_amd.parse_net(text, False)).reshape(-1, 3)
+    assert raw.shape[0] == (0 if text.startswith(b"#") else 1)
 
 
 def test_parse_net_large_vs_dat(gpu_ctx):
