@@ -102,11 +102,11 @@ def shuffled(d, seed):
     import torch
     g = torch.Generator(device=d.device)
     g.manual_seed(seed)
-    out = d[torch.randperm(d.shape[0], device=d.device, generator=g)]
+    out = d[torch.randperm(d.shape[0], device=d.device, generator=g, dtype=torch.int32)]
     flip = torch.rand(out.shape[0], device=d.device, generator=g) < 0.5
-    tail = out[:, 0].clone()
-    out[flip, 0] = out[flip, 1]
-    out[flip, 1] = tail[flip]
+    tail, head = out[:, 0].clone(), out[:, 1].clone()   # (elementwise selects: a boolean-mask
+    out[:, 0] = torch.where(flip, head, tail)            # index_put over >2^31 elements ran
+    out[:, 1] = torch.where(flip, tail, head)            # for minutes on the C4 records)
     return out
 
 

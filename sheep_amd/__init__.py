@@ -278,8 +278,13 @@ def degree_sequence(records, mode: str = "llama", vs_cap: int | None = None, ctx
     ctx = ctx or default_context()
     t = _torch()
     nrec = records.shape[0]
-    if vs_cap is None:   # 1 + max vid, the ids read as u32 (an int32 tensor holds them)
-        vs_cap = int((records[:, :2].to(t.int64) & 0xFFFFFFFF).max().item()) + 1 if nrec else 1
+    if vs_cap is None:   # 1 + max vid, the ids read as u32 (an int32 tensor holds them); no wide copies
+        if nrec:
+            ends = records[:, :2]
+            lo, hi = int(ends.min().item()), int(ends.max().item())
+            vs_cap = (0xFFFFFFFF if lo < 0 else hi) + 1
+        else:
+            vs_cap = 1
     deg = t.zeros(max(vs_cap, 1), dtype=t.int32, device=_dev(ctx))
     _, vs = degree_count(records, nrec, mode, deg, ctx=ctx)
     return sequence_from_degrees(deg, vs, ctx)

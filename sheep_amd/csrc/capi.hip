@@ -1,6 +1,7 @@
 // capi.hip — the extern "C" boundary of libsheep_hip.so (declared in include/sheep_hip.h).
 // Exceptions never cross it: every entry point maps sheep::Error / std::exception to a
 // status code and a thread-local message.
+#include <chrono>
 #include <cstring>
 #include <string>
 
@@ -10,6 +11,16 @@
 namespace sheep {
 static thread_local std::string g_last_error;
 void set_error(const char *msg) { g_last_error = msg; }
+bool trace_launches() {
+  static const bool on = getenv("SHEEP_TRACE_LAUNCHES") != nullptr;
+  return on;
+}
+void trace_launch(const char *file, int line) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const hipError_t e = hipDeviceSynchronize();
+  const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  fprintf(stderr, "sheep launch %s:%d %.1f us%s\n", file, line, us, e == hipSuccess ? "" : " FAILED");
+}
 
 void degree_count(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap, uint64_t *max_slot);
 uint64_t sequence_from_degrees(Ctx &c, const uint32_t *deg, uint64_t vs, uint32_t *seq, uint32_t *pos);

@@ -32,7 +32,15 @@ struct Error : std::runtime_error {
                            std::string(#expr) + ": " + hipGetErrorString(_e));            \
   } while (0)
 
-#define LAUNCH_CHECK() HIP_CHECK(hipGetLastError())
+// SHEEP_TRACE_LAUNCHES=1 (debugging): every launch is followed by a device-wide wait and a
+// stderr line naming its source line, so a kernel that never finishes names itself.
+bool trace_launches();
+void trace_launch(const char *file, int line);
+#define LAUNCH_CHECK()                                                   \
+  do {                                                                   \
+    HIP_CHECK(hipGetLastError());                                        \
+    if (::sheep::trace_launches()) ::sheep::trace_launch(__FILE__, __LINE__); \
+  } while (0)
 
 // Grid for a grid-stride streaming kernel: enough workgroups to fill 256 CUs x 8.
 inline unsigned grid_for(uint64_t items, unsigned per_block = BLOCK, unsigned cap = 256 * 8) {

@@ -418,11 +418,15 @@ __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict
 // Contract every cross edge (a,b) -> (m_r, b) where r = a's light component; drop it
 // when b == m_r.  parent(top(r)) = m_r (jnode.h:158-162 adopt) is stored by k_level_clean
 // in one pass over mt (tagged state) or here by the edges with b == m_r.  Dedup: claim[b] holds
-// the first contracted lo seen for b; an edge that finds its own m_r there is a duplicate
-// of a kept edge and dies.  (Exact: only equal (m_r, b) pairs die, and the claimant
-// itself is kept.  Lossy: a second distinct m for the same b is kept without a check —
-// the common duplicates, a giant component's many edges into one hub, all carry the same
-// m.)  claim is n x u32, L3-resident, unlike a global hash table of the pairs.
+// the m of a KEPT contraction (m, b); an edge that finds its own m_r there is a duplicate
+// of it and dies.  An edge that finds no claim of this level is kept and stores its m
+// with a plain store: only keepers ever store, so whatever value a later read returns —
+// the last store, or another XCD's older one — names a kept edge.  (Exact: only equal
+// (m_r, b) pairs die.  Lossy: edges racing on a fresh claim, or carrying a second
+// distinct m, are kept without a check — the common duplicates, a giant component's many
+// edges into one hub, all carry the same m.)  A compare-and-swap per first touch made
+// every lane of the level's first wave of tiles queue on the hubs' words.  claim is
+// n x u32, L3-resident, unlike a global hash table of the pairs.
 //
 // The surviving contractions are APPENDED to the next list, after the entries k_split
 // kept: each 2048-edge tile reserves its survivors' slots in a sharded append (one
@@ -464,12 +468,10 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restric
 #pragma unroll
     for (int k = 0; k < TILE_ITEMS; ++k) {
       if (r[k] == INVALID || b[k] == m[k]) continue;
-      uint32_t c = g.claim_get(cl[k]);
-      if (c == INVALID) {
-        const uint32_t old = atomicCAS(&claim[b[k]], cl[k], g.enc(m[k]));
-        c = old == cl[k] ? INVALID : g.claim_get(old);
-      }
-      if (c != m[k]) keep |= 1u << k;   // someone else's (m, b) is kept (our own successful CAS left INVALID)
+      const uint32_t c = g.claim_get(cl[k]);
+      if (c == m[k]) continue;   // a kept edge's (m, b): this one is its duplicate
+      keep |= 1u << k;
+      if (c == INVALID) claim[b[k]] = g.enc(m[k]);   // first seen this level: a plain store
     }
     uint64_t slot = shard_reserve((uint32_t)__popc(keep), counters, tile, ntiles, 1);
 #pragma unroll

@@ -192,3 +192,23 @@ def test_partition_sequence_length_semantics():
     want[short] = parts_full[short]
     assert np.array_equal(parts, want)
     assert info["created"] == int(want.max()) + 1
+
+
+@pytest.mark.parametrize("cfg", ["c3", "c4", "c5"])
+def test_scale_golden_digests_are_consistent(cfg):
+    """tests/golden/scale/<cfg>.json (the oracle's results at a BASELINE configuration,
+    tools/make_scale_golden.py): every field the GPU tests compare is there and the scalar
+    results agree with each other — simple graphs, so every record is one tree edge
+    (Σ pst = records = ECV's edge count), n nodes, k parts at most, TREEFAQS' counts."""
+    import json
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "scale", f"{cfg}.json")))
+    for key in ("records_digest", "seq_digest", "parent_digest", "pst_digest", "parts_digest"):
+        assert len(g[key]) == 32 and int(g[key], 16) >= 0
+    assert set(g["evaluate"]) == set(oracle.EVAL_FIELDS)
+    assert set(g["facts"]) == set(oracle.FACT_FIELDS)
+    assert g["pst_sum"] == g["records"] == g["evaluate"]["edges"] == g["facts"]["edge_cnt"]
+    assert g["n"] == g["evaluate"]["nodes"] == g["facts"]["vert_cnt"] <= g["pos_size"]
+    assert g["roots"] == g["facts"]["root_cnt"]
+    assert g["created"] <= g["k"] and g["packing_nodes"] > 0
+    assert g["max_component"] == int((g["pst_sum"] // g["k"]) * 1.03)          # partition.cpp:54-57
+    assert g["evaluate"]["max_down_bal"] <= g["max_component"]

@@ -1,16 +1,18 @@
 """Parity at BASELINE.json's configurations, at FULL size, against
 the CPU oracle (test infrastructure, OpenMP threads):
 
-* C2 — RMAT-22 ef16 seed 22, k = 16, one GPU: sequence, every parent and pst, parts,
-  created / first-two sizes, every evaluator count, TREEFAQS.
+* C2 — RMAT-22 ef16 seed 22, k = 16, one GPU, the oracle run live: sequence, every
+  parent and pst, parts, created / first-two sizes, every evaluator count, TREEFAQS.
+* C3-C5 — against the oracle's recorded digests (tests/golden/scale/, made by
+  tools/make_scale_golden.py on the GPU box: the oracle takes minutes per configuration
+  there, more than the GPU suite's time budget):
 * C3 — RMAT-26 ef16 seed 26, k = 64 (1.05e9 records): the oracle's sequence; every
   parent and pst against the oracle's tree (graph2tree -r form: 16 shard trees + the
   binomial mpi_merge, pinned to the golden trees by tests/test_oracle_golden.py); the
   whole tree == the one-pass merge of 8 contiguous shard trees; parts, created and every
-  evaluator count against the oracle.
+  evaluator count against the oracle; the same on the shuffled records.
 * C4 — Chung-Lu power law at twitter-2010 scale (41.65 M vertices, ~1.47e9 records,
-  seed 2010), k = 128: the same set, plus the 8-shard merge, on the generated and on a
-  shuffled copy of the records.
+  seed 2010), k = 128: the same set.
 * C5 — RMAT-28 ef16 seed 28 (4.24e9 records: more than 2^32), k = 256, as 8 edge shards
   on one GPU (the one-GPU form of the 8-GPU configuration): the sequence from the
   shards' summed degrees, the K-way merge of the 8 shard trees against the oracle's
@@ -20,6 +22,7 @@ the CPU oracle (test infrastructure, OpenMP threads):
 
 Each configuration's GPU state lives in a class-scoped fixture so it is freed before
 the next one is built."""
+import json
 import os
 
 import numpy as np
@@ -28,6 +31,7 @@ import pytest
 import oracle
 
 pytestmark = pytest.mark.gpu
+GOLDEN_SCALE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "scale")
 THREADS = min(16, os.cpu_count() or 1)
 
 
@@ -36,13 +40,13 @@ def _shuffled(d, seed):
     import torch
     g = torch.Generator(device=d.device)
     g.manual_seed(seed)
-    perm = torch.randperm(d.shape[0], device=d.device, generator=g)
+    perm = torch.randperm(d.shape[0], device=d.device, generator=g, dtype=torch.int32)
     out = d[perm]
     del perm
     flip = torch.rand(out.shape[0], device=d.device, generator=g) < 0.5
-    tail = out[:, 0].clone()
-    out[flip, 0] = out[flip, 1]
-    out[flip, 1] = tail[flip]
+    tail, head = out[:, 0].clone(), out[:, 1].clone()   # (elementwise selects: a boolean-mask
+    out[:, 0] = torch.where(flip, head, tail)            # index_put over >2^31 elements ran
+    out[:, 1] = torch.where(flip, tail, head)            # for minutes on the C4 records)
     return out
 
 
@@ -117,145 +121,165 @@ class TestC2:
 
 
 # ---------------------------------------------------------------------------------
-# C3: RMAT-26, k = 64, full size
+# C3-C5 at full size against the oracle's digests.  tools/make_scale_golden.py ran the
+# oracle on each configuration's seeded records on the GPU box's host cores (minutes per
+# configuration; the run logs are in profiles/r3/) and tests/golden/scale/<cfg>.json
+# holds xxh3-128 digests of its sequence, parent, pst and parts arrays with every scalar
+# result.  Each test regenerates the same records (their digest is checked first), runs
+# the GPU path through the C ABI and compares digests and counts: bit-exact, in seconds.
 # ---------------------------------------------------------------------------------
-class TestC3:
+def _golden(cfg):
+    return json.load(open(os.path.join(GOLDEN_SCALE, f"{cfg}.json")))
+
+
+def _digest(a):
+    import xxhash
+    h = xxhash.xxh3_128()
+    h.update(np.ascontiguousarray(a).view(np.uint8))
+    return h.hexdigest()
+
+
+def _records_digest(d):
+    """xxh3-128 of the (tail, head) pairs, streamed to the host in chunks."""
+    import xxhash
+    x = xxhash.xxh3_128()
+    step = 1 << 27
+    for a in range(0, d.shape[0], step):
+        x.update(np.ascontiguousarray(d[a:a + step, :2].cpu().numpy()).view(np.uint8))
+    return x.hexdigest()
+
+
+def _check_seq(s, g):
+    assert s.n == g["n"] and s.pos_size == g["pos_size"]
+    assert _digest(s.numpy()) == g["seq_digest"], "sequence"
+
+
+def _check_tree_digest(tree, g):
+    import sheep_amd
+    p, w = sheep_amd.tree_to_numpy(tree)
+    assert len(p) == g["n"]
+    assert _digest(w) == g["pst_digest"], "pst_weight"
+    assert _digest(p) == g["parent_digest"], "parent"
+    # SURVEY §0 invariant 1 on the GPU's own array: every parent is a later node
+    v = np.arange(len(p), dtype=np.int64)
+    assert np.all((p == 0xFFFFFFFF) | (p.astype(np.int64) > v))
+    assert int(np.count_nonzero(p == 0xFFFFFFFF)) == g["roots"]
+
+
+def _check_parts(res, g):
+    parts = res.numpy()
+    assert _digest(parts) == g["parts_digest"], "parts"
+    assert res.created == g["created"] and res.packing_nodes == g["packing_nodes"]
+    assert res.first_size == g["first_size"] and res.second_size == g["second_size"]
+
+
+def _gen(g):
+    import sheep_amd
+    gen = g["generator"]
+    if gen["graph"] == "rmat":
+        return sheep_amd.rmat(gen["scale"], 16, gen["seed"])
+    return sheep_amd.powerlaw(sheep_amd.TWITTER_VERTICES, gen["draws"], gen["gamma"], gen["seed"])
+
+
+class _FullSize:
+    """The whole path at one BASELINE configuration on one GPU against its digests."""
+    CFG = None
+
     @pytest.fixture(scope="class")
-    def c3(self, gpu_ctx):
+    def st(self, gpu_ctx):
         import sheep_amd
-        oracle.set_threads(THREADS)
-        state = {"d": sheep_amd.rmat(26, 16, 26)}
-        state["s"] = sheep_amd.degree_sequence(state["d"], vs_cap=1 << 26)
-        state["tree"] = sheep_amd.build_tree(state["d"], state["s"])
-        state["t"], state["h"] = _host(state["d"])
+        g = _golden(self.CFG)
+        d = _gen(g)
+        state = {"g": g, "d": d}
+        state["s"] = sheep_amd.degree_sequence(d, vs_cap=g["pos_size"])
+        state["tree"] = sheep_amd.build_tree(d, state["s"])
         yield state
         state.clear()
-        oracle.set_threads(1)
         _free()
 
-    def test_c3_rmat26_sequence_vs_oracle(self, c3):
-        c3["seq"] = oracle.sequence(c3["t"], c3["h"], "records")
-        assert np.array_equal(c3["s"].numpy(), c3["seq"])
+    def test_records_are_the_oracle_input(self, st):
+        assert st["d"].shape[0] == st["g"]["records"]
+        assert _records_digest(st["d"]) == st["g"]["records_digest"]
 
-    def test_c3_rmat26_tree_vs_oracle(self, c3):
-        """Every parent and pst against the oracle's tree (jtree.cpp:66-110 per shard,
-        jnode.cpp:174-250 reduce), and parent[v] > v (SURVEY §0 invariant 1)."""
-        seq = c3.get("seq")
-        if seq is None:
-            seq = c3["s"].numpy()
-        c3["op"], c3["ow"] = oracle.build_tree_mr(c3["t"], c3["h"], seq, 16)
-        _check_tree(c3["tree"], c3["op"], c3["ow"])
-        op = c3["op"].astype(np.int64)
-        v = np.arange(len(op))
-        assert np.all((op == 0xFFFFFFFF) | (op > v))
+    def test_sequence_and_tree_vs_oracle(self, st):
+        """degreeSequence (sequence.h:52-92); every parent and pst against the oracle's
+        map/reduce tree (jtree.cpp:66-110 per shard, jnode.cpp:174-250); TREEFAQS."""
+        import sheep_amd
+        _check_seq(st["s"], st["g"])
+        _check_tree_digest(st["tree"], st["g"])
+        assert sheep_amd.facts(st["tree"]).__dict__ == st["g"]["facts"]
 
-    def test_c3_rmat26_eight_shards_merge_to_whole_tree(self, c3):
+    def test_eight_shards_merge_to_whole_tree(self, st):
         import sheep_amd
         import torch
-        d, s, whole = c3["d"], c3["s"], c3["tree"]
+        d, s = st["d"], st["s"]
         R = d.shape[0]
         parts = torch.stack([sheep_amd.build_tree(d[i * R // 8:(i + 1) * R // 8], s) for i in range(8)])
         merged = sheep_amd.merge_trees_many(parts)
         del parts
-        assert torch.equal(merged, whole)
+        assert torch.equal(merged, st["tree"])
 
-    def test_c3_rmat26_k64_partition_and_evaluate_vs_oracle(self, c3):
+    def test_partition_and_full_evaluator_vs_oracle(self, st):
+        """Partition + forwardPartition (partition.cpp:50-157), every evaluator count
+        (partition.cpp:428-521)."""
         import sheep_amd
-        d, s, tree = c3["d"], c3["s"], c3["tree"]
-        p, w = c3.get("op"), c3.get("ow")
-        if p is None:
-            p, w = sheep_amd.tree_to_numpy(tree)
-        seq = s.numpy()
-        oparts, oinfo = oracle.partition(p, w, seq, 64)
-        res = sheep_amd.partition(s, tree, 64)
-        assert np.array_equal(res.numpy(), oparts)
-        assert res.created == oinfo["created"]
-        c3["parts"] = res
-        ev = sheep_amd.evaluate(d, s, res.parts)
-        oev = oracle.evaluate(c3["t"], c3["h"], seq, oparts)
-        assert ev.__dict__ == oev
-
-    def test_c3_rmat26_shuffled_records_same_results(self, c3):
-        """The whole path on the shuffled records: same sequence, tree, parts and counts."""
-        import sheep_amd
-        import torch
-        d = _shuffled(c3["d"], 2026)
-        s = sheep_amd.degree_sequence(d, vs_cap=1 << 26)
-        assert torch.equal(s.seq[: s.n], c3["s"].seq[: c3["s"].n])
-        tree = sheep_amd.build_tree(d, s)
-        assert torch.equal(tree, c3["tree"])
-        res = sheep_amd.partition(s, tree, 64)
-        ref = c3.get("parts") or sheep_amd.partition(c3["s"], c3["tree"], 64)
-        assert torch.equal(res.parts, ref.parts)
-        ev = sheep_amd.evaluate(d, s, res.parts, what=sheep_amd.EVAL_DOWN)
-        ev0 = sheep_amd.evaluate(c3["d"], c3["s"], ref.parts, what=sheep_amd.EVAL_DOWN)
-        assert ev == ev0
-
-
-# ---------------------------------------------------------------------------------
-# C4: Chung-Lu power law at twitter-2010 scale, k = 128
-# ---------------------------------------------------------------------------------
-class TestC4:
-    @pytest.fixture(scope="class")
-    def c4(self, gpu_ctx):
-        import sheep_amd
-        oracle.set_threads(THREADS)
-        d = sheep_amd.powerlaw(sheep_amd.TWITTER_VERTICES, 2_222_000_000, 1.9, 2010)
-        t, h = _host(d)
-        seq = oracle.sequence(t, h, "records")
-        op, ow = oracle.build_tree_mr(t, h, seq, 16)
-        oparts, oinfo = oracle.partition(op, ow, seq, 128)
-        state = dict(d=d, t=t, h=h, seq=seq, op=op, ow=ow, oparts=oparts, oinfo=oinfo)
-        yield state
-        state.clear()
-        oracle.set_threads(1)
-        _free()
-
-    def test_c4_size_is_twitter_scale(self, c4):
-        R = c4["d"].shape[0]
-        assert 1.40e9 < R < 1.55e9, R       # twitter-2010: 1,468,365,182 records
-        assert len(c4["seq"]) > 0.5 * 41_652_230
-
-    @pytest.mark.parametrize("variant", ["generated", "shuffled"])
-    def test_c4_powerlaw_k128_full_path(self, c4, variant):
-        import sheep_amd
-        import torch
-        _free()
-        d = c4["d"] if variant == "generated" else _shuffled(c4["d"], 2010)
-        s = sheep_amd.degree_sequence(d, vs_cap=sheep_amd.TWITTER_VERTICES)
-        assert np.array_equal(s.numpy(), c4["seq"]), "sequence"
-        tree = sheep_amd.build_tree(d, s)
-        _check_tree(tree, c4["op"], c4["ow"])
-        if variant == "generated":
-            R = d.shape[0]
-            stack = torch.stack([sheep_amd.build_tree(d[i * R // 8:(i + 1) * R // 8], s) for i in range(8)])
-            assert torch.equal(sheep_amd.merge_trees_many(stack), tree), "8-shard K-way merge"
-            del stack
-        kids = sheep_amd.KidTable(tree)
-        res = sheep_amd.partition(s, tree, 128, kids=kids)
+        g = st["g"]
+        kids = sheep_amd.KidTable(st["tree"])
+        res = sheep_amd.partition(st["s"], st["tree"], g["k"], kids=kids)
         kids.close()
-        assert np.array_equal(res.numpy(), c4["oparts"]), "parts"
-        assert res.created == c4["oinfo"]["created"]
-        ev = sheep_amd.evaluate(d, s, res.parts)
-        if "oev" not in c4:
-            c4["oev"] = oracle.evaluate(c4["t"], c4["h"], c4["seq"], c4["oparts"])
-        assert ev.__dict__ == c4["oev"]
+        _check_parts(res, g)
+        st["parts"] = res
+        ev = sheep_amd.evaluate(st["d"], st["s"], res.parts)
+        assert ev.__dict__ == g["evaluate"]
+
+    def test_shuffled_records_same_results(self, st):
+        """The whole path on the records in a random order, half of them reversed."""
+        import sheep_amd
+        g = st["g"]
+        _free()
+        d = _shuffled(st["d"], 2000 + g["generator"]["seed"])
+        s = sheep_amd.degree_sequence(d, vs_cap=g["pos_size"])
+        _check_seq(s, g)
+        tree = sheep_amd.build_tree(d, s)
+        _check_tree_digest(tree, g)
+        res = sheep_amd.partition(s, tree, g["k"])
+        _check_parts(res, g)
+        ev = sheep_amd.evaluate(d, s, res.parts, what=sheep_amd.EVAL_DOWN)
+        assert (ev.ecv_down, ev.max_down_bal) == (g["evaluate"]["ecv_down"], g["evaluate"]["max_down_bal"])
         del d, tree
         _free()
 
 
-# ---------------------------------------------------------------------------------
-# C5: RMAT-28, k = 256, 8 edge shards on one GPU, full evaluator
-# ---------------------------------------------------------------------------------
+class TestC3(_FullSize):
+    """C3: RMAT-26 ef16 seed 26, k = 64 (1.05e9 records)."""
+    CFG = "c3"
+
+
+class TestC4(_FullSize):
+    """C4: Chung-Lu power law at twitter-2010 scale (41.65 M vertices, ~1.47e9 records,
+    seed 2010), k = 128."""
+    CFG = "c4"
+
+    def test_size_is_twitter_scale(self, st):
+        R = st["d"].shape[0]
+        assert 1.40e9 < R < 1.55e9, R       # twitter-2010: 1,468,365,182 records
+        assert st["g"]["n"] > 0.5 * 41_652_230
+
+
 class TestC5:
+    """C5: RMAT-28 ef16 seed 28 (4.24e9 records: more than 2^32), k = 256, as 8 edge
+    shards on one GPU (the one-GPU form of the 8-GPU configuration): the sequence from the
+    shards' summed degrees (mpiSequence), the K-way merge of the 8 shard trees against the
+    oracle's tree AND against the binomial pairwise merges of the same shard trees
+    (mpi_merge's schedule), parts, and the full evaluator accumulated shard by shard."""
     SHARDS = 8
 
     @pytest.fixture(scope="class")
     def c5(self, gpu_ctx):
         import sheep_amd
         import torch
-        oracle.set_threads(THREADS)
-        d = sheep_amd.rmat(28, 16, 28)
+        g = _golden("c5")
+        d = _gen(g)
         R = d.shape[0]
         subs = [d[i * R // self.SHARDS:(i + 1) * R // self.SHARDS] for i in range(self.SHARDS)]
         deg = torch.zeros(1 << 28, dtype=torch.int32, device="cuda")
@@ -269,30 +293,23 @@ class TestC5:
         for i, sub in enumerate(subs):
             sheep_amd.build_tree(sub, s, out=stack[i])
         tree = sheep_amd.merge_trees_many(stack)
-        t, h = _host(d)
-        state = dict(d=d, subs=subs, s=s, stack=stack, tree=tree, t=t, h=h)
+        state = dict(g=g, d=d, subs=subs, s=s, stack=stack, tree=tree)
         yield state
         state.clear()
-        oracle.set_threads(1)
         _free()
 
-    def test_c5_rmat28_more_than_2e32_records(self, c5):
-        assert c5["d"].shape[0] > (1 << 32) - (1 << 28)
+    def test_c5_records_are_the_oracle_input(self, c5):
+        assert c5["d"].shape[0] == c5["g"]["records"] > (1 << 32) - (1 << 28)
         assert all(sub.shape[0] < (1 << 32) for sub in c5["subs"])
+        assert _records_digest(c5["d"]) == c5["g"]["records_digest"]
 
-    def test_c5_rmat28_sequence_vs_oracle(self, c5):
-        c5["seq"] = oracle.sequence(c5["t"], c5["h"], "records")
-        assert np.array_equal(c5["s"].numpy(), c5["seq"])
+    def test_c5_sequence_and_kway_tree_vs_oracle(self, c5):
+        import sheep_amd
+        _check_seq(c5["s"], c5["g"])
+        _check_tree_digest(c5["tree"], c5["g"])
+        assert sheep_amd.facts(c5["tree"]).__dict__ == c5["g"]["facts"]
 
-    def test_c5_rmat28_kway_merge_vs_oracle_tree(self, c5):
-        seq = c5.get("seq")
-        if seq is None:
-            seq = c5["s"].numpy()
-        c5["op"], c5["ow"] = oracle.build_tree_mr(c5["t"], c5["h"], seq, self.SHARDS)
-        _check_tree(c5["tree"], c5["op"], c5["ow"])
-
-    def test_c5_rmat28_kway_equals_binomial_pairwise(self, c5):
-        """mpi_merge's binomial schedule (pairwise sheep_merge_trees) == the K-way merge."""
+    def test_c5_kway_equals_binomial_pairwise(self, c5):
         import sheep_amd
         import torch
         cur = [c5["stack"][i] for i in range(self.SHARDS)]
@@ -304,27 +321,19 @@ class TestC5:
             d *= 2
         assert torch.equal(cur[0], c5["tree"])
 
-    def test_c5_rmat28_k256_partition_and_full_evaluator_vs_oracle(self, c5):
+    def test_c5_partition_and_full_evaluator_vs_oracle(self, c5):
         import sheep_amd
-        s, tree = c5["s"], c5["tree"]
-        p, w = c5.get("op"), c5.get("ow")
-        if p is None:
-            p, w = sheep_amd.tree_to_numpy(tree)
-        seq = s.numpy()
+        g = c5["g"]
         c5.pop("stack", None)
         _free()
-        kids = sheep_amd.KidTable(tree)
-        res = sheep_amd.partition(s, tree, 256, kids=kids)
+        kids = sheep_amd.KidTable(c5["tree"])
+        res = sheep_amd.partition(c5["s"], c5["tree"], g["k"], kids=kids)
         kids.close()
-        oparts, oinfo = oracle.partition(p, w, seq, 256)
-        assert np.array_equal(res.numpy(), oparts), "parts"
-        assert res.created == oinfo["created"]
-        ev = sheep_amd.ShardedEvaluator(s, res.parts, sheep_amd.EVAL_GRAPH | sheep_amd.EVAL_DOWN | sheep_amd.EVAL_UP)
+        _check_parts(res, g)
+        ev = sheep_amd.ShardedEvaluator(c5["s"], res.parts, sheep_amd.EVAL_GRAPH | sheep_amd.EVAL_DOWN | sheep_amd.EVAL_UP)
         for sub in c5["subs"]:
             ev.add(sub)
-        got = ev.finish()
-        oev = oracle.evaluate(c5["t"], c5["h"], seq, oparts)
-        assert got.__dict__ == oev
+        assert ev.finish().__dict__ == g["evaluate"]
 
 
 # ---------------------------------------------------------------------------------
