@@ -98,15 +98,32 @@ def make_records(a, seed, ctx):
 
 
 def shuffled(d, seed):
-    """The records in a random order, half of them with tail and head swapped."""
+    """The records in a scrambled order, half of them with tail and head swapped: record i
+    of the output is record (a * i + b) mod R of the input (a odd, coprime to R, and b drawn
+    from the seed) — consecutive outputs lie a apart, so the tails lose their order — and a
+    hash of its source index decides the swap.  Built column by column in chunks:
+    torch.randperm stalls above 2^30 elements on this stack (the C4 records), and whole-
+    tensor indexing of an R x 3 tensor past 2^32 elements is slow."""
+    import math
+    import random
     import torch
-    g = torch.Generator(device=d.device)
-    g.manual_seed(seed)
-    out = d[torch.randperm(d.shape[0], device=d.device, generator=g, dtype=torch.int32)]
-    flip = torch.rand(out.shape[0], device=d.device, generator=g) < 0.5
-    tail, head = out[:, 0].clone(), out[:, 1].clone()   # (elementwise selects: a boolean-mask
-    out[:, 0] = torch.where(flip, head, tail)            # index_put over >2^31 elements ran
-    out[:, 1] = torch.where(flip, tail, head)            # for minutes on the C4 records)
+    R = d.shape[0]
+    rng = random.Random(seed)
+    a = rng.randrange(R // 3, R) | 1 if R > 3 else 1
+    while math.gcd(a, R) != 1:
+        a += 2
+    b = rng.randrange(R) if R else 0
+    out = torch.empty_like(d)
+    cols = [d[:, j].contiguous() for j in range(3)]
+    step = 1 << 26
+    for s in range(0, R, step):
+        e = min(R, s + step)
+        src = (torch.arange(s, e, device=d.device, dtype=torch.int64) * a + b) % R
+        flip = ((src * 0x2545F4914F6CDD1D) >> 40) & 1 == 1
+        tail, head = cols[0][src], cols[1][src]
+        out[s:e, 0] = torch.where(flip, head, tail)
+        out[s:e, 1] = torch.where(flip, tail, head)
+        out[s:e, 2] = cols[2][src]
     return out
 
 

@@ -552,10 +552,10 @@ struct RelabelKeys {
 };
 
 // One tile of TKEYS records per workgroup, staged SUB = PER * HB at a time (u64 payloads:
-// a whole tile does not fit LDS), bucketed by head >> SHIFT.  gb[b] walks the tile's region of bucket b; every write
+// a whole tile does not fit LDS).  gb[b] walks the tile's region of bucket b; every write
 // is bounded by the region's end and a region not filled exactly raises flags[1] (stale
 // offsets) so the host recounts.  flags[0]: a sequenced endpoint's neighbour >= pos_size.
-template <int PER, int SHIFT>
+template <int PER>
 __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restrict__ rec, uint64_t n,
                                                         const uint32_t *__restrict__ pos, uint64_t pos_size, uint32_t nb,
                                                         const uint32_t *__restrict__ offsets, uint64_t ntiles,
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
         continue;
       }
       x[j] = ((uint64_t)ptm << 32) | h;
-      atomicAdd(&cur[h >> SHIFT], 1u);
+      atomicAdd(&cur[h >> WBITS], 1u);
     }
     lds_barrier();
     const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
@@ -606,11 +606,11 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
     lds_barrier();
 #pragma unroll
     for (int j = 0; j < PER; ++j)
-      if (x[j] != NO_PAIR) stage[atomicAdd(&cur[(uint32_t)x[j] >> SHIFT], 1u)] = x[j];
+      if (x[j] != NO_PAIR) stage[atomicAdd(&cur[(uint32_t)x[j] >> WBITS], 1u)] = x[j];
     lds_barrier();
     for (uint32_t j = threadIdx.x; j < total; j += HB) {
       const uint64_t v = stage[j];
-      const uint32_t b = (uint32_t)v >> SHIFT, dst = gb[b] + j;
+      const uint32_t b = (uint32_t)v >> WBITS, dst = gb[b] + j;
       if (dst < end[b]) out[dst] = v;
       else lost = true;
     }
@@ -624,93 +624,66 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
   if (__any(lost) && (threadIdx.x & 63) == 0) atomicAdd(&flags[1], 1ull);
 }
 
-// Coarse relabel buckets: 2^CBITS head slots (4 of the degree pass's 2^15-slot buckets).
-// The scatter's LDS counting sort then has 4x fewer buckets, so each bucket's run of a
-// 16K-record sub-tile is ~64 pairs at RMAT-26 (512 B) instead of ~4 (32 B): the writes
-// coalesce.  The gather no longer holds a bucket's pos slice in LDS; it reads pos[head]
-// through the XCD's L2 — xcd_tile() gives each XCD a contiguous range of the pairs, so the
-// ~64 workgroups an XCD runs at once sit in about one coarse bucket, a 512 KiB pos slice.
-constexpr int CBITS = 17;
-constexpr uint32_t FINE_PER_COARSE = 1u << (CBITS - WBITS);
-
-// offc[B * ntiles + t] = where (coarse bucket B, record tile t)'s run starts, from the
-// degree pass's scanned fine offsets off (bucket-major, nb fine rows, off[nb * ntiles] =
-// total): coarse B's region is fine buckets FPC*B .. FPC*B + FPC-1 back to back, so its
-// tile-t run starts at bstart(FPC*B) + the runs of tiles < t of those fine buckets.
-__global__ void k_coarse_offsets(const uint32_t *__restrict__ off, uint32_t nb, uint64_t ntiles, uint32_t nbc,
-                                 uint32_t *__restrict__ offc) {
-  const uint64_t total = (uint64_t)nbc * ntiles, stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= total; i += stride) {
-    if (i == total) { offc[i] = off[(uint64_t)nb * ntiles]; continue; }
-    const uint32_t B = (uint32_t)(i / ntiles);
-    const uint64_t t = i - (uint64_t)B * ntiles;
-    const uint32_t b0 = B * FINE_PER_COARSE;
-    uint32_t o = off[(uint64_t)b0 * ntiles];
-#pragma unroll
-    for (uint32_t k = 0; k < FINE_PER_COARSE; ++k)
-      if (b0 + k < nb) o += off[(uint64_t)(b0 + k) * ntiles + t] - off[(uint64_t)(b0 + k) * ntiles];
-    offc[i] = o;
-  }
-}
-
-// One workgroup per 32K-pair tile of the scattered pairs (xcd_tile order).  Same outcomes
-// as k_relabel: both endpoints sequenced -> tree edge (hi << 32 | lo); one sequenced, the
-// other an unsequenced slot -> POSTORDER pst for the sequenced one.  pos[head] is gathered
-// from global memory with all eight of a thread's pair loads, then all eight pos loads, in
-// flight.  COUNT: also the tile's (padded-lo bucket) counts of the grouping's count pass
-// (k_hist_count<EdgeLoPadded> over the same edges, which then does not run), stored whole
-// (zeros included) into tile_hist's column of this tile.
-constexpr int GI = 8;   // pairs per thread per step
+// One workgroup per (bucket, slice of <= CHUNK pairs): the bucket's pos slice in LDS.
+// Same outcomes as k_relabel: both endpoints sequenced -> tree edge (hi << 32 | lo);
+// one sequenced, the other an unsequenced slot -> POSTORDER pst for the sequenced one.
+// COUNT: also the edges' (padded-lo bucket, 32K-edge tile) counts of the grouping's
+// count pass (k_hist_count<EdgeLoPadded> over the same edges, which then does not run):
+// the chunk is walked one output tile at a time with the tile's counts in LDS after the
+// pos slice, flushed with one atomicAdd per non-zero bucket (a tile can span two chunks).
 template <bool COUNT>
-__global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restrict__ pairs, uint64_t m,
+__global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restrict__ pairs, const Chunk *__restrict__ chunks,
                                                        const uint32_t *__restrict__ pos, uint64_t pos_size,
                                                        uint32_t *__restrict__ pst, uint64_t *__restrict__ edges,
                                                        unsigned long long *__restrict__ flags, EdgeLoPadded lk,
                                                        uint32_t lnb, uint32_t *__restrict__ tile_hist, uint64_t ntiles,
                                                        uint64_t n_tree) {
-  extern __shared__ uint32_t lcnt[];
-  const uint64_t tile = xcd_tile();
-  const uint64_t t0 = tile << TLOG, t1 = t0 + TKEYS < m ? t0 + TKEYS : m;
-  if (COUNT) {
-    for (uint32_t b = threadIdx.x; b < lnb; b += HB) lcnt[b] = 0;
-    lds_barrier();
-  }
+  extern __shared__ uint32_t lds[];
+  uint32_t *const lcnt = lds + W;
+  const Chunk ch = chunks[blockIdx.x];
+  const uint64_t v0 = (uint64_t)ch.bucket << WBITS;
+  for (uint32_t i = threadIdx.x; i < W; i += HB) lds[i] = v0 + i < pos_size ? pos[v0 + i] : INVALID;
   bool bad = false;
-  for (uint64_t i0 = t0; i0 < t1; i0 += GI * HB) {
-    uint64_t x[GI];
-    uint32_t ph[GI];
-#pragma unroll
-    for (int j = 0; j < GI; ++j) {
-      const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
-      x[j] = i < t1 ? pairs[i] : NO_PAIR;
-    }
-#pragma unroll
-    for (int j = 0; j < GI; ++j) {
-      const uint32_t h = (uint32_t)x[j];
-      ph[j] = x[j] != NO_PAIR && h < pos_size ? pos[h] : INVALID;
-    }
-#pragma unroll
-    for (int j = 0; j < GI; ++j) {
-      const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
-      if (i >= t1) continue;
-      const uint32_t ptm = (uint32_t)(x[j] >> 32);
-      uint64_t e = ~0ull;   // DEAD
-      // (ptm is a position < n_tree, INVALID or PT_OOR; anything else is a stale region
-      // of a run the host discards, kept in bounds)
-      if (ph[j] != INVALID) {
-        if (ptm == PT_OOR) bad = true;                       // index.at(tail) throws
-        else if (ptm < n_tree) e = ptm < ph[j] ? ((uint64_t)ph[j] << 32) | ptm : ((uint64_t)ptm << 32) | ph[j];
-        else if (ptm == INVALID) atomicAdd(&pst[ph[j]], 1u);
-      } else if (ptm < n_tree) {
-        atomicAdd(&pst[ptm], 1u);
-      }
-      edges[i] = e;
-      if (COUNT && e != ~0ull) atomicAdd(&lcnt[lk.key(e) >> WBITS], 1u);
-    }
-  }
-  if (COUNT) {
+  for (uint64_t t0 = ch.beg; t0 < ch.end;) {
+    const uint64_t t1 = COUNT ? ((t0 >> TLOG) + 1) << TLOG : ch.end;   // this output tile's part of the chunk
+    const uint64_t s1 = t1 < ch.end ? t1 : ch.end;
+    if (COUNT)
+      for (uint32_t b = threadIdx.x; b < lnb; b += HB) lcnt[b] = 0;
     lds_barrier();
-    for (uint32_t b = threadIdx.x; b < lnb; b += HB) tile_hist[(uint64_t)b * ntiles + tile] = lcnt[b];
+    for (uint64_t i0 = t0; i0 < s1; i0 += 8 * HB) {
+      uint64_t x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
+        x[j] = i >= s1 ? NO_PAIR : pairs[i];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
+        if (i >= s1) continue;
+        const uint32_t ptm = (uint32_t)(x[j] >> 32), ph = lds[(uint32_t)x[j] & (W - 1)];
+        uint64_t e = ~0ull;   // DEAD
+        // (ptm is a position < n_tree, INVALID or PT_OOR; anything else is a stale region
+        // of a run the host discards, kept in bounds)
+        if (ph != INVALID) {
+          if (ptm == PT_OOR) bad = true;                       // index.at(tail) throws
+          else if (ptm < n_tree) e = ptm < ph ? ((uint64_t)ph << 32) | ptm : ((uint64_t)ptm << 32) | ph;
+          else if (ptm == INVALID) atomicAdd(&pst[ph], 1u);
+        } else if (ptm < n_tree) {
+          atomicAdd(&pst[ptm], 1u);
+        }
+        edges[i] = e;
+        if (COUNT && e != ~0ull) atomicAdd(&lcnt[lk.key(e) >> WBITS], 1u);
+      }
+    }
+    if (COUNT) {
+      lds_barrier();
+      const uint64_t tile = t0 >> TLOG;
+      for (uint32_t b = threadIdx.x; b < lnb; b += HB)
+        if (lcnt[b]) atomicAdd(&tile_hist[(uint64_t)b * ntiles + tile], lcnt[b]);
+      lds_barrier();   // lcnt is cleared for the next tile
+    }
+    t0 = s1;
   }
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(&flags[0], 1ull);
 }
@@ -762,9 +735,8 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
                           bool *counted) {
   if (counted) *counted = false;
   const uint64_t nb = (pos_size + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
-  const uint64_t nbc = (nb + FINE_PER_COARSE - 1) / FINE_PER_COARSE;
   if (nrec == 0 || nb == 0 || nb > 8192 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return UINT64_MAX;
-  for (const void *f : {(const void *)k_relabel_scatter<16, CBITS>, (const void *)k_relabel_scatter<8, CBITS>,
+  for (const void *f : {(const void *)k_relabel_scatter<8>, (const void *)k_relabel_scatter<4>,
                         (const void *)k_relabel_gather<false>, (const void *)k_relabel_gather<true>})
     allow_full_lds(f);
   Ctx::HeadLayout &hl = c.head_layout;
@@ -790,49 +762,62 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   uint32_t *off = cached ? c.get_as<uint32_t>("head_offsets", ntiles * nb + 1) : recount();
   const uint64_t total = hl.bstart[nb];
   uint64_t *pairs = c.get_as<uint64_t>("rl_pairs", total ? total : 1);
-  uint32_t *offc = c.get_as<uint32_t>("rl_offc", ntiles * nbc + 1);
-  const size_t fixed = ((3 * nbc + HB / WAVE + 1) & ~1ull) * 4;
+  const size_t fixed = ((3 * nb + HB / WAVE + 1) & ~1ull) * 4;
   auto scatter = [&]() {
     HIP_CHECK(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c.stream));
-    hipLaunchKernelGGL(k_coarse_offsets, dim3(grid_for(ntiles * nbc + 1)), dim3(BLOCK), 0, c.stream, (const uint32_t *)off,
-                       (uint32_t)nb, ntiles, (uint32_t)nbc, offc);
-    LAUNCH_CHECK();
-    // 16K-record sub-tiles (8K when the bucket cursors take more LDS: ids above 2^27)
-    const int per = fixed + 16 * HB * 8 <= 160 * 1024 ? 16 : 8;
+    // 8K-record sub-tiles (4K / 16K measured 15.8 / 15.3 ms against 14.3 at RMAT-26);
+    // 4K when the bucket cursors take more LDS (vertex ids above 2^27)
+    const int per = fixed + 8 * HB * 8 <= 160 * 1024 ? 8 : 4;
     if (fixed + (size_t)per * HB * 8 > 160 * 1024) throw Error(SHEEP_ERR_ARG, "relabel: bucket layout exceeds LDS");
     const size_t lds = fixed + (size_t)per * HB * 8;
     const dim3 g((unsigned)ntiles), b(HB);
-    const uint32_t nbc32 = (uint32_t)nbc;
-    const uint32_t *o = offc;
-    if (per == 16)
-      hipLaunchKernelGGL((k_relabel_scatter<16, CBITS>), g, b, lds, c.stream, rec, nrec, pos, pos_size, nbc32, o, ntiles,
-                         pairs, flags);
+    const uint32_t nb32 = (uint32_t)nb;
+    const uint32_t *o = off;
+    if (per == 8)
+      hipLaunchKernelGGL(k_relabel_scatter<8>, g, b, lds, c.stream, rec, nrec, pos, pos_size, nb32, o, ntiles, pairs, flags);
     else
-      hipLaunchKernelGGL((k_relabel_scatter<8, CBITS>), g, b, lds, c.stream, rec, nrec, pos, pos_size, nbc32, o, ntiles,
-                         pairs, flags);
+      hipLaunchKernelGGL(k_relabel_scatter<4>, g, b, lds, c.stream, rec, nrec, pos, pos_size, nb32, o, ntiles, pairs, flags);
     LAUNCH_CHECK();
     HIP_CHECK(hipMemcpyAsync(c.h_scalars + 12, flags, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   };
-  // Pass B is launched right behind pass A, and ONE sync then checks pass A's flags: a
-  // stale layout (the same record buffer refilled) is recounted and both passes run again;
-  // the first run's writes stay in bounds (the gather checks every head against pos_size
-  // and every tail position against n) and its pst / error counts are cleared.
+  // Pass B is launched right behind pass A on the layout's chunk list (pinned host memory,
+  // built from the bucket starts), and ONE sync then checks pass A's flags: a stale layout
+  // (the same record buffer refilled) is recounted and both passes run again; the first
+  // run's writes stay in bounds (the gather checks every tail position against n) and its
+  // pst / error counts are cleared.
+  const uint64_t ntiles_e_max = (total + TKEYS - 1) >> TLOG;
   auto gather = [&]() -> bool {
     const uint64_t m = hl.bstart[nb];
-    if (!m) return false;
+    const uint64_t chunk = chunk_for(m);
+    uint64_t nch = 0;
+    for (uint32_t b = 0; b < nb; ++b) nch += (hl.bstart[b + 1] - hl.bstart[b] + chunk - 1) / chunk;
+    // the grouping's count pass fused in when its bucket counters fit beside the pos slice
     const uint64_t ntiles_e = (m + TKEYS - 1) >> TLOG;
-    // the grouping's count pass fused in (its bucket counters in LDS)
-    const bool count = lg && lg->nb && (size_t)lg->nb * 4 <= 160 * 1024 && ntiles_e * lg->nb + 1 < (1ull << 32) &&
-                       m < (1ull << 32);
+    const bool count = lg && m && lg->nb && ((size_t)W + lg->nb) * 4 <= 160 * 1024 &&
+                       ntiles_e * lg->nb + 1 < (1ull << 32) && m < (1ull << 32);
+    uint32_t *tile_hist = nullptr;
+    if (count) {
+      tile_hist = c.get_as<uint32_t>("hist_tiles", std::max(ntiles_e, ntiles_e_max) * lg->nb + 1);
+      HIP_CHECK(hipMemsetAsync(tile_hist, 0, ntiles_e * lg->nb * sizeof(uint32_t), c.stream));
+    }
+    if (!nch) return count;
+    Chunk *hch = (Chunk *)c.get_pinned("rl_chunks_host", nch * sizeof(Chunk));
+    uint64_t j = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+      const uint64_t beg = hl.bstart[b], end = hl.bstart[b + 1];
+      for (uint64_t x = beg; x < end; x += chunk) hch[j++] = {x, x + chunk < end ? x + chunk : end, b, 0};
+    }
+    Chunk *dch = c.get_as<Chunk>("rl_chunks", nch);
+    HIP_CHECK(hipMemcpyAsync(dch, hch, nch * sizeof(Chunk), hipMemcpyHostToDevice, c.stream));
     const EdgeLoPadded lk{edges, lg ? lg->d_pad : nullptr, lg ? lg->clo : 0, lg ? lg->mask : 0};
     if (count)
-      hipLaunchKernelGGL(k_relabel_gather<true>, dim3((unsigned)ntiles_e), dim3(HB), lg->nb * 4, c.stream,
-                         (const uint64_t *)pairs, m, pos, pos_size, pst, edges, err, lk, lg->nb,
-                         c.get_as<uint32_t>("hist_tiles", ntiles_e * lg->nb + 1), ntiles_e, n_tree);
+      hipLaunchKernelGGL(k_relabel_gather<true>, dim3((unsigned)nch), dim3(HB), (W + lg->nb) * 4, c.stream,
+                         (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err, lk, lg->nb,
+                         tile_hist, ntiles_e, n_tree);
     else
-      hipLaunchKernelGGL(k_relabel_gather<false>, dim3((unsigned)ntiles_e), dim3(HB), 0, c.stream,
-                         (const uint64_t *)pairs, m, pos, pos_size, pst, edges, err, lk, 0u, (uint32_t *)nullptr,
-                         (uint64_t)0, n_tree);
+      hipLaunchKernelGGL(k_relabel_gather<false>, dim3((unsigned)nch), dim3(HB), W * 4, c.stream,
+                         (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err, lk, 0u,
+                         (uint32_t *)nullptr, (uint64_t)0, n_tree);
     LAUNCH_CHECK();
     return count;
   };

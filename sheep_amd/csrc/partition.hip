@@ -336,55 +336,32 @@ __device__ __forceinline__ EvView load_table(const uint32_t *gpos, const uint64_
   return EvView{spos, spre, m};
 }
 
-// A batch of packing-event CANDIDATES in one launch.  Every workgroup scans 512-entry
-// chunks of the heavy set (index order = id order) after the last candidate examined,
-// keeps each chunk's hits (residual > max_component) in index order, and stops once the
-// first known hit lies more than EV_WIN chunks below its chunk; so every chunk up to EV_WIN
-// chunks past the final first hit has been scanned.  The last workgroup to finish takes
-// the hits of those chunks in order, up to EV_B, and stages each candidate for the host
-// in mapped host memory: {v, koff[v], #kids, tD(v) (INVALID for a root), its tour interval,
-// its residual at the search, where its kids went} and the kids in their current order
-// with their residuals and tour intervals (EV_INLINE kids per batch, the last workgroup's
-// share of work one event had before; a first candidate with more goes alone, its kids
-// through k_event_kids).  It raises hdr[7] =
-// seq (system scope), which the host polls.
-// Why candidates, not events: after the first candidate packs, a later one is the next
-// packing node iff its residual, less what the batch's earlier packings removed inside
-// its interval, still exceeds max_component (nodes between two candidates had residual
-// <= max_component and residuals only fall).  The host replays forwardPartition over the
-// batch with those corrections (two binary searches each), so ONE device round trip
-// serves a run of events instead of one per event.
-// 512-entry chunks: a scan reaches its hits in fewer dependent rounds per workgroup
-// (RMAT-26 / Chung-Lu events: 2048-entry chunks 2.2 / 4.6 ms, 512 2.0 / 3.9 ms, one event
-// per launch).
+// One packing event in one launch.  Every workgroup scans 2048-entry chunks of the heavy
+// set in index order for the lowest-index node after the last packing node whose
+// residual exceeds max_component, and stops once a hit below its chunk is known (an
+// event reads about the distance to the next packing node, not the whole heavy set).
+// The last workgroup to finish then knows the node and stages the event straight into
+// mapped host memory: hdr = {v, koff[v], #kids, R[v] lo, R[v] hi, tD(v) (INVALID for a
+// root), kids staged?}, the node's kids in their current order and their residuals (up
+// to EV_INLINE of them; larger kid lists go through k_event_kids).  It resets the
+// search state for the next event and raises hdr[7] = seq (system scope), which the
+// host polls instead of synchronising the stream.  The event table is read from mapped
+// host memory too (the host rewrites it between events), so an event is ONE launch.
+// 512-entry chunks: an event's scan reaches its hit in fewer dependent rounds per
+// workgroup (RMAT-26 / Chung-Lu events: 2048-entry chunks 2.2 / 4.6 ms, 512 2.0 / 3.9 ms)
 constexpr int EVI = 2, EV_CH = BLOCK * EVI;
-constexpr uint32_t EV_STAGE = 1u << 16;     // mapped staging area (kids)
-constexpr uint32_t EV_INLINE = 4096;        // kid lists staged by the event kernel itself
-constexpr uint32_t EV_WIN = 64;             // chunks scanned past the first hit
-constexpr uint32_t EV_B = 64;               // candidates per batch
-
-// one candidate as staged for the host
-struct EvCand {
-  uint32_t v, beg, cnt, vpos, ilo, ihi, kofs, staged;
-  uint64_t r;
-};
+constexpr uint32_t EV_STAGE = 1u << 16;   // mapped staging area (kids)
+constexpr uint32_t EV_INLINE = 4096;      // kid lists staged by the event kernel itself
 
 __device__ __forceinline__ void stage_kids(const EvView &ev, uint32_t beg, uint32_t lim, uint32_t j0, uint32_t stride,
                                            const uint32_t *kids, const uint64_t *S, const uint32_t *cparent,
-                                           const uint32_t *tD, const uint32_t *tU, uint32_t *kid_out, uint64_t *r_out,
-                                           uint32_t *ktd_out, uint32_t *ktu_out) {
+                                           const uint32_t *tD, const uint32_t *tU, uint32_t *kid_out, uint64_t *r_out) {
   for (uint32_t j = j0; j < lim; j += stride) {
     const uint32_t kid = kids[beg + j];
     uint64_t r = S[kid];
-    uint32_t a = INVALID, b = INVALID;
-    if (cparent[kid] != INVALID) {   // fringe kids never had a packing below
-      a = tD[kid];
-      b = tU[kid];
-      r -= ev.removed(a, b);
-    }
+    if (cparent[kid] != INVALID) r -= ev.removed(tD[kid], tU[kid]);   // fringe kids never had a packing below
     kid_out[j] = kid;
     r_out[j] = r;
-    if (ktd_out) { ktd_out[j] = a; ktu_out[j] = b; }
   }
 }
 
@@ -395,26 +372,22 @@ __global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hi
                                                  uint64_t *__restrict__ evprev, unsigned long long *__restrict__ found,
                                                  unsigned *__restrict__ done, const uint32_t *__restrict__ koff,
                                                  const uint32_t *__restrict__ kids, const uint64_t *__restrict__ S,
-                                                 const uint32_t *__restrict__ cparent, const uint32_t *__restrict__ tD,
-                                                 const uint32_t *__restrict__ tU, uint32_t *__restrict__ chunk_cnt,
-                                                 uint32_t *__restrict__ chunk_hits, uint32_t *__restrict__ hdr,
-                                                 EvCand *__restrict__ cand_out, uint32_t *__restrict__ kid_out,
-                                                 uint64_t *__restrict__ r_out, uint32_t *__restrict__ ktd_out,
-                                                 uint32_t *__restrict__ ktu_out, uint32_t seq, const EvArg arg) {
+                                                 const uint32_t *__restrict__ cparent, const uint32_t *__restrict__ ckoff,
+                                                 const uint32_t *__restrict__ tD, const uint32_t *__restrict__ tU,
+                                                 const uint32_t *__restrict__ rst, const uint32_t *__restrict__ ren,
+                                                 uint32_t *__restrict__ hdr, uint32_t *__restrict__ kid_out,
+                                                 uint64_t *__restrict__ r_out, uint32_t seq, const EvArg arg) {
   __shared__ uint32_t spos[EV_LDS];
   __shared__ uint64_t spre[EV_LDS + 1];
   __shared__ unsigned long long s_best[BLOCK / WAVE];
-  __shared__ uint32_t s_wc[BLOCK / WAVE];
   __shared__ unsigned long long s_word;   // one thread's atomic read, for the workgroup
-  __shared__ uint32_t s_cand[EV_B];
-  __shared__ uint32_t s_hoff[EV_WIN + 1];
-  __shared__ uint32_t s_nc;
   __shared__ bool last;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t t_start = wall_clock64();
   const EvView ev = epos ? load_table(epos, epre, m, spos, spre) : load_arg(arg, spos, spre);
+  uint64_t t_table = wall_clock64();
   // The search state (evprev, found, done) is only ever touched by atomic read-modify-writes,
   // which every XCD sees at one coherent point: a plain or atomic LOAD is served from the
-  // reading XCD's own L2 and can return a value an earlier search left there (a stale hit
+  // reading XCD's own L2 and can return a value an earlier event left there (a stale hit
   // below every chunk made one search end empty: seen with 512-entry chunks on C4).
   if (threadIdx.x == 0) s_word = atomicOr((unsigned long long *)evprev, 0ull);
   __syncthreads();
@@ -428,8 +401,7 @@ __global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hi
     if (threadIdx.x == 0) s_word = atomicOr(found, 0ull);
     __syncthreads();
     const unsigned long long f = s_word;
-    // past the window behind a known hit (uniform)
-    if (f != ~0ull && (uint64_t)(uint32_t)f + (uint64_t)EV_WIN * EV_CH < base) break;
+    if (f != ~0ull && (uint32_t)f < base) break;   // a hit below this chunk is known (uniform)
     unsigned long long best = ~0ull;
     // every candidate's four words loaded before any is decoded (a load behind the id
     // check of the same candidate serialised two latencies per candidate: 24 us a scan)
@@ -444,33 +416,19 @@ __global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hi
       cs[j] = in ? hst[h] : INVALID;
       ce[j] = in ? hen[h] : INVALID;
     }
-    uint32_t nhit = 0;
 #pragma unroll
     for (int j = 0; j < EVI; ++j) {
       const uint64_t h = base + (uint64_t)j * BLOCK + threadIdx.x;
       const uint32_t a = ca[j];
-      bool hit = false;
-      if (a != INVALID && (vlast == INVALID || a > vlast)) {
-        const uint64_t r = cr[j] - ev.removed(cs[j], ce[j]);
-        hit = r > maxc;
-        if (hit) {
-          const unsigned long long key = ((unsigned long long)a << 32) | h;
-          best = key < best ? key : best;
-        }
+      if (a == INVALID || (vlast != INVALID && a <= vlast)) continue;
+      const uint64_t r = cr[j] - ev.removed(cs[j], ce[j]);
+      if (r > maxc) {
+        const unsigned long long key = ((unsigned long long)a << 32) | h;
+        best = key < best ? key : best;
       }
-      // the chunk's hits in index order: row j of the chunk, then row j + 1
-      const uint64_t bm = __ballot(hit);
-      if (lane == 0) s_wc[wave] = (uint32_t)__popcll(bm);
-      __syncthreads();
-      uint32_t off = nhit;
-      for (int w = 0; w < wave; ++w) off += s_wc[w];
-      if (hit) chunk_hits[ch * EV_CH + off + (uint32_t)__popcll(bm & lanemask_lt())] = (uint32_t)h;
-      for (int w = 0; w < BLOCK / WAVE; ++w) nhit += s_wc[w];
-      __syncthreads();
     }
-    if (threadIdx.x == 0) chunk_cnt[ch] = nhit;
     best = wave_min(best);
-    if (lane == 0) s_best[wave] = best;
+    if ((threadIdx.x & 63) == 0) s_best[threadIdx.x >> 6] = best;
     __syncthreads();
     if (threadIdx.x == 0) {
       unsigned long long b = s_best[0];
@@ -479,73 +437,43 @@ __global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hi
     }
     __syncthreads();
   }
-  // the last workgroup to finish sees every other workgroup's hits and atomicMin
+  // the last workgroup to finish sees every other workgroup's atomicMin
   __threadfence();
   __syncthreads();
   if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  __threadfence();   // acquire: the other workgroups' chunk lists
+  const uint64_t t_search = wall_clock64();
   if (threadIdx.x == 0) s_word = atomicOr(found, 0ull);
   __syncthreads();
   const unsigned long long e = s_word;
-  uint32_t nc = 0;
-  if (e != ~0ull) {
-    // the hits of chunks cf .. cf + EV_WIN in order (every one of them was scanned)
-    const uint64_t fh = (uint32_t)e, cf = (fh - start) / EV_CH;
-    const uint64_t nch = (nh - start + EV_CH - 1) / EV_CH;
-    const uint64_t cl = cf + EV_WIN + 1 < nch ? cf + EV_WIN + 1 : nch;
-    // (plain loads: every workgroup released its chunk lists before its done-counter
-    // increment, and this one acquired them after seeing the last count)
-    const uint64_t mc = cf + threadIdx.x;   // this thread's chunk
-    const uint32_t mcnt = threadIdx.x <= EV_WIN && mc < cl ? chunk_cnt[mc] : 0u;
-    if (threadIdx.x <= EV_WIN) s_hoff[threadIdx.x] = mcnt;
-    __syncthreads();
+  const uint32_t v = e == ~0ull ? INVALID : (uint32_t)(e >> 32);
+  if (v != INVALID) {
+    const uint32_t beg = koff[v], cnt = koff[v + 1] - beg;
+    if (cnt <= EV_INLINE) stage_kids(ev, beg, cnt, threadIdx.x, BLOCK, kids, S, cparent, tD, tU, kid_out, r_out);
     if (threadIdx.x == 0) {
-      uint32_t run = 0;
-      for (uint32_t w = 0; w <= EV_WIN; ++w) { const uint32_t x = s_hoff[w]; s_hoff[w] = run; run += x; }
-      s_nc = run < EV_B ? run : EV_B;
+      atomicExch((unsigned long long *)evprev, e);
+      uint32_t lo, hi;
+      node_interval(v, cparent, ckoff, tD, tU, rst, ren, lo, hi);
+      const uint64_t r = S[v] - ev.removed(lo, hi);
+      hdr[0] = v;
+      hdr[1] = beg;
+      hdr[2] = cnt;
+      hdr[3] = (uint32_t)r;
+      hdr[4] = (uint32_t)(r >> 32);
+      hdr[5] = cparent[v] == INVALID ? INVALID : tD[v];
+      hdr[6] = cnt <= EV_INLINE;
     }
-    __syncthreads();
-    if (mcnt) {
-      const uint32_t off = s_hoff[threadIdx.x];
-      for (uint32_t i = 0; i < mcnt && off + i < EV_B; ++i) s_cand[off + i] = chunk_hits[mc * EV_CH + i];
-    }
-    __syncthreads();
-    nc = s_nc;
-    uint32_t kofs = 0, taken = 0;
-    for (uint32_t i = 0; i < nc; ++i) {
-      const uint32_t h = s_cand[i], v = hids[h];
-      const uint32_t beg = koff[v], cnt = koff[v + 1] - beg;
-      if (i > 0 && kofs + cnt > EV_INLINE) break;   // the next batch's first candidate
-      const bool inl = cnt <= EV_INLINE;             // (only a first candidate can exceed it)
-      if (inl) stage_kids(ev, beg, cnt, threadIdx.x, BLOCK, kids, S, cparent, tD, tU, kid_out + kofs, r_out + kofs,
-                          ktd_out + kofs, ktu_out + kofs);
-      if (threadIdx.x == 0) {
-        EvCand cd;
-        cd.v = v;
-        cd.beg = beg;
-        cd.cnt = cnt;
-        cd.vpos = cparent[v] == INVALID ? INVALID : tD[v];
-        cd.ilo = hst[h];
-        cd.ihi = hen[h];
-        cd.kofs = kofs;
-        cd.staged = inl;
-        cd.r = SH[h] - ev.removed(cd.ilo, cd.ihi);
-        cand_out[i] = cd;
-      }
-      taken = i + 1;
-      if (!inl) break;   // a long kid list goes alone (k_event_kids)
-      kofs += cnt;
-    }
-    nc = taken;
-    if (threadIdx.x == 0)   // the last candidate examined: the next search starts after it
-      atomicExch((unsigned long long *)evprev, ((unsigned long long)hids[s_cand[nc - 1]] << 32) | s_cand[nc - 1]);
+  } else if (threadIdx.x == 0) {
+    hdr[0] = INVALID;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    hdr[0] = nc;
-    atomicExch(found, ~0ull);   // the next search starts clean
+    const uint64_t t_stage = wall_clock64();
+    hdr[8] = (uint32_t)(t_table - t_start);
+    hdr[9] = (uint32_t)(t_search - t_table);
+    hdr[10] = (uint32_t)(t_stage - t_search);
+    atomicExch(found, ~0ull);   // the next event's search starts clean
     atomicExch(done, 0u);
     __threadfence_system();
     __hip_atomic_store(&hdr[7], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -575,7 +503,7 @@ __global__ __launch_bounds__(BLOCK) void k_event_kids(uint64_t *__restrict__ evp
   const uint32_t beg = koff[v] + beg_j, cnt = koff[v + 1] - koff[v];
   const uint32_t lim = cnt - beg_j < cap ? cnt - beg_j : cap;
   stage_kids(ev, beg, lim, blockIdx.x * BLOCK + threadIdx.x, gridDim.x * BLOCK, kids, S, cparent, tD, tU, kid_out,
-             r_out, nullptr, nullptr);
+             r_out);
   __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
@@ -855,27 +783,18 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   HIP_CHECK(hipMemsetAsync(done_ctr, 0, sizeof(uint64_t), c.stream));
   HIP_CHECK(hipMemsetAsync(found, 0xFF, sizeof(uint64_t), c.stream));   // k_event resets it after each event
   static const bool dbg = getenv("SHEEP_DEBUG_PART") != nullptr;
-  double dbg_wait = 0, dbg_host = 0;
-  uint32_t batches = 0;
-  // mapped staging area: header, the batch's candidates, their kids (ids, residuals and
-  // tour intervals)
-  const size_t o_cand = 64, o_kids = o_cand + (size_t)EV_B * sizeof(EvCand), o_r = o_kids + (size_t)EV_STAGE * 4,
-               o_ktd = o_r + (size_t)EV_STAGE * 8, o_ktu = o_ktd + (size_t)EV_INLINE * 4;
-  uint8_t *stage = (uint8_t *)c.get_pinned("pt_event", o_ktu + (size_t)EV_INLINE * 4);
+  double dbg_tab = 0, dbg_search = 0, dbg_stage = 0, dbg_wait = 0, dbg_host = 0;
+  uint8_t *stage = (uint8_t *)c.get_pinned("pt_event", 64 + (size_t)EV_STAGE * 12);
   volatile uint32_t *hdr = (volatile uint32_t *)stage;
-  const EvCand *st_cand = (const EvCand *)(stage + o_cand);
-  const uint32_t *st_kids = (const uint32_t *)(stage + o_kids), *st_ktd = (const uint32_t *)(stage + o_ktd),
-                 *st_ktu = (const uint32_t *)(stage + o_ktu);
-  const uint64_t *st_r = (const uint64_t *)(stage + o_r);
-  uint8_t *d_stage;
-  HIP_CHECK(hipHostGetDevicePointer((void **)&d_stage, stage, 0));
-  uint32_t *d_hdr = (uint32_t *)d_stage, *d_kids = (uint32_t *)(d_stage + o_kids);
-  uint64_t *d_r = (uint64_t *)(d_stage + o_r);
-  // per-chunk hit lists of a search (chunks past the last candidate: at most nh / EV_CH + 1)
-  uint32_t *chunk_cnt = c.get_as<uint32_t>("pt_chcnt", nh / EV_CH + 2);
-  uint32_t *chunk_hits = c.get_as<uint32_t>("pt_chhits", (nh / EV_CH + 2) * (uint64_t)EV_CH);
+  uint32_t *st_kids = (uint32_t *)(stage + 64);
+  uint64_t *st_r = (uint64_t *)(stage + 64 + (size_t)EV_STAGE * 4);
+  uint32_t *d_hdr, *d_kids;
+  uint64_t *d_r;
+  HIP_CHECK(hipHostGetDevicePointer((void **)&d_hdr, stage, 0));
+  HIP_CHECK(hipHostGetDevicePointer((void **)&d_kids, st_kids, 0));
+  HIP_CHECK(hipHostGetDevicePointer((void **)&d_r, st_r, 0));
   // the event table (sorted tD of the non-root packings, prefix sums of their deltas),
-  // written by the host into mapped memory between batches; the kernels read it there
+  // written by the host into mapped memory between events; the kernels read it there
   // (into LDS) — a device copy only when it outgrows the LDS copy, and once at the end
   std::vector<std::pair<uint32_t, uint64_t>> evs;
   uint32_t *ev_pos = c.get_as<uint32_t>("pt_evpos", nh + 1);
@@ -914,17 +833,6 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
       t_pre = (const uint64_t *)(d_ev_stage + pre_off);
     }
   };
-  // the current batch's non-root packings (tD, delta), sorted by tD: what they removed
-  // inside a tour interval is what the search's residuals do not know yet
-  std::vector<std::pair<uint32_t, uint64_t>> bev;
-  auto batch_removed = [&](uint32_t lo, uint32_t hi) -> uint64_t {
-    if (lo == INVALID || bev.empty()) return 0;
-    uint64_t r = 0;
-    for (auto it = std::lower_bound(bev.begin(), bev.end(), std::make_pair(lo, (uint64_t)0));
-         it != bev.end() && it->first <= hi; ++it)
-      r += it->second;
-    return r;
-  };
   std::vector<std::pair<uint32_t, uint64_t>> root_own;   // a root's own packing delta
   uint32_t seq_no = 0;
   // waits for the event kernels' completion flag (hdr[7]): a poll of mapped memory wakes
@@ -940,9 +848,9 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   std::vector<uint32_t> seg, order, sorted, upl_pos, upl_ids;
   std::vector<uint64_t> segR, scb;
   std::vector<char> done;
-  // 64 workgroups: a scan usually ends within its first round of chunks, and every extra
-  // workgroup adds to the last-workgroup hand-off (RMAT-26 k=64, us per event with one
-  // event per launch: 16 WGs 26.5, 32 19.4, 64 16.5, 128 18.1, 256 27.3, 512 48)
+  // 64 workgroups: an event's scan usually ends within its first round of chunks, and every
+  // extra workgroup adds to the last-workgroup hand-off (RMAT-26 k=64, us per event:
+  // 16 WGs 26.5, 32 19.4, 64 16.5, 128 18.1, 256 27.3, 512 48)
   const unsigned gev = nh ? (unsigned)std::min<uint64_t>((nh + EV_CH - 1) / EV_CH, 64) : 1;
   auto stage_kids_of = [&](uint32_t beg_j, uint32_t cap, uint32_t *o_kids, uint64_t *o_r) {
     ++seq_no;
@@ -960,99 +868,86 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
       ++seq_no;
       const bool by_arg = m_ev <= EV_ARG;
       hipLaunchKernelGGL(k_event, dim3(gev), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh, (const uint64_t *)SH,
-                         (const uint32_t *)hst, (const uint32_t *)hen, by_arg ? nullptr : t_pos,
-                         by_arg ? nullptr : t_pre, m_ev, max_component, evprev, found, done_ctr,
-                         (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
-                         (const uint32_t *)core.parent, (const uint32_t *)t.tD, (const uint32_t *)t.tU, chunk_cnt,
-                         chunk_hits, d_hdr, (EvCand *)(d_stage + o_cand), d_kids, d_r, (uint32_t *)(d_stage + o_ktd),
-                         (uint32_t *)(d_stage + o_ktu), seq_no, evarg);
+                         (const uint32_t *)hst, (const uint32_t *)hen, by_arg ? nullptr : t_pos, by_arg ? nullptr : t_pre, m_ev, max_component, evprev, found,
+                         done_ctr, (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
+                         (const uint32_t *)core.parent, (const uint32_t *)core.koff, (const uint32_t *)t.tD,
+                         (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren, d_hdr, d_kids, d_r, seq_no,
+                         evarg);
       LAUNCH_CHECK();
       const auto h0 = std::chrono::steady_clock::now();
       wait_stage(seq_no);
       const auto h1 = std::chrono::steady_clock::now();
-      if (dbg) dbg_wait += std::chrono::duration<double, std::micro>(h1 - h0).count();
-      const uint32_t nc = hdr[0];
-      if (nc == 0) break;
-      ++batches;
-      bev.clear();
-      for (uint32_t ci = 0; ci < nc; ++ci) {
-        const EvCand cd = st_cand[ci];
-        // the candidate's residual now: the search's, less what this batch packed inside it
-        uint64_t cb = cd.r - batch_removed(cd.ilo, cd.ihi);
-        if (cb <= max_component) continue;   // not a packing node any more
-        info->packing_nodes++;
-        const uint32_t v = cd.v, beg = cd.beg, cnt = cd.cnt, vpos = cd.vpos;
-        if (cd.staged) {
-          seg.assign(st_kids + cd.kofs, st_kids + cd.kofs + cnt);
-          segR.resize(cnt);
-          for (uint32_t j = 0; j < cnt; ++j) segR[j] = st_r[cd.kofs + j] - batch_removed(st_ktd[cd.kofs + j], st_ktu[cd.kofs + j]);
-        } else {   // a first candidate with more kids than the event kernel stages (bev is empty)
-          stage_kids_of(0, EV_STAGE, d_kids, d_r);
-          seg.assign(st_kids, st_kids + std::min(cnt, EV_STAGE));
-          segR.assign(st_r, st_r + std::min(cnt, EV_STAGE));
-          if (cnt > EV_STAGE) {   // more kids than the staging area: fetch the rest
-            seg.resize(cnt); segR.resize(cnt);
-            uint32_t *kk = c.get_as<uint32_t>("pt_kK", cnt);
-            uint64_t *kR = c.get_as<uint64_t>("pt_kR", cnt);
-            stage_kids_of(EV_STAGE, cnt - EV_STAGE, kk, kR);
-            d2h(c, seg.data() + EV_STAGE, (const uint32_t *)kk, cnt - EV_STAGE);
-            d2h(c, segR.data() + EV_STAGE, (const uint64_t *)kR, cnt - EV_STAGE);
-            c.sync();
-          }
-        }
-        const uint64_t cb0 = cb;
-        // std::sort on the current kid order with the reference comparator (:104-106);
-        // sorting positions with a comparator on their keys is the same sort.
-        order.resize(cnt);
-        for (uint32_t j = 0; j < cnt; ++j) order[j] = j;
-        std::sort(order.begin(), order.end(), [&segR](uint32_t a, uint32_t b) { return segR[a] > segR[b]; });
-        sorted.resize(cnt); scb.resize(cnt);
-        for (uint32_t j = 0; j < cnt; ++j) {
-          sorted[j] = seg[order[j]];
-          scb[j] = segR[order[j]];
-          if (j != order[j]) { upl_pos.push_back(beg + j); upl_ids.push_back(sorted[j]); }
-        }
-        done.assign(cnt, 0);
-        do {
-          for (uint32_t j = 0; cb > max_component && j < cnt; ++j) {
-            if (scb[j] > max_component) throw Error(SHEEP_ERR_PACK, "forwardPartition: kid exceeds max_component");
-            if (done[j]) continue;
-            for (size_t p = 0; p != part_size.size(); ++p) {
-              if (part_size[p] + scb[j] <= max_component) {
-                cb -= scb[j];
-                part_size[p] += scb[j];
-                done[j] = 1;
-                asg_ids.push_back(sorted[j]);
-                asg_part.push_back((int16_t)p);
-                break;
-              }
+      if (dbg) {
+        dbg_tab += hdr[8] / 100.0;   // wall_clock64: 100 MHz
+        dbg_search += hdr[9] / 100.0;
+        dbg_stage += hdr[10] / 100.0;
+        dbg_wait += std::chrono::duration<double, std::micro>(h1 - h0).count();
+      }
+      const uint32_t v = hdr[0];
+      if (v == INVALID) break;
+      info->packing_nodes++;
+      const uint32_t beg = hdr[1], cnt = hdr[2], vpos = hdr[5];
+      uint64_t cb = (uint64_t)hdr[3] | ((uint64_t)hdr[4] << 32);
+      if (!hdr[6]) stage_kids_of(0, EV_STAGE, d_kids, d_r);   // more kids than the event kernel stages
+      seg.assign(st_kids, st_kids + std::min(cnt, EV_STAGE));
+      segR.assign(st_r, st_r + std::min(cnt, EV_STAGE));
+      if (cnt > EV_STAGE) {   // a node with more kids than the staging area: fetch the rest
+        seg.resize(cnt); segR.resize(cnt);
+        uint32_t *kk = c.get_as<uint32_t>("pt_kK", cnt);
+        uint64_t *kR = c.get_as<uint64_t>("pt_kR", cnt);
+        stage_kids_of(EV_STAGE, cnt - EV_STAGE, kk, kR);
+        d2h(c, seg.data() + EV_STAGE, (const uint32_t *)kk, cnt - EV_STAGE);
+        d2h(c, segR.data() + EV_STAGE, (const uint64_t *)kR, cnt - EV_STAGE);
+        c.sync();
+      }
+      const uint64_t cb0 = cb;
+      // std::sort on the current kid order with the reference comparator (:104-106);
+      // sorting positions with a comparator on their keys is the same sort.
+      order.resize(cnt);
+      for (uint32_t j = 0; j < cnt; ++j) order[j] = j;
+      std::sort(order.begin(), order.end(), [&segR](uint32_t a, uint32_t b) { return segR[a] > segR[b]; });
+      sorted.resize(cnt); scb.resize(cnt);
+      for (uint32_t j = 0; j < cnt; ++j) {
+        sorted[j] = seg[order[j]];
+        scb[j] = segR[order[j]];
+        if (j != order[j]) { upl_pos.push_back(beg + j); upl_ids.push_back(sorted[j]); }
+      }
+      done.assign(cnt, 0);
+      do {
+        for (uint32_t j = 0; cb > max_component && j < cnt; ++j) {
+          if (scb[j] > max_component) throw Error(SHEEP_ERR_PACK, "forwardPartition: kid exceeds max_component");
+          if (done[j]) continue;
+          for (size_t p = 0; p != part_size.size(); ++p) {
+            if (part_size[p] + scb[j] <= max_component) {
+              cb -= scb[j];
+              part_size[p] += scb[j];
+              done[j] = 1;
+              asg_ids.push_back(sorted[j]);
+              asg_part.push_back((int16_t)p);
+              break;
             }
           }
-          if (cb > max_component) {
-            bool any = false;
-            for (uint32_t j = 0; j < cnt; ++j) any |= !done[j];
-            if (!any || part_size.size() >= 32767)
-              throw Error(SHEEP_ERR_PACK, "forwardPartition: node weight exceeds max_component (reference loops forever)");
-            part_size.push_back(0);
-          }
-        } while (cb > max_component);
-        // the event into the table for the next search (sorted by tD; a root keeps its own)
-        // and into the batch's own list for the candidates after it
-        if (vpos != INVALID) {
-          const std::pair<uint32_t, uint64_t> e{vpos, cb0 - cb};
-          evs.insert(std::upper_bound(evs.begin(), evs.end(), std::make_pair(vpos, (uint64_t)~0ull)), e);
-          bev.insert(std::upper_bound(bev.begin(), bev.end(), std::make_pair(vpos, (uint64_t)~0ull)), e);
-        } else {
-          root_own.push_back({v, cb0 - cb});
         }
-      }
+        if (cb > max_component) {
+          bool any = false;
+          for (uint32_t j = 0; j < cnt; ++j) any |= !done[j];
+          if (!any || part_size.size() >= 32767)
+            throw Error(SHEEP_ERR_PACK, "forwardPartition: node weight exceeds max_component (reference loops forever)");
+          part_size.push_back(0);
+        }
+      } while (cb > max_component);
+      // the event into the table for the next scan (sorted by tD; a root keeps its own)
+      if (vpos != INVALID)
+        evs.insert(std::upper_bound(evs.begin(), evs.end(), std::make_pair(vpos, (uint64_t)~0ull)), {vpos, cb0 - cb});
+      else
+        root_own.push_back({v, cb0 - cb});
       write_table(false);   // (no kernel reads the table now: the last one has finished)
       if (dbg) dbg_host += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h1).count();
     }
   }
   if (dbg)
-    fprintf(stderr, "partition events %u in %u batches (us total): host wait %.1f host pack %.1f\n",
-            (unsigned)info->packing_nodes, batches, dbg_wait, dbg_host);
+    fprintf(stderr, "partition events %u (us total): table %.1f search %.1f stage %.1f | host wait %.1f host pack %.1f\n",
+            (unsigned)info->packing_nodes, dbg_tab, dbg_search, dbg_stage, dbg_wait, dbg_host);
   write_table(true);   // the device copy k_roots_r reads
   if (!upl_pos.empty()) {   // persist the sorted kid orders (forwardPartition mutates kids, :104-106)
     const uint64_t mu = upl_pos.size();
