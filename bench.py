@@ -43,7 +43,7 @@ REGION_KERNELS = {"degree": ["k_degree_fused"], "relabel": ["k_relabel_scatter",
                   "etree_split": ["k_split_count", "k_split_write"], "etree_union": ["k_hook_round", "k_hook_finish", "k_light_top"],
                   "etree_cross": ["k_cross_find"], "etree_apply": ["k_cross_apply", "k_level_clean"],
                   "evaluate": ["k_pp", "k_eval_records", "k_eval_nodes"]}
-PMC_FILE = os.path.join(ROOT, "profiles", "r2", "pmc_traffic_rmat{scale}_k{k}.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r3", "pmc_traffic_rmat{scale}_k{k}.json")
 
 
 def parse():
