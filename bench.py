@@ -67,9 +67,10 @@ def parse():
     ap.add_argument("--eval-reps", type=int, default=3, help="timed evaluator runs (0: skip)")
     ap.add_argument("--cpu-scale", type=int, default=None,
                     help="RMAT scale of the CPU-baseline sample (default: the bench's own RMAT scale up to 26, else 22)")
-    ap.add_argument("--cpu-ranks", type=int, nargs="+", default=[16, 32, 64],
+    ap.add_argument("--cpu-ranks", type=int, nargs="+", default=[8, 16],
                     help="MPI rank counts of the reference CPU baseline (capped by the host cores this process may "
-                         "use, os.sched_getaffinity); the best is reported")
+                         "use, os.sched_getaffinity); the best is reported.  More ranks only add merge hops on "
+                         "rank 0: at RMAT-26, P = 16 / 32 / 64 ran 28 / 71 / 172 s (profiles/r3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on cuda:0: rehearse N ranks on a 1-GPU box (the world's host link over TCP "

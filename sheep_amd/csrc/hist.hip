@@ -158,15 +158,16 @@ __global__ __launch_bounds__(HB) void k_hist_scatter(Src src, uint64_t n, uint32
   lds_barrier();
   const uint32_t tile = xcd_tile();
   const uint64_t base = (uint64_t)tile << TLOG;
-  uint32_t k[KPT];
+  uint32_t k[KPT], rk[KPT];
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
     const uint64_t i = base + (uint64_t)j * HB + threadIdx.x;
     k[j] = i < n ? src(i) : NO_KEY;
   }
+  // the counting atomic's old value is the key's rank in its bucket: placing it then needs
+  // a read of the bucket's start, not a second atomic
 #pragma unroll
-  for (int j = 0; j < KPT; ++j)
-    if (k[j] != NO_KEY) atomicAdd(&cur[k[j] >> WBITS], 1u);
+  for (int j = 0; j < KPT; ++j) rk[j] = k[j] != NO_KEY ? atomicAdd(&cur[k[j] >> WBITS], 1u) : 0u;
   lds_barrier();
   const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
   for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] = offsets[(uint64_t)b * ntiles + tile] - cur[b];
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(HB) void k_hist_scatter(Src src, uint64_t n, uint32
   for (int j = 0; j < KPT; ++j)
     if (k[j] != NO_KEY) {
       const uint32_t b = k[j] >> WBITS;
-      stage[atomicAdd(&cur[b], 1u)] = (b << 16) | (k[j] & (W - 1));
+      stage[cur[b] + rk[j]] = (b << 16) | (k[j] & (W - 1));
     }
   lds_barrier();
   for (uint32_t j = threadIdx.x; j < total; j += HB) {
@@ -202,29 +203,28 @@ __global__ __launch_bounds__(HB) void k_hist_scatter_staged(Src src, uint64_t n,
   for (uint32_t s0 = 0; s0 < TKEYS; s0 += SUB) {
     for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
     lds_barrier();
-    uint32_t k[PER];
+    uint32_t k[PER], rk[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const uint64_t i = base + s0 + (uint64_t)j * HB + threadIdx.x;
       k[j] = i < n ? src(i) : NO_KEY;
     }
 #pragma unroll
-    for (int j = 0; j < PER; ++j)
-      if (k[j] != NO_KEY) atomicAdd(&cur[k[j] >> WBITS], 1u);
+    for (int j = 0; j < PER; ++j) rk[j] = k[j] != NO_KEY ? atomicAdd(&cur[k[j] >> WBITS], 1u) : 0u;   // rank in bucket
     lds_barrier();
     const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
     for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] -= cur[b];
     lds_barrier();
 #pragma unroll
     for (int j = 0; j < PER; ++j)
-      if (k[j] != NO_KEY) stage[atomicAdd(&cur[k[j] >> WBITS], 1u)] = k[j];
+      if (k[j] != NO_KEY) stage[cur[k[j] >> WBITS] + rk[j]] = k[j];
     lds_barrier();
     for (uint32_t j = threadIdx.x; j < total; j += HB) {
       const uint32_t key = stage[j];
       out[gb[key >> WBITS] + j] = (uint16_t)(key & (W - 1));
     }
     lds_barrier();
-    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += cur[b];
+    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += b + 1 < nb ? cur[b + 1] : total;   // past the run
     lds_barrier();
   }
 }
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(HB) void k_lo_scatter_staged(EdgeLoPadded src, uint
     for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
     lds_barrier();
     uint64_t e[PER];
-    uint32_t k[PER];
+    uint32_t k[PER], rk[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const uint64_t i = base + s0 + (uint64_t)j * HB + threadIdx.x;
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(HB) void k_lo_scatter_staged(EdgeLoPadded src, uint
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       k[j] = src.key(e[j]);
-      if (k[j] != NO_KEY) atomicAdd(&cur[k[j] >> WBITS], 1u);
+      rk[j] = k[j] != NO_KEY ? atomicAdd(&cur[k[j] >> WBITS], 1u) : 0u;   // rank in bucket
     }
     lds_barrier();
     const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(HB) void k_lo_scatter_staged(EdgeLoPadded src, uint
     lds_barrier();
 #pragma unroll
     for (int j = 0; j < PER; ++j)
-      if (k[j] != NO_KEY) stage[atomicAdd(&cur[k[j] >> WBITS], 1u)] = e[j];
+      if (k[j] != NO_KEY) stage[cur[k[j] >> WBITS] + rk[j]] = e[j];
     lds_barrier();
     for (uint32_t j = threadIdx.x; j < total; j += HB) {
       const uint64_t v = stage[j];
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(HB) void k_lo_scatter_staged(EdgeLoPadded src, uint
       out[dst] = (uint16_t)(key & (W - 1));
     }
     lds_barrier();
-    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += cur[b];
+    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += b + 1 < nb ? cur[b + 1] : total;   // past the run
     lds_barrier();
   }
 }
@@ -576,7 +576,7 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
     for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
     lds_barrier();
     uint64_t x[PER];
-    uint32_t pt[PER], hd[PER];
+    uint32_t pt[PER], hd[PER], rk[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {   // all record loads, then all pos[tail] loads in flight
       const uint64_t i = base + s0 + (uint64_t)j * HB + threadIdx.x;
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
         continue;
       }
       x[j] = ((uint64_t)ptm << 32) | h;
-      atomicAdd(&cur[h >> WBITS], 1u);
+      rk[j] = atomicAdd(&cur[h >> WBITS], 1u);   // the pair's rank in its bucket
     }
     lds_barrier();
     const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
@@ -606,7 +606,7 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
     lds_barrier();
 #pragma unroll
     for (int j = 0; j < PER; ++j)
-      if (x[j] != NO_PAIR) stage[atomicAdd(&cur[(uint32_t)x[j] >> WBITS], 1u)] = x[j];
+      if (x[j] != NO_PAIR) stage[cur[(uint32_t)x[j] >> WBITS] + rk[j]] = x[j];
     lds_barrier();
     for (uint32_t j = threadIdx.x; j < total; j += HB) {
       const uint64_t v = stage[j];
@@ -615,7 +615,7 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
       else lost = true;
     }
     lds_barrier();
-    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += cur[b];   // past this sub-tile's run
+    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += b + 1 < nb ? cur[b + 1] : total;   // past this sub-tile's run
     lds_barrier();
   }
   for (uint32_t b = threadIdx.x; b < nb; b += HB)
