@@ -49,3 +49,12 @@ clean:
 	rm -rf build sheep_amd/lib sheep_amd/bin oracle/lib
 
 .PHONY: all hip cli oracle ref clean
+
+# A kernel variant for A/B runs: make variant V=name DEFS="-DFOO=1" -> sheep_amd/lib/variants/libsheep_hip_$(V).so
+# (bench.py / tests load it with SHEEP_HIP_LIB=...)
+variant:
+	@mkdir -p build/var_$(V) sheep_amd/lib/variants
+	for f in $(HIPSRC); do $(HIPCC) $(HIPFLAGS) $(DEFS) -c $$f -o build/var_$(V)/$$(basename $$f .hip).o & done; wait
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o sheep_amd/lib/variants/libsheep_hip_$(V).so build/var_$(V)/*.o \
+	    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+.PHONY: variant

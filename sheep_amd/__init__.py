@@ -31,7 +31,9 @@ from dataclasses import dataclass, field
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libsheep_hip.so")
+# SHEEP_HIP_LIB: another build of the same library (A/B measurements of kernel variants,
+# e.g. sheep_amd/lib/variants/*.so); the default is the in-tree build
+LIB_PATH = os.environ.get("SHEEP_HIP_LIB") or os.path.join(_HERE, "lib", "libsheep_hip.so")
 
 INVALID_ID = 0xFFFFFFFF
 INVALID_PART = -1

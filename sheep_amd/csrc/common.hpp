@@ -124,9 +124,12 @@ struct Ctx {
   // algorithmic bytes learned only after the launches (device-side counts)
   void add_bytes(const char *name, uint64_t bytes) { if (timing) timers[name].bytes += bytes; }
 
+  // Timing events only (TimedRegion): without the system-scope fence a record is a bare
+  // timestamp — a default event's record writes back and invalidates the caches, which
+  // showed as a ~10 us idle gap at every region boundary and cold caches after it.
   hipEvent_t ev() {
     if (!event_pool.empty()) { hipEvent_t e = event_pool.back(); event_pool.pop_back(); return e; }
-    hipEvent_t e; HIP_CHECK(hipEventCreate(&e)); return e;
+    hipEvent_t e; HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence)); return e;
   }
   void collect_timers() {
     for (auto &kv : timers) {
