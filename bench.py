@@ -328,8 +328,9 @@ def main():
 def verify_tree(a, seed, ctx, shard, subs, s, tree, stacked, world):
     """After the timed steps, rank 0 checks the reduced tree.  N ranks: against the
     whole graph's tree built on rank 0 alone.  One GPU with --shards: against the whole
-    graph's tree when it holds fewer than 2^32 records, and always against the binomial
-    pairwise merges (mpi_merge's schedule, jnode.cpp:203-250) of the same shard trees."""
+    graph's tree when its workspace fits the device (about 72 B per record: C5's 4.24 G
+    records do not), and always against the binomial pairwise merges (mpi_merge's
+    schedule, jnode.cpp:203-250) of the same shard trees."""
     import torch
     import sheep_amd
     if world > 1:
@@ -341,7 +342,9 @@ def verify_tree(a, seed, ctx, shard, subs, s, tree, stacked, world):
         torch.cuda.empty_cache()
         return ok
     ok = True
-    if shard.shape[0] < (1 << 32):
+    ctx.trim()
+    torch.cuda.empty_cache()
+    if shard.shape[0] < (1 << 32) and shard.shape[0] * 72 < torch.cuda.mem_get_info()[0]:
         ok = bool(torch.equal(sheep_amd.build_tree(shard, s, ctx=ctx), tree))
     cur = [stacked[i] for i in range(len(subs))]
     d = 1
