@@ -415,6 +415,81 @@ __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict
   }
 }
 
+// k_cross_find with a workgroup-private window of mt in LDS.  The first levels' cross
+// edges come from distinct, mostly singleton, low-degree left endpoints: every atomicMin
+// hits its own line, and 64 lanes to 64 lines run ~17x slower than one contiguous
+// wave-instruction (MI355X_MICROARCH.md, atomics).  The level's list keeps each edge group
+// in lo-bucket order, so a workgroup's chunk of XW_CH edges mostly has its roots inside a
+// 2^XW_BITS-position window starting at the chunk's smallest lo: their minima go to LDS
+// and leave in one coalesced pass; roots outside the window take the global path.
+// Used for the first XW_LEVELS levels only (RMAT-26, per level: 1.30 / 2.46 ms -> 0.77 /
+// 1.16 ms; from level 2 on the light components have merged, fewer roots fall inside the
+// window and the coarse chunks leave CUs idle: 1.60 -> 1.74 ms, later levels ~1.5x slower).
+// A 2^14 window: 1.07 / 1.58 ms.
+constexpr int XW_BITS = 15, XWB = 1024, XW_ITEMS = 8, XW_LEVELS = 2;
+constexpr uint32_t XW = 1u << XW_BITS;
+constexpr uint64_t XW_CH = (uint64_t)XWB * XW_ITEMS * 8;
+__global__ __launch_bounds__(XWB) void k_cross_find_win(const uint64_t *__restrict__ xbuf, const uint64_t *__restrict__ n_x,
+                                                        uint32_t *uf, uint32_t *__restrict__ mt,
+                                                        uint32_t *__restrict__ xtop, Tg g) {
+  extern __shared__ uint32_t lmin[];
+  uint32_t *const s_red = lmin + XW;   // (dynamic only: allow_full_lds admits no static LDS)
+  const uint64_t nx = *n_x;
+  const uint64_t c0 = (uint64_t)blockIdx.x * XW_CH;
+  if (c0 >= nx) return;   // uniform
+  const uint64_t c1 = c0 + XW_CH < nx ? c0 + XW_CH : nx;
+  uint32_t mn = INVALID;
+  for (uint64_t i = c0 + threadIdx.x; i < c1; i += XWB) {
+    const uint32_t lo = (uint32_t)xbuf[i];
+    mn = lo < mn ? lo : mn;
+  }
+  mn = wave_min(mn);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = mn;
+  for (uint32_t j = threadIdx.x; j < XW; j += XWB) lmin[j] = INVALID;
+  __syncthreads();
+  uint32_t w0 = INVALID;
+  for (int w = 0; w < XWB / WAVE; ++w) w0 = s_red[w] < w0 ? s_red[w] : w0;
+  for (uint64_t base = c0 + threadIdx.x; base < c0 + XW_CH; base += (uint64_t)XWB * XW_ITEMS) {   // uniform trip count
+    uint32_t t[XW_ITEMS], b[XW_ITEMS];
+    bool live[XW_ITEMS];
+#pragma unroll
+    for (int k = 0; k < XW_ITEMS; ++k) {
+      const uint64_t i = base + (uint64_t)k * XWB;
+      live[k] = i < c1;
+      const uint64_t e = live[k] ? xbuf[i] : 0;
+      t[k] = (uint32_t)e;
+      b[k] = (uint32_t)(e >> 32);
+    }
+    find_many<XW_ITEMS>(uf, g, t, live);
+    bool glob[XW_ITEMS];
+#pragma unroll
+    for (int k = 0; k < XW_ITEMS; ++k) {
+      if (live[k]) xtop[base + (uint64_t)k * XWB] = t[k];
+      const bool in = live[k] && t[k] - w0 < XW;
+      if (in) atomicMin(&lmin[t[k] - w0], b[k]);
+      glob[k] = live[k] && !in;
+    }
+#pragma unroll
+    for (int k = 0; k < XW_ITEMS; ++k) {
+      const uint64_t cm = __ballot(glob[k]);
+      if (!cm) continue;
+      const int first = __ffsll((unsigned long long)cm) - 1;
+      const uint32_t t0 = __shfl(t[k], first, 64);
+      const bool same = glob[k] && t[k] == t0;
+      const uint32_t v = wave_min(same ? b[k] : INVALID);
+      if ((int)__lane_id() == first && g.m_enc(v) < mt[t0]) atomicMin(&mt[t0], g.m_enc(v));
+      if (glob[k] && !same && g.m_enc(b[k]) < mt[t[k]]) atomicMin(&mt[t[k]], g.m_enc(b[k]));
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < XW; j += XWB) {
+    const uint32_t v = lmin[j];
+    if (v == INVALID) continue;
+    const uint32_t e = g.m_enc(v);
+    if (e < mt[w0 + j]) atomicMin(&mt[w0 + j], e);
+  }
+}
+
 // Contract every cross edge (a,b) -> (m_r, b) where r = a's light component; drop it
 // when b == m_r.  parent(top(r)) = m_r (jnode.h:158-162 adopt) is stored by k_level_clean
 // in one pass over mt (tagged state) or here by the edges with b == m_r.  Dedup: claim[b] holds
@@ -967,6 +1042,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   const bool tagged = n < TAG_MAX_N;
   hipLaunchKernelGGL(k_reset, dim3(gn), dim3(BLOCK), 0, c.stream, uf, mt, top, claim, n, csets);
   LAUNCH_CHECK();
+  allow_full_lds((const void *)k_cross_find_win);
   for (int lvl = 0; lvl < nglobal; ++lvl) {
     const int s = L - 1 - lvl;
     uint64_t *st = stats + (uint64_t)lvl * ST_ROW;
@@ -1003,8 +1079,13 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     }
     {
       TimedRegion tr(c, "etree_cross");
-      hipLaunchKernelGGL(k_cross_find, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)xbuf,
-                         (const uint64_t *)(st + ST_NX), uf, mt, xtop, g);
+      if (lvl < XW_LEVELS)
+        hipLaunchKernelGGL(k_cross_find_win, dim3((unsigned)((mcap + XW_CH - 1) / XW_CH)), dim3(XWB),
+                           (XW + XWB / WAVE) * 4, c.stream, (const uint64_t *)xbuf, (const uint64_t *)(st + ST_NX), uf,
+                           mt, xtop, g);
+      else
+        hipLaunchKernelGGL(k_cross_find, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)xbuf,
+                           (const uint64_t *)(st + ST_NX), uf, mt, xtop, g);
       LAUNCH_CHECK();
     }
     {
