@@ -108,10 +108,12 @@ __global__ __launch_bounds__(CB) void k_hist_count(Src src, uint64_t n, uint32_t
   for (uint32_t b = threadIdx.x; b < nb; b += CB) tile_hist[(uint64_t)b * ntiles + tile] = lds[b];
 }
 
-// Block-wide exclusive scan of a[0, nb) in LDS (nb <= 8 * HB), in place; returns total.
+// Block-wide exclusive scan of a[0, nb) in LDS (nb <= 8 * NT, NT threads), in place;
+// returns total.
+template <int NT = HB>
 __device__ uint32_t lds_exclusive_scan(uint32_t *a, uint32_t nb, uint32_t *wsum) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t per = (nb + HB - 1) / HB, b0 = threadIdx.x * per;
+  const uint32_t per = (nb + NT - 1) / NT, b0 = threadIdx.x * per;
   uint32_t v[8];
   uint32_t s = 0;
 #pragma unroll
@@ -128,7 +130,7 @@ __device__ uint32_t lds_exclusive_scan(uint32_t *a, uint32_t nb, uint32_t *wsum)
   if (lane == 63) wsum[wave] = inc;
   lds_barrier();
   uint32_t off = 0, tot = 0;
-  for (int w = 0; w < HB / WAVE; ++w) {
+  for (int w = 0; w < NT / WAVE; ++w) {
     const uint32_t x = wsum[w];
     if (w < wave) off += x;
     tot += x;
@@ -555,17 +557,17 @@ struct RelabelKeys {
 // a whole tile does not fit LDS).  gb[b] walks the tile's region of bucket b; every write
 // is bounded by the region's end and a region not filled exactly raises flags[1] (stale
 // offsets) so the host recounts.  flags[0]: a sequenced endpoint's neighbour >= pos_size.
-template <int PER>
-__global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restrict__ rec, uint64_t n,
+template <int PER, int NT = HB>
+__global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restrict__ rec, uint64_t n,
                                                         const uint32_t *__restrict__ pos, uint64_t pos_size, uint32_t nb,
                                                         const uint32_t *__restrict__ offsets, uint64_t ntiles,
                                                         uint64_t *__restrict__ out, unsigned long long *__restrict__ flags) {
-  constexpr uint32_t SUB = PER * HB;
+  constexpr uint32_t SUB = PER * NT;
   extern __shared__ uint32_t lds[];
   uint32_t *cur = lds, *gb = lds + nb, *end = lds + 2 * nb, *wsum = lds + 3 * nb;
-  uint64_t *stage = (uint64_t *)(lds + ((3 * nb + HB / WAVE + 1) & ~1u));
+  uint64_t *stage = (uint64_t *)(lds + ((3 * nb + NT / WAVE + 1) & ~1u));
   const uint64_t tile = xcd_tile();
-  for (uint32_t b = threadIdx.x; b < nb; b += HB) {
+  for (uint32_t b = threadIdx.x; b < nb; b += NT) {
     const uint64_t o = (uint64_t)b * ntiles + tile;
     gb[b] = offsets[o];
     end[b] = offsets[o + 1];
@@ -573,13 +575,13 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
   bool bad = false, lost = false;
   const uint64_t base = tile << TLOG;
   for (uint32_t s0 = 0; s0 < TKEYS; s0 += SUB) {
-    for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
+    for (uint32_t b = threadIdx.x; b < nb; b += NT) cur[b] = 0;
     lds_barrier();
     uint64_t x[PER];
     uint32_t pt[PER], hd[PER], rk[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {   // all record loads, then all pos[tail] loads in flight
-      const uint64_t i = base + s0 + (uint64_t)j * HB + threadIdx.x;
+      const uint64_t i = base + s0 + (uint64_t)j * NT + threadIdx.x;
       hd[j] = INVALID;
       pt[j] = INVALID;
       if (i < n) {
@@ -601,24 +603,24 @@ __global__ __launch_bounds__(HB) void k_relabel_scatter(const sheep_xs1 *__restr
       rk[j] = atomicAdd(&cur[h >> WBITS], 1u);   // the pair's rank in its bucket
     }
     lds_barrier();
-    const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
-    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] -= cur[b];   // region cursor - local start
+    const uint32_t total = lds_exclusive_scan<NT>(cur, nb, wsum);
+    for (uint32_t b = threadIdx.x; b < nb; b += NT) gb[b] -= cur[b];   // region cursor - local start
     lds_barrier();
 #pragma unroll
     for (int j = 0; j < PER; ++j)
       if (x[j] != NO_PAIR) stage[cur[(uint32_t)x[j] >> WBITS] + rk[j]] = x[j];
     lds_barrier();
-    for (uint32_t j = threadIdx.x; j < total; j += HB) {
+    for (uint32_t j = threadIdx.x; j < total; j += NT) {
       const uint64_t v = stage[j];
       const uint32_t b = (uint32_t)v >> WBITS, dst = gb[b] + j;
       if (dst < end[b]) out[dst] = v;
       else lost = true;
     }
     lds_barrier();
-    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += b + 1 < nb ? cur[b + 1] : total;   // past this sub-tile's run
+    for (uint32_t b = threadIdx.x; b < nb; b += NT) gb[b] += b + 1 < nb ? cur[b + 1] : total;   // past this sub-tile's run
     lds_barrier();
   }
-  for (uint32_t b = threadIdx.x; b < nb; b += HB)
+  for (uint32_t b = threadIdx.x; b < nb; b += NT)
     if (gb[b] != end[b]) lost = true;
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(&flags[0], 1ull);
   if (__any(lost) && (threadIdx.x & 63) == 0) atomicAdd(&flags[1], 1ull);
@@ -737,6 +739,7 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   const uint64_t nb = (pos_size + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
   if (nrec == 0 || nb == 0 || nb > 8192 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return UINT64_MAX;
   for (const void *f : {(const void *)k_relabel_scatter<8>, (const void *)k_relabel_scatter<4>,
+                        (const void *)k_relabel_scatter<8, 512>,
                         (const void *)k_relabel_gather<false>, (const void *)k_relabel_gather<true>})
     allow_full_lds(f);
   Ctx::HeadLayout &hl = c.head_layout;
@@ -765,8 +768,22 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   const size_t fixed = ((3 * nb + HB / WAVE + 1) & ~1ull) * 4;
   auto scatter = [&]() {
     HIP_CHECK(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c.stream));
-    // 8K-record sub-tiles (4K / 16K measured 15.8 / 15.3 ms against 14.3 at RMAT-26);
-    // 4K when the bucket cursors take more LDS (vertex ids above 2^27)
+    // Two 512-thread workgroups per CU, 4K-record sub-tiles (81 VGPRs keep a 1024-thread
+    // workgroup alone on its CU, idle at every barrier): RMAT-26 9.18 -> 8.92 ms.  Up to
+    // 4096 buckets (vertex ids below 2^27), the scan's limit for 512 threads.
+    {
+      constexpr int NT = 512, P = 8;
+      const size_t fx = ((3 * nb + NT / WAVE + 1) & ~1ull) * 4, lds = fx + (size_t)P * NT * 8;
+      if (nb <= 8 * (uint64_t)NT && lds <= 160 * 1024) {
+        hipLaunchKernelGGL((k_relabel_scatter<P, NT>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec, nrec, pos,
+                           pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
+        LAUNCH_CHECK();
+        HIP_CHECK(hipMemcpyAsync(c.h_scalars + 12, flags, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+        return;
+      }
+    }
+    // one 1024-thread workgroup per CU: 8K-record sub-tiles (4K / 16K measured 15.8 / 15.3
+    // ms against 14.3 at RMAT-26); 4K when the bucket cursors take more LDS
     const int per = fixed + 8 * HB * 8 <= 160 * 1024 ? 8 : 4;
     if (fixed + (size_t)per * HB * 8 > 160 * 1024) throw Error(SHEEP_ERR_ARG, "relabel: bucket layout exceeds LDS");
     const size_t lds = fixed + (size_t)per * HB * 8;

@@ -3,7 +3,10 @@
 a bench.py run): the dispatches from the last k_degree_fused up to the evaluator's first
 kernel (k_pp) or the end.  Prints ms per kernel base name, calls, and the step span.
 
-    python tools/trace_step.py run_kernel_trace.csv [--levels]
+    python tools/trace_step.py run_kernel_trace.csv [--levels] [--from KERNEL]
+
+--from KERNEL: the step starts at the last dispatch of KERNEL instead (e.g. k_tree_count
+for the last merge of tools/merge_trace.py).
 """
 import csv
 import re
@@ -18,7 +21,8 @@ def base(name):
 
 def main():
     rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if base(r["Kernel_Name"]) == "k_degree_fused"]
+    first = sys.argv[sys.argv.index("--from") + 1] if "--from" in sys.argv else "k_degree_fused"
+    starts = [i for i, r in enumerate(rows) if base(r["Kernel_Name"]) == first]
     step = rows[starts[-1]:]
     ends = [i for i, r in enumerate(step) if base(r["Kernel_Name"]) == "k_pp"]
     step = step[:ends[0]] if ends else step
