@@ -982,10 +982,7 @@ static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
 // Hub blocks go to whole waves (k_fin_heavy).  A merge's edges spread evenly over the
 // blocks, so its finish takes 11 bits (RMAT-26, 8 shard trees: K-way merge 19.5 -> 17.9
 // ms; 10: 18.1, 12: 18.2).
-#ifndef SHEEP_EXP_FIN_MAP
-#define SHEEP_EXP_FIN_MAP 8
-#endif
-constexpr int FIN_MERGE = 11, FIN_MAP = SHEEP_EXP_FIN_MAP;
+constexpr int FIN_MERGE = 11, FIN_MAP = 8;
 
 // spread(x) = floor(x * c / 2^32), c = floor(2^(32+L) / n) in [2^32, 2^33), L = ceil(log2 n):
 // monotone, injective on [0,n), image in [0, 2^L).  clo = c - 2^32.

@@ -3,7 +3,7 @@ import json
 import sys
 from pathlib import Path
 
-d = Path("gpurun_out/abt")
+d = Path(sys.argv[3] if len(sys.argv) > 3 else "gpurun_out/abt")
 variants, phases = sys.argv[1].split(), sys.argv[2].split() if len(sys.argv) > 2 else []
 for v in ["base"] + variants:
     p = d / f"p_{v}.log"
