@@ -235,14 +235,27 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t *__restrict__ uf, uint
 // values — entry by entry when the level's lists are short against n (only light
 // endpoints, cross roots and cross hi ends were written), else densely; the choice is
 // made on the device from the level's counts (no host round trip).
-__global__ __launch_bounds__(BLOCK) void k_level_clean(const uint64_t *__restrict__ lbuf, const uint64_t *__restrict__ xbuf,
-                                                       const uint32_t *__restrict__ xtop,
-                                                       const uint64_t *__restrict__ st, uint32_t *__restrict__ uf,
-                                                       uint32_t *__restrict__ mt, uint32_t *__restrict__ top,
-                                                       uint32_t *__restrict__ claim, uint64_t n, bool tagged, int lvl,
-                                                       uint32_t *__restrict__ parent,
-                                                       unsigned long long *__restrict__ csets) {
-  const uint64_t nl = st[ST_NL], nx = st[ST_NX];
+struct LevelClean {   // what k_level_clean needs of the level it closes
+  const uint64_t *lbuf, *xbuf;
+  const uint32_t *xtop;
+  const uint64_t *st;
+  uint32_t *uf, *mt, *top, *claim;
+  uint64_t n;
+  bool tagged;
+  int lvl;
+  uint32_t *parent;
+  unsigned long long *csets;
+};
+__device__ void level_clean(const LevelClean &lc) {
+  const uint64_t *__restrict__ lbuf = lc.lbuf, *__restrict__ xbuf = lc.xbuf;
+  const uint32_t *__restrict__ xtop = lc.xtop;
+  uint32_t *__restrict__ uf = lc.uf, *__restrict__ mt = lc.mt, *__restrict__ top = lc.top, *__restrict__ claim = lc.claim;
+  uint32_t *__restrict__ parent = lc.parent;
+  unsigned long long *__restrict__ csets = lc.csets;
+  const uint64_t n = lc.n;
+  const bool tagged = lc.tagged;
+  const int lvl = lc.lvl;
+  const uint64_t nl = lc.st[ST_NL], nx = lc.st[ST_NX];
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   const uint64_t t0 = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
   for (uint64_t i = t0; i < NCSET * CSET_WORDS; i += stride) csets[i] = 0;
@@ -277,6 +290,9 @@ __global__ __launch_bounds__(BLOCK) void k_level_clean(const uint64_t *__restric
     claim[(uint32_t)(xbuf[i] >> 32)] = INVALID;
   }
 }
+// The last global level's clean (the others run at the start of the next level's
+// k_split_count: one launch fewer per level).
+__global__ __launch_bounds__(BLOCK) void k_level_clean(LevelClean lc) { level_clean(lc); }
 
 constexpr int XK = 8;   // items per thread in the gather kernels (independent chains in flight)
 
@@ -357,18 +373,42 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
 // The edges still unresolved after HOOK_ROUNDS rounds (few: the pile-ups are gone) are
 // hooked in place, retrying until each one's roots agree.  Lock-free: a failed CAS
 // means another hook made progress.
-__global__ __launch_bounds__(BLOCK) void k_hook_finish(const uint64_t *__restrict__ in, const uint64_t *__restrict__ n_in,
-                                                       uint32_t *uf, Tg g) {
-  const uint64_t nin = *n_in;
+__global__ __launch_bounds__(BLOCK) void k_hook_finish(const uint64_t *__restrict__ src, const uint64_t *__restrict__ n_in,
+                                                       const unsigned long long *__restrict__ counters, uint32_t *uf, Tg g,
+                                                       uint64_t *__restrict__ n_left) {
+  // the hook round's survivors straight from its shard regions (no pack launch): the
+  // NSHARD counts' prefix in LDS, each entry's shard by binary search over it
+  static_assert(NSHARD == WAVE, "one lane per shard counter");
+  __shared__ uint64_t s_pre[NSHARD + 1];
+  const uint64_t ntiles = (*n_in + TILE - 1) / TILE;
+  if (threadIdx.x < WAVE) {
+    const uint64_t c = counters[(uint64_t)threadIdx.x * SHARD_STRIDE];
+    uint64_t inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t u = __shfl_up(inc, o, 64);
+      if ((int)threadIdx.x >= o) inc += u;
+    }
+    s_pre[threadIdx.x + 1] = inc;
+    if (threadIdx.x == 0) s_pre[0] = 0;
+  }
+  lds_barrier();
+  const uint64_t nin = s_pre[NSHARD];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *n_left = nin;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nin; i += stride) {
-    const uint64_t e = in[i];
+    uint32_t lo = 0, hi = NSHARD;   // s_pre[lo] <= i < s_pre[hi]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) / 2;
+      if (s_pre[mid] <= i) lo = mid; else hi = mid;
+    }
+    const uint64_t e = src[shard_base(ntiles, lo, 1) + (i - s_pre[lo])];
     uint32_t a = (uint32_t)e, b = (uint32_t)(e >> 32);
     for (;;) {
       find2(uf, g, a, b);
       if (a == b) break;
-      const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-      if (hook(uf, g, hi, lo)) break;
+      const uint32_t l = a < b ? a : b, h = a < b ? b : a;
+      if (hook(uf, g, h, l)) break;
     }
   }
 }
@@ -428,65 +468,71 @@ __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict
 // A 2^14 window: 1.07 / 1.58 ms.
 constexpr int XW_BITS = 15, XWB = 1024, XW_ITEMS = 8, XW_LEVELS = 2;
 constexpr uint32_t XW = 1u << XW_BITS;
-constexpr uint64_t XW_CH = (uint64_t)XWB * XW_ITEMS * 8;
+constexpr uint64_t XW_STEP = (uint64_t)XWB * XW_ITEMS, XW_CH = XW_STEP * 8;
 __global__ __launch_bounds__(XWB) void k_cross_find_win(const uint64_t *__restrict__ xbuf, const uint64_t *__restrict__ n_x,
                                                         uint32_t *uf, uint32_t *__restrict__ mt,
                                                         uint32_t *__restrict__ xtop, Tg g) {
   extern __shared__ uint32_t lmin[];
   uint32_t *const s_red = lmin + XW;   // (dynamic only: allow_full_lds admits no static LDS)
   const uint64_t nx = *n_x;
-  const uint64_t c0 = (uint64_t)blockIdx.x * XW_CH;
-  if (c0 >= nx) return;   // uniform
-  const uint64_t c1 = c0 + XW_CH < nx ? c0 + XW_CH : nx;
-  uint32_t mn = INVALID;
-  for (uint64_t i = c0 + threadIdx.x; i < c1; i += XWB) {
-    const uint32_t lo = (uint32_t)xbuf[i];
-    mn = lo < mn ? lo : mn;
-  }
-  mn = wave_min(mn);
-  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = mn;
-  for (uint32_t j = threadIdx.x; j < XW; j += XWB) lmin[j] = INVALID;
-  __syncthreads();
-  uint32_t w0 = INVALID;
-  for (int w = 0; w < XWB / WAVE; ++w) w0 = s_red[w] < w0 ? s_red[w] : w0;
-  for (uint64_t base = c0 + threadIdx.x; base < c0 + XW_CH; base += (uint64_t)XWB * XW_ITEMS) {   // uniform trip count
-    uint32_t t[XW_ITEMS], b[XW_ITEMS];
-    bool live[XW_ITEMS];
-#pragma unroll
-    for (int k = 0; k < XW_ITEMS; ++k) {
-      const uint64_t i = base + (uint64_t)k * XWB;
-      live[k] = i < c1;
-      const uint64_t e = live[k] ? xbuf[i] : 0;
-      t[k] = (uint32_t)e;
-      b[k] = (uint32_t)(e >> 32);
+  // chunks of XW_STEP..XW_CH edges, so that even a short list spreads over the CUs
+  // (RMAT-22's first levels: ~2M cross edges, 29 chunks of XW_CH)
+  uint64_t ch = (nx / 1024 + XW_STEP - 1) / XW_STEP * XW_STEP;
+  ch = ch < XW_STEP ? XW_STEP : ch > XW_CH ? XW_CH : ch;
+  const uint64_t nchunks = (nx + ch - 1) / ch;
+  for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {   // uniform
+    const uint64_t c0 = chunk * ch, c1 = c0 + ch < nx ? c0 + ch : nx;
+    uint32_t mn = INVALID;
+    for (uint64_t i = c0 + threadIdx.x; i < c1; i += XWB) {
+      const uint32_t lo = (uint32_t)xbuf[i];
+      mn = lo < mn ? lo : mn;
     }
-    find_many<XW_ITEMS>(uf, g, t, live);
-    bool glob[XW_ITEMS];
+    mn = wave_min(mn);
+    __syncthreads();   // the previous chunk's flush is done with lmin and s_red
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = mn;
+    for (uint32_t j = threadIdx.x; j < XW; j += XWB) lmin[j] = INVALID;
+    __syncthreads();
+    uint32_t w0 = INVALID;
+    for (int w = 0; w < XWB / WAVE; ++w) w0 = s_red[w] < w0 ? s_red[w] : w0;
+    for (uint64_t base = c0 + threadIdx.x; base < c0 + ch; base += XW_STEP) {   // uniform trip count
+      uint32_t t[XW_ITEMS], b[XW_ITEMS];
+      bool live[XW_ITEMS];
 #pragma unroll
-    for (int k = 0; k < XW_ITEMS; ++k) {
-      if (live[k]) xtop[base + (uint64_t)k * XWB] = t[k];
-      const bool in = live[k] && t[k] - w0 < XW;
-      if (in) atomicMin(&lmin[t[k] - w0], b[k]);
-      glob[k] = live[k] && !in;
-    }
+      for (int k = 0; k < XW_ITEMS; ++k) {
+        const uint64_t i = base + (uint64_t)k * XWB;
+        live[k] = i < c1;
+        const uint64_t e = live[k] ? xbuf[i] : 0;
+        t[k] = (uint32_t)e;
+        b[k] = (uint32_t)(e >> 32);
+      }
+      find_many<XW_ITEMS>(uf, g, t, live);
+      bool glob[XW_ITEMS];
 #pragma unroll
-    for (int k = 0; k < XW_ITEMS; ++k) {
-      const uint64_t cm = __ballot(glob[k]);
-      if (!cm) continue;
-      const int first = __ffsll((unsigned long long)cm) - 1;
-      const uint32_t t0 = __shfl(t[k], first, 64);
-      const bool same = glob[k] && t[k] == t0;
-      const uint32_t v = wave_min(same ? b[k] : INVALID);
-      if ((int)__lane_id() == first && g.m_enc(v) < mt[t0]) atomicMin(&mt[t0], g.m_enc(v));
-      if (glob[k] && !same && g.m_enc(b[k]) < mt[t[k]]) atomicMin(&mt[t[k]], g.m_enc(b[k]));
+      for (int k = 0; k < XW_ITEMS; ++k) {
+        if (live[k]) xtop[base + (uint64_t)k * XWB] = t[k];
+        const bool in = live[k] && t[k] - w0 < XW;
+        if (in) atomicMin(&lmin[t[k] - w0], b[k]);
+        glob[k] = live[k] && !in;
+      }
+#pragma unroll
+      for (int k = 0; k < XW_ITEMS; ++k) {
+        const uint64_t cm = __ballot(glob[k]);
+        if (!cm) continue;
+        const int first = __ffsll((unsigned long long)cm) - 1;
+        const uint32_t t0 = __shfl(t[k], first, 64);
+        const bool same = glob[k] && t[k] == t0;
+        const uint32_t v = wave_min(same ? b[k] : INVALID);
+        if ((int)__lane_id() == first && g.m_enc(v) < mt[t0]) atomicMin(&mt[t0], g.m_enc(v));
+        if (glob[k] && !same && g.m_enc(b[k]) < mt[t[k]]) atomicMin(&mt[t[k]], g.m_enc(b[k]));
+      }
     }
-  }
-  __syncthreads();
-  for (uint32_t j = threadIdx.x; j < XW; j += XWB) {
-    const uint32_t v = lmin[j];
-    if (v == INVALID) continue;
-    const uint32_t e = g.m_enc(v);
-    if (e < mt[w0 + j]) atomicMin(&mt[w0 + j], e);
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < XW; j += XWB) {
+      const uint32_t v = lmin[j];
+      if (v == INVALID) continue;
+      const uint32_t e = g.m_enc(v);
+      if (e < mt[w0 + j]) atomicMin(&mt[w0 + j], e);
+    }
   }
 }
 
@@ -611,9 +657,11 @@ __device__ __forceinline__ uint64_t pack3(uint32_t c) {
 __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
                                                        uint64_t *__restrict__ st, int s, uint32_t clo, YRange yr,
                                                        const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
-                                                       int L, uint64_t *__restrict__ cnt) {
+                                                       int L, uint64_t *__restrict__ cnt, LevelClean clean) {
   // the three count rows at stride ntiles (this level's), then one 0: scanned as one
-  // exclusive scan of 3 ntiles + 1 entries (the length in st, read by the scan)
+  // exclusive scan of 3 ntiles + 1 entries (the length in st, read by the scan).
+  // clean: the previous level's k_level_clean, run first (clean.st == nullptr: none).
+  if (clean.st) level_clean(clean);
   const SplitIn in(list, prev, r0, seg, s, L);
   const uint64_t ntiles = (in.m + SPLIT_TILE - 1) / SPLIT_TILE, cstride = ntiles;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1024,12 +1072,8 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   // the two list buffers (level l reads one and writes the other) and the bucketed input r0
   uint64_t *lists[2] = {c.get_as<uint64_t>("et_list1", lcap), c.get_as<uint64_t>("et_list2", lcap)};
   const uint64_t *r0 = edges;
-  // a split reads at most the list plus a bucket: (lcap + m) entries, in TILE tiles
-  const uint64_t cstride = (lcap + m + SPLIT_TILE - 1) / SPLIT_TILE + 1;
-  uint64_t *tcnt = c.get_as<uint64_t>("et_tilecnt", 3 * cstride + 1);
-  uint64_t *lbuf = c.get_as<uint64_t>("et_light", mcap);  // must outlive the hook rounds (k_level_clean)
-  uint64_t *alt = c.get_as<uint64_t>("et_alt", mcap);     // shard scratch of the hook rounds
-  uint64_t *hk[2] = {c.get_as<uint64_t>("et_lwa", mcap), c.get_as<uint64_t>("et_lwb", mcap)};
+  uint64_t *lbuf = c.get_as<uint64_t>("et_light", mcap);  // must outlive the level (its clean, next level)
+  uint64_t *alt = c.get_as<uint64_t>("et_alt", mcap);     // shard scratch of the hook round and the contractions
   unsigned long long *csets = c.get_as<unsigned long long>("et_csets", NCSET * CSET_WORDS);
   uint64_t *stats = c.get_as<uint64_t>("et_stats", (uint64_t)(L + 1) * ST_ROW);
   HIP_CHECK(hipMemsetAsync(stats, 0, (uint64_t)(L + 1) * ST_ROW * sizeof(uint64_t), c.stream));
@@ -1043,6 +1087,9 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   hipLaunchKernelGGL(k_reset, dim3(gn), dim3(BLOCK), 0, c.stream, uf, mt, top, claim, n, csets);
   LAUNCH_CHECK();
   allow_full_lds((const void *)k_cross_find_win);
+  // a split reads at most the list plus a bucket: (lcap + m) entries, in SPLIT_TILE tiles
+  const uint64_t cstride = (lcap + m + SPLIT_TILE - 1) / SPLIT_TILE + 1;
+  uint64_t *tcnt = c.get_as<uint64_t>("et_tilecnt", 3 * cstride + 1);
   for (int lvl = 0; lvl < nglobal; ++lvl) {
     const int s = L - 1 - lvl;
     uint64_t *st = stats + (uint64_t)lvl * ST_ROW;
@@ -1052,8 +1099,11 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     const YRange yr{ylo, yhi, lvl == filt_lvl};
     {
       TimedRegion tr(c, "etree_split");
+      // the previous level's clean first (its counters, adoptions and resets)
+      const LevelClean clean = lvl ? LevelClean{lbuf, xbuf, xtop, prev, uf, mt, top, claim, n, tagged, lvl - 1, parent, csets}
+                                   : LevelClean{};
       hipLaunchKernelGGL(k_split_count, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo, yr,
-                         (const uint64_t *)r0, (const uint64_t *)seg, L, tcnt);
+                         (const uint64_t *)r0, (const uint64_t *)seg, L, tcnt, clean);
       LAUNCH_CHECK();
       scan_exclusive_u64_dev(c, tcnt, tcnt, 3 * cstride + 1, st + ST_SCANN);
       hipLaunchKernelGGL(k_split_write, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo, yr,
@@ -1062,16 +1112,12 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     }
     {
       TimedRegion tr(c, "etree_union");
-      const uint64_t *in = lbuf, *n_in = st + ST_NL;
-      for (int round = 0; round < HOOK_ROUNDS; ++round) {
-        uint64_t *dst = hk[round & 1];
-        hipLaunchKernelGGL(k_hook_round, dim3(gt), dim3(BLOCK), 0, c.stream, in, n_in, uf, g, alt, cset(CSET_HOOK + round));
-        LAUNCH_CHECK();
-        pack_shards<uint64_t>(c, alt, dst, n_in, cset(CSET_HOOK + round), st + ST_HOOK + round);
-        in = dst;
-        n_in = st + ST_HOOK + round;
-      }
-      hipLaunchKernelGGL(k_hook_finish, dim3(gf), dim3(BLOCK), 0, c.stream, in, n_in, uf, g);
+      static_assert(HOOK_ROUNDS == 1, "k_hook_finish reads the one round's shard regions");
+      hipLaunchKernelGGL(k_hook_round, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
+                         (const uint64_t *)(st + ST_NL), uf, g, alt, cset(CSET_HOOK));
+      LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_hook_finish, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)alt,
+                         (const uint64_t *)(st + ST_NL), (const unsigned long long *)cset(CSET_HOOK), uf, g, st + ST_HOOK);
       LAUNCH_CHECK();
       hipLaunchKernelGGL(k_light_top, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
                          (const uint64_t *)(st + ST_NL), uf, top, g);
@@ -1080,7 +1126,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     {
       TimedRegion tr(c, "etree_cross");
       if (lvl < XW_LEVELS)
-        hipLaunchKernelGGL(k_cross_find_win, dim3((unsigned)((mcap + XW_CH - 1) / XW_CH)), dim3(XWB),
+        hipLaunchKernelGGL(k_cross_find_win, dim3(grid_for(mcap, XW_STEP, 1024)), dim3(XWB),
                            (XW + XWB / WAVE) * 4, c.stream, (const uint64_t *)xbuf, (const uint64_t *)(st + ST_NX), uf,
                            mt, xtop, g);
       else
@@ -1095,11 +1141,14 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
                          alt, cset(CSET_APPLY), parent, g);
       LAUNCH_CHECK();
       pack_shards<uint64_t>(c, alt, next, st + ST_NX, cset(CSET_APPLY), st + ST_CONTR, nullptr, nullptr, st + ST_KEPT);
-      hipLaunchKernelGGL(k_level_clean, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
-                         (const uint64_t *)xbuf, (const uint32_t *)xtop, (const uint64_t *)st, uf, mt, top, claim, n,
-                         tagged, lvl, parent, csets);
-      LAUNCH_CHECK();
     }
+  }
+  if (nglobal) {   // the last level's clean (the others ran in the next level's split)
+    TimedRegion tr(c, "etree_apply");
+    hipLaunchKernelGGL(k_level_clean, dim3(gf), dim3(BLOCK), 0, c.stream,
+                       LevelClean{lbuf, xbuf, xtop, stats + (uint64_t)(nglobal - 1) * ST_ROW, uf, mt, top, claim, n, tagged,
+                                  nglobal - 1, parent, csets});
+    LAUNCH_CHECK();
   }
   if (FINB) {
     // the last min(L, B) levels: the list plus the groups s < B, sorted by hi, then
