@@ -1,4 +1,4 @@
-// radix.hip — stable LSD radix sort (8-bit digits) for the degree sequence
+// radix.hip — stable LSD radix sort (digits of up to 9 bits) for the degree sequence
 // (key = degree, value = vid), the kid table (key = parent, value = id) and the RMAT
 // generator's dedup (64-bit keys).
 //
@@ -12,13 +12,15 @@ namespace {
 
 constexpr int R_ITEMS = 16;
 constexpr int R_TILE = BLOCK * R_ITEMS;   // 4096 keys per workgroup
-constexpr int RADIX = 256;
+// A sort of `bits` key bits takes ceil(bits / 9) passes of near-equal digits (25-bit kid
+// keys: 9 + 8 + 8 instead of 8 + 8 + 8 + 1; each pass reads and writes every pair).
+constexpr int MAX_DBITS = 9;
 
 // 64-lane mask of the valid lanes whose digit equals mine.
-__device__ __forceinline__ uint64_t digit_peers(bool valid, uint32_t d) {
+template <int DB> __device__ __forceinline__ uint64_t digit_peers(bool valid, uint32_t d) {
   uint64_t peers = __ballot(valid);
 #pragma unroll
-  for (int b = 0; b < 8; ++b) {
+  for (int b = 0; b < DB; ++b) {
     bool bit = (d >> b) & 1;
     uint64_t bb = __ballot(bit);
     peers &= bit ? bb : ~bb;
@@ -26,29 +28,31 @@ __device__ __forceinline__ uint64_t digit_peers(bool valid, uint32_t d) {
   return peers;
 }
 
-template <typename K>
+template <typename K, int DB>
 __global__ __launch_bounds__(BLOCK) void k_hist(const K *__restrict__ keys, uint64_t n, int shift,
                                                 uint32_t ntiles, uint32_t *__restrict__ hist) {
+  constexpr int RADIX = 1 << DB;
   __shared__ uint32_t h[RADIX];
-  h[threadIdx.x] = 0;
+  for (int d = threadIdx.x; d < RADIX; d += BLOCK) h[d] = 0;
   lds_barrier();
   uint64_t base = (uint64_t)blockIdx.x * R_TILE;
   for (int j = 0; j < R_ITEMS; ++j) {
     uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
     bool valid = i < n;
     uint32_t d = valid ? (uint32_t)((keys[i] >> shift) & (RADIX - 1)) : 0;
-    uint64_t peers = digit_peers(valid, d);
+    uint64_t peers = digit_peers<DB>(valid, d);
     if (valid && (peers & lanemask_lt()) == 0) atomicAdd(&h[d], (uint32_t)__popcll(peers));
   }
   lds_barrier();
-  hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+  for (int d = threadIdx.x; d < RADIX; d += BLOCK) hist[(uint64_t)d * ntiles + blockIdx.x] = h[d];
 }
 
-template <typename K, bool VALS>
+template <typename K, bool VALS, int DB>
 __global__ __launch_bounds__(BLOCK) void k_scatter(const K *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                    K *__restrict__ kout, uint32_t *__restrict__ vout,
                                                    uint64_t n, int shift, uint32_t ntiles,
                                                    const uint32_t *__restrict__ offsets) {
+  constexpr int RADIX = 1 << DB, DPT = RADIX > BLOCK ? RADIX / BLOCK : 1;   // digits per thread
   __shared__ uint32_t run[RADIX];
   __shared__ uint32_t wcnt[BLOCK / WAVE][RADIX];
   __shared__ uint32_t dstart[RADIX];
@@ -57,8 +61,10 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const K *__restrict__ kin, co
   __shared__ uint32_t svals[VALS ? R_TILE : 1];
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  run[t] = 0;
-  for (int w = 0; w < BLOCK / WAVE; ++w) wcnt[w][t] = 0;
+  for (int d = t; d < RADIX; d += BLOCK) {
+    run[d] = 0;
+    for (int w = 0; w < BLOCK / WAVE; ++w) wcnt[w][d] = 0;
+  }
   lds_barrier();
 
   const uint64_t base = (uint64_t)blockIdx.x * R_TILE;
@@ -71,7 +77,7 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const K *__restrict__ kin, co
     key[j] = valid ? kin[i] : K(0);
     if (VALS) val[j] = valid ? vin[i] : 0u;
     uint32_t d = (uint32_t)((key[j] >> shift) & (RADIX - 1));
-    uint64_t peers = digit_peers(valid, d);
+    uint64_t peers = digit_peers<DB>(valid, d);
     uint32_t lrank = (uint32_t)__popcll(peers & lanemask_lt());
     if (valid && lrank == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
     lds_barrier();
@@ -81,13 +87,18 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const K *__restrict__ kin, co
       rank[j] = before + lrank;
     }
     lds_barrier();
-    uint32_t add = 0;
-    for (int w = 0; w < BLOCK / WAVE; ++w) { add += wcnt[w][t]; wcnt[w][t] = 0; }
-    run[t] += add;
+    for (int dd = t; dd < RADIX; dd += BLOCK) {
+      uint32_t add = 0;
+      for (int w = 0; w < BLOCK / WAVE; ++w) { add += wcnt[w][dd]; wcnt[w][dd] = 0; }
+      run[dd] += add;
+    }
     lds_barrier();
   }
-  // tile-local digit starts (exclusive scan of run[] over the 256 digits)
-  uint32_t v = run[t], inc = v;
+  // tile-local digit starts: exclusive scan of run[] (thread t owns digits t*DPT .. +DPT)
+  uint32_t v = 0;
+  if (t * DPT < RADIX)
+    for (int q = 0; q < DPT; ++q) v += run[t * DPT + q];
+  uint32_t inc = v;
   for (int o = 1; o < 64; o <<= 1) {
     uint32_t u = __shfl_up(inc, o, 64);
     if (lane >= o) inc += u;
@@ -96,7 +107,10 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const K *__restrict__ kin, co
   lds_barrier();
   uint32_t woff = 0;
   for (int w = 0; w < wave; ++w) woff += wtot[w];
-  dstart[t] = woff + inc - v;
+  if (t * DPT < RADIX) {
+    uint32_t x = woff + inc - v;
+    for (int q = 0; q < DPT; ++q) { dstart[t * DPT + q] = x; x += run[t * DPT + q]; }
+  }
   lds_barrier();
   for (int j = 0; j < R_ITEMS; ++j) {
     uint64_t i = base + (uint64_t)j * BLOCK + t;
@@ -118,22 +132,37 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const K *__restrict__ kin, co
   }
 }
 
+template <typename K, bool VALS, int DB>
+void radix_pass(Ctx &c, const K *src, const uint32_t *vs, K *dst, uint32_t *vd, uint64_t n, int shift, uint32_t ntiles,
+                uint32_t *hist) {
+  hipLaunchKernelGGL((k_hist<K, DB>), dim3(ntiles), dim3(BLOCK), 0, c.stream, src, n, shift, ntiles, hist);
+  LAUNCH_CHECK();
+  scan_exclusive_u32(c, hist, hist, ((uint64_t)1 << DB) * ntiles, nullptr);
+  hipLaunchKernelGGL((k_scatter<K, VALS, DB>), dim3(ntiles), dim3(BLOCK), 0, c.stream, src, vs, dst, vd, n, shift, ntiles,
+                     (const uint32_t *)hist);
+  LAUNCH_CHECK();
+}
+
 template <typename K, bool VALS>
 void radix_sort_impl(Ctx &c, K *keys, uint32_t *vals, uint64_t n, int end_bit, K *kalt, uint32_t *valt) {
   if (n <= 1 || end_bit <= 0) return;
   if (n >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "radix sort: n >= 2^32");
   uint32_t ntiles = (uint32_t)((n + R_TILE - 1) / R_TILE);
-  uint32_t *hist = c.get_as<uint32_t>("radix_hist", (uint64_t)RADIX * ntiles);
+  uint32_t *hist = c.get_as<uint32_t>("radix_hist", ((uint64_t)1 << MAX_DBITS) * ntiles);
   K *src = keys, *dst = kalt;
   uint32_t *vs = vals, *vd = valt;
-  int passes = 0;
-  for (int shift = 0; shift < end_bit; shift += 8, ++passes) {
-    hipLaunchKernelGGL(k_hist<K>, dim3(ntiles), dim3(BLOCK), 0, c.stream, (const K *)src, n, shift, ntiles, hist);
-    LAUNCH_CHECK();
-    scan_exclusive_u32(c, hist, hist, (uint64_t)RADIX * ntiles, nullptr);
-    hipLaunchKernelGGL((k_scatter<K, VALS>), dim3(ntiles), dim3(BLOCK), 0, c.stream, (const K *)src,
-                       (const uint32_t *)vs, dst, vd, n, shift, ntiles, (const uint32_t *)hist);
-    LAUNCH_CHECK();
+  const int passes = (end_bit + MAX_DBITS - 1) / MAX_DBITS;
+  for (int p = 0, shift = 0; p < passes; ++p) {
+    const int db = (end_bit - shift + (passes - p) - 1) / (passes - p);   // near-equal digits, widest first
+    switch (db) {
+#define SHEEP_RADIX_PASS(B) \
+      case B: radix_pass<K, VALS, B>(c, src, vs, dst, vd, n, shift, ntiles, hist); break;
+      SHEEP_RADIX_PASS(1) SHEEP_RADIX_PASS(2) SHEEP_RADIX_PASS(3) SHEEP_RADIX_PASS(4) SHEEP_RADIX_PASS(5)
+      SHEEP_RADIX_PASS(6) SHEEP_RADIX_PASS(7) SHEEP_RADIX_PASS(8) SHEEP_RADIX_PASS(9)
+#undef SHEEP_RADIX_PASS
+      default: throw Error(SHEEP_ERR_ARG, "radix sort: bad digit width");
+    }
+    shift += db;
     std::swap(src, dst);
     std::swap(vs, vd);
   }
