@@ -117,7 +117,9 @@ int sheep_ctx_trim(sheep_ctx *ctx) {
   for (auto &kv : c.ws) if (kv.second.p) HIP_CHECK(hipFree(kv.second.p));
   c.ws.clear();
   c.head_layout = sheep::Ctx::HeadLayout();   // its offsets lived in the workspace
-  if (c.kid_spare.parent) { hipFree(c.kid_spare.parent); hipFree(c.kid_spare.koff); hipFree(c.kid_spare.kids); }
+  if (c.kid_spare.parent) {
+    hipFree(c.kid_spare.parent); hipFree(c.kid_spare.koff); hipFree(c.kid_spare.kids); hipFree(c.kid_spare.kpar);
+  }
   c.kid_spare = sheep::Ctx::KidBufs();
   API_END
 }
@@ -130,7 +132,9 @@ int sheep_ctx_destroy(sheep_ctx *ctx) {
   HIP_CHECK(hipSetDevice(c.device));
   HIP_CHECK(hipStreamSynchronize(c.stream));
   for (auto &kv : c.ws) if (kv.second.p) hipFree(kv.second.p);
-  if (c.kid_spare.parent) { hipFree(c.kid_spare.parent); hipFree(c.kid_spare.koff); hipFree(c.kid_spare.kids); }
+  if (c.kid_spare.parent) {
+    hipFree(c.kid_spare.parent); hipFree(c.kid_spare.koff); hipFree(c.kid_spare.kids); hipFree(c.kid_spare.kpar);
+  }
   for (auto &kv : c.pinned) if (kv.second.p) hipHostFree(kv.second.p);
   for (auto &kv : c.timers) for (auto &p : kv.second.pending) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
   for (hipEvent_t e : c.event_pool) hipEventDestroy(e);
@@ -302,7 +306,7 @@ int sheep_kids_create(sheep_ctx *ctx, const sheep_jnode *tree, uint64_t n, sheep
   try {
     sheep::build_kids(ctx->c, tree, n, k);
   } catch (...) {
-    hipFree(k->parent); hipFree(k->koff); hipFree(k->kids);
+    hipFree(k->parent); hipFree(k->koff); hipFree(k->kids); hipFree(k->kpar);
     delete k;
     throw;
   }

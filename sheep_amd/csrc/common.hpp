@@ -86,7 +86,7 @@ struct Ctx {
   // The last destroyed kid table's buffers, taken by the next sheep_kids_create: a
   // partition per tree would otherwise pay three hipMalloc / hipFree pairs of n words
   // (hipFree waits for the device), ~1 ms of idle GPU per step at RMAT-26.
-  struct KidBufs { uint32_t *parent = nullptr, *koff = nullptr, *kids = nullptr; uint64_t cap = 0; };
+  struct KidBufs { uint32_t *parent = nullptr, *koff = nullptr, *kids = nullptr, *kpar = nullptr; uint64_t cap = 0; };
   KidBufs kid_spare;
 
   bool timing = false;

@@ -212,14 +212,44 @@ constexpr int RAKE_ROUNDS = 2;
 constexpr int RAKE_CNT_BITS = 24;
 constexpr uint64_t RAKE_CNT_MASK = (1ull << RAKE_CNT_BITS) - 1;
 
-// round 1's mark fused in: a leaf finishes when its weight is <= max_component
+// round 1's mark fused in: a leaf finishes when its weight is <= max_component.  lw[v] =
+// the push a round-1 leaf makes on its parent (0 for every other node), for k_rake_pull1.
 __global__ void k_rake_init(const uint32_t *__restrict__ koff, const uint64_t *__restrict__ w, uint64_t n, uint64_t maxc,
-                            bool rake, uint64_t *__restrict__ pk, uint8_t *__restrict__ fin) {
+                            bool rake, uint64_t *__restrict__ pk, uint8_t *__restrict__ fin, uint64_t *__restrict__ lw) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride) {
     const uint32_t nk = koff[v + 1] - koff[v];
+    const bool f = rake && nk == 0 && w[v] <= maxc;
     pk[v] = (w[v] << RAKE_CNT_BITS) | nk;
-    fin[v] = rake && nk == 0 && w[v] <= maxc;
+    fin[v] = f;
+    lw[v] = f ? (w[v] << RAKE_CNT_BITS) - 1 : 0;
+  }
+}
+// Round 1 as a PULL over the kid table: kids[i] sits in the list of kpar[i] (lists are
+// contiguous, parents ascending), so a wave sums its lanes' pushes per parent run and
+// adds each run with one atomic — a few neighbouring lines per wave instead of one
+// scattered atomic per leaf (66% of the nodes; ~1.1 ms of pushes at RMAT-26).
+__global__ __launch_bounds__(BLOCK) void k_rake_pull1(const uint32_t *__restrict__ kids, const uint32_t *__restrict__ kpar,
+                                                      uint64_t nkids, const uint64_t *__restrict__ lw,
+                                                      uint64_t *__restrict__ pk) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const uint64_t iters = (nkids + stride - 1) / stride;
+  const int lane = (int)__lane_id();
+  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (uint64_t it = 0; it < iters; ++it, i += stride) {   // wave-uniform trip count (shuffles)
+    const bool live = i < nkids;
+    const uint32_t p = live ? kpar[i] : INVALID;
+    uint64_t x = live ? lw[kids[i]] : 0;
+    // inclusive segmented sum over runs of equal p (runs are contiguous lanes)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o, 64);
+      const uint32_t q = __shfl_up(p, o, 64);
+      if (lane >= o && q == p) x += y;
+    }
+    const uint32_t pn = __shfl_down(p, 1, 64);
+    const bool last = lane == 63 || pn != p;   // the run's last lane holds its sum
+    if (live && last && x) atomicAdd((unsigned long long *)&pk[p], (unsigned long long)x);
   }
 }
 // mark, then push: the two phases keep a round's finished set independent of timing
@@ -693,16 +723,23 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   uint64_t *S = c.get_as<uint64_t>("pt_S", n);   // the rake's packed state, then acc, then every node's subtree sum
   uint8_t *fin = c.get_as<uint8_t>("pt_fin", n);
   const bool rake = k->max_kids <= RAKE_CNT_MASK && total < (1ull << (64 - RAKE_CNT_BITS));
+  uint64_t *lw = c.get_as<uint64_t>("pt_lw", n);
   hipLaunchKernelGGL(k_rake_init, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->koff,
-                     (const uint64_t *)w, n, max_component, rake, S, fin);
+                     (const uint64_t *)w, n, max_component, rake, S, fin, lw);
   LAUNCH_CHECK();
   const int rake_rounds = RAKE_ROUNDS;   // 1 / 2 / 3 measured 9.37 / 8.71 / 8.62 ms of partition at RMAT-26
   for (int r = 1; rake && r <= rake_rounds; ++r) {
-    if (r > 1) {
-      hipLaunchKernelGGL(k_rake_mark, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint64_t *)S, n, max_component,
-                         (uint8_t)r, fin);
-      LAUNCH_CHECK();
+    if (r == 1) {
+      if (k->nkids) {
+        hipLaunchKernelGGL(k_rake_pull1, dim3(grid_for(k->nkids)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->kids,
+                           (const uint32_t *)k->kpar, (uint64_t)k->nkids, (const uint64_t *)lw, S);
+        LAUNCH_CHECK();
+      }
+      continue;
     }
+    hipLaunchKernelGGL(k_rake_mark, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint64_t *)S, n, max_component,
+                       (uint8_t)r, fin);
+    LAUNCH_CHECK();
     hipLaunchKernelGGL(k_rake_push, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->parent,
                        (const uint8_t *)fin, n, (uint8_t)r, S);
     LAUNCH_CHECK();

@@ -225,19 +225,20 @@ void gather_u32(Ctx &c, const uint32_t *src, const uint32_t *idx, uint64_t m, ui
 // buffers are kept), or freed.  The caller has made the context's device current.
 void release_kids(Ctx *c, sheep_kids *k) {
   Ctx::KidBufs *sp = c ? &c->kid_spare : nullptr;
-  if (sp && k->parent && k->koff && k->kids && (!sp->parent || sp->cap < k->cap)) {
+  if (sp && k->parent && k->koff && k->kids && k->kpar && (!sp->parent || sp->cap < k->cap)) {
     if (sp->parent) {
       c->sync();
-      hipFree(sp->parent); hipFree(sp->koff); hipFree(sp->kids);
+      hipFree(sp->parent); hipFree(sp->koff); hipFree(sp->kids); hipFree(sp->kpar);
     }
-    *sp = {k->parent, k->koff, k->kids, k->cap};
+    *sp = {k->parent, k->koff, k->kids, k->kpar, k->cap};
   } else {
     if (c) c->sync();
     hipFree(k->parent);
     hipFree(k->koff);
     hipFree(k->kids);
+    hipFree(k->kpar);
   }
-  k->parent = k->koff = k->kids = nullptr;
+  k->parent = k->koff = k->kids = k->kpar = nullptr;
 }
 
 void build_kids(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_kids *k) {
@@ -245,12 +246,13 @@ void build_kids(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_kids *k) {
   k->n = n;
   Ctx::KidBufs &sp = c.kid_spare;
   if (sp.parent && sp.cap >= n) {   // stream-ordered reuse: the old table's work is queued before ours
-    k->parent = sp.parent; k->koff = sp.koff; k->kids = sp.kids; k->cap = sp.cap;
+    k->parent = sp.parent; k->koff = sp.koff; k->kids = sp.kids; k->kpar = sp.kpar; k->cap = sp.cap;
     sp = Ctx::KidBufs();
   } else {
     HIP_CHECK(hipMalloc(&k->parent, (n + 1) * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&k->koff, (n + 2) * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&k->kids, (n + 1) * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&k->kpar, (n + 1) * sizeof(uint32_t)));
     k->cap = n;
   }
   if (n == 0) { HIP_CHECK(hipMemsetAsync(k->koff, 0, sizeof(uint32_t), c.stream)); return; }
@@ -272,6 +274,7 @@ void build_kids(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_kids *k) {
   // counts -> offsets; total = number of kids
   scan_exclusive_u32(c, k->koff, k->koff, n + 1, (uint32_t *)(d + 1));
   HIP_CHECK(hipMemcpyAsync(k->kids, vals, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
+  HIP_CHECK(hipMemcpyAsync(k->kpar, keys, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
   HIP_CHECK(hipMemcpyAsync(c.h_scalars + 16, d, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
   if (c.h_scalars[16]) throw Error(SHEEP_ERR_RANGE, "tree: parent out of range or not later than its kid");

@@ -9,6 +9,7 @@ struct sheep_kids {
   uint32_t *koff = nullptr;    // n+1 offsets into kids
   uint32_t *kids = nullptr;    // child lists, initially ascending id (jnode.h:190-204);
                                // FFD sorts segments in place (persistent, partition.cpp:104-106)
+  uint32_t *kpar = nullptr;    // kpar[i] = the parent whose list holds kids[i] (the sorted keys)
   uint64_t nkids = 0;
   uint64_t max_kids = 0;       // the largest kid count
   uint64_t cap = 0;            // the buffers hold cap + 2 / cap + 1 words
