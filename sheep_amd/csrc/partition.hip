@@ -252,7 +252,7 @@ __global__ __launch_bounds__(BLOCK) void k_rake_pull1(const uint32_t *__restrict
     if (live && last && x) atomicAdd((unsigned long long *)&pk[p], (unsigned long long)x);
   }
 }
-// mark, then push: the two phases keep a round's finished set independent of timing
+// mark, then pull: the two phases keep a round's finished set independent of timing
 __global__ void k_rake_mark(const uint64_t *__restrict__ pk, uint64_t n, uint64_t maxc, uint8_t round,
                             uint8_t *__restrict__ fin) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
@@ -261,14 +261,33 @@ __global__ void k_rake_mark(const uint64_t *__restrict__ pk, uint64_t n, uint64_
     if (!fin[v] && (x & RAKE_CNT_MASK) == 0 && (x >> RAKE_CNT_BITS) <= maxc) fin[v] = round;
   }
 }
-__global__ void k_rake_push(const uint32_t *__restrict__ parent, const uint8_t *__restrict__ fin, uint64_t n,
-                            uint8_t round, uint64_t *__restrict__ pk) {
+// Round 2 as a pull too, after k_rake_mark: a kid marked 2 pushes its packed sum on its
+// parent (a node marked 2 has no kid marked 2, so its own word is stable here), and every
+// list entry's core flag (kid not finished) is written in list order — the core table's
+// scan input, which k_core_flags built with a second random read of fin per kid.
+__global__ __launch_bounds__(BLOCK) void k_rake_pull2(const uint32_t *__restrict__ kids, const uint32_t *__restrict__ kpar,
+                                                      uint64_t nkids, const uint8_t *__restrict__ fin,
+                                                      uint64_t *__restrict__ pk, uint32_t *__restrict__ flag) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride) {
-    if (fin[v] != round) continue;
-    const uint32_t p = parent[v];
-    if (p == INVALID) continue;
-    atomicAdd((unsigned long long *)&pk[p], (unsigned long long)(((pk[v] >> RAKE_CNT_BITS) << RAKE_CNT_BITS) - 1));
+  const uint64_t iters = (nkids + stride - 1) / stride;
+  const int lane = (int)__lane_id();
+  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (uint64_t it = 0; it < iters; ++it, i += stride) {   // wave-uniform trip count (shuffles)
+    const bool live = i < nkids;
+    const uint32_t p = live ? kpar[i] : INVALID;
+    const uint32_t k = live ? kids[i] : 0;
+    const uint8_t f = live ? fin[k] : 1;
+    if (live) flag[i] = f == 0;
+    uint64_t x = f == 2 ? ((pk[k] >> RAKE_CNT_BITS) << RAKE_CNT_BITS) - 1 : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o, 64);
+      const uint32_t q = __shfl_up(p, o, 64);
+      if (lane >= o && q == p) x += y;
+    }
+    const uint32_t pn = __shfl_down(p, 1, 64);
+    const bool last = lane == 63 || pn != p;
+    if (live && last && x) atomicAdd((unsigned long long *)&pk[p], (unsigned long long)x);
   }
 }
 // acc out of the packed words, in place
@@ -290,9 +309,9 @@ __global__ void k_core_build(const uint32_t *__restrict__ kids, uint64_t nk, con
                              uint32_t *__restrict__ ckoff, uint32_t *__restrict__ cparent) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   const uint64_t t0 = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  for (uint64_t j = t0; j < nk; j += stride) {
-    const uint32_t kid = kids[j];
-    if (!fin[kid]) ckids[pref[j]] = kid;
+  for (uint64_t j = t0; j < nk; j += stride) {   // the scanned core flags: entry j is core iff pref steps
+    const uint32_t pj = pref[j];
+    if (pref[j + 1] != pj) ckids[pj] = kids[j];
   }
   for (uint64_t v = t0; v <= n; v += stride) {
     ckoff[v] = pref[koff[v]];
@@ -727,21 +746,28 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   hipLaunchKernelGGL(k_rake_init, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->koff,
                      (const uint64_t *)w, n, max_component, rake, S, fin, lw);
   LAUNCH_CHECK();
-  const int rake_rounds = RAKE_ROUNDS;   // 1 / 2 / 3 measured 9.37 / 8.71 / 8.62 ms of partition at RMAT-26
-  for (int r = 1; rake && r <= rake_rounds; ++r) {
-    if (r == 1) {
-      if (k->nkids) {
-        hipLaunchKernelGGL(k_rake_pull1, dim3(grid_for(k->nkids)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->kids,
-                           (const uint32_t *)k->kpar, (uint64_t)k->nkids, (const uint64_t *)lw, S);
-        LAUNCH_CHECK();
-      }
-      continue;
+  // two rounds (1 / 2 / 3 measured 9.37 / 8.71 / 8.62 ms of partition at RMAT-26), both
+  // pulls over the kid table; the second also writes the core table's flags
+  static_assert(RAKE_ROUNDS == 2, "round 1 and round 2 pulls");
+  const int rake_rounds = RAKE_ROUNDS;
+  uint32_t *pref = c.get_as<uint32_t>("pt_cpref", k->nkids + 1);
+  if (rake) {
+    if (k->nkids) {
+      hipLaunchKernelGGL(k_rake_pull1, dim3(grid_for(k->nkids)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->kids,
+                         (const uint32_t *)k->kpar, (uint64_t)k->nkids, (const uint64_t *)lw, S);
+      LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(k_rake_mark, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint64_t *)S, n, max_component,
-                       (uint8_t)r, fin);
+                       (uint8_t)2, fin);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_rake_push, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->parent,
-                       (const uint8_t *)fin, n, (uint8_t)r, S);
+    if (k->nkids) {
+      hipLaunchKernelGGL(k_rake_pull2, dim3(grid_for(k->nkids)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->kids,
+                         (const uint32_t *)k->kpar, (uint64_t)k->nkids, (const uint8_t *)fin, S, pref);
+      LAUNCH_CHECK();
+    }
+  } else if (k->nkids) {   // no raking: every kid is core
+    hipLaunchKernelGGL(k_core_flags, dim3(grid_for(k->nkids)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->kids,
+                       k->nkids, (const uint8_t *)fin, pref);
     LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(k_rake_acc, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, S, n);
@@ -753,13 +779,7 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   core.koff = c.get_as<uint32_t>("pt_ckoff", n + 1);
   core.kids = c.get_as<uint32_t>("pt_ckids", k->nkids + 1);
   {
-    uint32_t *pref = c.get_as<uint32_t>("pt_cpref", k->nkids + 1);
     uint32_t *tot = (uint32_t *)(c.d_scalars + 31);
-    if (k->nkids) {
-      hipLaunchKernelGGL(k_core_flags, dim3(grid_for(k->nkids)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->kids,
-                         k->nkids, (const uint8_t *)fin, pref);
-      LAUNCH_CHECK();
-    }
     HIP_CHECK(hipMemsetAsync(pref + k->nkids, 0, sizeof(uint32_t), c.stream));
     scan_exclusive_u32(c, pref, pref, k->nkids + 1, tot);
     hipLaunchKernelGGL(k_core_build, dim3(grid_for(n + 1)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->kids,
