@@ -191,42 +191,42 @@ __global__ __launch_bounds__(HB) void k_hist_scatter(Src src, uint64_t n, uint32
 // LDS together (more than ~4087 buckets, vertex ids above 2^27): the tile's keys are
 // counting-sorted SUB = PER * HB at a time, each bucket's run of a sub-tile written at the
 // bucket's running cursor (the same (bucket, tile) regions as k_hist_scatter).
-template <typename Src, int PER>
-__global__ __launch_bounds__(HB) void k_hist_scatter_staged(Src src, uint64_t n, uint32_t nb,
+template <typename Src, int PER, int NT = HB>
+__global__ __launch_bounds__(NT) void k_hist_scatter_staged(Src src, uint64_t n, uint32_t nb,
                                                             const uint32_t *__restrict__ offsets, uint64_t ntiles,
                                                             uint16_t *__restrict__ out) {
-  constexpr uint32_t SUB = PER * HB;
+  constexpr uint32_t SUB = PER * NT;
   extern __shared__ uint32_t lds[];
   uint32_t *cur = lds, *gb = lds + nb, *wsum = lds + 2 * nb;
-  uint32_t *stage = lds + 2 * nb + HB / WAVE;
+  uint32_t *stage = lds + 2 * nb + NT / WAVE;
   const uint64_t tile = xcd_tile();
-  for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] = offsets[(uint64_t)b * ntiles + tile];
+  for (uint32_t b = threadIdx.x; b < nb; b += NT) gb[b] = offsets[(uint64_t)b * ntiles + tile];
   const uint64_t base = tile << TLOG;
   for (uint32_t s0 = 0; s0 < TKEYS; s0 += SUB) {
-    for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
+    for (uint32_t b = threadIdx.x; b < nb; b += NT) cur[b] = 0;
     lds_barrier();
     uint32_t k[PER], rk[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      const uint64_t i = base + s0 + (uint64_t)j * HB + threadIdx.x;
+      const uint64_t i = base + s0 + (uint64_t)j * NT + threadIdx.x;
       k[j] = i < n ? src(i) : NO_KEY;
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) rk[j] = k[j] != NO_KEY ? atomicAdd(&cur[k[j] >> WBITS], 1u) : 0u;   // rank in bucket
     lds_barrier();
-    const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
-    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] -= cur[b];
+    const uint32_t total = lds_exclusive_scan<NT>(cur, nb, wsum);
+    for (uint32_t b = threadIdx.x; b < nb; b += NT) gb[b] -= cur[b];
     lds_barrier();
 #pragma unroll
     for (int j = 0; j < PER; ++j)
       if (k[j] != NO_KEY) stage[cur[k[j] >> WBITS] + rk[j]] = k[j];
     lds_barrier();
-    for (uint32_t j = threadIdx.x; j < total; j += HB) {
+    for (uint32_t j = threadIdx.x; j < total; j += NT) {
       const uint32_t key = stage[j];
       out[gb[key >> WBITS] + j] = (uint16_t)(key & (W - 1));
     }
     lds_barrier();
-    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += b + 1 < nb ? cur[b + 1] : total;   // past the run
+    for (uint32_t b = threadIdx.x; b < nb; b += NT) gb[b] += b + 1 < nb ? cur[b + 1] : total;   // past the run
     lds_barrier();
   }
 }
@@ -237,25 +237,25 @@ __global__ __launch_bounds__(HB) void k_hist_scatter_staged(Src src, uint64_t n,
 // counting-sorted by bucket in LDS and each bucket's run is written with consecutive
 // lanes (the u16 key beside it); one scattered 8-B store per lane took 15.4 ms at RMAT-26
 // against 9.8.
-template <int PER>
-__global__ __launch_bounds__(HB) void k_lo_scatter_staged(EdgeLoPadded src, uint64_t n, uint32_t nb,
+template <int PER, int NT = HB>
+__global__ __launch_bounds__(NT) void k_lo_scatter_staged(EdgeLoPadded src, uint64_t n, uint32_t nb,
                                                           const uint32_t *__restrict__ offsets, uint64_t ntiles,
                                                           uint16_t *__restrict__ out, uint64_t *__restrict__ grouped) {
-  constexpr uint32_t SUB = PER * HB;
+  constexpr uint32_t SUB = PER * NT;
   extern __shared__ uint32_t lds[];
   uint32_t *cur = lds, *gb = lds + nb, *wsum = lds + 2 * nb;
-  uint64_t *stage = (uint64_t *)(lds + ((2 * nb + HB / WAVE + 1) & ~1u));
+  uint64_t *stage = (uint64_t *)(lds + ((2 * nb + NT / WAVE + 1) & ~1u));
   const uint64_t tile = xcd_tile();
-  for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] = offsets[(uint64_t)b * ntiles + tile];
+  for (uint32_t b = threadIdx.x; b < nb; b += NT) gb[b] = offsets[(uint64_t)b * ntiles + tile];
   const uint64_t base = tile << TLOG;
   for (uint32_t s0 = 0; s0 < TKEYS; s0 += SUB) {
-    for (uint32_t b = threadIdx.x; b < nb; b += HB) cur[b] = 0;
+    for (uint32_t b = threadIdx.x; b < nb; b += NT) cur[b] = 0;
     lds_barrier();
     uint64_t e[PER];
     uint32_t k[PER], rk[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      const uint64_t i = base + s0 + (uint64_t)j * HB + threadIdx.x;
+      const uint64_t i = base + s0 + (uint64_t)j * NT + threadIdx.x;
       e[j] = i < n ? src.edges[i] : ~0ull;
     }
 #pragma unroll
@@ -264,21 +264,21 @@ __global__ __launch_bounds__(HB) void k_lo_scatter_staged(EdgeLoPadded src, uint
       rk[j] = k[j] != NO_KEY ? atomicAdd(&cur[k[j] >> WBITS], 1u) : 0u;   // rank in bucket
     }
     lds_barrier();
-    const uint32_t total = lds_exclusive_scan(cur, nb, wsum);
-    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] -= cur[b];
+    const uint32_t total = lds_exclusive_scan<NT>(cur, nb, wsum);
+    for (uint32_t b = threadIdx.x; b < nb; b += NT) gb[b] -= cur[b];
     lds_barrier();
 #pragma unroll
     for (int j = 0; j < PER; ++j)
       if (k[j] != NO_KEY) stage[cur[k[j] >> WBITS] + rk[j]] = e[j];
     lds_barrier();
-    for (uint32_t j = threadIdx.x; j < total; j += HB) {
+    for (uint32_t j = threadIdx.x; j < total; j += NT) {
       const uint64_t v = stage[j];
       const uint32_t key = src.key(v), dst = gb[key >> WBITS] + j;
       grouped[dst] = v;
       out[dst] = (uint16_t)(key & (W - 1));
     }
     lds_barrier();
-    for (uint32_t b = threadIdx.x; b < nb; b += HB) gb[b] += b + 1 < nb ? cur[b + 1] : total;   // past the run
+    for (uint32_t b = threadIdx.x; b < nb; b += NT) gb[b] += b + 1 < nb ? cur[b + 1] : total;   // past the run
     lds_barrier();
   }
 }
@@ -398,6 +398,25 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
     HIP_CHECK(hipMemcpyAsync(save_offsets, tile_hist, ntiles * nb * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
     HIP_CHECK(hipMemcpyAsync(save_offsets + ntiles * nb, total, sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
   }
+#ifdef SHEEP_EXP_H512
+  if constexpr (std::is_same<Src, EdgeLoPadded>::value) {
+    const size_t l512 = ((2 * (size_t)nb + 512 / WAVE + 1) & ~(size_t)1) * 4 + 16 * 512 * 8;
+    if (nb <= 8 * 512 && l512 <= 160 * 1024) {
+      allow_full_lds((const void *)k_lo_scatter_staged<16, 512>);
+      hipLaunchKernelGGL((k_lo_scatter_staged<16, 512>), dim3((unsigned)ntiles), dim3(512), l512, c.stream, src, n, nb,
+                         (const uint32_t *)tile_hist, ntiles, keys, grouped);
+      goto scattered;
+    }
+  } else {
+    const size_t l512 = (2 * (size_t)nb + 512 / WAVE + 16 * 512) * 4;
+    if (nb <= 8 * 512 && l512 <= 160 * 1024) {
+      allow_full_lds((const void *)k_hist_scatter_staged<Src, 16, 512>);
+      hipLaunchKernelGGL((k_hist_scatter_staged<Src, 16, 512>), dim3((unsigned)ntiles), dim3(512), l512, c.stream, src, n,
+                         nb, (const uint32_t *)tile_hist, ntiles, keys);
+      goto scattered;
+    }
+  }
+#endif
   if constexpr (std::is_same<Src, EdgeLoPadded>::value) {
     if (lds_staged16 <= 160 * 1024)
       hipLaunchKernelGGL(k_lo_scatter_staged<16>, dim3((unsigned)ntiles), dim3(HB), lds_staged16, c.stream, src, n, nb,
@@ -412,6 +431,9 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
     hipLaunchKernelGGL((k_hist_scatter_staged<Src, 16>), dim3((unsigned)ntiles), dim3(HB), lds_scatter16, c.stream, src, n,
                        nb, (const uint32_t *)tile_hist, ntiles, keys);
   }
+#ifdef SHEEP_EXP_H512
+scattered:
+#endif
   LAUNCH_CHECK();
   // bucket starts (column 0 of the bucket-major offsets) -> chunk list.  Host buffers are
   // pinned, so the chunk list's copy needs no sync of its own (the next call's first sync
