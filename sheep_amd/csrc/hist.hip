@@ -398,25 +398,6 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
     HIP_CHECK(hipMemcpyAsync(save_offsets, tile_hist, ntiles * nb * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
     HIP_CHECK(hipMemcpyAsync(save_offsets + ntiles * nb, total, sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
   }
-#ifdef SHEEP_EXP_H512
-  if constexpr (std::is_same<Src, EdgeLoPadded>::value) {
-    const size_t l512 = ((2 * (size_t)nb + 512 / WAVE + 1) & ~(size_t)1) * 4 + 16 * 512 * 8;
-    if (nb <= 8 * 512 && l512 <= 160 * 1024) {
-      allow_full_lds((const void *)k_lo_scatter_staged<16, 512>);
-      hipLaunchKernelGGL((k_lo_scatter_staged<16, 512>), dim3((unsigned)ntiles), dim3(512), l512, c.stream, src, n, nb,
-                         (const uint32_t *)tile_hist, ntiles, keys, grouped);
-      goto scattered;
-    }
-  } else {
-    const size_t l512 = (2 * (size_t)nb + 512 / WAVE + 16 * 512) * 4;
-    if (nb <= 8 * 512 && l512 <= 160 * 1024) {
-      allow_full_lds((const void *)k_hist_scatter_staged<Src, 16, 512>);
-      hipLaunchKernelGGL((k_hist_scatter_staged<Src, 16, 512>), dim3((unsigned)ntiles), dim3(512), l512, c.stream, src, n,
-                         nb, (const uint32_t *)tile_hist, ntiles, keys);
-      goto scattered;
-    }
-  }
-#endif
   if constexpr (std::is_same<Src, EdgeLoPadded>::value) {
     if (lds_staged16 <= 160 * 1024)
       hipLaunchKernelGGL(k_lo_scatter_staged<16>, dim3((unsigned)ntiles), dim3(HB), lds_staged16, c.stream, src, n, nb,
@@ -431,9 +412,6 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
     hipLaunchKernelGGL((k_hist_scatter_staged<Src, 16>), dim3((unsigned)ntiles), dim3(HB), lds_scatter16, c.stream, src, n,
                        nb, (const uint32_t *)tile_hist, ntiles, keys);
   }
-#ifdef SHEEP_EXP_H512
-scattered:
-#endif
   LAUNCH_CHECK();
   // bucket starts (column 0 of the bucket-major offsets) -> chunk list.  Host buffers are
   // pinned, so the chunk list's copy needs no sync of its own (the next call's first sync
