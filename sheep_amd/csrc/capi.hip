@@ -103,6 +103,7 @@ int sheep_ctx_create(int device, void *hip_stream, sheep_ctx **out) {
   }
   HIP_CHECK(hipHostMalloc((void **)&x->c.h_scalars, sheep::Ctx::NSCALARS * sizeof(uint64_t), hipHostMallocDefault));
   HIP_CHECK(hipMalloc((void **)&x->c.d_scalars, sheep::Ctx::NSCALARS * sizeof(uint64_t)));
+  HIP_CHECK(hipMemset(x->c.d_scalars, 0, sheep::Ctx::NSCALARS * sizeof(uint64_t)));
   *out = x;
   API_END
 }

@@ -73,7 +73,8 @@ struct Ctx {
 
   uint64_t *h_scalars = nullptr;   // pinned host mirror
   uint64_t *d_scalars = nullptr;   // device scalars (counters / flags)
-  static constexpr int NSCALARS = 64;
+  static constexpr int NSCALARS = 72;
+  static constexpr int SCAN_TICKET = 64;   // d_scalars word of the scans' last-block ticket (zero between scans)
 
   // Bucket layout of the last degree_count's head histogram (LLAMA mode): the scanned
   // (bucket, tile) offsets live in ws["head_offsets"]; relabel_bucketed reuses them when

@@ -30,11 +30,16 @@ template <typename T> __device__ __forceinline__ T block_exclusive_scan(T v, T *
   return wave_off + inc - v;
 }
 
-// n_dev (optional): the length is read on the device (at most n; the grid is sized for n)
+// n_dev (optional): the length is read on the device (at most n; the grid is sized for n).
+// fold (one-level scans, gridDim <= SCAN_TILE): the block sums go out by atomic exchange
+// and the LAST block to finish (a ticket, reset by that block) scans them in place, so
+// the scan is two launches instead of three.  Sums and ticket are read-modify-write
+// atomics, performed coherently however the blocks spread over the XCDs.
 template <typename T>
 __global__ __launch_bounds__(BLOCK) void k_reduce(const T *__restrict__ in, uint64_t n, T *__restrict__ sums,
-                                                  const uint64_t *__restrict__ n_dev) {
+                                                  const uint64_t *__restrict__ n_dev, unsigned *__restrict__ ticket) {
   __shared__ T lds[BLOCK / WAVE];
+  __shared__ bool s_last;
   if (n_dev && *n_dev < n) n = *n_dev;
   uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
   T s = 0;
@@ -46,11 +51,38 @@ __global__ __launch_bounds__(BLOCK) void k_reduce(const T *__restrict__ in, uint
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = s;
   lds_barrier();
+  if (!ticket) {
+    if (threadIdx.x == 0) {
+      T t = 0;
+      for (int w = 0; w < BLOCK / WAVE; ++w) t += lds[w];
+      sums[blockIdx.x] = t;
+    }
+    return;
+  }
+  __shared__ T s_old;
   if (threadIdx.x == 0) {
     T t = 0;
     for (int w = 0; w < BLOCK / WAVE; ++w) t += lds[w];
-    sums[blockIdx.x] = t;
+    s_old = atomicExch(&sums[blockIdx.x], t);   // consumed below: the sum has landed before the ticket
   }
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1u) + (unsigned)(s_old & 0) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x == 0) atomicExch(ticket, 0u);   // ready for the next scan
+  // exclusive scan of the gridDim.x sums, SCAN_ITEMS per thread
+  const uint32_t nb = gridDim.x, b0 = threadIdx.x * SCAN_ITEMS;
+  T v[SCAN_ITEMS], tsum = 0;
+#pragma unroll
+  for (int q = 0; q < SCAN_ITEMS; ++q) {
+    v[q] = b0 + q < nb ? atomicAdd(&sums[b0 + q], T(0)) : T(0);
+    tsum += v[q];
+  }
+  T total;
+  T run = block_exclusive_scan(tsum, lds, total);
+#pragma unroll
+  for (int q = 0; q < SCAN_ITEMS; ++q)
+    if (b0 + q < nb) { sums[b0 + q] = run; run += v[q]; }
 }
 
 template <typename T>
@@ -98,9 +130,16 @@ void scan_rec(Ctx &c, const T *in, T *out, uint64_t n, T *total_dev, int depth, 
   T *sums = nullptr;
   if (nb > 1) {
     sums = c.get_as<T>("scan_sums_" + std::to_string(depth) + (sizeof(T) == 8 ? "_64" : "_32"), nb);
-    hipLaunchKernelGGL(k_reduce<T>, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, in, n, sums, n_dev);
-    LAUNCH_CHECK();
-    scan_rec<T>(c, sums, sums, nb, nullptr, depth + 1);
+    if (nb <= (uint64_t)SCAN_TILE) {   // one level: the last block scans the sums
+      unsigned *ticket = (unsigned *)(c.d_scalars + Ctx::SCAN_TICKET);
+      hipLaunchKernelGGL(k_reduce<T>, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, in, n, sums, n_dev, ticket);
+      LAUNCH_CHECK();
+    } else {
+      hipLaunchKernelGGL(k_reduce<T>, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, in, n, sums, n_dev,
+                         (unsigned *)nullptr);
+      LAUNCH_CHECK();
+      scan_rec<T>(c, sums, sums, nb, nullptr, depth + 1);
+    }
   }
   hipLaunchKernelGGL(k_apply<T>, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, in, out, n,
                      (const T *)sums, total_dev, n_dev);
