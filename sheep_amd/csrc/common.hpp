@@ -347,10 +347,12 @@ void scan_exclusive_u64(Ctx &c, const uint64_t *in, uint64_t *out, uint64_t n, u
 // the first *n_dev (<= n_max) entries, the length read on the device (launch sized for n_max)
 void scan_exclusive_u64_dev(Ctx &c, const uint64_t *in, uint64_t *out, uint64_t n_max, const uint64_t *n_dev);
 // radix.hip — stable LSD sort of (key, value) pairs on bits [0, end_bit); results end
-// in (keys, vals); alt buffers are scratch of the same size.
+// in (keys, vals); alt buffers are scratch of the same size.  With in_alt, a result left
+// in the alt buffers (an odd number of passes) stays there and *in_alt says so (no copy).
 void radix_sort_pairs_u32(Ctx &c, uint32_t *keys, uint32_t *vals, uint64_t n, int end_bit,
-                          uint32_t *keys_alt, uint32_t *vals_alt);
-void radix_sort_keys_u64(Ctx &c, uint64_t *keys, uint64_t n, int end_bit, uint64_t *keys_alt);
+                          uint32_t *keys_alt, uint32_t *vals_alt, bool *in_alt = nullptr);
+void radix_sort_keys_u64(Ctx &c, uint64_t *keys, uint64_t n, int end_bit, uint64_t *keys_alt,
+                         bool *in_alt = nullptr);
 // hist.hip — cnt[key] += occurrences, keys bucketed through LDS (no scattered atomics)
 void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt,
                      bool counted = false);

@@ -1171,7 +1171,9 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     const uint64_t nf = c.h_scalars[15];
     if (nf) {
       // L + 1 bits: hi < 2^L, and DEAD (all ones) sorts after every edge
-      radix_sort_keys_u64(c, fin, nf, L + 1, fin_alt);
+      bool in_alt = false;
+      radix_sort_keys_u64(c, fin, nf, L + 1, fin_alt, &in_alt);
+      if (in_alt) std::swap(fin, fin_alt);
       const uint64_t nb = L > FINB ? 1ull << (L - FINB) : 1;
       uint64_t *eb = c.get_as<uint64_t>("et_fin_eb", nb + 1);
       uint32_t *vb = c.get_as<uint32_t>("et_fin_vb", nb + 1);

@@ -144,7 +144,8 @@ void radix_pass(Ctx &c, const K *src, const uint32_t *vs, K *dst, uint32_t *vd, 
 }
 
 template <typename K, bool VALS>
-void radix_sort_impl(Ctx &c, K *keys, uint32_t *vals, uint64_t n, int end_bit, K *kalt, uint32_t *valt) {
+void radix_sort_impl(Ctx &c, K *keys, uint32_t *vals, uint64_t n, int end_bit, K *kalt, uint32_t *valt, bool *in_alt) {
+  if (in_alt) *in_alt = false;
   if (n <= 1 || end_bit <= 0) return;
   if (n >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "radix sort: n >= 2^32");
   uint32_t ntiles = (uint32_t)((n + R_TILE - 1) / R_TILE);
@@ -166,7 +167,9 @@ void radix_sort_impl(Ctx &c, K *keys, uint32_t *vals, uint64_t n, int end_bit, K
     std::swap(src, dst);
     std::swap(vs, vd);
   }
-  if (src != keys) {
+  if (src != keys && in_alt) {   // the caller reads the alternate buffers
+    *in_alt = true;
+  } else if (src != keys) {
     HIP_CHECK(hipMemcpyAsync(keys, src, n * sizeof(K), hipMemcpyDeviceToDevice, c.stream));
     if (VALS) HIP_CHECK(hipMemcpyAsync(vals, vs, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
   }
@@ -175,11 +178,11 @@ void radix_sort_impl(Ctx &c, K *keys, uint32_t *vals, uint64_t n, int end_bit, K
 }  // namespace
 
 void radix_sort_pairs_u32(Ctx &c, uint32_t *keys, uint32_t *vals, uint64_t n, int end_bit,
-                          uint32_t *keys_alt, uint32_t *vals_alt) {
-  radix_sort_impl<uint32_t, true>(c, keys, vals, n, end_bit, keys_alt, vals_alt);
+                          uint32_t *keys_alt, uint32_t *vals_alt, bool *in_alt) {
+  radix_sort_impl<uint32_t, true>(c, keys, vals, n, end_bit, keys_alt, vals_alt, in_alt);
 }
-void radix_sort_keys_u64(Ctx &c, uint64_t *keys, uint64_t n, int end_bit, uint64_t *keys_alt) {
-  radix_sort_impl<uint64_t, false>(c, keys, nullptr, n, end_bit, keys_alt, nullptr);
+void radix_sort_keys_u64(Ctx &c, uint64_t *keys, uint64_t n, int end_bit, uint64_t *keys_alt, bool *in_alt) {
+  radix_sort_impl<uint64_t, false>(c, keys, nullptr, n, end_bit, keys_alt, nullptr, in_alt);
 }
 
 }  // namespace sheep

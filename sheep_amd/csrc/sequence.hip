@@ -207,7 +207,10 @@ uint64_t sequence_from_degrees(Ctx &c, const uint32_t *deg, uint64_t vs, uint32_
   LAUNCH_CHECK();
   int bits = 0;
   while (bits < 32 && (maxdeg >> bits)) ++bits;
-  radix_sort_pairs_u32(c, keys, seq, n, bits, kalt, valt);
+  bool in_alt = false;
+  radix_sort_pairs_u32(c, keys, seq, n, bits, kalt, valt, &in_alt);
+  if (in_alt)   // the sorted vids are in valt: only they go back (the degree keys are not needed)
+    HIP_CHECK(hipMemcpyAsync(seq, valt, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
   hipLaunchKernelGGL(k_scatter_pos, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, seq, n, pos);
   LAUNCH_CHECK();
   return n;

@@ -257,8 +257,10 @@ void build_kids(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_kids *k) {
   }
   if (n == 0) { HIP_CHECK(hipMemsetAsync(k->koff, 0, sizeof(uint32_t), c.stream)); return; }
   TimedRegion tr(c, "kids", 8 * n + 12 * n);   // tree read; parent copy, offsets, kid ids written
+  // the table's own kpar / kids serve as the sort's alternate buffers: with an odd number of
+  // passes (1 or 3: up to 2^9 or 2^27 nodes) the sorted pairs end there, with no copy
   uint32_t *keys = c.get_as<uint32_t>("kid_keys", n), *vals = c.get_as<uint32_t>("kid_vals", n);
-  uint32_t *kalt = c.get_as<uint32_t>("kid_kalt", n), *valt = c.get_as<uint32_t>("kid_valt", n);
+  uint32_t *kalt = k->kpar, *valt = k->kids;
   HIP_CHECK(hipMemsetAsync(k->koff, 0, (n + 1) * sizeof(uint32_t), c.stream));
   unsigned long long *d = (unsigned long long *)c.d_scalars + 16;
   HIP_CHECK(hipMemsetAsync(d, 0, 3 * sizeof(uint64_t), c.stream));
@@ -266,15 +268,19 @@ void build_kids(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_kids *k) {
   LAUNCH_CHECK();
   int bits = 0;
   while (bits < 32 && (n >> bits)) ++bits;
-  radix_sort_pairs_u32(c, keys, vals, n, bits, kalt, valt);   // stable: kids ascending per parent
+  bool in_alt = false;
+  radix_sort_pairs_u32(c, keys, vals, n, bits, kalt, valt, &in_alt);   // stable: kids ascending per parent
+  if (!in_alt) {   // an even number of passes: the sorted pairs are in keys / vals
+    HIP_CHECK(hipMemcpyAsync(k->kids, vals, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
+    HIP_CHECK(hipMemcpyAsync(k->kpar, keys, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
+  }
+  keys = k->kpar;
   hipLaunchKernelGGL(k_kid_counts, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)keys, n, k->koff);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_max_u32, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->koff, n, d + 2);
   LAUNCH_CHECK();   // the largest kid count (the partition's packed rake state needs it < 2^24)
   // counts -> offsets; total = number of kids
   scan_exclusive_u32(c, k->koff, k->koff, n + 1, (uint32_t *)(d + 1));
-  HIP_CHECK(hipMemcpyAsync(k->kids, vals, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
-  HIP_CHECK(hipMemcpyAsync(k->kpar, keys, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
   HIP_CHECK(hipMemcpyAsync(c.h_scalars + 16, d, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
   if (c.h_scalars[16]) throw Error(SHEEP_ERR_RANGE, "tree: parent out of range or not later than its kid");
