@@ -253,9 +253,11 @@ def main():
     ctx.timing(False)
 
     verified = None
+    checks = {}
     if a.verify and (world > 1 or a.shards > 1):
         if rank == 0:
-            verified = verify_tree(a, seed, ctx, shard, subs, s, tree, stack[0], world)
+            checks = verify_tree(a, seed, ctx, shard, subs, s, tree, stack[0], world)
+            verified = all(checks.values())
             if not verified:
                 print("bench: merged tree differs from its cross-check", file=sys.stderr, flush=True)
         if world > 1:
@@ -310,8 +312,7 @@ def main():
             "evaluator": evaluator,
             "phases": phases,
         }
-        if verified is not None:
-            out["verified_vs_whole_graph" if world > 1 or R < (1 << 32) else "verified_vs_pairwise_merges"] = verified
+        out.update(checks)   # verified_vs_whole_graph / verified_vs_pairwise_merges: the checks that ran
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a, ctx)
     del shard
@@ -326,11 +327,12 @@ def main():
 
 
 def verify_tree(a, seed, ctx, shard, subs, s, tree, stacked, world):
-    """After the timed steps, rank 0 checks the reduced tree.  N ranks: against the
-    whole graph's tree built on rank 0 alone.  One GPU with --shards: against the whole
-    graph's tree when its workspace fits the device (about 72 B per record: C5's 4.24 G
-    records do not), and always against the binomial pairwise merges (mpi_merge's
-    schedule, jnode.cpp:203-250) of the same shard trees."""
+    """After the timed steps, rank 0 checks the reduced tree; returns {check: passed} for
+    the checks that ran.  N ranks: against the whole graph's tree built on rank 0 alone.
+    One GPU with --shards: against the whole graph's tree when its workspace fits the
+    device (about 72 B per record: C5's 4.24 G records do not), and always against the
+    binomial pairwise merges (mpi_merge's schedule, jnode.cpp:203-250) of the same shard
+    trees."""
     import torch
     import sheep_amd
     if world > 1:
@@ -340,12 +342,12 @@ def verify_tree(a, seed, ctx, shard, subs, s, tree, stacked, world):
         ok = bool(torch.equal(whole, tree))
         del whole
         torch.cuda.empty_cache()
-        return ok
-    ok = True
+        return {"verified_vs_whole_graph": ok}
+    checks = {}
     ctx.trim()
     torch.cuda.empty_cache()
     if shard.shape[0] < (1 << 32) and shard.shape[0] * 72 < torch.cuda.mem_get_info()[0]:
-        ok = bool(torch.equal(sheep_amd.build_tree(shard, s, ctx=ctx), tree))
+        checks["verified_vs_whole_graph"] = bool(torch.equal(sheep_amd.build_tree(shard, s, ctx=ctx), tree))
     cur = [stacked[i] for i in range(len(subs))]
     d = 1
     while d < len(cur):
@@ -353,7 +355,8 @@ def verify_tree(a, seed, ctx, shard, subs, s, tree, stacked, world):
             if i + d < len(cur):
                 cur[i] = sheep_amd.merge_trees(cur[i], cur[i + d], ctx=ctx)
         d *= 2
-    return ok and bool(torch.equal(cur[0], tree))
+    checks["verified_vs_pairwise_merges"] = bool(torch.equal(cur[0], tree))
+    return checks
 
 
 def time_evaluator(a, ctx, group, shard, subs, s, res, rank, world, dev, barrier):
