@@ -166,7 +166,13 @@ def main():
     torch.cuda.set_device(local)
     seed = (a.scale if a.graph == "rmat" else 2010) if a.seed is None else a.seed
     group = None
+    json_out = sys.stdout
     if world > 1:
+        # stdout carries rank 0's JSON line only: the launcher's and gloo's banners and every
+        # other rank's output go to stderr (the saved descriptor keeps rank 0's line)
+        sys.stdout.flush()
+        json_out = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
         # torch.distributed (gloo, host) is the control plane only: the rendezvous port,
         # barriers and the max over ranks of the wall time.  The data path is the world of
         # include/sheep_hip.h (sheep_group_join, group.hip): RCCL over xGMI between the
@@ -190,17 +196,28 @@ def main():
     subs = [shard[i * shard.shape[0] // a.shards:(i + 1) * shard.shape[0] // a.shards] for i in range(a.shards)]
     stack = [None]
     bufs = {}
+    walls = {}   # N ranks: this rank's host wall time per part of the step (the group calls return complete)
+
+    def lap(name, t0):
+        t1 = time.perf_counter()
+        walls[name] = walls.get(name, 0.0) + (t1 - t0)
+        return t1
 
     def step():
         deg.zero_()
         if group is not None:                                   # graph2tree -i -r over the world
+            t0 = time.perf_counter()
             if "seq" not in bufs:
                 bufs["seq"] = torch.empty(vs_cap, dtype=torch.int32, device=dev)
                 bufs["pos"] = torch.empty(vs_cap, dtype=torch.int32, device=dev)
             s = group.sequence([shard], vs_cap, deg=[deg], seq=[bufs["seq"]], pos=[bufs["pos"]])[0]
+            t0 = lap("sequence", t0)                            # incl. the wait for the slowest rank
             if "tree" not in bufs or bufs["tree"].shape[0] < s.n:
                 bufs["tree"] = torch.empty((max(s.n, 1), 2), dtype=torch.int32, device=dev)
-            tree = group.build_tree([shard], [s], a.reduce, trees=[bufs["tree"]])[0]
+            tree = group.build_tree([shard], [s], "none", trees=[bufs["tree"]])[0]
+            t0 = lap("map", t0)
+            tree = group.reduce_trees([bufs["tree"][:s.n]], a.reduce)[0]
+            t0 = lap("reduce", t0)                              # gather + merge on rank 0, the send elsewhere
         else:
             vs = 0
             for sub in subs:                                    # shards accumulate into one histogram
@@ -217,9 +234,13 @@ def main():
                 tree = sheep_amd.build_tree(shard, s, ctx=ctx)
         res = None
         if rank == 0:                                           # graph2tree.cpp:203-208
+            t0 = time.perf_counter()
             kids = sheep_amd.KidTable(tree, ctx)
             res = sheep_amd.partition(s, tree, a.k, kids=kids, ctx=ctx)
             kids.close()
+            if group is not None:
+                ctx.sync()
+                lap("kids_partition", t0)
         return s, tree, res
 
     def barrier():
@@ -233,6 +254,7 @@ def main():
     barrier()
     ctx.timing(True)
     ctx.timer_reset()
+    walls.clear()
     barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -246,6 +268,12 @@ def main():
         ms, launches, nbytes = ctx.timer(name)
         phases[name] = {"ms_per_step": round(ms / a.steps, 4), "launches": launches, "alg_bytes": nbytes}
     ctx.timer_reset()
+    per_rank = None
+    if world > 1:   # every rank's split of the step, for diagnosing the N-rank run (rank 0 reports)
+        mine = {"rank": rank, "wall_ms_per_step": {k: round(1e3 * v / a.steps, 3) for k, v in walls.items()},
+                "device_ms_per_step": {k: phases[k]["ms_per_step"] for k in ("gather", "merge", "etree", "relabel")
+                                       if k in phases}}
+        per_rank = sdist.gather_objects(mine)
 
     evaluator = None
     if a.eval_reps > 0:
@@ -312,6 +340,8 @@ def main():
             "evaluator": evaluator,
             "phases": phases,
         }
+        if per_rank is not None:
+            out["per_rank"] = per_rank
         out.update(checks)   # verified_vs_whole_graph / verified_vs_pairwise_merges: the checks that ran
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a, ctx)
@@ -321,7 +351,7 @@ def main():
         group.close()
         sdist.shutdown()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if verified is False:
         sys.exit(1)
 

@@ -245,7 +245,9 @@ int sheep_edge_parts(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec, co
  * ncclCommInitRank with rank 0's id sent over the TCP links; xGMI), by device copies when
  * one process lists a device twice, and through host memory over the TCP links when
  * processes share a device (a one-GPU rehearsal).  `link` forces the choice for a joined
- * world (SHEEP_LINK_RCCL fails when two ranks share a device).
+ * world (SHEEP_LINK_RCCL fails when two ranks share a device; a world of ONE with
+ * SHEEP_LINK_RCCL opens a one-rank communicator, so every collective below and a self
+ * send/recv run through RCCL on one GPU).
  * Per-rank array arguments (rec_dev[i], deg_dev[i], ...) are indexed by the LOCAL ranks of
  * the calling process (sheep_group_local_count of them; local i is global rank
  * sheep_group_rank(g, i)) and live on that rank's device.  Every call is collective: all
@@ -265,7 +267,11 @@ int sheep_edge_parts(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec, co
  *   sheep_group_evaluate        Partition::evaluate over the shards: per-rank part bitsets,
  *                               binomial OR-reduction, the node pass on rank 0 (*out is
  *                               zero on the other ranks)
- *   sheep_group_barrier / sheep_group_allreduce_max_u64   MPI_Barrier / MPI_Allreduce(MAX) */
+ *   sheep_group_barrier / sheep_group_allreduce_max_u64   MPI_Barrier / MPI_Allreduce(MAX)
+ *   sheep_group_transfer        one point-to-point move of `bytes` from rank `from`'s src to
+ *                               rank `to`'s dst (ncclSend/ncclRecv in one group under RCCL; the
+ *                               hop of mpi_merge's MPI_Reduce, jnode.cpp:238-241); src / dst
+ *                               matter only where that rank is local */
 typedef struct sheep_group sheep_group;
 #define SHEEP_LINK_AUTO 0
 #define SHEEP_LINK_RCCL 1
@@ -289,6 +295,7 @@ int sheep_group_build_tree(sheep_group *g, const sheep_xs1 *const *rec_dev, cons
 /* the reduction step alone (tree_dev[r] = rank r's partial tree; reduce 1 or 2 as above) */
 int sheep_group_reduce_trees(sheep_group *g, sheep_jnode *const *tree_dev, uint64_t n, int reduce);
 int sheep_group_broadcast_parts(sheep_group *g, int16_t *const *parts_vid_dev, uint64_t pos_size);
+int sheep_group_transfer(sheep_group *g, int from, int to, const void *src_dev, void *dst_dev, uint64_t bytes);
 int sheep_device_count(int *out);
 int sheep_group_evaluate(sheep_group *g, const sheep_xs1 *const *rec_dev, const uint64_t *nrec,
                          const uint32_t *const *pos_dev, uint64_t pos_size,

@@ -124,6 +124,7 @@ def lib() -> ctypes.CDLL:
         "sheep_group_sequence": ([P, P, P, P, U64, P, P, ctypes.POINTER(U64), ctypes.POINTER(U64)], I32),
         "sheep_group_build_tree": ([P, P, P, P, U64, U64, P, I32], I32),
         "sheep_group_broadcast_parts": ([P, P, U64], I32),
+        "sheep_group_transfer": ([P, I32, I32, P, P, U64], I32),
         "sheep_group_evaluate": ([P, P, P, P, U64, P, I32, ctypes.POINTER(_Eval)], I32),
         "sheep_parse_net": ([P, P, U64, I32, P, U64, ctypes.POINTER(U64)], I32),
         "sheep_powerlaw_generate": ([P, U64, U64, D, U64, P, U64, ctypes.POINTER(U64)], I32),
@@ -284,7 +285,9 @@ def degree_sequence(records, mode: str = "llama", vs_cap: int | None = None, ctx
         if nrec:
             ends = records[:, :2]
             lo, hi = int(ends.min().item()), int(ends.max().item())
-            vs_cap = (0xFFFFFFFF if lo < 0 else hi) + 1
+            # ids >= 2^31 read negative: the u32 maximum is then the largest negative one
+            # (only those are copied out), not 2^32 - 1
+            vs_cap = ((int(ends[ends < 0].max().item()) & 0xFFFFFFFF) if lo < 0 else hi) + 1
         else:
             vs_cap = 1
     deg = t.zeros(max(vs_cap, 1), dtype=t.int32, device=_dev(ctx))
@@ -691,6 +694,18 @@ class Group:
         self._ready()
         _check(lib().sheep_group_broadcast_parts(self.handle, _ptr_array(parts), pos_size))
         return [p[:pos_size] for p in parts]
+
+    def transfer(self, src_rank: int, dst_rank: int, src=None, dst=None, nbytes: int | None = None):
+        """One point-to-point move (ncclSend/ncclRecv under RCCL) of src_rank's tensor
+        `src` into dst_rank's tensor `dst`; every rank of the world calls it."""
+        if nbytes is None:
+            t = src if src is not None else dst
+            nbytes = t.numel() * t.element_size()
+        self._ready()
+        _check(lib().sheep_group_transfer(self.handle, int(src_rank), int(dst_rank),
+                                          ctypes.c_void_p(_ptr(src) if src is not None else 0),
+                                          ctypes.c_void_p(_ptr(dst) if dst is not None else 0), int(nbytes)))
+        return dst
 
     def evaluate(self, shards, seqs, parts, what: int = 0) -> "EvalResult":
         """The evaluator over the shards; the counts are rank 0's (zero elsewhere)."""

@@ -1018,6 +1018,19 @@ __global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t 
   }
 }
 
+// Debug statistic (SHEEP_DEBUG_ETREE): live entries per block of 2^s spread positions
+// after a level (its next list plus the groups not yet activated).
+__global__ void k_dbg_blocks(const uint64_t *__restrict__ a, const uint64_t *__restrict__ st, const uint64_t *__restrict__ b,
+                             uint64_t nb_edges, int s, uint32_t clo, unsigned *__restrict__ cnt) {
+  const uint64_t na = st[ST_KEPT] + st[ST_CONTR];
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na + nb_edges; i += stride) {
+    const uint64_t e = i < na ? a[i] : b[i - na];
+    if (e == DEAD) continue;
+    atomicAdd(&cnt[spread((uint32_t)e, clo) >> s], 1u);
+  }
+}
+
 }  // namespace
 
 void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
@@ -1141,6 +1154,35 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
                          alt, cset(CSET_APPLY), parent, g);
       LAUNCH_CHECK();
       pack_shards<uint64_t>(c, alt, next, st + ST_NX, cset(CSET_APPLY), st + ST_CONTR, nullptr, nullptr, st + ST_KEPT);
+    }
+    if (g_debug_etree && s >= 8 && s <= 15) {   // how the live edges spread over the 2^s blocks
+      uint64_t hs[2] = {0, 0};
+      if (s > 0) {
+        HIP_CHECK(hipMemcpyAsync(&hs[0], seg + (s - 1), sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipMemcpyAsync(&hs[1], seg + L, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+      }
+      const uint64_t nblk = (1ull << L) >> s;
+      unsigned *cnt = c.get_as<unsigned>("et_dbg_blocks", nblk);
+      HIP_CHECK(hipMemsetAsync(cnt, 0, nblk * sizeof(unsigned), c.stream));
+      c.sync();
+      hipLaunchKernelGGL(k_dbg_blocks, dim3(1024), dim3(BLOCK), 0, c.stream, (const uint64_t *)next, (const uint64_t *)st,
+                         r0 + hs[0], hs[1] - hs[0], s, clo, cnt);
+      LAUNCH_CHECK();
+      std::vector<unsigned> h(nblk);
+      HIP_CHECK(hipMemcpyAsync(h.data(), cnt, nblk * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
+      c.sync();
+      std::sort(h.begin(), h.end());
+      uint64_t tot = 0, ne = 0, over[5] = {0, 0, 0, 0, 0};
+      const uint64_t caps[5] = {4096, 8192, 16384, 32768, 65536};
+      for (unsigned x : h) {
+        tot += x;
+        ne += x > 0;
+        for (int k = 0; k < 5; ++k) if (x > caps[k]) over[k] += x;
+      }
+      fprintf(stderr, "etree blocks after s %d (2^%d positions): edges %lu blocks %lu nonempty %lu max %u p99 %u p90 %u | edges in blocks > 4K %lu 8K %lu 16K %lu 32K %lu 64K %lu\n",
+              s, s, (unsigned long)tot, (unsigned long)nblk, (unsigned long)ne, h.back(), h[(size_t)(nblk * 0.99)],
+              h[(size_t)(nblk * 0.9)], (unsigned long)over[0], (unsigned long)over[1], (unsigned long)over[2],
+              (unsigned long)over[3], (unsigned long)over[4]);
     }
   }
   if (nglobal) {   // the last level's clean (the others ran in the next level's split)

@@ -204,8 +204,8 @@ void transfer(sheep_group *g, const std::vector<Xfer> &xs) {
 // In-place sum of one u32 array per rank (the degree all-reduce); buf[li] per local rank.
 void allreduce_sum_u32(sheep_group *g, uint32_t *const *buf, uint64_t count) {
   const int P = g->world;
-  if (P == 1 || count == 0) return;
-  if (!g->comm.empty()) {
+  if (count == 0) return;
+  if (!g->comm.empty()) {   // (also a world of one that asked for RCCL: the identity, through RCCL)
     sync_all(g);
     NCCL_CHECK(ncclGroupStart());
     for (int i = 0; i < nlocal(g); ++i)
@@ -214,6 +214,7 @@ void allreduce_sum_u32(sheep_group *g, uint32_t *const *buf, uint64_t count) {
     sync_all(g);
     return;
   }
+  if (P == 1) return;
   // reduce to rank 0, one rank at a time into a scratch array, then broadcast
   const int l0 = local_of(g, 0);
   uint32_t *tmp = nullptr;
@@ -242,7 +243,7 @@ void allreduce_sum_u32(sheep_group *g, uint32_t *const *buf, uint64_t count) {
 // rank 0's bytes to every rank; buf[li] per local rank
 void broadcast(sheep_group *g, void *const *buf, size_t bytes) {
   const int P = g->world;
-  if (P == 1 || bytes == 0) return;
+  if (bytes == 0) return;
   if (!g->comm.empty()) {
     sync_all(g);
     NCCL_CHECK(ncclGroupStart());
@@ -252,6 +253,7 @@ void broadcast(sheep_group *g, void *const *buf, size_t bytes) {
     sync_all(g);
     return;
   }
+  if (P == 1) return;
   const int l0 = local_of(g, 0);
   std::vector<Xfer> xs;
   for (int r = 1; r < P; ++r) {
@@ -354,7 +356,10 @@ int sheep_group_join(int device, int rank, int world, const char *host, int port
       for (int q = 0; q < r; ++q) distinct &= bus[q] != bus[r];
     if (link == SHEEP_LINK_RCCL && !distinct)
       throw sheep::Error(SHEEP_ERR_ARG, "RCCL needs every rank on its own device (two ranks share one)");
-    if (world > 1 && (link == SHEEP_LINK_RCCL || (link == SHEEP_LINK_AUTO && distinct))) {
+    // RCCL when asked for (a world of one included: every collective and a self send/recv
+    // then run through RCCL, the one-GPU check of this transport) or, by default, when
+    // every rank has a device of its own
+    if (link == SHEEP_LINK_RCCL || (world > 1 && link == SHEEP_LINK_AUTO && distinct)) {
       ncclUniqueId id;
       if (rank == 0) NCCL_CHECK(ncclGetUniqueId(&id));
       g->mesh->bcast(&id, sizeof id);
@@ -446,7 +451,20 @@ int sheep_group_reduce_trees(sheep_group *g, sheep_jnode *const *tree, uint64_t 
       const int lr = sheep::local_of(g, r);
       xs.push_back(sheep::Xfer{r, 0, lr >= 0 ? tree[lr] : nullptr, stack ? stack + (uint64_t)r * n : nullptr, tb});
     }
-    sheep::transfer(g, xs);
+    {
+      // the gather as a timed region of every local rank's context ("gather": send on the
+      // others, receive on rank 0; the host link's copies fall inside the events too)
+      std::vector<std::unique_ptr<sheep::TimedRegion>> tr;
+      for (int i = 0; i < sheep::nlocal(g); ++i) {
+        HIP_CHECK(hipSetDevice(g->dev[i]));
+        tr.emplace_back(new sheep::TimedRegion(sheep::C(g, i), "gather", tb));
+      }
+      sheep::transfer(g, xs);
+      for (int i = 0; i < sheep::nlocal(g); ++i) {
+        HIP_CHECK(hipSetDevice(g->dev[i]));
+        tr[i].reset();
+      }
+    }
     if (l0 >= 0) {
       HIP_CHECK(hipSetDevice(g->dev[l0]));
       sheep::merge_trees_many(sheep::C(g, l0), stack, (uint32_t)P, n, tree[l0]);
@@ -494,6 +512,16 @@ int sheep_group_build_tree(sheep_group *g, const sheep_xs1 *const *rec, const ui
   });
   const int rc = sheep_group_reduce_trees(g, tree, n, reduce);
   if (rc != SHEEP_OK) return rc;
+  GAPI_END
+}
+
+int sheep_group_transfer(sheep_group *g, int from, int to, const void *src, void *dst, uint64_t bytes) {
+  DeviceRestore dr;
+  GAPI_BEGIN
+  GNEED(g && from >= 0 && from < g->world && to >= 0 && to < g->world, "bad argument");
+  const int lf = sheep::local_of(g, from), lt = sheep::local_of(g, to);
+  GNEED((lf < 0 || src) && (lt < 0 || dst), "null buffer on a local rank");
+  sheep::transfer(g, {sheep::Xfer{from, to, src, dst, (size_t)bytes}});
   GAPI_END
 }
 

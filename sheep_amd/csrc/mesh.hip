@@ -90,7 +90,7 @@ int listen_on(const sockaddr_in &a, int backlog) {
   return fd;
 }
 
-int accept_within(int lfd, std::chrono::steady_clock::time_point until) {
+int accept_within(int lfd, std::chrono::steady_clock::time_point until, in_addr *peer = nullptr) {
   for (;;) {
     const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(until - std::chrono::steady_clock::now());
     if (left.count() <= 0) { errno = 0; fail("timed out waiting for the other ranks"); }
@@ -98,8 +98,11 @@ int accept_within(int lfd, std::chrono::steady_clock::time_point until) {
     const int r = poll(&p, 1, (int)std::min<long long>(left.count(), 1000));
     if (r < 0 && errno != EINTR) fail("poll");
     if (r <= 0) continue;
-    const int fd = accept(lfd, nullptr, nullptr);
+    sockaddr_in from{};
+    socklen_t len = sizeof from;
+    const int fd = accept(lfd, (sockaddr *)&from, &len);
     if (fd < 0) { if (errno == EINTR) continue; fail("accept"); }
+    if (peer) *peer = from.sin_addr;
     tune(fd);
     return fd;
   }
@@ -128,21 +131,26 @@ Mesh::Mesh(int rank, int world, const std::string &host, int port, const std::st
   if (world == 1) return;
   const auto until = std::chrono::steady_clock::now() + std::chrono::seconds(timeout_s);
   const sockaddr_in root = resolve(host, port);
-  std::vector<uint32_t> ports(world, 0);
+  // every rank's listening port and address: rank 0 learns a rank's address from its
+  // accepted connection (the address the other ranks can reach it at, whichever host it
+  // runs on) and relays the table
+  std::vector<uint32_t> ports(world, 0), addrs(world, root.sin_addr.s_addr);
   int own = -1;
   try {
     if (rank == 0) {                                   // star: everyone reports to rank 0
       own = listen_on(root, world);
       for (int i = 1; i < world; ++i) {
-        const int fd = accept_within(own, until);
+        in_addr from{};
+        const int fd = accept_within(own, until, &from);
         const uint32_t r = get_u32(fd);
         if (r == 0 || r >= (uint32_t)world || fd_[r] >= 0) { close(fd); errno = 0; fail("bad or repeated rank"); }
         fd_[r] = fd;
         ports[r] = get_u32(fd);
+        addrs[r] = from.s_addr;
         bus_[r] = get_str(fd);
       }
       for (int r = 1; r < world; ++r) {
-        for (int q = 0; q < world; ++q) { put_u32(fd_[r], ports[q]); put_str(fd_[r], bus_[q]); }
+        for (int q = 0; q < world; ++q) { put_u32(fd_[r], ports[q]); put_u32(fd_[r], addrs[q]); put_str(fd_[r], bus_[q]); }
       }
     } else {
       sockaddr_in any{};
@@ -157,9 +165,10 @@ Mesh::Mesh(int rank, int world, const std::string &host, int port, const std::st
       put_u32(fd_[0], (uint32_t)rank);
       put_u32(fd_[0], ntohs(me.sin_port));
       put_str(fd_[0], bus_id);
-      for (int q = 0; q < world; ++q) { ports[q] = get_u32(fd_[0]); bus_[q] = get_str(fd_[0]); }
+      for (int q = 0; q < world; ++q) { ports[q] = get_u32(fd_[0]); addrs[q] = get_u32(fd_[0]); bus_[q] = get_str(fd_[0]); }
       for (int i = 1; i < rank; ++i) {                 // j connects to every 0 < i < j ...
         sockaddr_in a = root;
+        a.sin_addr.s_addr = addrs[i];
         a.sin_port = htons((uint16_t)ports[i]);
         fd_[i] = connect_within(a, until);
         put_u32(fd_[i], (uint32_t)rank);

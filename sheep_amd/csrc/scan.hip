@@ -59,14 +59,16 @@ __global__ __launch_bounds__(BLOCK) void k_reduce(const T *__restrict__ in, uint
     }
     return;
   }
-  __shared__ T s_old;
   if (threadIdx.x == 0) {
     T t = 0;
     for (int w = 0; w < BLOCK / WAVE; ++w) t += lds[w];
-    s_old = atomicExch(&sums[blockIdx.x], t);   // consumed below: the sum has landed before the ticket
+    (void)atomicExch(&sums[blockIdx.x], t);
+    // the block sum is visible device-wide before the ticket: a release fence, and the
+    // ticket add itself a release at agent scope; the last block's reads of the sums are
+    // atomics (performed coherently, after its acquire below)
+    __threadfence();
+    s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1u) + (unsigned)(s_old & 0) == gridDim.x - 1;
   __syncthreads();
   if (!s_last) return;
   if (threadIdx.x == 0) atomicExch(ticket, 0u);   // ready for the next scan

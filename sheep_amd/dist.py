@@ -9,7 +9,8 @@ reduce and the parts broadcast — and uses torch.distributed over gloo (host TC
                      MASTER_ADDR / MASTER_PORT);
   * shared_port    — a free TCP port chosen by rank 0 for sheep_group_join's rendezvous;
   * barrier        — MPI_Barrier around the timed region;
-  * max_over_ranks — the wall time of the slowest rank (bench.py's contract).
+  * max_over_ranks — the wall time of the slowest rank (bench.py's contract);
+  * gather_objects — every rank's timing split, collected on rank 0.
 """
 from __future__ import annotations
 
@@ -47,6 +48,13 @@ def max_over_ranks(t: float) -> float:
     x = torch.tensor([float(t)], dtype=torch.float64)
     dist.all_reduce(x, op=dist.ReduceOp.MAX)
     return float(x.item())
+
+
+def gather_objects(obj):
+    """Rank 0 gets the list of every rank's `obj` (in rank order); the others get None."""
+    out = [None] * dist.get_world_size() if dist.get_rank() == 0 else None
+    dist.gather_object(obj, out, dst=0)
+    return out
 
 
 def shutdown() -> None:

@@ -429,6 +429,38 @@ def test_group_rehearsal_matches_single_gpu(gpu_ctx, ranks):
     g.close()
 
 
+def test_rccl_world_of_one(gpu_ctx):
+    """The RCCL transport on the one-GPU box: a joined world of ONE with link=rccl forced
+    opens a one-rank communicator (ncclGetUniqueId + ncclCommInitRank), and then the
+    degree ncclAllReduce (mpiSequence, sequence.h:72,78), the parts ncclBroadcast
+    (mpi_sync, partition.cpp:69-79) and a grouped self ncclSend/ncclRecv of a tree (the hop
+    of mpi_merge's MPI_Reduce, jnode.cpp:238-241) all run through RCCL.  Each result equals
+    the host-link world's and the single-GPU path's."""
+    import torch
+    import sheep_amd
+    d = sheep_amd.rmat(16, 16, 16)
+    s = sheep_amd.degree_sequence(d)
+    whole = sheep_amd.build_tree(d, s)
+    res = sheep_amd.partition(s, whole, 32)
+    ev = sheep_amd.evaluate(d, s, res.parts)
+    out = {}
+    for link in ("rccl", "host"):
+        g = sheep_amd.Group.join(0, 0, 1, link=link)
+        assert g.rccl == (link == "rccl"), link
+        seqs = g.sequence([d], 1 << 16)
+        assert seqs[0].n == s.n and torch.equal(seqs[0].seq[: s.n], s.seq[: s.n]), link
+        tree = g.build_tree([d], seqs, "kway")[0]
+        assert torch.equal(tree, whole), link
+        got = torch.full_like(whole, -1)
+        g.transfer(0, 0, whole, got)
+        assert torch.equal(got, whole), link
+        parts = g.broadcast_parts([res.parts.clone()], s.pos_size)
+        assert torch.equal(parts[0], res.parts), link
+        out[link] = g.evaluate([d], seqs, parts)
+        g.close()
+    assert out["rccl"] == out["host"] == ev
+
+
 @pytest.mark.parametrize("ranks", [2, 3])
 def test_group_join_processes_match_single_gpu(gpu_ctx, tmp_path, ranks):
     """sheep_group_join: `ranks` PROCESSES, one rank each (the mpiexec / torch.distributed

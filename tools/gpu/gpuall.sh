@@ -7,8 +7,8 @@ mkdir -p gpurun_out && export HSA_ENABLE_IPC_MODE_LEGACY=0 && export TMPDIR=/tmp
 HB=$!
 trap 'kill $HB' EXIT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit 1
-W=26 K=64 bash gpuprof.sh || exit 1
-W=22 K=16 bash gpuprof.sh || exit 1
+W=26 K=64 bash tools/gpu/gpuprof.sh || exit 1
+W=22 K=16 bash tools/gpu/gpuprof.sh || exit 1
 timeout -k 10 400 python -u bench.py --graph powerlaw --k 128 --steps 3 > gpurun_out/bench_c4.json 2> gpurun_out/bench_c4.err || exit 1
 timeout -k 10 600 python -u bench.py --scale 28 --k 256 --shards 8 --steps 2 --warmup 1 --no-cpu-baseline --eval-reps 1 > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err || exit 1
 timeout -k 10 400 python -u bench.py --shuffle --steps 5 --no-cpu-baseline > gpurun_out/bench_r26_shuffled.json 2> gpurun_out/bench_r26s.err || exit 1

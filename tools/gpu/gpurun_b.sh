@@ -5,4 +5,4 @@ HB=$!
 trap 'kill $HB' EXIT
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
   > gpurun_out/gpu_tests.log 2>&1 || exit 1
-SCALES="22 26" bash gpuprobe.sh
+SCALES="22 26" bash tools/gpu/gpuprobe.sh

@@ -8,5 +8,5 @@ HB=$!
 trap 'kill $HB' EXIT
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --durations 30 --timeout 300 --timeout-method thread \
   > gpurun_out/gpu_tests.log 2>&1 || exit 1
-W=26 K=64 bash gpuprof.sh || exit 1
-W=22 K=16 bash gpuprof.sh
+W=26 K=64 bash tools/gpu/gpuprof.sh || exit 1
+W=22 K=16 bash tools/gpu/gpuprof.sh
