@@ -67,10 +67,12 @@ def parse():
     ap.add_argument("--eval-reps", type=int, default=3, help="timed evaluator runs (0: skip)")
     ap.add_argument("--cpu-scale", type=int, default=None,
                     help="RMAT scale of the CPU-baseline sample (default: the bench's own RMAT scale up to 26, else 22)")
-    ap.add_argument("--cpu-ranks", type=int, nargs="+", default=[8, 16],
-                    help="MPI rank counts of the reference CPU baseline (capped by the host cores this process may "
-                         "use, os.sched_getaffinity); the best is reported.  More ranks only add merge hops on "
-                         "rank 0: at RMAT-26, P = 16 / 32 / 64 ran 28 / 71 / 172 s (profiles/r3)")
+    ap.add_argument("--cpu-configs", nargs="+", default=["8x1", "16x1", "16x16"],
+                    help="PxT configurations of the reference CPU baseline: P MPI ranks x T OpenMP threads each "
+                         "(the threads serve the reference's __gnu_parallel::sort, sequence.h:55,85); P x T is capped "
+                         "by the host cores this process may use (os.sched_getaffinity) and the best is reported.  "
+                         "More ranks only add merge hops on rank 0: at RMAT-26, P = 16 / 32 / 64 ran 28 / 71 / 172 s "
+                         "(profiles/r3); the wider sweep is tools/cpu_sweep.py (profiles/r4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on cuda:0: rehearse N ranks on a 1-GPU box (the world's host link over TCP "
@@ -503,10 +505,11 @@ def cpu_baseline(a, ctx):
     (graph2tree -l semantics, untimed), then mpiSequence's degree all-reduce with
     degreeSequence's sort, JTree on the shard (map), JNodeTable::mpi_merge (the custom-op
     MPI_Reduce), makeKids + Partition(k) + mpi_sync on rank 0.  The timed region starts at
-    a barrier after the load.  P runs over --cpu-ranks, capped by the cores this process
-    may run on (os.sched_getaffinity); the fastest P is the value.  The literal `-ir` is
-    not used: its sort copies the whole degree vector per comparison (sequence.h:85,
-    BASELINE.md §2).  Test infrastructure timed as a baseline; never the measured path."""
+    a barrier after the load.  (P ranks, T OpenMP threads each) runs over --cpu-configs,
+    P x T capped by the cores this process may run on (os.sched_getaffinity); the fastest
+    is the value and `cores` = its P x T.  The literal `-ir` is not used: its sort copies
+    the whole degree vector with every comparator copy (sequence.h:85; its box record is
+    profiles/r4/cpu_ir_literal.json, tools/cpu_ir.py).  Test infrastructure timed as a baseline; never the measured path."""
     import shutil
     import subprocess
     import tempfile
@@ -518,7 +521,13 @@ def cpu_baseline(a, ctx):
     if not os.path.exists(harness) or not mpiexec:
         return {"value": None, "unit": "edges/s", "cores": 0, "kind": "reference",
                 "sample": "oracle/_ref/ref_harness or mpiexec missing on this host"}
-    ranks = sorted({max(1, min(p, usable or 1)) for p in a.cpu_ranks})
+    configs = []
+    for c in a.cpu_configs:
+        p, t = (int(x) for x in str(c).split("x"))
+        p = max(1, min(p, usable or 1))
+        t = max(1, min(t, (usable or 1) // p))
+        if (p, t) not in configs:
+            configs.append((p, t))
     runs = []
     with tempfile.TemporaryDirectory(dir="/tmp") as td:
         path = os.path.join(td, f"rmat{sc}.dat")
@@ -530,27 +539,29 @@ def cpu_baseline(a, ctx):
                 f.write(sheep_amd.to_numpy_u32(d[b:b + step]).tobytes())
         del d
         ctx.sync()
-        env = dict(os.environ, OMP_NUM_THREADS="1")
-        for p in ranks:
+        for p, th in configs:
+            env = dict(os.environ, OMP_NUM_THREADS=str(th))
             r = subprocess.run([mpiexec, "-n", str(p), harness, "mpi", path, str(a.k)], capture_output=True,
                                text=True, timeout=900, env=env)
             if r.returncode != 0:
-                runs.append({"ranks": p, "error": r.stderr.strip()[-300:]})
+                runs.append({"ranks": p, "threads": th, "error": r.stderr.strip()[-300:]})
                 continue
             res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-            runs.append({"ranks": p, "seconds": round(res["seconds"], 3), "edges_per_s": round(R / res["seconds"], 1),
+            runs.append({"ranks": p, "threads": th, "seconds": round(res["seconds"], 3),
+                         "edges_per_s": round(R / res["seconds"], 1),
                          "phases_s": {k: round(v, 3) for k, v in res.get("phases", {}).items()}})
-            print(f"cpu_baseline: {p} ranks {res['seconds']:.2f} s", file=sys.stderr, flush=True)
+            print(f"cpu_baseline: {p} ranks x {th} threads {res['seconds']:.2f} s", file=sys.stderr, flush=True)
     ok = [x for x in runs if "seconds" in x]
     if not ok:
         return {"value": None, "unit": "edges/s", "cores": 0, "kind": "reference", "sample": f"failed: {runs}"}
     best = min(ok, key=lambda x: x["seconds"])
-    return {"value": best["edges_per_s"], "unit": "edges/s", "cores": best["ranks"], "kind": "reference",
-            "cpu_model": model, "host_cpus": ncpu, "usable_cpus": usable,
+    return {"value": best["edges_per_s"], "unit": "edges/s", "cores": best["ranks"] * best["threads"],
+            "kind": "reference", "cpu_model": model, "host_cpus": ncpu, "usable_cpus": usable,
             "sample": f"RMAT-{sc} ef{a.ef} seed {sc} ({R} records), k={a.k}: reference lib/ graph2tree -r -p flow "
                       f"(mpiSequence all-reduce + degreeSequence sort, JTree per shard, JNodeTable::mpi_merge, "
-                      f"makeKids + Partition + mpi_sync) on P MPI ranks x 1 thread, P in {ranks} (best P="
-                      f"{best['ranks']}, {best['seconds']:.2f} s), shards loaded untimed",
+                      f"makeKids + Partition + mpi_sync) on P MPI ranks x T OpenMP threads, PxT in "
+                      f"{['%dx%d' % c for c in configs]} (best {best['ranks']}x{best['threads']}, "
+                      f"{best['seconds']:.2f} s), shards loaded untimed",
             "phases_s": best["phases_s"], "sweep": runs}
 
 

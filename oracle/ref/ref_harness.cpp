@@ -26,6 +26,8 @@
 #include "partition.h"
 #include "sequence.h"
 
+#include <omp.h>
+
 #include <chrono>
 #include <cstdio>
 #include <fstream>
@@ -143,6 +145,7 @@ static int usage() {
           "ref_harness writefile G SEQ|- TREE k PREFIX    Partition + file-based writePartitionedGraph\n"
           "ref_harness time G k                           seconds for degreeSequence + JTree + Partition(k)\n"
           "mpiexec -n P ref_harness mpi G k              graph2tree -r -p k over P MPI ranks (timed)\n"
+          "mpiexec -n P ref_harness mpi_ir G k           the same with the literal -i mpiSequence (sequence.h:85)\n"
           "ref_harness snap FILE                          SNAPReader::read pairs, one \"X Y\" per line\n");
   return 1;
 }
@@ -217,7 +220,12 @@ int main(int argc, char **argv) {
            (size_t)g.getEdges(), seq.size(), part.parts.size());
     return 0;
   }
-  if (cmd == "mpi" && argc == 4) {   // bench.py cpu_baseline: graph2tree.cpp:134-216 (-i -r -p k)
+  // bench.py cpu_baseline: graph2tree.cpp:134-216 (-i -r -p k).  "mpi_ir" is the literal
+  // -ir: the reference's own mpiSequence (sequence.h:65-93), whose sort comparator captures
+  // the degree vector BY VALUE (sequence.h:85); "mpi" sorts the same all-reduced degrees
+  // with degreeSequence's by-reference comparator (sequence.h:52-63).
+  if ((cmd == "mpi" || cmd == "mpi_ir") && argc == 4) {
+    const bool literal = cmd == "mpi_ir";
     MPI_Init(nullptr, nullptr);
     int rank = 0, size = 1;
     MPI_Comm_rank(MPI_COMM_WORLD, &rank);
@@ -229,12 +237,17 @@ int main(int argc, char **argv) {
     // sort is degreeSequence's (by-reference comparator) over the summed degrees -- the
     // by-value capture at sequence.h:85 copies the degree vector per comparison and does
     // not finish at these sizes
-    vid_t max_vid = 0, local_max = g.getMaxVid();
-    MPI_Allreduce(&local_max, &max_vid, 1, MPI_UINT32_T, MPI_MAX, MPI_COMM_WORLD);
-    std::vector<esize_t> degree(max_vid + 1), local_degree(max_vid + 1, 0);
-    for (auto nitr = g.getNodeItr(); !nitr.isEnd(); ++nitr) local_degree[*nitr] = g.getDeg(*nitr);
-    MPI_Allreduce(local_degree.data(), degree.data(), max_vid, MPI_UINT32_T, MPI_SUM, MPI_COMM_WORLD);
-    std::vector<vid_t> seq = degreeSequence(DegreeGraph(degree));
+    std::vector<vid_t> seq;
+    if (literal) {
+      seq = mpiSequence(g);
+    } else {
+      vid_t max_vid = 0, local_max = g.getMaxVid();
+      MPI_Allreduce(&local_max, &max_vid, 1, MPI_UINT32_T, MPI_MAX, MPI_COMM_WORLD);
+      std::vector<esize_t> degree(max_vid + 1), local_degree(max_vid + 1, 0);
+      for (auto nitr = g.getNodeItr(); !nitr.isEnd(); ++nitr) local_degree[*nitr] = g.getDeg(*nitr);
+      MPI_Allreduce(local_degree.data(), degree.data(), max_vid, MPI_UINT32_T, MPI_SUM, MPI_COMM_WORLD);
+      seq = degreeSequence(DegreeGraph(degree));
+    }
     auto const t1 = std::chrono::steady_clock::now();
     JTree tree(g, seq);                                   // map (graph2tree.cpp:185-189)
     auto const t2 = std::chrono::steady_clock::now();
@@ -249,9 +262,10 @@ int main(int argc, char **argv) {
       return std::chrono::duration<double>(b - a).count();
     };
     if (rank == 0)
-      printf("{\"seconds\": %.6f, \"ranks\": %d, \"nodes\": %zu, \"phases\": {\"sort\": %.6f, \"map\": %.6f, "
-             "\"reduce\": %.6f, \"partition\": %.6f}}\n", sec(t0, t4), size, seq.size(), sec(t0, t1), sec(t1, t2),
-             sec(t2, t3), sec(t3, t4));
+      printf("{\"seconds\": %.6f, \"ranks\": %d, \"threads\": %d, \"nodes\": %zu, \"sequence\": \"%s\", "
+             "\"phases\": {\"sort\": %.6f, \"map\": %.6f, \"reduce\": %.6f, \"partition\": %.6f}}\n",
+             sec(t0, t4), size, omp_get_max_threads(), seq.size(), literal ? "mpiSequence" : "degreeSequence",
+             sec(t0, t1), sec(t1, t2), sec(t2, t3), sec(t3, t4));
     MPI_Finalize();
     return 0;
   }

@@ -51,15 +51,18 @@ inline unsigned grid_for(uint64_t items, unsigned per_block = BLOCK, unsigned ca
 
 // Raises a kernel's dynamic-LDS limit to the gfx950 CU's 160 KiB, once per (kernel,
 // device): the attribute belongs to the device that is current when it is set.
-inline void allow_full_lds(const void *kernel) {
+// allow_lds: the same for a kernel that also has static LDS (the limit is then the dynamic
+// part it launches with: static + dynamic <= 160 KiB).
+inline void allow_lds(const void *kernel, int bytes) {
   static std::mutex m;
   static std::set<std::pair<const void *, int>> done;
   int dev = 0;
   HIP_CHECK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> g(m);
   if (done.insert({kernel, dev}).second)
-    HIP_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
 }
+inline void allow_full_lds(const void *kernel) { allow_lds(kernel, 160 * 1024); }
 
 // Per-context state: device, stream, grow-only named workspaces, pinned scalars, timers.
 struct Ctx {
@@ -357,7 +360,11 @@ void radix_sort_keys_u64(Ctx &c, uint64_t *keys, uint64_t n, int end_bit, uint64
 void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt,
                      bool counted = false);
 // both endpoints (every tail, and the heads as above) for records in no particular order
-void histogram_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt);
+void histogram_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt,
+                         bool counted = false);
+// records in any order: the degree pass with both endpoints' bucket counts (hist.hip)
+bool degree_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap,
+                      unsigned long long *d_max, unsigned long long *d_err);
 // the degree pass fused with the heads' bucket counts; false (nothing launched) when the
 // capacity does not fit the bucket layout
 bool degree_fused(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap,
@@ -388,9 +395,11 @@ void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGroup 
                        uint64_t *seg, bool counted);
 // etree.hip
 // filt_lvl >= 0: at that level only entries with spread(lo) in [ylo, yhi) are kept (one
-// subproblem of a split merge; the caller cuts the later groups to it)
+// subproblem of a split merge; the caller cuts the later groups to it).  top_bits > 0: the
+// block of the 2^top_bits highest positions is replaced by its minimum spanning forest when
+// dense (maps; etree.hip "the dense top block").
 void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
-                      int fin_bits, int filt_lvl = -1, uint32_t ylo = 0, uint32_t yhi = 0);
+                      int fin_bits, int filt_lvl = -1, uint32_t ylo = 0, uint32_t yhi = 0, int top_bits = 0);
 void spread_params(uint64_t n, int *L, uint32_t *clo);
 // append.hip — sharded appends: counters (NSHARD * SHARD_STRIDE u64, zeroed).  The pack
 // step moves the shard regions of a producer that streamed *n_in items together in dst

@@ -197,6 +197,10 @@ __global__ __launch_bounds__(BLOCK) void k_relabel(const sheep_xs1 *__restrict__
 // level's bucket.
 constexpr int ST_ROW = 16, ST_LIVE = 0, ST_NL = 1, ST_NX = 2, ST_KEPT = 3, ST_CONTR = 4, ST_HOOK = 5, ST_R0 = 10,
               ST_SCANN = 11;
+// [12] the top block's MSF edges appended after the contractions, [13] the cut (the next
+// split drops the list entries with spread(lo) >= cut ahead of them), [14] the tile count
+// of the top block's list extraction (the dense top block, below)
+constexpr int ST_EXTRA = 12, ST_CUT = 13, ST_TOPNT = 14;
 // One deferred round, then the in-place finish (swept: 0 / 1 / 2 / 3 rounds = union 8.4 /
 // 6.3 / 6.6 / 6.7 ms at RMAT-26; 1 also best on the Chung-Lu graph, RMAT-28 and merges):
 // the first round clears the pile-up on a forming giant component's root, and what is
@@ -627,19 +631,30 @@ __device__ __forceinline__ uint32_t classify(uint64_t e, int s, uint32_t clo, YR
   return ((yb >> s) & 1) == 0 ? 3 : 1;           // light (bit 1: light, bit 0: stays) / right
 }
 
-// The level's virtual input: the list (prev level's kept entries + contraction slots),
-// then the bucket of edges first active at this level.
+// The level's virtual input: the list (prev level's kept entries + contraction slots,
+// then the top block's MSF edges when the previous level cut it), then the bucket of edges
+// first active at this level (none below gcut: the groups of a cut top block).  After a
+// cut, the list entries inside the top block (spread(lo) >= cut, ahead of the MSF edges)
+// read as dead.
 struct SplitIn {
   const uint64_t *list, *r0;
-  uint64_t len, rb, m;
-  __device__ SplitIn(const uint64_t *l, const uint64_t *prev, const uint64_t *r, const uint64_t *seg, int s, int L)
-      : list(l), r0(r) {
-    len = prev ? prev[ST_KEPT] + prev[ST_CONTR] : 0;
+  uint64_t len, base, rb, m;
+  uint32_t cut, clo;
+  __device__ SplitIn(const uint64_t *l, const uint64_t *prev, const uint64_t *r, const uint64_t *seg, int s, int L,
+                     int gcut, uint32_t c)
+      : list(l), r0(r), clo(c) {
+    base = prev ? prev[ST_KEPT] + prev[ST_CONTR] : 0;
+    len = prev ? base + prev[ST_EXTRA] : 0;
+    cut = prev ? (uint32_t)prev[ST_CUT] : 0;
     rb = seg[s];
-    m = len + (seg[L + s] - rb);
+    m = len + (s < gcut ? 0 : seg[L + s] - rb);
   }
   __device__ __forceinline__ uint64_t operator[](uint64_t i) const {
-    return i < len ? list[i] : i < m ? r0[rb + (i - len)] : DEAD;
+    if (i < len) {
+      const uint64_t e = list[i];
+      return (cut && i < base && e != DEAD && spread((uint32_t)e, clo) >= cut) ? DEAD : e;
+    }
+    return i < m ? r0[rb + (i - len)] : DEAD;
   }
 };
 
@@ -657,12 +672,12 @@ __device__ __forceinline__ uint64_t pack3(uint32_t c) {
 __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
                                                        uint64_t *__restrict__ st, int s, uint32_t clo, YRange yr,
                                                        const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
-                                                       int L, uint64_t *__restrict__ cnt, LevelClean clean) {
+                                                       int L, int gcut, uint64_t *__restrict__ cnt, LevelClean clean) {
   // the three count rows at stride ntiles (this level's), then one 0: scanned as one
   // exclusive scan of 3 ntiles + 1 entries (the length in st, read by the scan).
   // clean: the previous level's k_level_clean, run first (clean.st == nullptr: none).
   if (clean.st) level_clean(clean);
-  const SplitIn in(list, prev, r0, seg, s, L);
+  const SplitIn in(list, prev, r0, seg, s, L, gcut, clo);
   const uint64_t ntiles = (in.m + SPLIT_TILE - 1) / SPLIT_TILE, cstride = ntiles;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st[ST_LIVE] = in.len;
@@ -697,10 +712,10 @@ __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restric
 __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
                                                        uint64_t *__restrict__ st, int s, uint32_t clo, YRange yr,
                                                        const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
-                                                       int L, const uint64_t *__restrict__ cnt,
+                                                       int L, int gcut, const uint64_t *__restrict__ cnt,
                                                        uint64_t *__restrict__ next, uint64_t *__restrict__ lbuf,
                                                        uint64_t *__restrict__ xbuf) {
-  const SplitIn in(list, prev, r0, seg, s, L);
+  const SplitIn in(list, prev, r0, seg, s, L, gcut, clo);
   const uint64_t ntiles = (in.m + SPLIT_TILE - 1) / SPLIT_TILE, cstride = ntiles;
   const uint64_t b0 = cnt[0], b1 = cnt[cstride], b2 = cnt[2 * cstride], b3 = cnt[3 * cstride];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -773,7 +788,8 @@ __global__ void k_fin_gather(const uint64_t *__restrict__ list, const uint64_t *
                              const uint64_t *__restrict__ r0, uint64_t rb, uint64_t re, uint64_t *__restrict__ out,
                              uint64_t *__restrict__ n_out) {
   // out = list ++ r0[rb, re), halves swapped (lo << 32 | hi) so a sort on the low bits sorts by hi
-  const uint64_t len = prev ? prev[ST_KEPT] + prev[ST_CONTR] : 0, m = len + (re - rb);
+  // (the top block is only ever cut above the finishing levels: prev carries no cut)
+  const uint64_t len = prev ? prev[ST_KEPT] + prev[ST_CONTR] + prev[ST_EXTRA] : 0, m = len + (re - rb);
   if (blockIdx.x == 0 && threadIdx.x == 0) *n_out = m;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
@@ -1018,6 +1034,311 @@ __global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t 
   }
 }
 
+// ---- the dense top block: its minimum spanning forest in place of its edges -----------
+// After the level that splits at s = TB, the block of the 2^TB highest spread positions is
+// a subproblem of its own: every live edge with lo in it lies inside it — the groups
+// 0..TB-1 (exactly the edges whose lo is in the block) and the list entries (contractions)
+// that landed there.  On power-law graphs it is the hub core, and the later levels spend
+// most of their time re-hooking it (RMAT-26: 50.8 M of the 75.4 M live edges after s = 15
+// sit in its 2^15 positions; the next largest block holds < 1 M).  The elimination tree of
+// a graph is that of ANY minimum spanning forest of it under the weight hi (etree(G) =
+// etree(MSF(G)): parent(x) is the first t > x at which x's component in the threshold
+// graph G_t grows, and every MSF keeps the components of every G_t).  So the block's edges
+// are replaced by their MSF under the total order (hi, lo) — the edge word itself — found
+// by Borůvka rounds with the block's labels in LDS (u16: <= 2^15 vertices).  Dense blocks
+// converge in a few rounds (RMAT-22's top 2^15: 3); every round at least halves the
+// components that have an outgoing edge, so TB + 1 rounds always finish.
+constexpr int TOP_BITS = 15;
+constexpr int TOPB = 1024;                  // threads per workgroup of the top-block kernels
+constexpr uint32_t TOP_LDS_BEST = 8192;     // components whose minima a round keeps in LDS
+constexpr uint64_t TOP_DENSE = 16;          // used when the block's groups hold >= 16 edges per vertex
+constexpr uint64_t NO_EDGE = ~0ull;
+
+struct TopState {
+  uint32_t *minlo, *minhi;          // round 0: per vertex, the lowest lower / upper neighbour
+  uint16_t *comp;                   // per vertex: its component's id
+  unsigned long long *best;         // per component: the smallest edge word leaving it
+  unsigned *scal;                   // [0] components, [1] a round saw an inter-component edge, [2] done
+  uint64_t *st;                     // the cut level's stats row (ST_EXTRA: edges written so far)
+  uint64_t *out;                    // the MSF edges go to out[st[KEPT] + st[CONTR] + ...] (the next list)
+  uint32_t v0, V;                   // the block's first vertex and its vertex count
+};
+
+// The block's edges: the list entries the extraction moved out (sharded append regions,
+// st[ST_TOPNT] = the extraction's tile count) followed by groups [g0, g1) of r0.
+struct TopEdges {
+  const uint64_t *tl;
+  const unsigned long long *tcnt;
+  const uint64_t *r0;
+  uint64_t g0, g1;
+};
+__device__ __forceinline__ void top_prefix(const TopEdges &te, uint64_t *s_pre) {
+  if (threadIdx.x < WAVE) {
+    uint64_t inc = te.tcnt[(uint64_t)threadIdx.x * SHARD_STRIDE];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t u = __shfl_up(inc, o, 64);
+      if ((int)threadIdx.x >= o) inc += u;
+    }
+    s_pre[threadIdx.x + 1] = inc;
+    if (threadIdx.x == 0) s_pre[0] = 0;
+  }
+}
+__device__ __forceinline__ uint64_t top_at(const TopEdges &te, const uint64_t *s_pre, uint64_t ntiles, uint64_t i) {
+  const uint64_t nl = s_pre[NSHARD];
+  if (i >= nl) return te.r0[te.g0 + (i - nl)];
+  uint32_t a = 0, b = NSHARD;   // s_pre[a] <= i < s_pre[b]
+  while (b - a > 1) {
+    const uint32_t mid = (a + b) / 2;
+    if (s_pre[mid] <= i) a = mid; else b = mid;
+  }
+  return te.tl[shard_base(ntiles, a, 1) + (i - s_pre[a])];
+}
+
+// The list entries of the top block (spread(lo) >= cut) out of the cut level's next list.
+__global__ __launch_bounds__(BLOCK) void k_top_extract(const uint64_t *__restrict__ list, uint64_t *__restrict__ st,
+                                                       uint32_t cut, uint32_t clo, uint64_t *__restrict__ tl,
+                                                       unsigned long long *__restrict__ tcnt) {
+  const uint64_t nl = st[ST_KEPT] + st[ST_CONTR];
+  const uint64_t ntiles = (nl + TILE - 1) / TILE;
+  if (blockIdx.x == 0 && threadIdx.x == 0) st[ST_TOPNT] = ntiles;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    uint64_t ev[TILE_ITEMS];
+    uint32_t keep = 0;
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
+      ev[j] = i < nl ? list[i] : DEAD;
+      if (ev[j] != DEAD && spread((uint32_t)ev[j], clo) >= cut) keep |= 1u << j;
+    }
+    uint64_t slot = shard_reserve((uint32_t)__popc(keep), tcnt, tile, ntiles, 1);
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j)
+      if (keep & (1u << j)) tl[slot++] = ev[j];
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_top_init(TopState ts) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < ts.V; v += stride) {
+    ts.minlo[v] = INVALID;
+    ts.minhi[v] = INVALID;
+    ts.best[v] = NO_EDGE;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 3) ts.scal[threadIdx.x] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) ts.st[ST_EXTRA] = 0;
+}
+
+__global__ void k_set_u64(uint64_t *p, uint64_t v) { *p = v; }
+
+// Round 0: every vertex's smallest incident edge under (hi, lo) is (minlo(v), v) when v has
+// a lower neighbour in the block, else (v, minhi(v)).  Read-checked atomics (the minima
+// only fall: a stale read can only cost a redundant atomic); the edges come grouped by lo,
+// so lanes sharing the first lane's lo combine their minhi first.
+__global__ __launch_bounds__(BLOCK) void k_top_min0(TopEdges te, TopState ts, const uint64_t *__restrict__ st) {
+  __shared__ uint64_t s_pre[NSHARD + 1];
+  top_prefix(te, s_pre);
+  __syncthreads();
+  const uint64_t ntiles = st[ST_TOPNT], total = s_pre[NSHARD] + (te.g1 - te.g0);
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const uint64_t iters = (total + stride - 1) / stride;
+  for (uint64_t it = 0, i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; it < iters; ++it, i += stride) {
+    const bool live = i < total;
+    const uint64_t e = live ? top_at(te, s_pre, ntiles, i) : DEAD;
+    const bool ok = live && e != DEAD;
+    const uint32_t l = (uint32_t)e - ts.v0, h = (uint32_t)(e >> 32) - ts.v0;
+    if (ok && l < ts.minlo[h]) atomicMin(&ts.minlo[h], l);
+    const uint64_t lm = __ballot(ok);
+    if (!lm) continue;
+    const int first = __ffsll((unsigned long long)lm) - 1;
+    const uint32_t l0 = __shfl(l, first, 64);
+    const bool same = ok && l == l0;
+    const uint32_t v = wave_min(same ? h : INVALID);
+    if ((int)__lane_id() == first && v < ts.minhi[l0]) atomicMin(&ts.minhi[l0], v);
+    if (ok && !same && h < ts.minhi[l]) atomicMin(&ts.minhi[l], h);
+  }
+}
+
+// One workgroup: after par[] (u16, in LDS) holds every component's pick (itself for a
+// root), the forest is pointer-jumped, the roots renumbered 0..C-1 and ts.comp rewritten
+// through them.  `rec` edges were appended to ts.out.  lds: par[cap], cid[cap].
+__device__ void top_relabel(TopState &ts, uint16_t *par, uint16_t *cid, uint32_t cnt, bool first_round) {
+  __shared__ unsigned s_w[TOPB / WAVE];
+  for (;;) {   // pointer jumping (every pick points to a neighbour component; the picks form a forest)
+    bool changed = false;
+    for (uint32_t c = threadIdx.x; c < cnt; c += TOPB) {
+      const uint32_t p = par[c], q = par[p];
+      if (q != p) { par[c] = (uint16_t)q; changed = true; }
+    }
+    if (!__syncthreads_or(changed)) break;
+  }
+  // roots -> 0..C-1: each thread owns a contiguous run of entries
+  const uint32_t per = (cnt + TOPB - 1) / TOPB, b0 = threadIdx.x * per;
+  uint32_t r = 0;
+  for (uint32_t k = 0; k < per && b0 + k < cnt; ++k) r += par[b0 + k] == b0 + k;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t inc = r;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) s_w[wave] = inc;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+  for (int w = 0; w < TOPB / WAVE; ++w) {
+    if (w < wave) off += s_w[w];
+    tot += s_w[w];
+  }
+  uint32_t run = off + inc - r;
+  for (uint32_t k = 0; k < per && b0 + k < cnt; ++k)
+    if (par[b0 + k] == b0 + k) cid[b0 + k] = (uint16_t)run++;
+  __syncthreads();
+  for (uint32_t v = threadIdx.x; v < ts.V; v += TOPB) {
+    const uint32_t c = first_round ? v : ts.comp[v];
+    ts.comp[v] = cid[par[c]];
+  }
+  for (uint32_t c = threadIdx.x; c < tot; c += TOPB) ts.best[c] = NO_EDGE;
+  if (threadIdx.x == 0) {
+    ts.scal[0] = tot;
+    ts.scal[1] = 0;
+  }
+}
+
+// Appends the MSF edges a workgroup recorded (s_cnt of them in its LDS list) to the list.
+__device__ __forceinline__ uint32_t top_record(unsigned *s_cnt, uint64_t e, uint64_t *rec_lds, uint32_t cap) {
+  const uint32_t k = atomicAdd(s_cnt, 1u);
+  if (k < cap) rec_lds[k] = e;
+  return k;
+}
+
+constexpr uint32_t TOP_REC = 2048;   // MSF edges staged per hook launch before a flush
+__device__ void top_flush(TopState &ts, const uint64_t *rec, unsigned n) {
+  const uint64_t base = ts.st[ST_KEPT] + ts.st[ST_CONTR] + ts.st[ST_EXTRA];
+  for (uint32_t k = threadIdx.x; k < n; k += TOPB) ts.out[base + k] = rec[k];
+  __syncthreads();
+  if (threadIdx.x == 0) ts.st[ST_EXTRA] += n;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(TOPB) void k_top_hook0(TopState ts) {
+  extern __shared__ uint16_t lds16[];
+  uint16_t *par = lds16, *cid = lds16 + (1u << TOP_BITS);
+  __shared__ uint64_t rec[TOP_REC];
+  __shared__ unsigned s_cnt;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < ts.V; base += TOP_REC) {   // TOP_REC vertices (<= one edge each) a pass
+    const uint32_t end = base + TOP_REC < ts.V ? base + TOP_REC : ts.V;
+    for (uint32_t v = base + threadIdx.x; v < end; v += TOPB) {
+      const uint32_t ml = ts.minlo[v];
+      uint32_t p = v;
+      if (ml != INVALID) {
+        p = ml;
+        top_record(&s_cnt, ((uint64_t)(ts.v0 + v) << 32) | (ts.v0 + ml), rec, TOP_REC);
+      } else {
+        const uint32_t mh = ts.minhi[v];
+        // v's pick (v, mh) is also mh's own pick when minlo(mh) = v: mh records it, v stays a root
+        if (mh != INVALID && ts.minlo[mh] != v) {
+          p = mh;
+          top_record(&s_cnt, ((uint64_t)(ts.v0 + mh) << 32) | (ts.v0 + v), rec, TOP_REC);
+        }
+      }
+      par[v] = (uint16_t)p;
+    }
+    __syncthreads();
+    top_flush(ts, rec, s_cnt);
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+  }
+  top_relabel(ts, par, cid, ts.V, true);
+}
+
+// A Borůvka round over the block's edges: each component's smallest outgoing edge word.
+// The labels (u16) in LDS; the minima in LDS when the components fit, flushed with one
+// read-checked atomic per component and workgroup.
+__global__ __launch_bounds__(TOPB) void k_top_round(TopEdges te, TopState ts, const uint64_t *__restrict__ st) {
+  if (ts.scal[2]) return;   // done (uniform)
+  extern __shared__ uint16_t lds16[];
+  uint16_t *comp = lds16;
+  unsigned long long *lbest = (unsigned long long *)(lds16 + (1u << TOP_BITS));
+  __shared__ uint64_t s_pre[NSHARD + 1];
+  const uint32_t C = ts.scal[0];
+  const bool in_lds = C <= TOP_LDS_BEST;
+  for (uint32_t v = threadIdx.x; v < ts.V; v += TOPB) comp[v] = ts.comp[v];
+  if (in_lds)
+    for (uint32_t c = threadIdx.x; c < C; c += TOPB) lbest[c] = NO_EDGE;
+  top_prefix(te, s_pre);
+  __syncthreads();
+  const uint64_t ntiles = st[ST_TOPNT], total = s_pre[NSHARD] + (te.g1 - te.g0);
+  const uint64_t stride = (uint64_t)gridDim.x * TOPB;
+  bool inter = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * TOPB + threadIdx.x; i < total; i += stride) {
+    const uint64_t e = top_at(te, s_pre, ntiles, i);
+    if (e == DEAD) continue;
+    const uint32_t cl = comp[(uint32_t)e - ts.v0], ch = comp[(uint32_t)(e >> 32) - ts.v0];
+    if (cl == ch) continue;
+    inter = true;
+    if (in_lds) {
+      if (e < lbest[cl]) atomicMin(&lbest[cl], (unsigned long long)e);
+      if (e < lbest[ch]) atomicMin(&lbest[ch], (unsigned long long)e);
+    } else {
+      if (e < ts.best[cl]) atomicMin(&ts.best[cl], (unsigned long long)e);
+      if (e < ts.best[ch]) atomicMin(&ts.best[ch], (unsigned long long)e);
+    }
+  }
+  inter = __syncthreads_or(inter);
+  if (in_lds)
+    for (uint32_t c = threadIdx.x; c < C; c += TOPB) {
+      const unsigned long long w = lbest[c];
+      if (w != NO_EDGE && w < ts.best[c]) atomicMin(&ts.best[c], w);
+    }
+  if (inter && threadIdx.x == 0) atomicOr(&ts.scal[1], 1u);
+}
+
+// One workgroup: every component hooks to the component across its smallest outgoing
+// edge (a pair that picked the same edge keeps the smaller id as the root), the picked
+// edges are the MSF's, then the labels are rewritten.  A round without an inter-component
+// edge ends the rounds.
+__global__ __launch_bounds__(TOPB) void k_top_hook(TopState ts) {
+  __shared__ unsigned s_flag;
+  if (threadIdx.x == 0) s_flag = ts.scal[2] ? 2u : atomicOr(&ts.scal[1], 0u) ? 1u : 0u;
+  __syncthreads();
+  if (s_flag == 2) return;
+  if (s_flag == 0) {
+    if (threadIdx.x == 0) ts.scal[2] = 1;
+    return;
+  }
+  extern __shared__ uint16_t lds16[];
+  uint16_t *par = lds16, *cid = lds16 + (1u << TOP_BITS);
+  __shared__ uint64_t rec[TOP_REC];
+  __shared__ unsigned s_cnt;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  const uint32_t C = ts.scal[0];
+  for (uint32_t base = 0; base < C; base += TOP_REC) {
+    const uint32_t end = base + TOP_REC < C ? base + TOP_REC : C;
+    for (uint32_t c = base + threadIdx.x; c < end; c += TOPB) {
+      const unsigned long long w = ts.best[c];
+      uint32_t p = c;
+      if (w != NO_EDGE) {
+        const uint32_t a = ts.comp[(uint32_t)w - ts.v0], b = ts.comp[(uint32_t)(w >> 32) - ts.v0];
+        const uint32_t other = a == c ? b : a;
+        if (!(ts.best[other] == w && c < other)) {
+          p = other;
+          top_record(&s_cnt, w, rec, TOP_REC);
+        }
+      }
+      par[c] = (uint16_t)p;
+    }
+    __syncthreads();
+    top_flush(ts, rec, s_cnt);
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+  }
+  top_relabel(ts, par, cid, C, false);
+}
+
 // Debug statistic (SHEEP_DEBUG_ETREE): live entries per block of 2^s spread positions
 // after a level (its next list plus the groups not yet activated).
 __global__ void k_dbg_blocks(const uint64_t *__restrict__ a, const uint64_t *__restrict__ st, const uint64_t *__restrict__ b,
@@ -1064,8 +1385,58 @@ static uint64_t list_capacity(uint64_t m) { return 2 * m + TILE; }
 // read only.
 // One pass of launches per level, no host synchronisation inside the loop (see the
 // stats row above); the stats come back once at the end for the timers / debug log.
+// The dense top block's edges -> their minimum spanning forest (see k_top_extract..k_top_hook):
+// appended to `next` behind the cut level's contractions (st[ST_EXTRA]); st[ST_CUT] makes
+// the next split drop the block's list entries, and the caller stops activating its groups.
+static void top_block(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, uint64_t g0, uint64_t g1, uint32_t cut,
+                      uint32_t clo, uint32_t v0, uint32_t V, uint64_t lcap) {
+  const uint64_t tcap = (lcap + TILE - 1) / TILE * TILE + TILE;
+  uint64_t *tl = c.get_as<uint64_t>("et_top_list", tcap);
+  unsigned long long *tcnt = c.get_as<unsigned long long>("et_top_cnt", (uint64_t)NSHARD * SHARD_STRIDE);
+  HIP_CHECK(hipMemsetAsync(tcnt, 0, (uint64_t)NSHARD * SHARD_STRIDE * sizeof(unsigned long long), c.stream));
+  hipLaunchKernelGGL(k_top_extract, dim3(grid_tiles(lcap)), dim3(BLOCK), 0, c.stream, (const uint64_t *)next, st, cut,
+                     clo, tl, tcnt);
+  LAUNCH_CHECK();
+  TopState ts;
+  ts.minlo = c.get_as<uint32_t>("et_top_minlo", V);
+  ts.minhi = c.get_as<uint32_t>("et_top_minhi", V);
+  ts.comp = c.get_as<uint16_t>("et_top_comp", V);
+  ts.best = c.get_as<unsigned long long>("et_top_best", V);
+  ts.scal = c.get_as<unsigned>("et_top_scal", 4);
+  ts.st = st;
+  ts.out = next;
+  ts.v0 = v0;
+  ts.V = V;
+  hipLaunchKernelGGL(k_top_init, dim3(grid_for(V)), dim3(BLOCK), 0, c.stream, ts);
+  LAUNCH_CHECK();
+  const TopEdges te{tl, tcnt, r0, g0, g1};
+  hipLaunchKernelGGL(k_top_min0, dim3(grid_for(lcap + (g1 - g0))), dim3(BLOCK), 0, c.stream, te, ts, (const uint64_t *)st);
+  LAUNCH_CHECK();
+  const size_t lds2 = 2 * ((size_t)1 << TOP_BITS) * sizeof(uint16_t);                        // par + cid
+  const size_t ldsr = ((size_t)1 << TOP_BITS) * sizeof(uint16_t) + TOP_LDS_BEST * sizeof(uint64_t);   // comp + minima
+  allow_lds((const void *)k_top_hook0, (int)lds2);
+  allow_lds((const void *)k_top_hook, (int)lds2);
+  allow_lds((const void *)k_top_round, (int)ldsr);
+  hipLaunchKernelGGL(k_top_hook0, dim3(1), dim3(TOPB), lds2, c.stream, ts);
+  LAUNCH_CHECK();
+  for (int r = 0; r <= TOP_BITS; ++r) {   // <= TOP_BITS + 1 rounds always finish (each halves the components)
+    if (r == 6) {   // dense blocks are done by now: skip the idle launches
+      HIP_CHECK(hipMemcpyAsync(c.h_scalars + 20, ts.scal + 2, sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
+      c.sync();
+      if (*(unsigned *)(c.h_scalars + 20)) break;
+    }
+    hipLaunchKernelGGL(k_top_round, dim3(256), dim3(TOPB), ldsr, c.stream, te, ts, (const uint64_t *)st);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_top_hook, dim3(1), dim3(TOPB), lds2, c.stream, ts);
+    LAUNCH_CHECK();
+  }
+  // the cut for the next split (k_top_init zeroed ST_EXTRA before the hooks appended)
+  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, c.stream, st + ST_CUT, (uint64_t)cut);
+  LAUNCH_CHECK();
+}
+
 void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
-                      int fin_bits, int filt_lvl, uint32_t ylo, uint32_t yhi) {
+                      int fin_bits, int filt_lvl, uint32_t ylo, uint32_t yhi, int top_bits) {
   fill_u32(c, parent, n, INVALID);
   if (n < 2 || m == 0) return;
   if (m >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "too many edges for one shard");
@@ -1100,6 +1471,30 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   hipLaunchKernelGGL(k_reset, dim3(gn), dim3(BLOCK), 0, c.stream, uf, mt, top, claim, n, csets);
   LAUNCH_CHECK();
   allow_full_lds((const void *)k_cross_find_win);
+  // The dense top block (maps): after the level that splits at s = top_bits, its edges are
+  // replaced by their minimum spanning forest when its groups are dense.
+  int top_lvl = -1, gcut = 0;
+  uint64_t top_g0 = 0, top_g1 = 0;
+  uint32_t top_v0 = 0, top_V = 0, top_cut = 0;
+  if (top_bits > FINB && top_bits <= L - 1 && top_bits <= TOP_BITS) {
+    std::vector<uint64_t> hs(2 * (size_t)L);
+    HIP_CHECK(hipMemcpyAsync(hs.data(), seg, hs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+    top_cut = (uint32_t)((1ull << L) - (1ull << top_bits));
+    uint64_t a = 0, z = n;   // the block's first vertex: min x with spread(x) >= cut
+    while (a < z) {
+      const uint64_t x = (a + z) / 2;
+      if (x + ((x * (uint64_t)clo) >> 32) >= top_cut) z = x; else a = x + 1;
+    }
+    top_v0 = (uint32_t)a;
+    top_V = (uint32_t)(n - a);
+    top_g0 = hs[top_bits - 1];
+    top_g1 = hs[L];
+    if (top_V >= 2 && top_g1 - top_g0 >= TOP_DENSE * top_V && getenv("SHEEP_NO_TOP") == nullptr) {
+      top_lvl = L - 1 - top_bits;
+      gcut = top_bits;
+    }
+  }
   // a split reads at most the list plus a bucket: (lcap + m) entries, in SPLIT_TILE tiles
   const uint64_t cstride = (lcap + m + SPLIT_TILE - 1) / SPLIT_TILE + 1;
   uint64_t *tcnt = c.get_as<uint64_t>("et_tilecnt", 3 * cstride + 1);
@@ -1116,11 +1511,11 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       const LevelClean clean = lvl ? LevelClean{lbuf, xbuf, xtop, prev, uf, mt, top, claim, n, tagged, lvl - 1, parent, csets}
                                    : LevelClean{};
       hipLaunchKernelGGL(k_split_count, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo, yr,
-                         (const uint64_t *)r0, (const uint64_t *)seg, L, tcnt, clean);
+                         (const uint64_t *)r0, (const uint64_t *)seg, L, gcut, tcnt, clean);
       LAUNCH_CHECK();
       scan_exclusive_u64_dev(c, tcnt, tcnt, 3 * cstride + 1, st + ST_SCANN);
       hipLaunchKernelGGL(k_split_write, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo, yr,
-                         (const uint64_t *)r0, (const uint64_t *)seg, L, (const uint64_t *)tcnt, next, lbuf, xbuf);
+                         (const uint64_t *)r0, (const uint64_t *)seg, L, gcut, (const uint64_t *)tcnt, next, lbuf, xbuf);
       LAUNCH_CHECK();
     }
     {
@@ -1154,6 +1549,20 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
                          alt, cset(CSET_APPLY), parent, g);
       LAUNCH_CHECK();
       pack_shards<uint64_t>(c, alt, next, st + ST_NX, cset(CSET_APPLY), st + ST_CONTR, nullptr, nullptr, st + ST_KEPT);
+    }
+    if (lvl == top_lvl) {
+      TimedRegion tr(c, "etree_top");
+      top_block(c, next, st, r0, top_g0, top_g1, top_cut, clo, top_v0, top_V, lcap);
+      if (g_debug_etree) {
+        uint64_t h[ST_ROW];
+        unsigned hs[4];
+        HIP_CHECK(hipMemcpyAsync(h, st, sizeof h, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipMemcpyAsync(hs, c.get_as<unsigned>("et_top_scal", 4), sizeof hs, hipMemcpyDeviceToHost, c.stream));
+        c.sync();
+        fprintf(stderr, "etree top block after s %d: vertices %u group edges %lu list entries scanned %lu -> MSF edges %lu "
+                        "(components left %u, done %u)\n", top_bits, top_V, (unsigned long)(top_g1 - top_g0),
+                (unsigned long)(h[ST_KEPT] + h[ST_CONTR]), (unsigned long)h[ST_EXTRA], hs[0], hs[2]);
+      }
     }
     if (g_debug_etree && s >= 8 && s <= 15) {   // how the live edges spread over the 2^s blocks
       uint64_t hs[2] = {0, 0};
@@ -1201,6 +1610,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     HIP_CHECK(hipMemcpyAsync(&hseg[0], seg + sg, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
     HIP_CHECK(hipMemcpyAsync(&hseg[1], seg + L, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
     c.sync();
+    if (gcut > sg) hseg[0] = hseg[1];   // the top block's groups were replaced by its MSF
     const uint64_t *prev = nglobal ? stats + (uint64_t)(nglobal - 1) * ST_ROW : nullptr;
     const uint64_t cap = lcap + (hseg[1] - hseg[0]);
     uint64_t *fin = c.get_as<uint64_t>("et_fin", cap), *fin_alt = c.get_as<uint64_t>("et_fin_alt", cap);
@@ -1328,7 +1738,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
       group_edges_by_lo(c, edges, m, lg, pst, r0, seg, counted);
     }
     TimedRegion tr(c, "etree", 8 * m);
-    etree_from_edges(c, r0, m, n, parent, seg, FIN_MAP);
+    etree_from_edges(c, r0, m, n, parent, seg, FIN_MAP, -1, 0, 0, TOP_BITS);
   } else {
     fill_u32(c, parent, n, INVALID);
   }

@@ -52,6 +52,19 @@ struct EndpointKeys {
     return (llama && r.tail == r.head) ? NO_KEY : r.head;
   }
 };
+// Both endpoints with the tail part padded to whole tiles: keys [0, np) are the tails
+// (NO_KEY past n), [np, np + n) the heads — so head tile t covers exactly the records of
+// record tile t (their (bucket, tile) counts are the relabel's head layout).
+struct EndpointKeysP {
+  const sheep_xs1 *rec;
+  uint64_t n, np;
+  int llama;
+  __device__ __forceinline__ uint32_t operator()(uint64_t i) const {
+    if (i < np) return i < n ? rec[i].tail : NO_KEY;
+    const sheep_xs1 r = rec[i - np];
+    return (llama && r.tail == r.head) ? NO_KEY : r.head;
+  }
+};
 // lo = low 32 bits of a (hi << 32 | lo) tree edge; DEAD edges carry no key.
 struct EdgeLoKeys {
   const uint64_t *edges;
@@ -381,6 +394,7 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
   }
   for (const void *f : {(const void *)k_hist_scatter<HeadKeys>, (const void *)k_hist_scatter<EdgeLoKeys>,
                         (const void *)k_hist_scatter<EndpointKeys>, (const void *)k_hist_scatter_staged<EndpointKeys, 16>,
+                        (const void *)k_hist_scatter<EndpointKeysP>, (const void *)k_hist_scatter_staged<EndpointKeysP, 16>,
                         (const void *)k_hist_scatter_staged<HeadKeys, 16>,
                         (const void *)k_hist_scatter_staged<EdgeLoKeys, 16>, (const void *)k_hist_final,
                         (const void *)k_lo_scatter_staged<16>, (const void *)k_lo_scatter_staged<8>})
@@ -540,6 +554,67 @@ __global__ __launch_bounds__(CB) void k_degree_fused(const sheep_xs1 *__restrict
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(d_err, 1ull);
 }
 
+// ---- degree pass for records in any order (sequence.h:65-107) --------------------------
+// Tails are not in runs, so both endpoints go through the bucketed histogram; this pass
+// makes its whole count step in ONE read of the records: per record tile, the range check,
+// the max slot, the FILE_DAT last record's extra counts (global atomics, as k_degree) and
+// the tails' and heads' bucket counts (two LDS histograms) — written as the count rows of
+// EndpointKeysP's tail tile t and head tile NT + t (bucket-major, 2 NT tiles per bucket).
+__global__ __launch_bounds__(CB) void k_degree_endpoints(const sheep_xs1 *__restrict__ rec, uint64_t n, int mode,
+                                                         uint32_t *__restrict__ deg, uint64_t cap, uint32_t nb,
+                                                         uint32_t *__restrict__ tile_hist, uint64_t nt,
+                                                         unsigned long long *__restrict__ d_max,
+                                                         unsigned long long *__restrict__ d_err) {
+  extern __shared__ uint32_t lds[];
+  uint32_t *tc = lds, *hc = lds + nb;
+  const uint32_t tile = xcd_tile();
+  const uint64_t base = (uint64_t)tile << TLOG;
+  for (uint32_t b = threadIdx.x; b < 2 * nb; b += CB) lds[b] = 0;
+  lds_barrier();
+  uint32_t lmax = 0;
+  bool bad = false;
+  for (uint32_t step = 0; step < TKEYS; step += CB * DPT) {
+    sheep_xs1 r[DPT];
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+      const uint64_t i = base + step + (uint64_t)j * CB + threadIdx.x;
+      if (i < n) r[j] = rec[i];
+    }
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+      const uint64_t i = base + step + (uint64_t)j * CB + threadIdx.x;
+      if (i >= n) continue;
+      const uint32_t t = r[j].tail, h = r[j].head;
+      if (t >= cap || h >= cap) { bad = true; continue; }
+      const bool loop_once = mode == SHEEP_DEGREE_LLAMA && t == h;   // LLAMA: a self-loop stored once
+      if (mode == SHEEP_DEGREE_FILE_DAT && i == n - 1) {   // the XS1 reader's repeated last record
+        atomicAdd(&deg[t], 1u);
+        if (!loop_once) atomicAdd(&deg[h], 1u);
+      }
+      const uint32_t m = (t > h ? t : h) + 1;
+      lmax = m > lmax ? m : lmax;
+      atomicAdd(&tc[t >> WBITS], 1u);
+      if (!loop_once) atomicAdd(&hc[h >> WBITS], 1u);
+    }
+  }
+  lds_barrier();
+  for (uint32_t b = threadIdx.x; b < nb; b += CB) {
+    tile_hist[(uint64_t)b * 2 * nt + tile] = tc[b];
+    tile_hist[(uint64_t)b * 2 * nt + nt + tile] = hc[b];
+  }
+  block_atomic_max(d_max, lmax);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(d_err, 1ull);
+}
+
+// head layout = the head columns of the endpoint counts: out[b * nt + t] = in[b * 2nt + nt + t]
+__global__ void k_head_cols(const uint32_t *__restrict__ in, uint64_t nt, uint32_t nb, uint32_t *__restrict__ out) {
+  const uint64_t total = (uint64_t)nb * nt, stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const uint64_t b = i / nt, t = i - b * nt;
+    out[i] = in[b * 2 * nt + nt + t];
+  }
+}
+
 // ---- head-bucketed relabel (jtree.cpp:72-91) -----------------------------------------
 // k_relabel's pos[head] gather is random over the whole 4-B-per-slot index (268 MB at
 // RMAT-26): each 4-B load moves a full line.  Here the records are first scattered into
@@ -567,8 +642,10 @@ struct RelabelKeys {
 
 // One tile of TKEYS records per workgroup, staged SUB = PER * HB at a time (u64 payloads:
 // a whole tile does not fit LDS).  gb[b] walks the tile's region of bucket b; every write
-// is bounded by the region's end and a region not filled exactly raises flags[1] (stale
-// offsets) so the host recounts.  flags[0]: a sequenced endpoint's neighbour >= pos_size.
+// is bounded by the output's capacity and a region not filled exactly raises flags[1]
+// (stale offsets: the host recounts; a stale run's writes stay in bounds and are
+// discarded) — one random LDS read per record fewer than a per-region bound.  flags[0]: a
+// sequenced endpoint's neighbour >= pos_size.
 template <int PER, int NT = HB>
 __global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restrict__ rec, uint64_t n,
                                                         const uint32_t *__restrict__ pos, uint64_t pos_size, uint32_t nb,
@@ -576,14 +653,11 @@ __global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restr
                                                         uint64_t *__restrict__ out, unsigned long long *__restrict__ flags) {
   constexpr uint32_t SUB = PER * NT;
   extern __shared__ uint32_t lds[];
-  uint32_t *cur = lds, *gb = lds + nb, *end = lds + 2 * nb, *wsum = lds + 3 * nb;
-  uint64_t *stage = (uint64_t *)(lds + ((3 * nb + NT / WAVE + 1) & ~1u));
+  uint32_t *cur = lds, *gb = lds + nb, *wsum = lds + 2 * nb;
+  uint64_t *stage = (uint64_t *)(lds + ((2 * nb + NT / WAVE + 1) & ~1u));
   const uint64_t tile = xcd_tile();
-  for (uint32_t b = threadIdx.x; b < nb; b += NT) {
-    const uint64_t o = (uint64_t)b * ntiles + tile;
-    gb[b] = offsets[o];
-    end[b] = offsets[o + 1];
-  }
+  const uint32_t cap = offsets[(uint64_t)nb * ntiles];   // the scanned total: the output's length
+  for (uint32_t b = threadIdx.x; b < nb; b += NT) gb[b] = offsets[(uint64_t)b * ntiles + tile];
   bool bad = false, lost = false;
   const uint64_t base = tile << TLOG;
   for (uint32_t s0 = 0; s0 < TKEYS; s0 += SUB) {
@@ -625,7 +699,7 @@ __global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restr
     for (uint32_t j = threadIdx.x; j < total; j += NT) {
       const uint64_t v = stage[j];
       const uint32_t b = (uint32_t)v >> WBITS, dst = gb[b] + j;
-      if (dst < end[b]) out[dst] = v;
+      if (dst < cap) out[dst] = v;
       else lost = true;
     }
     lds_barrier();
@@ -633,7 +707,7 @@ __global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restr
     lds_barrier();
   }
   for (uint32_t b = threadIdx.x; b < nb; b += NT)
-    if (gb[b] != end[b]) lost = true;
+    if (gb[b] != offsets[(uint64_t)b * ntiles + tile + 1]) lost = true;   // the region's end
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(&flags[0], 1ull);
   if (__any(lost) && (threadIdx.x & 63) == 0) atomicAdd(&flags[1], 1ull);
 }
@@ -738,10 +812,51 @@ void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uin
   hl.valid = hl.bstart.size() == nb + 1;
 }
 
-void histogram_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt) {
-  c.head_layout.valid = false;   // the relabel counts its own head layout
-  c.head_layout.bstart.clear();
-  histogram_add(c, EndpointKeys{rec, nrec, llama}, 2 * nrec, K, cnt);
+bool degree_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_t *deg, uint64_t cap,
+                      unsigned long long *d_max, unsigned long long *d_err) {
+  const uint64_t nb = (cap + W - 1) >> WBITS, nt = (nrec + TKEYS - 1) >> TLOG;
+  if (nrec == 0 || nb == 0 || nb > 8192 || nrec >= (1ull << 31) || 2 * nt * nb + 1 >= (1ull << 32)) return false;
+  uint32_t *tile_hist = c.get_as<uint32_t>("hist_tiles", 2 * nt * nb + 1);
+  hipLaunchKernelGGL(k_degree_endpoints, dim3((unsigned)nt), dim3(CB), 2 * nb * 4, c.stream, rec, nrec, mode, deg, cap,
+                     (uint32_t)nb, tile_hist, nt, d_max, d_err);
+  LAUNCH_CHECK();
+  return true;
+}
+
+void histogram_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt,
+                         bool counted) {
+  Ctx::HeadLayout &hl = c.head_layout;
+  hl.valid = false;
+  hl.bstart.clear();
+  if (!counted) {   // the relabel counts its own head layout
+    histogram_add(c, EndpointKeys{rec, nrec, llama}, 2 * nrec, K, cnt);
+    return;
+  }
+  // degree_endpoints wrote the count rows (capacity buckets, 2 nt tiles each); the rows past
+  // K's buckets are zero, so the scan over K's buckets serves.  The head columns, scanned on
+  // their own, are the relabel's head layout (LLAMA heads: a self-loop not counted; every
+  // head is below K) — no recount of the records there.
+  const uint64_t nt = (nrec + TKEYS - 1) >> TLOG, nb = (K + W - 1) >> WBITS;
+  if (llama && nb && nb <= 8192 && nt * nb + 1 < (1ull << 32)) {
+    const uint32_t *tile_hist = c.get_as<uint32_t>("hist_tiles", 2 * nt * nb + 1);
+    uint32_t *off = c.get_as<uint32_t>("head_offsets", nt * nb + 1);
+    hipLaunchKernelGGL(k_head_cols, dim3(grid_for(nt * nb)), dim3(BLOCK), 0, c.stream, tile_hist, nt, (uint32_t)nb, off);
+    LAUNCH_CHECK();
+    scan_exclusive_u32(c, off, off, nt * nb, off + nt * nb);
+    uint32_t *bs_dev = c.get_as<uint32_t>("hist_bstart_dev", nb + 1);
+    hipLaunchKernelGGL(k_bucket_starts, dim3(grid_for(nb + 1)), dim3(BLOCK), 0, c.stream, (const uint32_t *)off, nt,
+                       (uint32_t)nb, (const uint32_t *)(off + nt * nb), bs_dev);
+    LAUNCH_CHECK();
+    hl.bstart.assign(nb + 1, 0);
+    HIP_CHECK(hipMemcpyAsync(hl.bstart.data(), bs_dev, (nb + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+    hl.rec = rec;
+    hl.nrec = nrec;
+    hl.K = K;
+    hl.valid = true;
+  }
+  histogram_add(c, EndpointKeysP{rec, nrec, nt * TKEYS, llama}, nt * TKEYS + nrec, K, cnt, nullptr, nullptr, nullptr,
+                nullptr, nullptr, true);
 }
 
 uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
@@ -779,7 +894,7 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   uint32_t *off = cached ? c.get_as<uint32_t>("head_offsets", ntiles * nb + 1) : recount();
   const uint64_t total = hl.bstart[nb];
   uint64_t *pairs = c.get_as<uint64_t>("rl_pairs", total ? total : 1);
-  const size_t fixed = ((3 * nb + HB / WAVE + 1) & ~1ull) * 4;
+  const size_t fixed = ((2 * nb + HB / WAVE + 1) & ~1ull) * 4;
   auto scatter = [&]() {
     HIP_CHECK(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c.stream));
     // Two 512-thread workgroups per CU, 4K-record sub-tiles (81 VGPRs keep a 1024-thread
@@ -787,7 +902,7 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
     // 4096 buckets (vertex ids below 2^27), the scan's limit for 512 threads.
     {
       constexpr int NT = 512, P = 8;
-      const size_t fx = ((3 * nb + NT / WAVE + 1) & ~1ull) * 4, lds = fx + (size_t)P * NT * 8;
+      const size_t fx = ((2 * nb + NT / WAVE + 1) & ~1ull) * 4, lds = fx + (size_t)P * NT * 8;
       if (nb <= 8 * (uint64_t)NT && lds <= 160 * 1024) {
         hipLaunchKernelGGL((k_relabel_scatter<P, NT>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec, nrec, pos,
                            pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);

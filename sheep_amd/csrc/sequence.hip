@@ -167,7 +167,8 @@ void degree_count(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_
   bool counted = false;   // heads' (bucket, tile) counts made by the same pass (hist.hip)
   if (nrec) {
     TimedRegion tr(c, "degree", 12 * nrec);   // one read of the 12-B records
-    if (sorted) counted = degree_fused(c, rec, nrec, mode, deg, cap, d, d + 1);
+    counted = sorted ? degree_fused(c, rec, nrec, mode, deg, cap, d, d + 1)
+                     : degree_endpoints(c, rec, nrec, mode, deg, cap, d, d + 1);
     if (!counted) {
       hipLaunchKernelGGL(k_degree, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, mode, deg, cap, d, d + 1,
                          sorted);
@@ -181,7 +182,7 @@ void degree_count(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_
   if (nrec) {
     TimedRegion tr(c, "degree_heads", 12 * nrec);
     if (sorted) histogram_heads(c, rec, nrec, mode == SHEEP_DEGREE_LLAMA, *max_slot, deg, counted);
-    else histogram_endpoints(c, rec, nrec, mode == SHEEP_DEGREE_LLAMA, *max_slot, deg);
+    else histogram_endpoints(c, rec, nrec, mode == SHEEP_DEGREE_LLAMA, *max_slot, deg, counted);
   }
 }
 
