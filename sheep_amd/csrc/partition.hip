@@ -841,6 +841,7 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   HIP_CHECK(hipMemsetAsync(found, 0xFF, sizeof(uint64_t), c.stream));   // k_event resets it after each event
   static const bool dbg = getenv("SHEEP_DEBUG_PART") != nullptr;
   double dbg_tab = 0, dbg_search = 0, dbg_stage = 0, dbg_wait = 0, dbg_host = 0;
+  uint64_t dbg_kids[4] = {0, 0, 0, 0}, dbg_kids_max = 0;   // packing nodes with <= 16 / 256 / 4096 / more kids
   uint8_t *stage = (uint8_t *)c.get_pinned("pt_event", 64 + (size_t)EV_STAGE * 12);
   volatile uint32_t *hdr = (volatile uint32_t *)stage;
   uint32_t *st_kids = (uint32_t *)(stage + 64);
@@ -957,6 +958,10 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
         d2h(c, segR.data() + EV_STAGE, (const uint64_t *)kR, cnt - EV_STAGE);
         c.sync();
       }
+      if (dbg) {
+        dbg_kids[cnt <= 16 ? 0 : cnt <= 256 ? 1 : cnt <= 4096 ? 2 : 3]++;
+        dbg_kids_max = std::max<uint64_t>(dbg_kids_max, cnt);
+      }
       const uint64_t cb0 = cb;
       // std::sort on the current kid order with the reference comparator (:104-106);
       // sorting positions with a comparator on their keys is the same sort.
@@ -1003,8 +1008,11 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
     }
   }
   if (dbg)
-    fprintf(stderr, "partition events %u (us total): table %.1f search %.1f stage %.1f | host wait %.1f host pack %.1f\n",
-            (unsigned)info->packing_nodes, dbg_tab, dbg_search, dbg_stage, dbg_wait, dbg_host);
+    fprintf(stderr, "partition events %u (us total): table %.1f search %.1f stage %.1f | host wait %.1f host pack %.1f"
+            " | kids <=16 %lu <=256 %lu <=4096 %lu more %lu max %lu\n",
+            (unsigned)info->packing_nodes, dbg_tab, dbg_search, dbg_stage, dbg_wait, dbg_host,
+            (unsigned long)dbg_kids[0], (unsigned long)dbg_kids[1], (unsigned long)dbg_kids[2], (unsigned long)dbg_kids[3],
+            (unsigned long)dbg_kids_max);
   write_table(true);   // the device copy k_roots_r reads
   if (!upl_pos.empty()) {   // persist the sorted kid orders (forwardPartition mutates kids, :104-106)
     const uint64_t mu = upl_pos.size();

@@ -212,3 +212,57 @@ def test_scale_golden_digests_are_consistent(cfg):
     assert g["created"] <= g["k"] and g["packing_nodes"] > 0
     assert g["max_component"] == int((g["pst_sum"] // g["k"]) * 1.03)          # partition.cpp:54-57
     assert g["evaluate"]["max_down_bal"] <= g["max_component"]
+
+
+def _kruskal_msf(lo, hi, n):
+    """Minimum spanning forest under the order (hi, lo) (Kruskal with a union-find)."""
+    order = np.lexsort((lo, hi))
+    uf = np.arange(n)
+
+    def find(x):
+        while uf[x] != x:
+            uf[x] = uf[uf[x]]
+            x = uf[x]
+        return x
+    keep = []
+    for e in order:
+        a, b = find(lo[e]), find(hi[e])
+        if a != b:
+            uf[max(a, b)] = min(a, b)
+            keep.append(e)
+    return np.asarray(keep, dtype=np.int64)
+
+
+@pytest.mark.parametrize("name", ["hep", "rmat12", "rmat14", "edge"])
+def test_etree_equals_etree_of_msf(name):
+    """The identity the dense top block rests on (etree.hip): the elimination
+    tree of a graph equals that of a minimum spanning forest of it under the weight hi
+    (sequence positions), here (hi, lo) as in the kernels — checked with the oracle against
+    the reference-built golden tree, for the whole edge set and for a cut-out top block."""
+    r = golden_records(name)
+    seq = golden_seq(name)
+    n = len(seq)
+    pos = np.full(int(max(r["tail"].max(), r["head"].max())) + 1, -1, np.int64)
+    pos[seq] = np.arange(n)
+    a, b = pos[r["tail"].astype(np.int64)], pos[r["head"].astype(np.int64)]
+    m = (a >= 0) & (b >= 0) & (a != b)
+    lo, hi = np.minimum(a, b)[m], np.maximum(a, b)[m]
+    ident = np.arange(n, dtype=np.uint32)
+    gp, _ = golden_tree(name)
+    # positions as vertex ids (sequence = identity): the same tree, the edges in position space
+    p_all, _ = oracle.build_tree(hi.astype(np.uint32), lo.astype(np.uint32), ident)
+    assert np.array_equal(p_all, gp)
+    keep = _kruskal_msf(lo, hi, n)
+    assert len(keep) < len(lo)
+    p_msf, _ = oracle.build_tree(hi[keep].astype(np.uint32), lo[keep].astype(np.uint32), ident)
+    assert np.array_equal(p_msf, gp)
+    # a top block [t0, n) whose vertices only see edges inside it: its tree is that of its MSF
+    t0 = n - n // 4
+    inb = lo >= t0
+    blo, bhi = lo[inb] - t0, hi[inb] - t0
+    nb = n - t0
+    idb = np.arange(nb, dtype=np.uint32)
+    pb, _ = oracle.build_tree(bhi.astype(np.uint32), blo.astype(np.uint32), idb)
+    kb = _kruskal_msf(blo, bhi, nb)
+    pbm, _ = oracle.build_tree(bhi[kb].astype(np.uint32), blo[kb].astype(np.uint32), idb)
+    assert np.array_equal(pb, pbm)
