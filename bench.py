@@ -38,12 +38,15 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-le
 # §8(d), whose B_alg covers the whole path).  Regions whose kernels are shared with other
 # regions (scans, radix passes) get traffic null.
 LEAF = ("degree", "degree_heads", "sequence", "relabel", "pst_group", "etree_split", "etree_union", "etree_cross",
-        "etree_apply", "merge", "kids", "partition")
+        "etree_apply", "etree_top", "merge", "kids", "partition")
 REGION_KERNELS = {"degree": ["k_degree_fused"], "relabel": ["k_relabel_scatter", "k_relabel_gather"],
                   "etree_split": ["k_split_count", "k_split_write"], "etree_union": ["k_hook_round", "k_hook_finish", "k_light_top"],
                   "etree_cross": ["k_cross_find"], "etree_apply": ["k_cross_apply", "k_level_clean"],
+                  "etree_top": ["k_top_extract", "k_top_init", "k_top_min0", "k_top_hook0", "k_top_round", "k_top_hook"],
                   "evaluate": ["k_pp", "k_eval_records", "k_eval_nodes"]}
-PMC_FILE = os.path.join(ROOT, "profiles", "r3", "pmc_traffic_rmat{scale}_k{k}.json")
+# the newest round's profile of this workload (profiles/rNN/), collected by tools/gpu/gpuprof.sh
+PMC_DIRS = ("r4", "r3")
+PMC_FILE = os.path.join(ROOT, "profiles", "{round}", "pmc_traffic_rmat{scale}_k{k}.json")
 
 
 def parse():
@@ -438,7 +441,12 @@ def time_evaluator(a, ctx, group, shard, subs, s, res, rank, world, dev, barrier
 
 
 def _pmc(a, world):
-    path = PMC_FILE.format(scale=a.scale, k=a.k)
+    path = PMC_FILE.format(round=PMC_DIRS[-1], scale=a.scale, k=a.k)
+    for r in PMC_DIRS:
+        p = PMC_FILE.format(round=r, scale=a.scale, k=a.k)
+        if os.path.exists(p):
+            path = p
+            break
     if world != 1 or a.shuffle or a.graph != "rmat" or a.shards != 1 or not os.path.exists(path):
         return None, path
     prof = json.load(open(path))

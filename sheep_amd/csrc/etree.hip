@@ -1048,9 +1048,11 @@ __global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t 
 // by Borůvka rounds with the block's labels in LDS (u16: <= 2^15 vertices).  Dense blocks
 // converge in a few rounds (RMAT-22's top 2^15: 3); every round at least halves the
 // components that have an outgoing edge, so TB + 1 rounds always finish.
-constexpr int TOP_BITS = 15;
+constexpr int TOP_BITS = 15;                 // the map's cut (blocks up to 2^TOP_BITS_MAX: SHEEP_TOP_BITS)
+constexpr int TOP_BITS_MAX = 16;            // u16 labels: <= 65536 vertices
 constexpr int TOPB = 1024;                  // threads per workgroup of the top-block kernels
-constexpr uint32_t TOP_LDS_BEST = 8192;     // components whose minima a round keeps in LDS
+constexpr uint32_t TOP_HOOK_LDS = 1u << 15; // hook kernels: par / cid in LDS up to this many components
+constexpr size_t TOP_ROUND_LDS = 144 * 1024; // a round's dynamic LDS: the labels, then the minima
 constexpr uint64_t TOP_DENSE = 16;          // used when the block's groups hold >= 16 edges per vertex
 constexpr uint64_t NO_EDGE = ~0ull;
 
@@ -1061,6 +1063,7 @@ struct TopState {
   unsigned *scal;                   // [0] components, [1] a round saw an inter-component edge, [2] done
   uint64_t *st;                     // the cut level's stats row (ST_EXTRA: edges written so far)
   uint64_t *out;                    // the MSF edges go to out[st[KEPT] + st[CONTR] + ...] (the next list)
+  uint16_t *gpar, *gcid;            // par / cid of a hook over more than TOP_HOOK_LDS components
   uint32_t v0, V;                   // the block's first vertex and its vertex count
 };
 
@@ -1097,7 +1100,7 @@ __device__ __forceinline__ uint64_t top_at(const TopEdges &te, const uint64_t *s
 
 // The list entries of the top block (spread(lo) >= cut) out of the cut level's next list.
 __global__ __launch_bounds__(BLOCK) void k_top_extract(const uint64_t *__restrict__ list, uint64_t *__restrict__ st,
-                                                       uint32_t cut, uint32_t clo, uint64_t *__restrict__ tl,
+                                                       uint32_t cut, uint32_t cut_hi, uint32_t clo, uint64_t *__restrict__ tl,
                                                        unsigned long long *__restrict__ tcnt) {
   const uint64_t nl = st[ST_KEPT] + st[ST_CONTR];
   const uint64_t ntiles = (nl + TILE - 1) / TILE;
@@ -1109,7 +1112,8 @@ __global__ __launch_bounds__(BLOCK) void k_top_extract(const uint64_t *__restric
     for (int j = 0; j < TILE_ITEMS; ++j) {
       const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
       ev[j] = i < nl ? list[i] : DEAD;
-      if (ev[j] != DEAD && spread((uint32_t)ev[j], clo) >= cut) keep |= 1u << j;
+      const uint32_t y = ev[j] == DEAD ? 0u : spread((uint32_t)ev[j], clo);
+      if (ev[j] != DEAD && y >= cut && (cut_hi == 0 || y < cut_hi)) keep |= 1u << j;
     }
     uint64_t slot = shard_reserve((uint32_t)__popc(keep), tcnt, tile, ntiles, 1);
 #pragma unroll
@@ -1118,7 +1122,7 @@ __global__ __launch_bounds__(BLOCK) void k_top_extract(const uint64_t *__restric
   }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_top_init(TopState ts) {
+__global__ __launch_bounds__(BLOCK) void k_top_init(TopState ts, bool first) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < ts.V; v += stride) {
     ts.minlo[v] = INVALID;
@@ -1126,7 +1130,7 @@ __global__ __launch_bounds__(BLOCK) void k_top_init(TopState ts) {
     ts.best[v] = NO_EDGE;
   }
   if (blockIdx.x == 0 && threadIdx.x < 3) ts.scal[threadIdx.x] = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) ts.st[ST_EXTRA] = 0;
+  if (first && blockIdx.x == 0 && threadIdx.x == 0) ts.st[ST_EXTRA] = 0;
 }
 
 __global__ void k_set_u64(uint64_t *p, uint64_t v) { *p = v; }
@@ -1223,7 +1227,8 @@ __device__ void top_flush(TopState &ts, const uint64_t *rec, unsigned n) {
 
 __global__ __launch_bounds__(TOPB) void k_top_hook0(TopState ts) {
   extern __shared__ uint16_t lds16[];
-  uint16_t *par = lds16, *cid = lds16 + (1u << TOP_BITS);
+  const bool big = ts.V > TOP_HOOK_LDS;
+  uint16_t *par = big ? ts.gpar : lds16, *cid = big ? ts.gcid : lds16 + TOP_HOOK_LDS;
   __shared__ uint64_t rec[TOP_REC];
   __shared__ unsigned s_cnt;
   if (threadIdx.x == 0) s_cnt = 0;
@@ -1261,10 +1266,11 @@ __global__ __launch_bounds__(TOPB) void k_top_round(TopEdges te, TopState ts, co
   if (ts.scal[2]) return;   // done (uniform)
   extern __shared__ uint16_t lds16[];
   uint16_t *comp = lds16;
-  unsigned long long *lbest = (unsigned long long *)(lds16 + (1u << TOP_BITS));
+  const uint32_t voff = (ts.V + 3) & ~3u;   // the minima 8-B aligned after the labels
+  unsigned long long *lbest = (unsigned long long *)(lds16 + voff);
   __shared__ uint64_t s_pre[NSHARD + 1];
   const uint32_t C = ts.scal[0];
-  const bool in_lds = C <= TOP_LDS_BEST;
+  const bool in_lds = C <= (uint32_t)((TOP_ROUND_LDS - voff * sizeof(uint16_t)) / sizeof(uint64_t));
   for (uint32_t v = threadIdx.x; v < ts.V; v += TOPB) comp[v] = ts.comp[v];
   if (in_lds)
     for (uint32_t c = threadIdx.x; c < C; c += TOPB) lbest[c] = NO_EDGE;
@@ -1310,12 +1316,13 @@ __global__ __launch_bounds__(TOPB) void k_top_hook(TopState ts) {
     return;
   }
   extern __shared__ uint16_t lds16[];
-  uint16_t *par = lds16, *cid = lds16 + (1u << TOP_BITS);
+  const uint32_t C = ts.scal[0];
+  const bool big = C > TOP_HOOK_LDS;
+  uint16_t *par = big ? ts.gpar : lds16, *cid = big ? ts.gcid : lds16 + TOP_HOOK_LDS;
   __shared__ uint64_t rec[TOP_REC];
   __shared__ unsigned s_cnt;
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
-  const uint32_t C = ts.scal[0];
   for (uint32_t base = 0; base < C; base += TOP_REC) {
     const uint32_t end = base + TOP_REC < C ? base + TOP_REC : C;
     for (uint32_t c = base + threadIdx.x; c < end; c += TOPB) {
@@ -1342,7 +1349,7 @@ __global__ __launch_bounds__(TOPB) void k_top_hook(TopState ts) {
 // Debug statistic (SHEEP_DEBUG_ETREE): live entries per block of 2^s spread positions
 // after a level (its next list plus the groups not yet activated).
 __global__ void k_dbg_blocks(const uint64_t *__restrict__ a, const uint64_t *__restrict__ st, const uint64_t *__restrict__ b,
-                             uint64_t nb_edges, int s, uint32_t clo, unsigned *__restrict__ cnt) {
+                             uint64_t nb_edges, int s, uint32_t clo, unsigned *__restrict__ cnt, uint32_t cut) {
   const uint64_t na = st[ST_KEPT] + st[ST_CONTR];
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na + nb_edges; i += stride) {
@@ -1388,14 +1395,16 @@ static uint64_t list_capacity(uint64_t m) { return 2 * m + TILE; }
 // The dense top block's edges -> their minimum spanning forest (see k_top_extract..k_top_hook):
 // appended to `next` behind the cut level's contractions (st[ST_EXTRA]); st[ST_CUT] makes
 // the next split drop the block's list entries, and the caller stops activating its groups.
+// The block is [cut, cut_hi) in spread positions (cut_hi 0: to the top) with vertices
+// [v0, v0 + V); its edges are its list entries plus groups [g0, g1) of r0 (the top block's).
 static void top_block(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, uint64_t g0, uint64_t g1, uint32_t cut,
-                      uint32_t clo, uint32_t v0, uint32_t V, uint64_t lcap) {
+                      uint32_t cut_hi, uint32_t clo, uint32_t v0, uint32_t V, uint64_t lcap, bool first) {
   const uint64_t tcap = (lcap + TILE - 1) / TILE * TILE + TILE;
   uint64_t *tl = c.get_as<uint64_t>("et_top_list", tcap);
   unsigned long long *tcnt = c.get_as<unsigned long long>("et_top_cnt", (uint64_t)NSHARD * SHARD_STRIDE);
   HIP_CHECK(hipMemsetAsync(tcnt, 0, (uint64_t)NSHARD * SHARD_STRIDE * sizeof(unsigned long long), c.stream));
   hipLaunchKernelGGL(k_top_extract, dim3(grid_tiles(lcap)), dim3(BLOCK), 0, c.stream, (const uint64_t *)next, st, cut,
-                     clo, tl, tcnt);
+                     cut_hi, clo, tl, tcnt);
   LAUNCH_CHECK();
   TopState ts;
   ts.minlo = c.get_as<uint32_t>("et_top_minlo", V);
@@ -1407,19 +1416,21 @@ static void top_block(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, 
   ts.out = next;
   ts.v0 = v0;
   ts.V = V;
-  hipLaunchKernelGGL(k_top_init, dim3(grid_for(V)), dim3(BLOCK), 0, c.stream, ts);
+  hipLaunchKernelGGL(k_top_init, dim3(grid_for(V)), dim3(BLOCK), 0, c.stream, ts, first);
   LAUNCH_CHECK();
   const TopEdges te{tl, tcnt, r0, g0, g1};
   hipLaunchKernelGGL(k_top_min0, dim3(grid_for(lcap + (g1 - g0))), dim3(BLOCK), 0, c.stream, te, ts, (const uint64_t *)st);
   LAUNCH_CHECK();
-  const size_t lds2 = 2 * ((size_t)1 << TOP_BITS) * sizeof(uint16_t);                        // par + cid
-  const size_t ldsr = ((size_t)1 << TOP_BITS) * sizeof(uint16_t) + TOP_LDS_BEST * sizeof(uint64_t);   // comp + minima
+  const size_t lds2 = 2 * (size_t)TOP_HOOK_LDS * sizeof(uint16_t);   // par + cid
+  const size_t ldsr = TOP_ROUND_LDS;                                  // labels + minima
+  ts.gpar = c.get_as<uint16_t>("et_top_gpar", V);
+  ts.gcid = c.get_as<uint16_t>("et_top_gcid", V);
   allow_lds((const void *)k_top_hook0, (int)lds2);
   allow_lds((const void *)k_top_hook, (int)lds2);
   allow_lds((const void *)k_top_round, (int)ldsr);
   hipLaunchKernelGGL(k_top_hook0, dim3(1), dim3(TOPB), lds2, c.stream, ts);
   LAUNCH_CHECK();
-  for (int r = 0; r <= TOP_BITS; ++r) {   // <= TOP_BITS + 1 rounds always finish (each halves the components)
+  for (int r = 0; r <= TOP_BITS_MAX; ++r) {   // <= bits + 1 rounds always finish (each halves the components)
     if (r == 6) {   // dense blocks are done by now: skip the idle launches
       HIP_CHECK(hipMemcpyAsync(c.h_scalars + 20, ts.scal + 2, sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
       c.sync();
@@ -1430,9 +1441,32 @@ static void top_block(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, 
     hipLaunchKernelGGL(k_top_hook, dim3(1), dim3(TOPB), lds2, c.stream, ts);
     LAUNCH_CHECK();
   }
-  // the cut for the next split (k_top_init zeroed ST_EXTRA before the hooks appended)
+  // the cut for the next split (the lowest block's; k_top_init zeroed ST_EXTRA before the
+  // first block's hooks appended)
   hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, c.stream, st + ST_CUT, (uint64_t)cut);
   LAUNCH_CHECK();
+}
+
+// Live list entries per block of 2^bits spread positions for the D blocks below cut0:
+// cnt[j] = entries with spread(lo) in [cut0 - (j + 1) 2^bits, cut0 - j 2^bits).
+__global__ __launch_bounds__(BLOCK) void k_top_counts(const uint64_t *__restrict__ list, const uint64_t *__restrict__ st,
+                                                      uint32_t cut0, int bits, uint32_t D, uint32_t clo,
+                                                      unsigned long long *__restrict__ cnt) {
+  __shared__ unsigned s_c[8];
+  if (threadIdx.x < 8) s_c[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t nl = st[ST_KEPT] + st[ST_CONTR];
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nl; i += stride) {
+    const uint64_t e = list[i];
+    if (e == DEAD) continue;
+    const uint32_t y = spread((uint32_t)e, clo);
+    if (y >= cut0) continue;
+    const uint32_t j = (cut0 - 1 - y) >> bits;
+    if (j < D) atomicAdd(&s_c[j], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < D && s_c[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], (unsigned long long)s_c[threadIdx.x]);
 }
 
 void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
@@ -1476,7 +1510,8 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   int top_lvl = -1, gcut = 0;
   uint64_t top_g0 = 0, top_g1 = 0;
   uint32_t top_v0 = 0, top_V = 0, top_cut = 0;
-  if (top_bits > FINB && top_bits <= L - 1 && top_bits <= TOP_BITS) {
+  if (getenv("SHEEP_TOP_BITS") && top_bits) top_bits = atoi(getenv("SHEEP_TOP_BITS"));   // (A/B runs)
+  if (top_bits > FINB && top_bits <= L - 1 && top_bits <= TOP_BITS_MAX) {
     std::vector<uint64_t> hs(2 * (size_t)L);
     HIP_CHECK(hipMemcpyAsync(hs.data(), seg, hs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
     c.sync();
@@ -1552,7 +1587,37 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     }
     if (lvl == top_lvl) {
       TimedRegion tr(c, "etree_top");
-      top_block(c, next, st, r0, top_g0, top_g1, top_cut, clo, top_v0, top_V, lcap);
+      top_block(c, next, st, r0, top_g0, top_g1, top_cut, 0, clo, top_v0, top_V, lcap, true);
+      // the blocks just below it are subproblems of their own too (list entries only): each
+      // dense one in a row is cut the same way (SHEEP_TOP_BLOCKS blocks in all, default 1)
+      static const int top_blocks = getenv("SHEEP_TOP_BLOCKS") ? atoi(getenv("SHEEP_TOP_BLOCKS")) : 1;
+      const uint32_t D = (uint32_t)std::min(std::max(top_blocks - 1, 0), 8);
+      if (D && ((uint64_t)(D + 1) << top_bits) <= (1ull << L)) {
+        unsigned long long *bc = c.get_as<unsigned long long>("et_top_bcnt", 8);
+        HIP_CHECK(hipMemsetAsync(bc, 0, 8 * sizeof(unsigned long long), c.stream));
+        hipLaunchKernelGGL(k_top_counts, dim3(grid_for(lcap)), dim3(BLOCK), 0, c.stream, (const uint64_t *)next,
+                           (const uint64_t *)st, top_cut, top_bits, D, clo, bc);
+        LAUNCH_CHECK();
+        unsigned long long hb[8];
+        HIP_CHECK(hipMemcpyAsync(hb, bc, sizeof hb, hipMemcpyDeviceToHost, c.stream));
+        c.sync();
+        auto first_at = [&](uint64_t y) {   // min vertex x with spread(x) >= y
+          uint64_t a = 0, z = n;
+          while (a < z) {
+            const uint64_t x = (a + z) / 2;
+            if (x + ((x * (uint64_t)clo) >> 32) >= y) z = x; else a = x + 1;
+          }
+          return a;
+        };
+        for (uint32_t j = 0; j < D; ++j) {
+          const uint32_t hi_cut = top_cut - (j << top_bits), lo_cut = hi_cut - (1u << top_bits);
+          const uint64_t v0 = first_at(lo_cut), V = first_at(hi_cut) - v0;
+          if (V < 2 || hb[j] < TOP_DENSE * V) break;
+          top_block(c, next, st, r0, 0, 0, lo_cut, hi_cut, clo, (uint32_t)v0, (uint32_t)V, lcap, false);
+          if (g_debug_etree) fprintf(stderr, "etree block %u below the top: vertices %lu list entries %llu -> MSF\n", j,
+                                     (unsigned long)V, hb[j]);
+        }
+      }
       if (g_debug_etree) {
         uint64_t h[ST_ROW];
         unsigned hs[4];
@@ -1566,7 +1631,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     }
     if (g_debug_etree && s >= 8 && s <= 15) {   // how the live edges spread over the 2^s blocks
       uint64_t hs[2] = {0, 0};
-      if (s > 0) {
+      if (s > 0 && gcut == 0) {   // (a cut top block's groups are not live any more)
         HIP_CHECK(hipMemcpyAsync(&hs[0], seg + (s - 1), sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
         HIP_CHECK(hipMemcpyAsync(&hs[1], seg + L, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
       }
@@ -1575,7 +1640,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       HIP_CHECK(hipMemsetAsync(cnt, 0, nblk * sizeof(unsigned), c.stream));
       c.sync();
       hipLaunchKernelGGL(k_dbg_blocks, dim3(1024), dim3(BLOCK), 0, c.stream, (const uint64_t *)next, (const uint64_t *)st,
-                         r0 + hs[0], hs[1] - hs[0], s, clo, cnt);
+                         r0 + hs[0], hs[1] - hs[0], s, clo, cnt, lvl > top_lvl && top_lvl >= 0 ? top_cut : 0u);
       LAUNCH_CHECK();
       std::vector<unsigned> h(nblk);
       HIP_CHECK(hipMemcpyAsync(h.data(), cnt, nblk * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));

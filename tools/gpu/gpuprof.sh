@@ -1,4 +1,4 @@
-# Round-2 profile set (see profiles/r2/README.md): kernel stats + trace of a bench run,
+# Round-2 profile set (see profiles/r4/README.md): kernel stats + trace of a bench run,
 # generation-free PMC traffic per path step (2-step minus 1-step runs), bench lines
 set -o pipefail
 W=${W:-26}; K=${K:-64}
