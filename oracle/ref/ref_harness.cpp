@@ -261,11 +261,28 @@ int main(int argc, char **argv) {
     auto sec = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
       return std::chrono::duration<double>(b - a).count();
     };
-    if (rank == 0)
+    if (rank == 0) {
+      // FNV-1a digests of what the flow produced (untimed): the sequence, the merged tree and
+      // the parts, so runs of the two sequence forms can be compared
+      auto fnv = [](const void *p, size_t bytes) {
+        uint64_t h = 1469598103934665603ull;
+        for (size_t i = 0; i < bytes; ++i) h = (h ^ ((const unsigned char *)p)[i]) * 1099511628211ull;
+        return (unsigned long long)h;
+      };
+      const unsigned long long hs = fnv(seq.data(), seq.size() * sizeof(vid_t));
+      std::vector<uint32_t> tw(2 * (size_t)tree.jnodes.size());
+      for (jnid_t i = 0; i < tree.jnodes.size(); ++i) {
+        tw[2 * (size_t)i] = tree.jnodes.parent(i);
+        tw[2 * (size_t)i + 1] = tree.jnodes.pst_weight(i);
+      }
+      const unsigned long long ht = fnv(tw.data(), tw.size() * sizeof(uint32_t));
+      const unsigned long long hp = fnv(p.parts.data(), p.parts.size() * sizeof(part_t));
       printf("{\"seconds\": %.6f, \"ranks\": %d, \"threads\": %d, \"nodes\": %zu, \"sequence\": \"%s\", "
-             "\"phases\": {\"sort\": %.6f, \"map\": %.6f, \"reduce\": %.6f, \"partition\": %.6f}}\n",
+             "\"phases\": {\"sort\": %.6f, \"map\": %.6f, \"reduce\": %.6f, \"partition\": %.6f}, "
+             "\"fnv\": {\"seq\": \"%016llx\", \"tree\": \"%016llx\", \"parts\": \"%016llx\"}}\n",
              sec(t0, t4), size, omp_get_max_threads(), seq.size(), literal ? "mpiSequence" : "degreeSequence",
-             sec(t0, t1), sec(t1, t2), sec(t2, t3), sec(t3, t4));
+             sec(t0, t1), sec(t1, t2), sec(t2, t3), sec(t3, t4), hs, ht, hp);
+    }
     MPI_Finalize();
     return 0;
   }
