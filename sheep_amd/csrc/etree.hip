@@ -636,6 +636,9 @@ __device__ __forceinline__ uint32_t classify(uint64_t e, int s, uint32_t clo, YR
 // first active at this level (none below gcut: the groups of a cut top block).  After a
 // cut, the list entries inside the top block (spread(lo) >= cut, ahead of the MSF edges)
 // read as dead.
+// CUT: the one level right after a cut (the level kernels are instantiated without the
+// filter everywhere else: the extra test in every load cost the split ~50 % at RMAT-26).
+template <bool CUT>
 struct SplitIn {
   const uint64_t *list, *r0;
   uint64_t len, base, rb, m;
@@ -644,17 +647,17 @@ struct SplitIn {
                      int gcut, uint32_t c)
       : list(l), r0(r), clo(c) {
     base = prev ? prev[ST_KEPT] + prev[ST_CONTR] : 0;
-    len = prev ? base + prev[ST_EXTRA] : 0;
-    cut = prev ? (uint32_t)prev[ST_CUT] : 0;
+    len = CUT ? base + prev[ST_EXTRA] : base;
+    cut = CUT ? (uint32_t)prev[ST_CUT] : 0;
     rb = seg[s];
     m = len + (s < gcut ? 0 : seg[L + s] - rb);
   }
   __device__ __forceinline__ uint64_t operator[](uint64_t i) const {
-    if (i < len) {
+    if (CUT && i < len) {
       const uint64_t e = list[i];
-      return (cut && i < base && e != DEAD && spread((uint32_t)e, clo) >= cut) ? DEAD : e;
+      return (i < base && e != DEAD && spread((uint32_t)e, clo) >= cut) ? DEAD : e;
     }
-    return i < m ? r0[rb + (i - len)] : DEAD;
+    return i < len ? list[i] : i < m ? r0[rb + (i - len)] : DEAD;
   }
 };
 
@@ -669,6 +672,7 @@ __device__ __forceinline__ uint64_t pack3(uint32_t c) {
   return (uint64_t)(c & 1) | ((uint64_t)((c >> 1) & 1) << 16) | ((uint64_t)(c >> 2) << 32);
 }
 
+template <bool CUT>
 __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
                                                        uint64_t *__restrict__ st, int s, uint32_t clo, YRange yr,
                                                        const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
@@ -677,7 +681,7 @@ __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restric
   // exclusive scan of 3 ntiles + 1 entries (the length in st, read by the scan).
   // clean: the previous level's k_level_clean, run first (clean.st == nullptr: none).
   if (clean.st) level_clean(clean);
-  const SplitIn in(list, prev, r0, seg, s, L, gcut, clo);
+  const SplitIn<CUT> in(list, prev, r0, seg, s, L, gcut, clo);
   const uint64_t ntiles = (in.m + SPLIT_TILE - 1) / SPLIT_TILE, cstride = ntiles;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st[ST_LIVE] = in.len;
@@ -709,13 +713,14 @@ __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restric
 // row's offsets are relative to its first entry; the row totals go to st.  Each class's
 // run of the tile is first placed in LDS at its thread-major rank, then copied out by
 // consecutive lanes (per-thread stores to the same positions: 16.6 against 12.2 ms).
+template <bool CUT>
 __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
                                                        uint64_t *__restrict__ st, int s, uint32_t clo, YRange yr,
                                                        const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
                                                        int L, int gcut, const uint64_t *__restrict__ cnt,
                                                        uint64_t *__restrict__ next, uint64_t *__restrict__ lbuf,
                                                        uint64_t *__restrict__ xbuf) {
-  const SplitIn in(list, prev, r0, seg, s, L, gcut, clo);
+  const SplitIn<CUT> in(list, prev, r0, seg, s, L, gcut, clo);
   const uint64_t ntiles = (in.m + SPLIT_TILE - 1) / SPLIT_TILE, cstride = ntiles;
   const uint64_t b0 = cnt[0], b1 = cnt[cstride], b2 = cnt[2 * cstride], b3 = cnt[3 * cstride];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1545,11 +1550,14 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       // the previous level's clean first (its counters, adoptions and resets)
       const LevelClean clean = lvl ? LevelClean{lbuf, xbuf, xtop, prev, uf, mt, top, claim, n, tagged, lvl - 1, parent, csets}
                                    : LevelClean{};
-      hipLaunchKernelGGL(k_split_count, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo, yr,
+      const bool after_cut = top_lvl >= 0 && lvl == top_lvl + 1;
+      hipLaunchKernelGGL(after_cut ? k_split_count<true> : k_split_count<false>, dim3(gt2), dim3(BLOCK), 0, c.stream,
+                         (const uint64_t *)cur, prev, st, s, clo, yr,
                          (const uint64_t *)r0, (const uint64_t *)seg, L, gcut, tcnt, clean);
       LAUNCH_CHECK();
       scan_exclusive_u64_dev(c, tcnt, tcnt, 3 * cstride + 1, st + ST_SCANN);
-      hipLaunchKernelGGL(k_split_write, dim3(gt2), dim3(BLOCK), 0, c.stream, (const uint64_t *)cur, prev, st, s, clo, yr,
+      hipLaunchKernelGGL(after_cut ? k_split_write<true> : k_split_write<false>, dim3(gt2), dim3(BLOCK), 0, c.stream,
+                         (const uint64_t *)cur, prev, st, s, clo, yr,
                          (const uint64_t *)r0, (const uint64_t *)seg, L, gcut, (const uint64_t *)tcnt, next, lbuf, xbuf);
       LAUNCH_CHECK();
     }
@@ -1803,7 +1811,8 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
       group_edges_by_lo(c, edges, m, lg, pst, r0, seg, counted);
     }
     TimedRegion tr(c, "etree", 8 * m);
-    etree_from_edges(c, r0, m, n, parent, seg, FIN_MAP, -1, 0, 0, TOP_BITS);
+    static const int fin_map = getenv("SHEEP_FIN_MAP") ? atoi(getenv("SHEEP_FIN_MAP")) : FIN_MAP;   // (A/B runs)
+    etree_from_edges(c, r0, m, n, parent, seg, fin_map, -1, 0, 0, TOP_BITS);
   } else {
     fill_u32(c, parent, n, INVALID);
   }

@@ -62,12 +62,17 @@ __global__ __launch_bounds__(BLOCK) void k_reduce(const T *__restrict__ in, uint
   if (threadIdx.x == 0) {
     T t = 0;
     for (int w = 0; w < BLOCK / WAVE; ++w) t += lds[w];
-    (void)atomicExch(&sums[blockIdx.x], t);
-    // the block sum is visible device-wide before the ticket: a release fence, and the
-    // ticket add itself a release at agent scope; the last block's reads of the sums are
-    // atomics (performed coherently, after its acquire below)
-    __threadfence();
-    s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    // The block sum, then the ticket: both read-modify-write atomics, performed at the
+    // coherence point, and the ticket add is issued only after the sum's atomic has
+    // RETURNED — `zero` is 0 computed from its result inside asm, so the compiler must wait
+    // for the result and cannot fold the dependency away.  The last block reads the sums
+    // with atomics too, after its own ticket add returned.  (A __threadfence() or a release
+    // ticket add orders the same at agent scope but writes back the XCD's L2 in every
+    // block: the etree's level scans took +4 ms per RMAT-26 step with it.)
+    const T old = atomicExch(&sums[blockIdx.x], t);
+    uint32_t zero;
+    asm volatile("v_and_b32 %0, 0, %1" : "=v"(zero) : "v"((uint32_t)old));
+    s_last = atomicAdd(ticket, 1u + zero) == gridDim.x - 1;
   }
   __syncthreads();
   if (!s_last) return;
