@@ -1127,6 +1127,53 @@ __global__ __launch_bounds__(BLOCK) void k_top_extract(const uint64_t *__restric
   }
 }
 
+// The list entries of the cut blocks, one pass: block 0 = spread(lo) >= cut0 (the top
+// block), block j >= 1 = [cut0 - j 2^bits, cut0 - (j - 1) 2^bits); block j's entries go to
+// region j of tl (sharded appends on counter set j).  st[ST_TOPNT] = the pass's tile count.
+constexpr int TOP_NB_MAX = 9;   // the top block and up to 8 below it
+constexpr uint64_t TOP_CSET = (uint64_t)NSHARD * SHARD_STRIDE;
+__global__ __launch_bounds__(BLOCK) void k_top_extract_multi(const uint64_t *__restrict__ list, uint64_t *__restrict__ st,
+                                                             uint32_t cut0, int bits, uint32_t nb, uint32_t clo,
+                                                             uint64_t *__restrict__ tl, uint64_t tcap,
+                                                             unsigned long long *__restrict__ tcnt) {
+  const uint64_t nl = st[ST_KEPT] + st[ST_CONTR];
+  const uint64_t ntiles = (nl + TILE - 1) / TILE;
+  if (blockIdx.x == 0 && threadIdx.x == 0) st[ST_TOPNT] = ntiles;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    uint64_t ev[TILE_ITEMS];
+    uint32_t blk[TILE_ITEMS];
+#pragma unroll
+    for (int j = 0; j < TILE_ITEMS; ++j) {
+      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
+      ev[j] = i < nl ? list[i] : DEAD;
+      blk[j] = nb;
+      if (ev[j] != DEAD) {
+        const uint32_t y = spread((uint32_t)ev[j], clo);
+        blk[j] = y >= cut0 ? 0u : 1u + ((cut0 - 1 - y) >> bits);
+      }
+    }
+    for (uint32_t b = 0; b < nb; ++b) {   // (uniform: every thread takes part in each reserve)
+      uint32_t keep = 0;
+#pragma unroll
+      for (int j = 0; j < TILE_ITEMS; ++j) keep |= (blk[j] == b ? 1u : 0u) << j;
+      if (!__syncthreads_or(keep != 0)) continue;
+      uint64_t slot = shard_reserve((uint32_t)__popc(keep), tcnt + b * TOP_CSET, tile, ntiles, 1);
+#pragma unroll
+      for (int j = 0; j < TILE_ITEMS; ++j)
+        if (keep & (1u << j)) tl[b * tcap + slot++] = ev[j];
+    }
+  }
+}
+
+// cnt[b] = the extraction's entries of block b (its 64 shard counters summed)
+__global__ void k_top_sum_counts(const unsigned long long *__restrict__ tcnt, uint32_t nb,
+                                 unsigned long long *__restrict__ cnt) {
+  const uint32_t b = blockIdx.x, k = threadIdx.x;   // one wave per block
+  unsigned long long v = k < NSHARD ? tcnt[b * TOP_CSET + (uint64_t)k * SHARD_STRIDE] : 0;
+  v = wave_sum(v);
+  if (k == 0 && b < nb) cnt[b] = v;
+}
+
 __global__ __launch_bounds__(BLOCK) void k_top_init(TopState ts, bool first) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < ts.V; v += stride) {
@@ -1165,6 +1212,43 @@ __global__ __launch_bounds__(BLOCK) void k_top_min0(TopEdges te, TopState ts, co
     const uint32_t v = wave_min(same ? h : INVALID);
     if ((int)__lane_id() == first && v < ts.minhi[l0]) atomicMin(&ts.minhi[l0], v);
     if (ok && !same && h < ts.minhi[l]) atomicMin(&ts.minhi[l], h);
+  }
+}
+
+// Round 0 with each workgroup's lowest-lower-neighbour minima in LDS (<= 2^15 vertices, one
+// workgroup per CU): the random global atomics of k_top_min0 (RMAT-26's top block: 0.86 ms
+// for 50 M edges) become LDS atomics and one read-checked flush per vertex and workgroup.
+// minhi (only vertices without a lower neighbour use it) keeps the wave-combined global
+// atomics: the edges come grouped by lo, so a wave's lanes mostly share it.
+__global__ __launch_bounds__(TOPB) void k_top_min0_lds(TopEdges te, TopState ts, const uint64_t *__restrict__ st) {
+  extern __shared__ uint32_t lmin[];
+  __shared__ uint64_t s_pre[NSHARD + 1];
+  for (uint32_t v = threadIdx.x; v < ts.V; v += TOPB) lmin[v] = INVALID;
+  top_prefix(te, s_pre);
+  __syncthreads();
+  const uint64_t ntiles = st[ST_TOPNT], total = s_pre[NSHARD] + (te.g1 - te.g0);
+  const uint64_t per = (total + gridDim.x - 1) / gridDim.x;   // a contiguous chunk per workgroup
+  const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < total ? b0 + per : total;
+  const uint64_t iters = b1 > b0 ? (b1 - b0 + TOPB - 1) / TOPB : 0;
+  for (uint64_t it = 0, i = b0 + threadIdx.x; it < iters; ++it, i += TOPB) {   // wave-uniform trip count
+    const bool live = i < b1;
+    const uint64_t e = live ? top_at(te, s_pre, ntiles, i) : DEAD;
+    const bool ok = live && e != DEAD;
+    const uint32_t l = (uint32_t)e - ts.v0, h = (uint32_t)(e >> 32) - ts.v0;
+    if (ok && l < lmin[h]) atomicMin(&lmin[h], l);
+    const uint64_t lm = __ballot(ok);
+    if (!lm) continue;
+    const int first = __ffsll((unsigned long long)lm) - 1;
+    const uint32_t l0 = __shfl(l, first, 64);
+    const bool same = ok && l == l0;
+    const uint32_t v = wave_min(same ? h : INVALID);
+    if ((int)__lane_id() == first && v < ts.minhi[l0]) atomicMin(&ts.minhi[l0], v);
+    if (ok && !same && h < ts.minhi[l]) atomicMin(&ts.minhi[l], h);
+  }
+  __syncthreads();
+  for (uint32_t v = threadIdx.x; v < ts.V; v += TOPB) {
+    const uint32_t x = lmin[v];
+    if (x != INVALID && x < ts.minlo[v]) atomicMin(&ts.minlo[v], x);
   }
 }
 
@@ -1397,81 +1481,117 @@ static uint64_t list_capacity(uint64_t m) { return 2 * m + TILE; }
 // read only.
 // One pass of launches per level, no host synchronisation inside the loop (see the
 // stats row above); the stats come back once at the end for the timers / debug log.
-// The dense top block's edges -> their minimum spanning forest (see k_top_extract..k_top_hook):
-// appended to `next` behind the cut level's contractions (st[ST_EXTRA]); st[ST_CUT] makes
-// the next split drop the block's list entries, and the caller stops activating its groups.
-// The block is [cut, cut_hi) in spread positions (cut_hi 0: to the top) with vertices
-// [v0, v0 + V); its edges are its list entries plus groups [g0, g1) of r0 (the top block's).
-static void top_block(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, uint64_t g0, uint64_t g1, uint32_t cut,
-                      uint32_t cut_hi, uint32_t clo, uint32_t v0, uint32_t V, uint64_t lcap, bool first) {
+// The dense blocks' edges -> their minimum spanning forests (k_top_extract_multi ..
+// k_top_hook).  Block 0 is the top block [cut0, 2^L) (its list entries plus groups [g0, g1)
+// of r0), block j >= 1 the 2^bits positions below block j - 1 (list entries only); the
+// blocks below the top are cut while they are dense (up to nb_max - 1 of them,
+// SHEEP_TOP_BLOCKS).  The MSF edges are appended to `next` behind the cut level's
+// contractions (st[ST_EXTRA]); st[ST_CUT] (the lowest cut block's start) makes the next split
+// drop the blocks' list entries, and the caller stops activating the top block's groups.
+// One host sync for the blocks' sizes, one to skip the idle Borůvka rounds.  Returns the
+// number of blocks cut.
+static uint32_t top_blocks(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, uint64_t g0, uint64_t g1,
+                           uint32_t cut0, int bits, uint32_t nb_max, uint32_t clo, uint64_t n, uint64_t lcap) {
   const uint64_t tcap = (lcap + TILE - 1) / TILE * TILE + TILE;
-  uint64_t *tl = c.get_as<uint64_t>("et_top_list", tcap);
-  unsigned long long *tcnt = c.get_as<unsigned long long>("et_top_cnt", (uint64_t)NSHARD * SHARD_STRIDE);
-  HIP_CHECK(hipMemsetAsync(tcnt, 0, (uint64_t)NSHARD * SHARD_STRIDE * sizeof(unsigned long long), c.stream));
-  hipLaunchKernelGGL(k_top_extract, dim3(grid_tiles(lcap)), dim3(BLOCK), 0, c.stream, (const uint64_t *)next, st, cut,
-                     cut_hi, clo, tl, tcnt);
+  nb_max = std::min<uint32_t>(std::max<uint32_t>(nb_max, 1), TOP_NB_MAX);
+  while (nb_max > 1 && ((uint64_t)nb_max << bits) > cut0 + (1ull << bits)) --nb_max;   // blocks must lie above 0
+  uint64_t *tl = c.get_as<uint64_t>("et_top_list", nb_max * tcap);
+  unsigned long long *tcnt = c.get_as<unsigned long long>("et_top_cnt", nb_max * TOP_CSET + TOP_NB_MAX);
+  unsigned long long *bcnt = tcnt + nb_max * TOP_CSET;
+  HIP_CHECK(hipMemsetAsync(tcnt, 0, nb_max * TOP_CSET * sizeof(unsigned long long), c.stream));
+  hipLaunchKernelGGL(k_top_extract_multi, dim3(grid_tiles(lcap)), dim3(BLOCK), 0, c.stream, (const uint64_t *)next, st,
+                     cut0, bits, nb_max, clo, tl, tcap, tcnt);
   LAUNCH_CHECK();
-  TopState ts;
-  ts.minlo = c.get_as<uint32_t>("et_top_minlo", V);
-  ts.minhi = c.get_as<uint32_t>("et_top_minhi", V);
-  ts.comp = c.get_as<uint16_t>("et_top_comp", V);
-  ts.best = c.get_as<unsigned long long>("et_top_best", V);
-  ts.scal = c.get_as<unsigned>("et_top_scal", 4);
-  ts.st = st;
-  ts.out = next;
-  ts.v0 = v0;
-  ts.V = V;
-  hipLaunchKernelGGL(k_top_init, dim3(grid_for(V)), dim3(BLOCK), 0, c.stream, ts, first);
-  LAUNCH_CHECK();
-  const TopEdges te{tl, tcnt, r0, g0, g1};
-  hipLaunchKernelGGL(k_top_min0, dim3(grid_for(lcap + (g1 - g0))), dim3(BLOCK), 0, c.stream, te, ts, (const uint64_t *)st);
-  LAUNCH_CHECK();
+  auto first_at = [&](uint64_t y) {   // min vertex x with spread(x) >= y
+    uint64_t a = 0, z = n;
+    while (a < z) {
+      const uint64_t x = (a + z) / 2;
+      if (x + ((x * (uint64_t)clo) >> 32) >= y) z = x; else a = x + 1;
+    }
+    return a;
+  };
+  uint32_t nb = 1;
+  if (nb_max > 1) {   // the blocks below the top: how many in a row are dense
+    hipLaunchKernelGGL(k_top_sum_counts, dim3(nb_max), dim3(WAVE), 0, c.stream, (const unsigned long long *)tcnt, nb_max,
+                       bcnt);
+    LAUNCH_CHECK();
+    unsigned long long hb[TOP_NB_MAX];
+    HIP_CHECK(hipMemcpyAsync(hb, bcnt, nb_max * sizeof(unsigned long long), hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+    while (nb < nb_max) {
+      const uint64_t hi_cut = cut0 - ((uint64_t)(nb - 1) << bits), lo_cut = hi_cut - (1ull << bits);
+      const uint64_t V = first_at(hi_cut) - first_at(lo_cut);
+      if (V < 2 || hb[nb] < TOP_DENSE * V) break;
+      ++nb;
+    }
+  }
+  const uint64_t VMAX = 1ull << bits;
+  uint32_t *minlo = c.get_as<uint32_t>("et_top_minlo", nb * VMAX), *minhi = c.get_as<uint32_t>("et_top_minhi", nb * VMAX);
+  uint16_t *comp = c.get_as<uint16_t>("et_top_comp", nb * VMAX);
+  unsigned long long *best = c.get_as<unsigned long long>("et_top_best", nb * VMAX);
+  unsigned *scal = c.get_as<unsigned>("et_top_scal", 4 * nb);
+  uint16_t *gpar = c.get_as<uint16_t>("et_top_gpar", VMAX), *gcid = c.get_as<uint16_t>("et_top_gcid", VMAX);
+  std::vector<TopState> ts(nb);
+  std::vector<TopEdges> te(nb);
+  for (uint32_t b = 0; b < nb; ++b) {
+    const uint64_t hi_cut = b == 0 ? (1ull << 32) : cut0 - ((uint64_t)(b - 1) << bits);
+    const uint64_t lo_cut = b == 0 ? cut0 : hi_cut - (1ull << bits);
+    const uint64_t v0 = first_at(lo_cut), v1 = b == 0 ? n : first_at(hi_cut);
+    ts[b].minlo = minlo + b * VMAX;
+    ts[b].minhi = minhi + b * VMAX;
+    ts[b].comp = comp + b * VMAX;
+    ts[b].best = best + b * VMAX;
+    ts[b].scal = scal + 4 * b;
+    ts[b].st = st;
+    ts[b].out = next;
+    ts[b].gpar = gpar;   // (the hooks of the blocks run one after another)
+    ts[b].gcid = gcid;
+    ts[b].v0 = (uint32_t)v0;
+    ts[b].V = (uint32_t)(v1 - v0);
+    te[b] = TopEdges{tl + b * tcap, tcnt + b * TOP_CSET, r0, b == 0 ? g0 : 0, b == 0 ? g1 : 0};
+  }
   const size_t lds2 = 2 * (size_t)TOP_HOOK_LDS * sizeof(uint16_t);   // par + cid
   const size_t ldsr = TOP_ROUND_LDS;                                  // labels + minima
-  ts.gpar = c.get_as<uint16_t>("et_top_gpar", V);
-  ts.gcid = c.get_as<uint16_t>("et_top_gcid", V);
   allow_lds((const void *)k_top_hook0, (int)lds2);
   allow_lds((const void *)k_top_hook, (int)lds2);
   allow_lds((const void *)k_top_round, (int)ldsr);
-  hipLaunchKernelGGL(k_top_hook0, dim3(1), dim3(TOPB), lds2, c.stream, ts);
-  LAUNCH_CHECK();
+  allow_lds((const void *)k_top_min0_lds, (int)(TOP_HOOK_LDS * sizeof(uint32_t)));
+  for (uint32_t b = 0; b < nb; ++b) {
+    hipLaunchKernelGGL(k_top_init, dim3(grid_for(ts[b].V)), dim3(BLOCK), 0, c.stream, ts[b], b == 0);
+    LAUNCH_CHECK();
+    if (ts[b].V <= TOP_HOOK_LDS)
+      hipLaunchKernelGGL(k_top_min0_lds, dim3(256), dim3(TOPB), TOP_HOOK_LDS * sizeof(uint32_t), c.stream, te[b], ts[b],
+                         (const uint64_t *)st);
+    else
+      hipLaunchKernelGGL(k_top_min0, dim3(grid_for(lcap + (te[b].g1 - te[b].g0))), dim3(BLOCK), 0, c.stream, te[b], ts[b],
+                         (const uint64_t *)st);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_top_hook0, dim3(1), dim3(TOPB), lds2, c.stream, ts[b]);
+    LAUNCH_CHECK();
+  }
+  std::vector<bool> live(nb, true);
   for (int r = 0; r <= TOP_BITS_MAX; ++r) {   // <= bits + 1 rounds always finish (each halves the components)
-    if (r == 6) {   // dense blocks are done by now: skip the idle launches
-      HIP_CHECK(hipMemcpyAsync(c.h_scalars + 20, ts.scal + 2, sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
+    if (r == 2) {   // dense blocks are done by now: skip the idle launches
+      std::vector<unsigned> h(4 * nb);
+      HIP_CHECK(hipMemcpyAsync(h.data(), scal, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
       c.sync();
-      if (*(unsigned *)(c.h_scalars + 20)) break;
+      bool any = false;
+      for (uint32_t b = 0; b < nb; ++b) any |= (live[b] = h[4 * b + 2] == 0);
+      if (!any) break;
     }
-    hipLaunchKernelGGL(k_top_round, dim3(256), dim3(TOPB), ldsr, c.stream, te, ts, (const uint64_t *)st);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_top_hook, dim3(1), dim3(TOPB), lds2, c.stream, ts);
-    LAUNCH_CHECK();
+    for (uint32_t b = 0; b < nb; ++b) {
+      if (!live[b]) continue;
+      hipLaunchKernelGGL(k_top_round, dim3(256), dim3(TOPB), ldsr, c.stream, te[b], ts[b], (const uint64_t *)st);
+      LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_top_hook, dim3(1), dim3(TOPB), lds2, c.stream, ts[b]);
+      LAUNCH_CHECK();
+    }
   }
-  // the cut for the next split (the lowest block's; k_top_init zeroed ST_EXTRA before the
-  // first block's hooks appended)
-  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, c.stream, st + ST_CUT, (uint64_t)cut);
+  // the cut for the next split: the lowest cut block's start
+  const uint64_t low = nb == 1 ? cut0 : cut0 - ((uint64_t)(nb - 1) << bits);
+  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, c.stream, st + ST_CUT, low);
   LAUNCH_CHECK();
-}
-
-// Live list entries per block of 2^bits spread positions for the D blocks below cut0:
-// cnt[j] = entries with spread(lo) in [cut0 - (j + 1) 2^bits, cut0 - j 2^bits).
-__global__ __launch_bounds__(BLOCK) void k_top_counts(const uint64_t *__restrict__ list, const uint64_t *__restrict__ st,
-                                                      uint32_t cut0, int bits, uint32_t D, uint32_t clo,
-                                                      unsigned long long *__restrict__ cnt) {
-  __shared__ unsigned s_c[8];
-  if (threadIdx.x < 8) s_c[threadIdx.x] = 0;
-  __syncthreads();
-  const uint64_t nl = st[ST_KEPT] + st[ST_CONTR];
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nl; i += stride) {
-    const uint64_t e = list[i];
-    if (e == DEAD) continue;
-    const uint32_t y = spread((uint32_t)e, clo);
-    if (y >= cut0) continue;
-    const uint32_t j = (cut0 - 1 - y) >> bits;
-    if (j < D) atomicAdd(&s_c[j], 1u);
-  }
-  __syncthreads();
-  if (threadIdx.x < D && s_c[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], (unsigned long long)s_c[threadIdx.x]);
+  return nb;
 }
 
 void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
@@ -1514,7 +1634,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   // replaced by their minimum spanning forest when its groups are dense.
   int top_lvl = -1, gcut = 0;
   uint64_t top_g0 = 0, top_g1 = 0;
-  uint32_t top_v0 = 0, top_V = 0, top_cut = 0;
+  uint32_t top_V = 0, top_cut = 0;
   if (getenv("SHEEP_TOP_BITS") && top_bits) top_bits = atoi(getenv("SHEEP_TOP_BITS"));   // (A/B runs)
   if (top_bits > FINB && top_bits <= L - 1 && top_bits <= TOP_BITS_MAX) {
     std::vector<uint64_t> hs(2 * (size_t)L);
@@ -1526,7 +1646,6 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       const uint64_t x = (a + z) / 2;
       if (x + ((x * (uint64_t)clo) >> 32) >= top_cut) z = x; else a = x + 1;
     }
-    top_v0 = (uint32_t)a;
     top_V = (uint32_t)(n - a);
     top_g0 = hs[top_bits - 1];
     top_g1 = hs[L];
@@ -1595,46 +1714,18 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     }
     if (lvl == top_lvl) {
       TimedRegion tr(c, "etree_top");
-      top_block(c, next, st, r0, top_g0, top_g1, top_cut, 0, clo, top_v0, top_V, lcap, true);
-      // the blocks just below it are subproblems of their own too (list entries only): each
-      // dense one in a row is cut the same way (SHEEP_TOP_BLOCKS blocks in all, default 1)
-      static const int top_blocks = getenv("SHEEP_TOP_BLOCKS") ? atoi(getenv("SHEEP_TOP_BLOCKS")) : 1;
-      const uint32_t D = (uint32_t)std::min(std::max(top_blocks - 1, 0), 8);
-      if (D && ((uint64_t)(D + 1) << top_bits) <= (1ull << L)) {
-        unsigned long long *bc = c.get_as<unsigned long long>("et_top_bcnt", 8);
-        HIP_CHECK(hipMemsetAsync(bc, 0, 8 * sizeof(unsigned long long), c.stream));
-        hipLaunchKernelGGL(k_top_counts, dim3(grid_for(lcap)), dim3(BLOCK), 0, c.stream, (const uint64_t *)next,
-                           (const uint64_t *)st, top_cut, top_bits, D, clo, bc);
-        LAUNCH_CHECK();
-        unsigned long long hb[8];
-        HIP_CHECK(hipMemcpyAsync(hb, bc, sizeof hb, hipMemcpyDeviceToHost, c.stream));
-        c.sync();
-        auto first_at = [&](uint64_t y) {   // min vertex x with spread(x) >= y
-          uint64_t a = 0, z = n;
-          while (a < z) {
-            const uint64_t x = (a + z) / 2;
-            if (x + ((x * (uint64_t)clo) >> 32) >= y) z = x; else a = x + 1;
-          }
-          return a;
-        };
-        for (uint32_t j = 0; j < D; ++j) {
-          const uint32_t hi_cut = top_cut - (j << top_bits), lo_cut = hi_cut - (1u << top_bits);
-          const uint64_t v0 = first_at(lo_cut), V = first_at(hi_cut) - v0;
-          if (V < 2 || hb[j] < TOP_DENSE * V) break;
-          top_block(c, next, st, r0, 0, 0, lo_cut, hi_cut, clo, (uint32_t)v0, (uint32_t)V, lcap, false);
-          if (g_debug_etree) fprintf(stderr, "etree block %u below the top: vertices %lu list entries %llu -> MSF\n", j,
-                                     (unsigned long)V, hb[j]);
-        }
-      }
+      static const int top_nb = getenv("SHEEP_TOP_BLOCKS") ? atoi(getenv("SHEEP_TOP_BLOCKS")) : 1;
+      const uint32_t nbc = top_blocks(c, next, st, r0, top_g0, top_g1, top_cut, top_bits, (uint32_t)top_nb, clo, n, lcap);
       if (g_debug_etree) {
         uint64_t h[ST_ROW];
         unsigned hs[4];
         HIP_CHECK(hipMemcpyAsync(h, st, sizeof h, hipMemcpyDeviceToHost, c.stream));
         HIP_CHECK(hipMemcpyAsync(hs, c.get_as<unsigned>("et_top_scal", 4), sizeof hs, hipMemcpyDeviceToHost, c.stream));
         c.sync();
-        fprintf(stderr, "etree top block after s %d: vertices %u group edges %lu list entries scanned %lu -> MSF edges %lu "
-                        "(components left %u, done %u)\n", top_bits, top_V, (unsigned long)(top_g1 - top_g0),
-                (unsigned long)(h[ST_KEPT] + h[ST_CONTR]), (unsigned long)h[ST_EXTRA], hs[0], hs[2]);
+        fprintf(stderr, "etree top blocks after s %d: %u block(s) cut; top: vertices %u group edges %lu; list entries "
+                        "scanned %lu -> MSF edges %lu (top block: components left %u, done %u)\n", top_bits, nbc, top_V,
+                (unsigned long)(top_g1 - top_g0), (unsigned long)(h[ST_KEPT] + h[ST_CONTR]), (unsigned long)h[ST_EXTRA],
+                hs[0], hs[2]);
       }
     }
     if (g_debug_etree && s >= 8 && s <= 15) {   // how the live edges spread over the 2^s blocks
