@@ -95,6 +95,16 @@ __device__ __forceinline__ void find2(uint32_t *uf, Tg g, uint32_t &x, uint32_t 
   }
 }
 
+// Which of two roots goes under the other.  By id (PRIO false: the larger under the
+// smaller), or by a pseudo-random priority (a bijection of the id): concurrent id-ordered
+// hooks of a path v1 - v2 - ... - vP all succeed at once and leave a chain of depth P for
+// every later find; random priorities leave expected depth O(log P).
+template <bool PRIO> __device__ __forceinline__ uint32_t hook_key(uint32_t x) {
+  if (!PRIO) return x;
+  x *= 0x9E3779B1u;
+  return x ^ (x >> 15);
+}
+
 // Hooks root hi under lo: succeeds only while hi is still a root (its word unchanged).
 __device__ __forceinline__ bool hook(uint32_t *uf, Tg g, uint32_t hi, uint32_t lo) {
   const uint32_t w = uf[hi];
@@ -345,6 +355,7 @@ __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict_
 // another round trip); rounds instead resolve such a pile-up in a few passes.
 // (Batched finds of all the thread's edges before any hook left more hooks to later
 // rounds: 21-22 ms against 10.8 ms at RMAT-26.)
+template <bool PRIO>
 __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict__ in, const uint64_t *__restrict__ n_in,
                                                       uint32_t *uf, Tg g, uint64_t *__restrict__ out,
                                                       unsigned long long *__restrict__ counter) {
@@ -364,7 +375,8 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
       uint32_t a = (uint32_t)ev[j], b = (uint32_t)(ev[j] >> 32);
       find2(uf, g, a, b);
       if (a == b) continue;
-      const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+      const bool ab = hook_key<PRIO>(a) < hook_key<PRIO>(b);
+      const uint32_t lo = ab ? a : b, hi = ab ? b : a;
       if (!hook(uf, g, hi, lo)) keep |= 1u << j;
     }
     uint64_t slot = shard_reserve((uint32_t)__popc(keep), counter, tile, ntiles, 1);
@@ -377,6 +389,7 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
 // The edges still unresolved after HOOK_ROUNDS rounds (few: the pile-ups are gone) are
 // hooked in place, retrying until each one's roots agree.  Lock-free: a failed CAS
 // means another hook made progress.
+template <bool PRIO>
 __global__ __launch_bounds__(BLOCK) void k_hook_finish(const uint64_t *__restrict__ src, const uint64_t *__restrict__ n_in,
                                                        const unsigned long long *__restrict__ counters, uint32_t *uf, Tg g,
                                                        uint64_t *__restrict__ n_left) {
@@ -411,7 +424,8 @@ __global__ __launch_bounds__(BLOCK) void k_hook_finish(const uint64_t *__restric
     for (;;) {
       find2(uf, g, a, b);
       if (a == b) break;
-      const uint32_t l = a < b ? a : b, h = a < b ? b : a;
+      const bool ab = hook_key<PRIO>(a) < hook_key<PRIO>(b);
+      const uint32_t l = ab ? a : b, h = ab ? b : a;
       if (hook(uf, g, h, l)) break;
     }
   }
@@ -1492,14 +1506,20 @@ static uint64_t list_capacity(uint64_t m) { return 2 * m + TILE; }
 // number of blocks cut.
 static uint32_t top_blocks(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, uint64_t g0, uint64_t g1,
                            uint32_t cut0, int bits, uint32_t nb_max, uint32_t clo, uint64_t n, uint64_t lcap) {
-  const uint64_t tcap = (lcap + TILE - 1) / TILE * TILE + TILE;
+  // the regions are sized by the cut level's list (one sync: worst-case regions of several
+  // blocks would take tens of GB at RMAT-26)
+  uint64_t hrow[ST_ROW];
+  HIP_CHECK(hipMemcpyAsync(hrow, st, sizeof hrow, hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  const uint64_t nl = hrow[ST_KEPT] + hrow[ST_CONTR];
+  const uint64_t tcap = (nl + TILE - 1) / TILE * TILE + TILE;
   nb_max = std::min<uint32_t>(std::max<uint32_t>(nb_max, 1), TOP_NB_MAX);
   while (nb_max > 1 && ((uint64_t)nb_max << bits) > cut0 + (1ull << bits)) --nb_max;   // blocks must lie above 0
   uint64_t *tl = c.get_as<uint64_t>("et_top_list", nb_max * tcap);
   unsigned long long *tcnt = c.get_as<unsigned long long>("et_top_cnt", nb_max * TOP_CSET + TOP_NB_MAX);
   unsigned long long *bcnt = tcnt + nb_max * TOP_CSET;
   HIP_CHECK(hipMemsetAsync(tcnt, 0, nb_max * TOP_CSET * sizeof(unsigned long long), c.stream));
-  hipLaunchKernelGGL(k_top_extract_multi, dim3(grid_tiles(lcap)), dim3(BLOCK), 0, c.stream, (const uint64_t *)next, st,
+  hipLaunchKernelGGL(k_top_extract_multi, dim3(grid_tiles(nl)), dim3(BLOCK), 0, c.stream, (const uint64_t *)next, st,
                      cut0, bits, nb_max, clo, tl, tcap, tcnt);
   LAUNCH_CHECK();
   auto first_at = [&](uint64_t y) {   // min vertex x with spread(x) >= y
@@ -1683,10 +1703,11 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     {
       TimedRegion tr(c, "etree_union");
       static_assert(HOOK_ROUNDS == 1, "k_hook_finish reads the one round's shard regions");
-      hipLaunchKernelGGL(k_hook_round, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
+      static const bool prio = getenv("SHEEP_HOOK_PRIO") && atoi(getenv("SHEEP_HOOK_PRIO")) != 0;   // (A/B runs)
+      hipLaunchKernelGGL(prio ? k_hook_round<true> : k_hook_round<false>, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
                          (const uint64_t *)(st + ST_NL), uf, g, alt, cset(CSET_HOOK));
       LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_hook_finish, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)alt,
+      hipLaunchKernelGGL(prio ? k_hook_finish<true> : k_hook_finish<false>, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)alt,
                          (const uint64_t *)(st + ST_NL), (const unsigned long long *)cset(CSET_HOOK), uf, g, st + ST_HOOK);
       LAUNCH_CHECK();
       hipLaunchKernelGGL(k_light_top, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
