@@ -95,16 +95,6 @@ __device__ __forceinline__ void find2(uint32_t *uf, Tg g, uint32_t &x, uint32_t 
   }
 }
 
-// Which of two roots goes under the other.  By id (PRIO false: the larger under the
-// smaller), or by a pseudo-random priority (a bijection of the id): concurrent id-ordered
-// hooks of a path v1 - v2 - ... - vP all succeed at once and leave a chain of depth P for
-// every later find; random priorities leave expected depth O(log P).
-template <bool PRIO> __device__ __forceinline__ uint32_t hook_key(uint32_t x) {
-  if (!PRIO) return x;
-  x *= 0x9E3779B1u;
-  return x ^ (x >> 15);
-}
-
 // Hooks root hi under lo: succeeds only while hi is still a root (its word unchanged).
 __device__ __forceinline__ bool hook(uint32_t *uf, Tg g, uint32_t hi, uint32_t lo) {
   const uint32_t w = uf[hi];
@@ -355,7 +345,6 @@ __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict_
 // another round trip); rounds instead resolve such a pile-up in a few passes.
 // (Batched finds of all the thread's edges before any hook left more hooks to later
 // rounds: 21-22 ms against 10.8 ms at RMAT-26.)
-template <bool PRIO>
 __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict__ in, const uint64_t *__restrict__ n_in,
                                                       uint32_t *uf, Tg g, uint64_t *__restrict__ out,
                                                       unsigned long long *__restrict__ counter) {
@@ -375,8 +364,7 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
       uint32_t a = (uint32_t)ev[j], b = (uint32_t)(ev[j] >> 32);
       find2(uf, g, a, b);
       if (a == b) continue;
-      const bool ab = hook_key<PRIO>(a) < hook_key<PRIO>(b);
-      const uint32_t lo = ab ? a : b, hi = ab ? b : a;
+      const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
       if (!hook(uf, g, hi, lo)) keep |= 1u << j;
     }
     uint64_t slot = shard_reserve((uint32_t)__popc(keep), counter, tile, ntiles, 1);
@@ -389,7 +377,6 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
 // The edges still unresolved after HOOK_ROUNDS rounds (few: the pile-ups are gone) are
 // hooked in place, retrying until each one's roots agree.  Lock-free: a failed CAS
 // means another hook made progress.
-template <bool PRIO>
 __global__ __launch_bounds__(BLOCK) void k_hook_finish(const uint64_t *__restrict__ src, const uint64_t *__restrict__ n_in,
                                                        const unsigned long long *__restrict__ counters, uint32_t *uf, Tg g,
                                                        uint64_t *__restrict__ n_left) {
@@ -424,8 +411,7 @@ __global__ __launch_bounds__(BLOCK) void k_hook_finish(const uint64_t *__restric
     for (;;) {
       find2(uf, g, a, b);
       if (a == b) break;
-      const bool ab = hook_key<PRIO>(a) < hook_key<PRIO>(b);
-      const uint32_t l = ab ? a : b, h = ab ? b : a;
+      const uint32_t l = a < b ? a : b, h = a < b ? b : a;
       if (hook(uf, g, h, l)) break;
     }
   }
@@ -1069,6 +1055,9 @@ __global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t 
 // components that have an outgoing edge, so TB + 1 rounds always finish.
 constexpr int TOP_BITS = 15;                 // the map's cut (blocks up to 2^TOP_BITS_MAX: SHEEP_TOP_BITS)
 constexpr int TOP_BITS_MAX = 16;            // u16 labels: <= 65536 vertices
+// the top block and the dense blocks right below it, at most TOP_NB in all (RMAT-26 k=64, etree
+// ms: no cut 34.5; 1 block 34.1; 4 blocks 33.8; 8 blocks 33.8 — with the 10-bit finish below)
+constexpr int TOP_NB = 4;
 constexpr int TOPB = 1024;                  // threads per workgroup of the top-block kernels
 constexpr uint32_t TOP_HOOK_LDS = 1u << 15; // hook kernels: par / cid in LDS up to this many components
 constexpr size_t TOP_ROUND_LDS = 144 * 1024; // a round's dynamic LDS: the labels, then the minima
@@ -1471,10 +1460,13 @@ static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
 // map keep ~5M list entries each at RMAT-26 (0.6 ms per level for a dozen launches);
 // one sort + the per-block pass replaces the last 8 (RMAT-26: 49.7 -> 45.9 ms; B = 7:
 // 46.4; B = 10: 42.7 against 39.9, B = 12: 82.5 — hub blocks serialise on one wave).
+// With the dense top blocks cut to their MSFs (below) the hub blocks are gone and 10 bits
+// pay (RMAT-26, 4 blocks cut: etree 33.8 ms at B = 10 against 34.1 at B = 8 and 33.6 at 11;
+// no cut, B = 10: 37.4 — the finish alone 5.2 ms).
 // Hub blocks go to whole waves (k_fin_heavy).  A merge's edges spread evenly over the
 // blocks, so its finish takes 11 bits (RMAT-26, 8 shard trees: K-way merge 19.5 -> 17.9
 // ms; 10: 18.1, 12: 18.2).
-constexpr int FIN_MERGE = 11, FIN_MAP = 8;
+constexpr int FIN_MERGE = 11, FIN_MAP = 10;
 
 // spread(x) = floor(x * c / 2^32), c = floor(2^(32+L) / n) in [2^32, 2^33), L = ceil(log2 n):
 // monotone, injective on [0,n), image in [0, 2^L).  clo = c - 2^32.
@@ -1703,11 +1695,10 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     {
       TimedRegion tr(c, "etree_union");
       static_assert(HOOK_ROUNDS == 1, "k_hook_finish reads the one round's shard regions");
-      static const bool prio = getenv("SHEEP_HOOK_PRIO") && atoi(getenv("SHEEP_HOOK_PRIO")) != 0;   // (A/B runs)
-      hipLaunchKernelGGL(prio ? k_hook_round<true> : k_hook_round<false>, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
+      hipLaunchKernelGGL(k_hook_round, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
                          (const uint64_t *)(st + ST_NL), uf, g, alt, cset(CSET_HOOK));
       LAUNCH_CHECK();
-      hipLaunchKernelGGL(prio ? k_hook_finish<true> : k_hook_finish<false>, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)alt,
+      hipLaunchKernelGGL(k_hook_finish, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)alt,
                          (const uint64_t *)(st + ST_NL), (const unsigned long long *)cset(CSET_HOOK), uf, g, st + ST_HOOK);
       LAUNCH_CHECK();
       hipLaunchKernelGGL(k_light_top, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
@@ -1735,7 +1726,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     }
     if (lvl == top_lvl) {
       TimedRegion tr(c, "etree_top");
-      static const int top_nb = getenv("SHEEP_TOP_BLOCKS") ? atoi(getenv("SHEEP_TOP_BLOCKS")) : 1;
+      static const int top_nb = getenv("SHEEP_TOP_BLOCKS") ? atoi(getenv("SHEEP_TOP_BLOCKS")) : TOP_NB;
       const uint32_t nbc = top_blocks(c, next, st, r0, top_g0, top_g1, top_cut, top_bits, (uint32_t)top_nb, clo, n, lcap);
       if (g_debug_etree) {
         uint64_t h[ST_ROW];
