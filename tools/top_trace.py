@@ -18,7 +18,7 @@ def base(name):
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 starts = [i for i, r in enumerate(rows) if base(r["Kernel_Name"]) == "k_degree_fused"]
 step = rows[starts[-1]:]
-first = next(i for i, r in enumerate(step) if base(r["Kernel_Name"]) == "k_top_extract")
+first = next(i for i, r in enumerate(step) if base(r["Kernel_Name"]).startswith("k_top_extract"))
 end = next(i for i in range(first, len(step)) if base(step[i]["Kernel_Name"]) == "k_split_count")
 prev_end = int(step[first - 1]["End_Timestamp"])
 t0 = int(step[first]["Start_Timestamp"])
