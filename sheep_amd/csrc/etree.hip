@@ -1059,13 +1059,15 @@ constexpr int TOP_BITS_MAX = 16;            // u16 labels: <= 65536 vertices
 // ms: no cut 34.5; 1 block 34.1; 4 blocks 33.8; 8 blocks 33.8 — with the 10-bit finish below)
 constexpr int TOP_NB = 4;
 constexpr int TOPB = 1024;                  // threads per workgroup of the top-block kernels
+constexpr int TOP_WG = 256;                 // workgroups per block of the LDS edge passes (one per CU)
 constexpr uint32_t TOP_HOOK_LDS = 1u << 15; // hook kernels: par / cid in LDS up to this many components
 constexpr size_t TOP_ROUND_LDS = 144 * 1024; // a round's dynamic LDS: the labels, then the minima
 constexpr uint64_t TOP_DENSE = 16;          // used when the block's groups hold >= 16 edges per vertex
 constexpr uint64_t NO_EDGE = ~0ull;
 
 struct TopState {
-  uint32_t *minlo, *minhi;          // round 0: per vertex, the lowest lower / upper neighbour
+  uint32_t *minlo;                  // round 0: per vertex, its lowest lower neighbour (block-local id)
+  unsigned *hasup;                  // round 0: per vertex a bit, set when it has an upper neighbour
   uint16_t *comp;                   // per vertex: its component's id
   unsigned long long *best;         // per component: the smallest edge word leaving it
   unsigned *scal;                   // [0] components, [1] a round saw an inter-component edge, [2] done
@@ -1083,6 +1085,14 @@ struct TopEdges {
   const uint64_t *r0;
   uint64_t g0, g1;
 };
+constexpr int TOP_NB_MAX = 9;   // the top block and up to 8 below it
+// Every cut block in one launch: block b is blockIdx.y of the edge kernels and blockIdx.x of
+// the one-workgroup hooks, so the blocks' passes overlap instead of queueing one behind another.
+struct TopSet {
+  TopState s[TOP_NB_MAX];
+  TopEdges e[TOP_NB_MAX];
+};
+
 __device__ __forceinline__ void top_prefix(const TopEdges &te, uint64_t *s_pre) {
   if (threadIdx.x < WAVE) {
     uint64_t inc = te.tcnt[(uint64_t)threadIdx.x * SHARD_STRIDE];
@@ -1095,9 +1105,7 @@ __device__ __forceinline__ void top_prefix(const TopEdges &te, uint64_t *s_pre) 
     if (threadIdx.x == 0) s_pre[0] = 0;
   }
 }
-__device__ __forceinline__ uint64_t top_at(const TopEdges &te, const uint64_t *s_pre, uint64_t ntiles, uint64_t i) {
-  const uint64_t nl = s_pre[NSHARD];
-  if (i >= nl) return te.r0[te.g0 + (i - nl)];
+__device__ __forceinline__ uint64_t top_list_at(const TopEdges &te, const uint64_t *s_pre, uint64_t ntiles, uint64_t i) {
   uint32_t a = 0, b = NSHARD;   // s_pre[a] <= i < s_pre[b]
   while (b - a > 1) {
     const uint32_t mid = (a + b) / 2;
@@ -1106,34 +1114,32 @@ __device__ __forceinline__ uint64_t top_at(const TopEdges &te, const uint64_t *s
   return te.tl[shard_base(ntiles, a, 1) + (i - s_pre[a])];
 }
 
-// The list entries of the top block (spread(lo) >= cut) out of the cut level's next list.
-__global__ __launch_bounds__(BLOCK) void k_top_extract(const uint64_t *__restrict__ list, uint64_t *__restrict__ st,
-                                                       uint32_t cut, uint32_t cut_hi, uint32_t clo, uint64_t *__restrict__ tl,
-                                                       unsigned long long *__restrict__ tcnt) {
-  const uint64_t nl = st[ST_KEPT] + st[ST_CONTR];
-  const uint64_t ntiles = (nl + TILE - 1) / TILE;
-  if (blockIdx.x == 0 && threadIdx.x == 0) st[ST_TOPNT] = ntiles;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    uint64_t ev[TILE_ITEMS];
-    uint32_t keep = 0;
+// Calls f(e) for the block's edges in [b0, b1) of its index space (the list entries, then
+// the groups), `nt` threads striding.  The group part (nearly all of a dense block) is read
+// TOP_U words ahead per thread: the top-block passes run one 1024-thread workgroup per CU,
+// so without the unrolled loads every wave waits out one HBM latency per edge.
+constexpr int TOP_U = 8;
+template <typename F>
+__device__ __forceinline__ void top_edges(const TopEdges &te, const uint64_t *s_pre, uint64_t ntiles, uint64_t b0,
+                                          uint64_t b1, uint32_t t, uint32_t nt, F &&f) {
+  const uint64_t nl = s_pre[NSHARD];
+  for (uint64_t i = b0 + t; i < (b1 < nl ? b1 : nl); i += nt) f(top_list_at(te, s_pre, ntiles, i));
+  const uint64_t g0 = (b0 > nl ? b0 : nl) - nl, g1 = b1 > nl ? b1 - nl : 0;   // group-part range
+  const uint64_t *r = te.r0 + te.g0;
+  uint64_t i = g0 + t;
+  for (; i + (uint64_t)(TOP_U - 1) * nt < g1; i += (uint64_t)TOP_U * nt) {
+    uint64_t e[TOP_U];
 #pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) {
-      const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
-      ev[j] = i < nl ? list[i] : DEAD;
-      const uint32_t y = ev[j] == DEAD ? 0u : spread((uint32_t)ev[j], clo);
-      if (ev[j] != DEAD && y >= cut && (cut_hi == 0 || y < cut_hi)) keep |= 1u << j;
-    }
-    uint64_t slot = shard_reserve((uint32_t)__popc(keep), tcnt, tile, ntiles, 1);
+    for (int j = 0; j < TOP_U; ++j) e[j] = __builtin_nontemporal_load(r + i + (uint64_t)j * nt);
 #pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j)
-      if (keep & (1u << j)) tl[slot++] = ev[j];
+    for (int j = 0; j < TOP_U; ++j) f(e[j]);
   }
+  for (; i < g1; i += nt) f(r[i]);
 }
 
 // The list entries of the cut blocks, one pass: block 0 = spread(lo) >= cut0 (the top
 // block), block j >= 1 = [cut0 - j 2^bits, cut0 - (j - 1) 2^bits); block j's entries go to
 // region j of tl (sharded appends on counter set j).  st[ST_TOPNT] = the pass's tile count.
-constexpr int TOP_NB_MAX = 9;   // the top block and up to 8 below it
 constexpr uint64_t TOP_CSET = (uint64_t)NSHARD * SHARD_STRIDE;
 __global__ __launch_bounds__(BLOCK) void k_top_extract_multi(const uint64_t *__restrict__ list, uint64_t *__restrict__ st,
                                                              uint32_t cut0, int bits, uint32_t nb, uint32_t clo,
@@ -1177,88 +1183,82 @@ __global__ void k_top_sum_counts(const unsigned long long *__restrict__ tcnt, ui
   if (k == 0 && b < nb) cnt[b] = v;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_top_init(TopState ts, bool first) {
+__global__ __launch_bounds__(BLOCK) void k_top_init(TopSet t) {
+  const TopState &ts = t.s[blockIdx.y];
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < ts.V; v += stride) {
     ts.minlo[v] = INVALID;
-    ts.minhi[v] = INVALID;
     ts.best[v] = NO_EDGE;
+    if (v % 32 == 0) ts.hasup[v / 32] = 0;
   }
   if (blockIdx.x == 0 && threadIdx.x < 3) ts.scal[threadIdx.x] = 0;
-  if (first && blockIdx.x == 0 && threadIdx.x == 0) ts.st[ST_EXTRA] = 0;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) ts.st[ST_EXTRA] = 0;
 }
 
 __global__ void k_set_u64(uint64_t *p, uint64_t v) { *p = v; }
 
-// Round 0: every vertex's smallest incident edge under (hi, lo) is (minlo(v), v) when v has
-// a lower neighbour in the block, else (v, minhi(v)).  Read-checked atomics (the minima
-// only fall: a stale read can only cost a redundant atomic); the edges come grouped by lo,
-// so lanes sharing the first lane's lo combine their minhi first.
-__global__ __launch_bounds__(BLOCK) void k_top_min0(TopEdges te, TopState ts, const uint64_t *__restrict__ st) {
+// Round 0 hooks every vertex with a lower neighbour along its smallest incident edge under
+// (hi, lo): (minlo(v), v).  Any set of components may hook along their smallest outgoing
+// edges (each is an MSF edge), and these picks all point down, so they form a forest; the
+// vertices without a lower neighbour wait for the full rounds.  hasup marks the vertices
+// with an upper neighbour: when at most one root has an edge the block is one tree and
+// needs no round (k_top_hook0).  Read-checked atomics (the minima only fall).
+__global__ __launch_bounds__(BLOCK) void k_top_min0(TopSet t, const uint64_t *__restrict__ st) {
+  const TopState &ts = t.s[blockIdx.y];
+  const TopEdges &te = t.e[blockIdx.y];
   __shared__ uint64_t s_pre[NSHARD + 1];
   top_prefix(te, s_pre);
   __syncthreads();
-  const uint64_t ntiles = st[ST_TOPNT], total = s_pre[NSHARD] + (te.g1 - te.g0);
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  const uint64_t iters = (total + stride - 1) / stride;
-  for (uint64_t it = 0, i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; it < iters; ++it, i += stride) {
-    const bool live = i < total;
-    const uint64_t e = live ? top_at(te, s_pre, ntiles, i) : DEAD;
-    const bool ok = live && e != DEAD;
-    const uint32_t l = (uint32_t)e - ts.v0, h = (uint32_t)(e >> 32) - ts.v0;
-    if (ok && l < ts.minlo[h]) atomicMin(&ts.minlo[h], l);
-    const uint64_t lm = __ballot(ok);
-    if (!lm) continue;
-    const int first = __ffsll((unsigned long long)lm) - 1;
-    const uint32_t l0 = __shfl(l, first, 64);
-    const bool same = ok && l == l0;
-    const uint32_t v = wave_min(same ? h : INVALID);
-    if ((int)__lane_id() == first && v < ts.minhi[l0]) atomicMin(&ts.minhi[l0], v);
-    if (ok && !same && h < ts.minhi[l]) atomicMin(&ts.minhi[l], h);
-  }
+  const uint64_t total = s_pre[NSHARD] + (te.g1 - te.g0);
+  const uint32_t v0 = ts.v0;
+  top_edges(te, s_pre, st[ST_TOPNT], 0, total, blockIdx.x * BLOCK + threadIdx.x, gridDim.x * BLOCK, [&](uint64_t e) {
+    if (e == DEAD) return;
+    const uint32_t l = (uint32_t)e - v0, h = (uint32_t)(e >> 32) - v0;
+    if (l < ts.minlo[h]) atomicMin(&ts.minlo[h], l);
+    const unsigned bit = 1u << (l & 31);
+    if (!(ts.hasup[l >> 5] & bit)) atomicOr(&ts.hasup[l >> 5], bit);
+  });
 }
 
-// Round 0 with each workgroup's lowest-lower-neighbour minima in LDS (<= 2^15 vertices, one
-// workgroup per CU): the random global atomics of k_top_min0 (RMAT-26's top block: 0.86 ms
-// for 50 M edges) become LDS atomics and one read-checked flush per vertex and workgroup.
-// minhi (only vertices without a lower neighbour use it) keeps the wave-combined global
-// atomics: the edges come grouped by lo, so a wave's lanes mostly share it.
-__global__ __launch_bounds__(TOPB) void k_top_min0_lds(TopEdges te, TopState ts, const uint64_t *__restrict__ st) {
+// Round 0 with each workgroup's minima and hasup bits in LDS (<= 2^15 vertices, one
+// workgroup per CU, a contiguous chunk each), flushed with one read-checked atomic per
+// vertex and workgroup.
+__global__ __launch_bounds__(TOPB) void k_top_min0_lds(TopSet t, const uint64_t *__restrict__ st) {
+  const TopState &ts = t.s[blockIdx.y];
+  const TopEdges &te = t.e[blockIdx.y];
   extern __shared__ uint32_t lmin[];
+  __shared__ unsigned lup[TOP_HOOK_LDS / 32];
   __shared__ uint64_t s_pre[NSHARD + 1];
-  for (uint32_t v = threadIdx.x; v < ts.V; v += TOPB) lmin[v] = INVALID;
+  const uint32_t V = ts.V, W = (V + 31) / 32, v0 = ts.v0;
+  for (uint32_t v = threadIdx.x; v < V; v += TOPB) lmin[v] = INVALID;
+  for (uint32_t w = threadIdx.x; w < W; w += TOPB) lup[w] = 0;
   top_prefix(te, s_pre);
   __syncthreads();
-  const uint64_t ntiles = st[ST_TOPNT], total = s_pre[NSHARD] + (te.g1 - te.g0);
-  const uint64_t per = (total + gridDim.x - 1) / gridDim.x;   // a contiguous chunk per workgroup
+  const uint64_t total = s_pre[NSHARD] + (te.g1 - te.g0);
+  const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
   const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < total ? b0 + per : total;
-  const uint64_t iters = b1 > b0 ? (b1 - b0 + TOPB - 1) / TOPB : 0;
-  for (uint64_t it = 0, i = b0 + threadIdx.x; it < iters; ++it, i += TOPB) {   // wave-uniform trip count
-    const bool live = i < b1;
-    const uint64_t e = live ? top_at(te, s_pre, ntiles, i) : DEAD;
-    const bool ok = live && e != DEAD;
-    const uint32_t l = (uint32_t)e - ts.v0, h = (uint32_t)(e >> 32) - ts.v0;
-    if (ok && l < lmin[h]) atomicMin(&lmin[h], l);
-    const uint64_t lm = __ballot(ok);
-    if (!lm) continue;
-    const int first = __ffsll((unsigned long long)lm) - 1;
-    const uint32_t l0 = __shfl(l, first, 64);
-    const bool same = ok && l == l0;
-    const uint32_t v = wave_min(same ? h : INVALID);
-    if ((int)__lane_id() == first && v < ts.minhi[l0]) atomicMin(&ts.minhi[l0], v);
-    if (ok && !same && h < ts.minhi[l]) atomicMin(&ts.minhi[l], h);
-  }
+  top_edges(te, s_pre, st[ST_TOPNT], b0 < b1 ? b0 : b1, b1, threadIdx.x, TOPB, [&](uint64_t e) {
+    if (e == DEAD) return;
+    const uint32_t l = (uint32_t)e - v0, h = (uint32_t)(e >> 32) - v0;
+    if (l < lmin[h]) atomicMin(&lmin[h], l);
+    const unsigned bit = 1u << (l & 31);
+    if (!(lup[l >> 5] & bit)) atomicOr(&lup[l >> 5], bit);
+  });
   __syncthreads();
-  for (uint32_t v = threadIdx.x; v < ts.V; v += TOPB) {
+  for (uint32_t v = threadIdx.x; v < V; v += TOPB) {
     const uint32_t x = lmin[v];
     if (x != INVALID && x < ts.minlo[v]) atomicMin(&ts.minlo[v], x);
+  }
+  for (uint32_t w = threadIdx.x; w < W; w += TOPB) {
+    const unsigned x = lup[w];
+    if (x & ~ts.hasup[w]) atomicOr(&ts.hasup[w], x);
   }
 }
 
 // One workgroup: after par[] (u16, in LDS) holds every component's pick (itself for a
 // root), the forest is pointer-jumped, the roots renumbered 0..C-1 and ts.comp rewritten
-// through them.  `rec` edges were appended to ts.out.  lds: par[cap], cid[cap].
-__device__ void top_relabel(TopState &ts, uint16_t *par, uint16_t *cid, uint32_t cnt, bool first_round) {
+// through them.  lds: par[cap], cid[cap].
+__device__ void top_relabel(const TopState &ts, uint16_t *par, uint16_t *cid, uint32_t cnt, bool first_round) {
   __shared__ unsigned s_w[TOPB / WAVE];
   for (;;) {   // pointer jumping (every pick points to a neighbour component; the picks form a forest)
     bool changed = false;
@@ -1309,21 +1309,25 @@ __device__ __forceinline__ uint32_t top_record(unsigned *s_cnt, uint64_t e, uint
 }
 
 constexpr uint32_t TOP_REC = 2048;   // MSF edges staged per hook launch before a flush
-__device__ void top_flush(TopState &ts, const uint64_t *rec, unsigned n) {
-  const uint64_t base = ts.st[ST_KEPT] + ts.st[ST_CONTR] + ts.st[ST_EXTRA];
-  for (uint32_t k = threadIdx.x; k < n; k += TOPB) ts.out[base + k] = rec[k];
+// (the blocks' hooks run concurrently: each flush reserves its slots on ST_EXTRA)
+__device__ void top_flush(const TopState &ts, const uint64_t *rec, unsigned n) {
+  __shared__ uint64_t s_base;
+  if (n == 0) return;   // (uniform)
+  if (threadIdx.x == 0)
+    s_base = ts.st[ST_KEPT] + ts.st[ST_CONTR] + atomicAdd((unsigned long long *)&ts.st[ST_EXTRA], (unsigned long long)n);
   __syncthreads();
-  if (threadIdx.x == 0) ts.st[ST_EXTRA] += n;
+  for (uint32_t k = threadIdx.x; k < n; k += TOPB) ts.out[s_base + k] = rec[k];
   __syncthreads();
 }
 
-__global__ __launch_bounds__(TOPB) void k_top_hook0(TopState ts) {
+__global__ __launch_bounds__(TOPB) void k_top_hook0(TopSet t) {
+  const TopState &ts = t.s[blockIdx.x];
   extern __shared__ uint16_t lds16[];
   const bool big = ts.V > TOP_HOOK_LDS;
   uint16_t *par = big ? ts.gpar : lds16, *cid = big ? ts.gcid : lds16 + TOP_HOOK_LDS;
   __shared__ uint64_t rec[TOP_REC];
-  __shared__ unsigned s_cnt;
-  if (threadIdx.x == 0) s_cnt = 0;
+  __shared__ unsigned s_cnt, s_roots;
+  if (threadIdx.x == 0) s_cnt = s_roots = 0;
   __syncthreads();
   for (uint32_t base = 0; base < ts.V; base += TOP_REC) {   // TOP_REC vertices (<= one edge each) a pass
     const uint32_t end = base + TOP_REC < ts.V ? base + TOP_REC : ts.V;
@@ -1333,13 +1337,8 @@ __global__ __launch_bounds__(TOPB) void k_top_hook0(TopState ts) {
       if (ml != INVALID) {
         p = ml;
         top_record(&s_cnt, ((uint64_t)(ts.v0 + v) << 32) | (ts.v0 + ml), rec, TOP_REC);
-      } else {
-        const uint32_t mh = ts.minhi[v];
-        // v's pick (v, mh) is also mh's own pick when minlo(mh) = v: mh records it, v stays a root
-        if (mh != INVALID && ts.minlo[mh] != v) {
-          p = mh;
-          top_record(&s_cnt, ((uint64_t)(ts.v0 + mh) << 32) | (ts.v0 + v), rec, TOP_REC);
-        }
+      } else if (ts.hasup[v >> 5] & (1u << (v & 31))) {
+        atomicAdd(&s_roots, 1u);   // a root with edges
       }
       par[v] = (uint16_t)p;
     }
@@ -1349,33 +1348,36 @@ __global__ __launch_bounds__(TOPB) void k_top_hook0(TopState ts) {
     __syncthreads();
   }
   top_relabel(ts, par, cid, ts.V, true);
+  // every non-root's chain of picks ends at a root with an edge: with at most one such
+  // root every edge lies inside one component, and the MSF is complete
+  if (threadIdx.x == 0 && s_roots <= 1) ts.scal[2] = 1;
 }
 
 // A Borůvka round over the block's edges: each component's smallest outgoing edge word.
 // The labels (u16) in LDS; the minima in LDS when the components fit, flushed with one
 // read-checked atomic per component and workgroup.
-__global__ __launch_bounds__(TOPB) void k_top_round(TopEdges te, TopState ts, const uint64_t *__restrict__ st) {
+__global__ __launch_bounds__(TOPB) void k_top_round(TopSet t, const uint64_t *__restrict__ st) {
+  const TopState &ts = t.s[blockIdx.y];
+  const TopEdges &te = t.e[blockIdx.y];
   if (ts.scal[2]) return;   // done (uniform)
   extern __shared__ uint16_t lds16[];
   uint16_t *comp = lds16;
   const uint32_t voff = (ts.V + 3) & ~3u;   // the minima 8-B aligned after the labels
   unsigned long long *lbest = (unsigned long long *)(lds16 + voff);
   __shared__ uint64_t s_pre[NSHARD + 1];
-  const uint32_t C = ts.scal[0];
+  const uint32_t C = ts.scal[0], v0 = ts.v0;
   const bool in_lds = C <= (uint32_t)((TOP_ROUND_LDS - voff * sizeof(uint16_t)) / sizeof(uint64_t));
   for (uint32_t v = threadIdx.x; v < ts.V; v += TOPB) comp[v] = ts.comp[v];
   if (in_lds)
     for (uint32_t c = threadIdx.x; c < C; c += TOPB) lbest[c] = NO_EDGE;
   top_prefix(te, s_pre);
   __syncthreads();
-  const uint64_t ntiles = st[ST_TOPNT], total = s_pre[NSHARD] + (te.g1 - te.g0);
-  const uint64_t stride = (uint64_t)gridDim.x * TOPB;
+  const uint64_t total = s_pre[NSHARD] + (te.g1 - te.g0);
   bool inter = false;
-  for (uint64_t i = (uint64_t)blockIdx.x * TOPB + threadIdx.x; i < total; i += stride) {
-    const uint64_t e = top_at(te, s_pre, ntiles, i);
-    if (e == DEAD) continue;
-    const uint32_t cl = comp[(uint32_t)e - ts.v0], ch = comp[(uint32_t)(e >> 32) - ts.v0];
-    if (cl == ch) continue;
+  top_edges(te, s_pre, st[ST_TOPNT], 0, total, blockIdx.x * TOPB + threadIdx.x, gridDim.x * TOPB, [&](uint64_t e) {
+    if (e == DEAD) return;
+    const uint32_t cl = comp[(uint32_t)e - v0], ch = comp[(uint32_t)(e >> 32) - v0];
+    if (cl == ch) return;
     inter = true;
     if (in_lds) {
       if (e < lbest[cl]) atomicMin(&lbest[cl], (unsigned long long)e);
@@ -1384,7 +1386,7 @@ __global__ __launch_bounds__(TOPB) void k_top_round(TopEdges te, TopState ts, co
       if (e < ts.best[cl]) atomicMin(&ts.best[cl], (unsigned long long)e);
       if (e < ts.best[ch]) atomicMin(&ts.best[ch], (unsigned long long)e);
     }
-  }
+  });
   inter = __syncthreads_or(inter);
   if (in_lds)
     for (uint32_t c = threadIdx.x; c < C; c += TOPB) {
@@ -1394,11 +1396,12 @@ __global__ __launch_bounds__(TOPB) void k_top_round(TopEdges te, TopState ts, co
   if (inter && threadIdx.x == 0) atomicOr(&ts.scal[1], 1u);
 }
 
-// One workgroup: every component hooks to the component across its smallest outgoing
-// edge (a pair that picked the same edge keeps the smaller id as the root), the picked
-// edges are the MSF's, then the labels are rewritten.  A round without an inter-component
-// edge ends the rounds.
-__global__ __launch_bounds__(TOPB) void k_top_hook(TopState ts) {
+// One workgroup per block: every component hooks to the component across its smallest
+// outgoing edge (a pair that picked the same edge keeps the smaller id as the root), the
+// picked edges are the MSF's, then the labels are rewritten.  A round without an
+// inter-component edge ends the block's rounds.
+__global__ __launch_bounds__(TOPB) void k_top_hook(TopSet t) {
+  const TopState &ts = t.s[blockIdx.x];
   __shared__ unsigned s_flag;
   if (threadIdx.x == 0) s_flag = ts.scal[2] ? 2u : atomicOr(&ts.scal[1], 0u) ? 1u : 0u;
   __syncthreads();
@@ -1538,66 +1541,65 @@ static uint32_t top_blocks(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t 
     }
   }
   const uint64_t VMAX = 1ull << bits;
-  uint32_t *minlo = c.get_as<uint32_t>("et_top_minlo", nb * VMAX), *minhi = c.get_as<uint32_t>("et_top_minhi", nb * VMAX);
+  uint32_t *minlo = c.get_as<uint32_t>("et_top_minlo", nb * VMAX);
+  unsigned *hasup = c.get_as<unsigned>("et_top_hasup", nb * VMAX / 32);
   uint16_t *comp = c.get_as<uint16_t>("et_top_comp", nb * VMAX);
   unsigned long long *best = c.get_as<unsigned long long>("et_top_best", nb * VMAX);
   unsigned *scal = c.get_as<unsigned>("et_top_scal", 4 * nb);
-  uint16_t *gpar = c.get_as<uint16_t>("et_top_gpar", VMAX), *gcid = c.get_as<uint16_t>("et_top_gcid", VMAX);
-  std::vector<TopState> ts(nb);
-  std::vector<TopEdges> te(nb);
+  const bool big = VMAX > TOP_HOOK_LDS;   // (SHEEP_TOP_BITS = 16: the hooks keep par / cid in HBM)
+  uint16_t *gpar = big ? c.get_as<uint16_t>("et_top_gpar", nb * VMAX) : nullptr;
+  uint16_t *gcid = big ? c.get_as<uint16_t>("et_top_gcid", nb * VMAX) : nullptr;
+  TopSet set{};
+  uint32_t vmax = 0;
   for (uint32_t b = 0; b < nb; ++b) {
     const uint64_t hi_cut = b == 0 ? (1ull << 32) : cut0 - ((uint64_t)(b - 1) << bits);
     const uint64_t lo_cut = b == 0 ? cut0 : hi_cut - (1ull << bits);
     const uint64_t v0 = first_at(lo_cut), v1 = b == 0 ? n : first_at(hi_cut);
-    ts[b].minlo = minlo + b * VMAX;
-    ts[b].minhi = minhi + b * VMAX;
-    ts[b].comp = comp + b * VMAX;
-    ts[b].best = best + b * VMAX;
-    ts[b].scal = scal + 4 * b;
-    ts[b].st = st;
-    ts[b].out = next;
-    ts[b].gpar = gpar;   // (the hooks of the blocks run one after another)
-    ts[b].gcid = gcid;
-    ts[b].v0 = (uint32_t)v0;
-    ts[b].V = (uint32_t)(v1 - v0);
-    te[b] = TopEdges{tl + b * tcap, tcnt + b * TOP_CSET, r0, b == 0 ? g0 : 0, b == 0 ? g1 : 0};
+    TopState &ts = set.s[b];
+    ts.minlo = minlo + b * VMAX;
+    ts.hasup = hasup + b * VMAX / 32;
+    ts.comp = comp + b * VMAX;
+    ts.best = best + b * VMAX;
+    ts.scal = scal + 4 * b;
+    ts.st = st;
+    ts.out = next;
+    ts.gpar = big ? gpar + b * VMAX : nullptr;
+    ts.gcid = big ? gcid + b * VMAX : nullptr;
+    ts.v0 = (uint32_t)v0;
+    ts.V = (uint32_t)(v1 - v0);
+    vmax = std::max(vmax, ts.V);
+    set.e[b] = TopEdges{tl + b * tcap, tcnt + b * TOP_CSET, r0, b == 0 ? g0 : 0, b == 0 ? g1 : 0};
   }
   const size_t lds2 = 2 * (size_t)TOP_HOOK_LDS * sizeof(uint16_t);   // par + cid
   const size_t ldsr = TOP_ROUND_LDS;                                  // labels + minima
+  const size_t ldsm = TOP_HOOK_LDS * sizeof(uint32_t);                // round 0's minima
   allow_lds((const void *)k_top_hook0, (int)lds2);
   allow_lds((const void *)k_top_hook, (int)lds2);
   allow_lds((const void *)k_top_round, (int)ldsr);
-  allow_lds((const void *)k_top_min0_lds, (int)(TOP_HOOK_LDS * sizeof(uint32_t)));
-  for (uint32_t b = 0; b < nb; ++b) {
-    hipLaunchKernelGGL(k_top_init, dim3(grid_for(ts[b].V)), dim3(BLOCK), 0, c.stream, ts[b], b == 0);
-    LAUNCH_CHECK();
-    if (ts[b].V <= TOP_HOOK_LDS)
-      hipLaunchKernelGGL(k_top_min0_lds, dim3(256), dim3(TOPB), TOP_HOOK_LDS * sizeof(uint32_t), c.stream, te[b], ts[b],
-                         (const uint64_t *)st);
-    else
-      hipLaunchKernelGGL(k_top_min0, dim3(grid_for(lcap + (te[b].g1 - te[b].g0))), dim3(BLOCK), 0, c.stream, te[b], ts[b],
-                         (const uint64_t *)st);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_top_hook0, dim3(1), dim3(TOPB), lds2, c.stream, ts[b]);
-    LAUNCH_CHECK();
-  }
-  std::vector<bool> live(nb, true);
+  allow_lds((const void *)k_top_min0_lds, (int)ldsm);
+  hipLaunchKernelGGL(k_top_init, dim3(grid_for(vmax), nb), dim3(BLOCK), 0, c.stream, set);
+  LAUNCH_CHECK();
+  if (vmax <= TOP_HOOK_LDS)
+    hipLaunchKernelGGL(k_top_min0_lds, dim3(TOP_WG, nb), dim3(TOPB), ldsm, c.stream, set, (const uint64_t *)st);
+  else
+    hipLaunchKernelGGL(k_top_min0, dim3(grid_for(tcap + (g1 - g0)), nb), dim3(BLOCK), 0, c.stream, set,
+                       (const uint64_t *)st);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_top_hook0, dim3(nb), dim3(TOPB), lds2, c.stream, set);
+  LAUNCH_CHECK();
   for (int r = 0; r <= TOP_BITS_MAX; ++r) {   // <= bits + 1 rounds always finish (each halves the components)
-    if (r == 2) {   // dense blocks are done by now: skip the idle launches
-      std::vector<unsigned> h(4 * nb);
-      HIP_CHECK(hipMemcpyAsync(h.data(), scal, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
+    if (r == 0 || r == 2) {   // dense blocks are mostly one tree after round 0: skip the idle launches
+      unsigned h[4 * TOP_NB_MAX];
+      HIP_CHECK(hipMemcpyAsync(h, scal, 4 * nb * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
       c.sync();
       bool any = false;
-      for (uint32_t b = 0; b < nb; ++b) any |= (live[b] = h[4 * b + 2] == 0);
+      for (uint32_t b = 0; b < nb; ++b) any |= h[4 * b + 2] == 0;
       if (!any) break;
     }
-    for (uint32_t b = 0; b < nb; ++b) {
-      if (!live[b]) continue;
-      hipLaunchKernelGGL(k_top_round, dim3(256), dim3(TOPB), ldsr, c.stream, te[b], ts[b], (const uint64_t *)st);
-      LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_top_hook, dim3(1), dim3(TOPB), lds2, c.stream, ts[b]);
-      LAUNCH_CHECK();
-    }
+    hipLaunchKernelGGL(k_top_round, dim3(TOP_WG, nb), dim3(TOPB), ldsr, c.stream, set, (const uint64_t *)st);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_top_hook, dim3(nb), dim3(TOPB), lds2, c.stream, set);
+    LAUNCH_CHECK();
   }
   // the cut for the next split: the lowest cut block's start
   const uint64_t low = nb == 1 ? cut0 : cut0 - ((uint64_t)(nb - 1) << bits);
