@@ -1053,14 +1053,17 @@ __global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t 
 // by Borůvka rounds with the block's labels in LDS (u16: <= 2^15 vertices).  Dense blocks
 // converge in a few rounds (RMAT-22's top 2^15: 3); every round at least halves the
 // components that have an outgoing edge, so TB + 1 rounds always finish.
-constexpr int TOP_BITS = 15;                 // the map's cut (blocks up to 2^TOP_BITS_MAX: SHEEP_TOP_BITS)
+// the map's cut: blocks of 2^16 positions (RMAT-26 k=64, etree ms: 2^15 32.59 with the cut
+// 0.55; 2^16 32.15 / 0.81; 8 shard maps 77.0 -> 76.6).  SHEEP_TOP_BITS for A/B runs.
+constexpr int TOP_BITS = 16;
 constexpr int TOP_BITS_MAX = 16;            // u16 labels: <= 65536 vertices
 // the top block and the dense blocks right below it, at most TOP_NB in all (RMAT-26 k=64, etree
 // ms: no cut 34.5; 1 block 34.1; 4 blocks 33.8; 8 blocks 33.8 — with the 10-bit finish below)
 constexpr int TOP_NB = 4;
 constexpr int TOPB = 1024;                  // threads per workgroup of the top-block kernels
 constexpr int TOP_WG = 256;                 // workgroups per block of the LDS edge passes (one per CU)
-constexpr uint32_t TOP_HOOK_LDS = 1u << 15; // hook kernels: par / cid in LDS up to this many components
+constexpr uint32_t TOP_HOOK_LDS = 1u << 15; // hooks: par and cid in LDS up to this many components (par alone
+                                            // up to 2^16, with cid in HBM); round 0: u32 minima up to this
 constexpr size_t TOP_ROUND_LDS = 144 * 1024; // a round's dynamic LDS: the labels, then the minima
 constexpr uint64_t TOP_DENSE = 16;          // used when the block's groups hold >= 16 edges per vertex
 constexpr uint64_t NO_EDGE = ~0ull;
@@ -1073,7 +1076,7 @@ struct TopState {
   unsigned *scal;                   // [0] components, [1] a round saw an inter-component edge, [2] done
   uint64_t *st;                     // the cut level's stats row (ST_EXTRA: edges written so far)
   uint64_t *out;                    // the MSF edges go to out[st[KEPT] + st[CONTR] + ...] (the next list)
-  uint16_t *gpar, *gcid;            // par / cid of a hook over more than TOP_HOOK_LDS components
+  uint16_t *gcid;                   // cid of a hook over more than TOP_HOOK_LDS components
   uint32_t v0, V;                   // the block's first vertex and its vertex count
 };
 
@@ -1202,35 +1205,30 @@ __global__ void k_set_u64(uint64_t *p, uint64_t v) { *p = v; }
 // edges (each is an MSF edge), and these picks all point down, so they form a forest; the
 // vertices without a lower neighbour wait for the full rounds.  hasup marks the vertices
 // with an upper neighbour: when at most one root has an edge the block is one tree and
-// needs no round (k_top_hook0).  Read-checked atomics (the minima only fall).
-__global__ __launch_bounds__(BLOCK) void k_top_min0(TopSet t, const uint64_t *__restrict__ st) {
-  const TopState &ts = t.s[blockIdx.y];
-  const TopEdges &te = t.e[blockIdx.y];
-  __shared__ uint64_t s_pre[NSHARD + 1];
-  top_prefix(te, s_pre);
-  __syncthreads();
-  const uint64_t total = s_pre[NSHARD] + (te.g1 - te.g0);
-  const uint32_t v0 = ts.v0;
-  top_edges(te, s_pre, st[ST_TOPNT], 0, total, blockIdx.x * BLOCK + threadIdx.x, gridDim.x * BLOCK, [&](uint64_t e) {
-    if (e == DEAD) return;
-    const uint32_t l = (uint32_t)e - v0, h = (uint32_t)(e >> 32) - v0;
-    if (l < ts.minlo[h]) atomicMin(&ts.minlo[h], l);
-    const unsigned bit = 1u << (l & 31);
-    if (!(ts.hasup[l >> 5] & bit)) atomicOr(&ts.hasup[l >> 5], bit);
-  });
+// needs no round (k_top_hook0).  Each workgroup (one per CU, a contiguous chunk of the
+// edges) keeps its minima and hasup bits in LDS and flushes them with one read-checked
+// atomic per vertex (the minima only fall).
+// Up to 2^15 vertices the minima are u32 (atomicMin); up to 2^16 (SHEEP_TOP_BITS = 16) u16
+// pairs updated by a 32-bit CAS (0xFFFF = none: a lower neighbour is at most V - 2).
+__device__ __forceinline__ void lds_min_u16(uint32_t *w2, uint32_t i, uint32_t v) {
+  uint32_t *w = w2 + (i >> 1);
+  const uint32_t sh = (i & 1) * 16;
+  uint32_t old = *w;
+  while (((old >> sh) & 0xFFFFu) > v) {
+    const uint32_t prev = atomicCAS(w, old, (old & ~(0xFFFFu << sh)) | (v << sh));
+    if (prev == old) break;
+    old = prev;
+  }
 }
-
-// Round 0 with each workgroup's minima and hasup bits in LDS (<= 2^15 vertices, one
-// workgroup per CU, a contiguous chunk each), flushed with one read-checked atomic per
-// vertex and workgroup.
+template <bool W16>
 __global__ __launch_bounds__(TOPB) void k_top_min0_lds(TopSet t, const uint64_t *__restrict__ st) {
   const TopState &ts = t.s[blockIdx.y];
   const TopEdges &te = t.e[blockIdx.y];
   extern __shared__ uint32_t lmin[];
-  __shared__ unsigned lup[TOP_HOOK_LDS / 32];
+  __shared__ unsigned lup[2 * TOP_HOOK_LDS / 32];
   __shared__ uint64_t s_pre[NSHARD + 1];
-  const uint32_t V = ts.V, W = (V + 31) / 32, v0 = ts.v0;
-  for (uint32_t v = threadIdx.x; v < V; v += TOPB) lmin[v] = INVALID;
+  const uint32_t V = ts.V, W = (V + 31) / 32, v0 = ts.v0, NW = W16 ? (V + 1) / 2 : V;
+  for (uint32_t v = threadIdx.x; v < NW; v += TOPB) lmin[v] = INVALID;
   for (uint32_t w = threadIdx.x; w < W; w += TOPB) lup[w] = 0;
   top_prefix(te, s_pre);
   __syncthreads();
@@ -1240,13 +1238,15 @@ __global__ __launch_bounds__(TOPB) void k_top_min0_lds(TopSet t, const uint64_t 
   top_edges(te, s_pre, st[ST_TOPNT], b0 < b1 ? b0 : b1, b1, threadIdx.x, TOPB, [&](uint64_t e) {
     if (e == DEAD) return;
     const uint32_t l = (uint32_t)e - v0, h = (uint32_t)(e >> 32) - v0;
-    if (l < lmin[h]) atomicMin(&lmin[h], l);
+    if (W16) lds_min_u16(lmin, h, l);
+    else if (l < lmin[h]) atomicMin(&lmin[h], l);
     const unsigned bit = 1u << (l & 31);
     if (!(lup[l >> 5] & bit)) atomicOr(&lup[l >> 5], bit);
   });
   __syncthreads();
   for (uint32_t v = threadIdx.x; v < V; v += TOPB) {
-    const uint32_t x = lmin[v];
+    uint32_t x = W16 ? (lmin[v >> 1] >> ((v & 1) * 16)) & 0xFFFFu : lmin[v];
+    if (W16 && x == 0xFFFFu) x = INVALID;
     if (x != INVALID && x < ts.minlo[v]) atomicMin(&ts.minlo[v], x);
   }
   for (uint32_t w = threadIdx.x; w < W; w += TOPB) {
@@ -1324,7 +1324,7 @@ __global__ __launch_bounds__(TOPB) void k_top_hook0(TopSet t) {
   const TopState &ts = t.s[blockIdx.x];
   extern __shared__ uint16_t lds16[];
   const bool big = ts.V > TOP_HOOK_LDS;
-  uint16_t *par = big ? ts.gpar : lds16, *cid = big ? ts.gcid : lds16 + TOP_HOOK_LDS;
+  uint16_t *par = lds16, *cid = big ? ts.gcid : lds16 + TOP_HOOK_LDS;
   __shared__ uint64_t rec[TOP_REC];
   __shared__ unsigned s_cnt, s_roots;
   if (threadIdx.x == 0) s_cnt = s_roots = 0;
@@ -1413,7 +1413,7 @@ __global__ __launch_bounds__(TOPB) void k_top_hook(TopSet t) {
   extern __shared__ uint16_t lds16[];
   const uint32_t C = ts.scal[0];
   const bool big = C > TOP_HOOK_LDS;
-  uint16_t *par = big ? ts.gpar : lds16, *cid = big ? ts.gcid : lds16 + TOP_HOOK_LDS;
+  uint16_t *par = lds16, *cid = big ? ts.gcid : lds16 + TOP_HOOK_LDS;
   __shared__ uint64_t rec[TOP_REC];
   __shared__ unsigned s_cnt;
   if (threadIdx.x == 0) s_cnt = 0;
@@ -1546,8 +1546,7 @@ static uint32_t top_blocks(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t 
   uint16_t *comp = c.get_as<uint16_t>("et_top_comp", nb * VMAX);
   unsigned long long *best = c.get_as<unsigned long long>("et_top_best", nb * VMAX);
   unsigned *scal = c.get_as<unsigned>("et_top_scal", 4 * nb);
-  const bool big = VMAX > TOP_HOOK_LDS;   // (SHEEP_TOP_BITS = 16: the hooks keep par / cid in HBM)
-  uint16_t *gpar = big ? c.get_as<uint16_t>("et_top_gpar", nb * VMAX) : nullptr;
+  const bool big = VMAX > TOP_HOOK_LDS;   // (SHEEP_TOP_BITS = 16: the hooks keep cid in HBM)
   uint16_t *gcid = big ? c.get_as<uint16_t>("et_top_gcid", nb * VMAX) : nullptr;
   TopSet set{};
   uint32_t vmax = 0;
@@ -1563,27 +1562,26 @@ static uint32_t top_blocks(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t 
     ts.scal = scal + 4 * b;
     ts.st = st;
     ts.out = next;
-    ts.gpar = big ? gpar + b * VMAX : nullptr;
     ts.gcid = big ? gcid + b * VMAX : nullptr;
     ts.v0 = (uint32_t)v0;
     ts.V = (uint32_t)(v1 - v0);
     vmax = std::max(vmax, ts.V);
     set.e[b] = TopEdges{tl + b * tcap, tcnt + b * TOP_CSET, r0, b == 0 ? g0 : 0, b == 0 ? g1 : 0};
   }
-  const size_t lds2 = 2 * (size_t)TOP_HOOK_LDS * sizeof(uint16_t);   // par + cid
+  const size_t lds2 = 2 * (size_t)TOP_HOOK_LDS * sizeof(uint16_t);   // par + cid, or par alone up to 2^16
   const size_t ldsr = TOP_ROUND_LDS;                                  // labels + minima
   const size_t ldsm = TOP_HOOK_LDS * sizeof(uint32_t);                // round 0's minima
   allow_lds((const void *)k_top_hook0, (int)lds2);
   allow_lds((const void *)k_top_hook, (int)lds2);
   allow_lds((const void *)k_top_round, (int)ldsr);
-  allow_lds((const void *)k_top_min0_lds, (int)ldsm);
+  allow_lds((const void *)k_top_min0_lds<false>, (int)ldsm);
+  allow_lds((const void *)k_top_min0_lds<true>, (int)ldsm);
   hipLaunchKernelGGL(k_top_init, dim3(grid_for(vmax), nb), dim3(BLOCK), 0, c.stream, set);
   LAUNCH_CHECK();
   if (vmax <= TOP_HOOK_LDS)
-    hipLaunchKernelGGL(k_top_min0_lds, dim3(TOP_WG, nb), dim3(TOPB), ldsm, c.stream, set, (const uint64_t *)st);
-  else
-    hipLaunchKernelGGL(k_top_min0, dim3(grid_for(tcap + (g1 - g0)), nb), dim3(BLOCK), 0, c.stream, set,
-                       (const uint64_t *)st);
+    hipLaunchKernelGGL(k_top_min0_lds<false>, dim3(TOP_WG, nb), dim3(TOPB), ldsm, c.stream, set, (const uint64_t *)st);
+  else   // (<= 2^TOP_BITS_MAX)
+    hipLaunchKernelGGL(k_top_min0_lds<true>, dim3(TOP_WG, nb), dim3(TOPB), ldsm, c.stream, set, (const uint64_t *)st);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_top_hook0, dim3(nb), dim3(TOPB), lds2, c.stream, set);
   LAUNCH_CHECK();
