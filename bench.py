@@ -39,10 +39,11 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-le
 # regions (scans, radix passes) get traffic null.
 LEAF = ("degree", "degree_heads", "sequence", "relabel", "pst_group", "etree_split", "etree_union", "etree_cross",
         "etree_apply", "etree_top", "merge", "kids", "partition")
-REGION_KERNELS = {"degree": ["k_degree_fused"], "relabel": ["k_relabel_scatter", "k_relabel_gather"],
+REGION_KERNELS = {"degree": ["k_degree_fused"], "relabel": ["k_relabel_scatter", "k_relabel_direct", "k_relabel_gather"],
                   "etree_split": ["k_split_count", "k_split_write"], "etree_union": ["k_hook_round", "k_hook_finish", "k_light_top"],
                   "etree_cross": ["k_cross_find"], "etree_apply": ["k_cross_apply", "k_level_clean"],
-                  "etree_top": ["k_top_extract", "k_top_init", "k_top_min0", "k_top_hook0", "k_top_round", "k_top_hook"],
+                  "etree_top": ["k_top_extract_multi", "k_top_sum_counts", "k_top_init", "k_top_min0_lds", "k_top_hook0",
+                                "k_top_round", "k_top_hook"],
                   "evaluate": ["k_pp", "k_eval_records", "k_eval_nodes"]}
 # the newest round's profile of this workload (profiles/rNN/), collected by tools/gpu/gpuprof.sh
 PMC_DIRS = ("r4", "r3")
@@ -70,12 +71,13 @@ def parse():
     ap.add_argument("--eval-reps", type=int, default=3, help="timed evaluator runs (0: skip)")
     ap.add_argument("--cpu-scale", type=int, default=None,
                     help="RMAT scale of the CPU-baseline sample (default: the bench's own RMAT scale up to 26, else 22)")
-    ap.add_argument("--cpu-configs", nargs="+", default=["8x1", "16x1", "16x16"],
+    ap.add_argument("--cpu-configs", nargs="+", default=["8x1", "16x1"],
                     help="PxT configurations of the reference CPU baseline: P MPI ranks x T OpenMP threads each "
                          "(the threads serve the reference's __gnu_parallel::sort, sequence.h:55,85); P x T is capped "
-                         "by the host cores this process may use (os.sched_getaffinity) and the best is reported.  "
-                         "More ranks only add merge hops on rank 0: at RMAT-26, P = 16 / 32 / 64 ran 28 / 71 / 172 s "
-                         "(profiles/r3); the wider sweep is tools/cpu_sweep.py (profiles/r4)")
+                         "by the host cores this process may use (affinity mask and cgroup quota) and the best is "
+                         "reported.  The GPU box grants 16 CPUs' worth of time: at RMAT-26 8x1 / 16x1 / 16x4 / 16x16 / "
+                         "32x1 / 32x8 ran 30.6 / 25.9 / 27.9 / 28.9 / 58.1 / 60.3 s "
+                         "(profiles/r4/cpu_sweep_rmat26_k64.json, tools/cpu_sweep.py)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on cuda:0: rehearse N ranks on a 1-GPU box (the world's host link over TCP "
@@ -501,6 +503,14 @@ def cpu_info():
         usable = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         usable = os.cpu_count()
+    # a cgroup CPU quota caps what the affinity mask shows (the GPU box: 256 CPUs visible,
+    # cpu.max = 16 CPUs' worth of time; profiles/r4/cpu_quota.txt)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            usable = min(usable, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
     return model, os.cpu_count(), usable
 
 
