@@ -39,7 +39,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-le
 # regions (scans, radix passes) get traffic null.
 LEAF = ("degree", "degree_heads", "sequence", "relabel", "pst_group", "etree_split", "etree_union", "etree_cross",
         "etree_apply", "etree_top", "merge", "kids", "partition")
-REGION_KERNELS = {"degree": ["k_degree_fused"], "relabel": ["k_relabel_scatter", "k_relabel_direct", "k_relabel_gather"],
+REGION_KERNELS = {"degree": ["k_degree_fused"], "relabel": ["k_relabel_scatter", "k_relabel_gather"],
                   "etree_split": ["k_split_count", "k_split_write"], "etree_union": ["k_hook_round", "k_hook_finish", "k_light_top"],
                   "etree_cross": ["k_cross_find"], "etree_apply": ["k_cross_apply", "k_level_clean"],
                   "etree_top": ["k_top_extract_multi", "k_top_sum_counts", "k_top_init", "k_top_min0_lds", "k_top_hook0",

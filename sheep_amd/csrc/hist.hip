@@ -712,55 +712,6 @@ __global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restr
   if (__any(lost) && (threadIdx.x & 63) == 0) atomicAdd(&flags[1], 1ull);
 }
 
-// The same pass without staging: each pair's slot comes straight from an LDS atomic on
-// its bucket's region cursor, and the pair is stored from registers (no scan, no barrier
-// inside the tile; the stores are 8-B scattered over the tile's regions instead of runs).
-// SHEEP_RELABEL_DIRECT A/B.
-template <int PER, int NT>
-__global__ __launch_bounds__(NT) void k_relabel_direct(const sheep_xs1 *__restrict__ rec, uint64_t n,
-                                                       const uint32_t *__restrict__ pos, uint64_t pos_size, uint32_t nb,
-                                                       const uint32_t *__restrict__ offsets, uint64_t ntiles,
-                                                       uint64_t *__restrict__ out, unsigned long long *__restrict__ flags) {
-  extern __shared__ uint32_t gb[];
-  const uint64_t tile = xcd_tile();
-  const uint32_t cap = offsets[(uint64_t)nb * ntiles];
-  for (uint32_t b = threadIdx.x; b < nb; b += NT) gb[b] = offsets[(uint64_t)b * ntiles + tile];
-  lds_barrier();
-  bool bad = false, lost = false;
-  const uint64_t base = tile << TLOG;
-  for (uint32_t s0 = 0; s0 < TKEYS; s0 += PER * NT) {
-    uint32_t pt[PER], hd[PER];
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const uint64_t i = base + s0 + (uint64_t)j * NT + threadIdx.x;
-      hd[j] = INVALID;
-      pt[j] = INVALID;
-      if (i < n) {
-        const uint32_t t = rec[i].tail, h = rec[i].head;
-        if (t != h) { hd[j] = h; pt[j] = t; }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      if (hd[j] == INVALID && pt[j] == INVALID) continue;
-      const uint32_t t = pt[j], h = hd[j];
-      const uint32_t ptm = t < pos_size ? pos[t] : PT_OOR;
-      if (h >= pos_size) {
-        if (ptm < PT_OOR) bad = true;   // index.at(head) throws (jtree.cpp:75)
-        continue;
-      }
-      const uint32_t dst = atomicAdd(&gb[h >> WBITS], 1u);
-      if (dst < cap) out[dst] = ((uint64_t)ptm << 32) | h;
-      else lost = true;
-    }
-  }
-  lds_barrier();
-  for (uint32_t b = threadIdx.x; b < nb; b += NT)
-    if (gb[b] != offsets[(uint64_t)b * ntiles + tile + 1]) lost = true;   // the region's end
-  if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(&flags[0], 1ull);
-  if (__any(lost) && (threadIdx.x & 63) == 0) atomicAdd(&flags[1], 1ull);
-}
-
 // One workgroup per (bucket, slice of <= CHUNK pairs): the bucket's pos slice in LDS.
 // Same outcomes as k_relabel: both endpoints sequenced -> tree edge (hi << 32 | lo);
 // one sequenced, the other an unsequenced slot -> POSTORDER pst for the sequenced one.
@@ -946,22 +897,6 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   const size_t fixed = ((2 * nb + HB / WAVE + 1) & ~1ull) * 4;
   auto scatter = [&]() {
     HIP_CHECK(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c.stream));
-    static const int direct = getenv("SHEEP_RELABEL_DIRECT") ? atoi(getenv("SHEEP_RELABEL_DIRECT")) : 0;
-    if (direct) {
-      const size_t lds = nb * 4;
-      if (direct == 1) {
-        allow_lds((const void *)k_relabel_direct<8, 512>, (int)lds);
-        hipLaunchKernelGGL((k_relabel_direct<8, 512>), dim3((unsigned)ntiles), dim3(512), lds, c.stream, rec, nrec, pos,
-                           pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
-      } else {
-        allow_lds((const void *)k_relabel_direct<16, 256>, (int)lds);
-        hipLaunchKernelGGL((k_relabel_direct<16, 256>), dim3((unsigned)ntiles), dim3(256), lds, c.stream, rec, nrec, pos,
-                           pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
-      }
-      LAUNCH_CHECK();
-      HIP_CHECK(hipMemcpyAsync(c.h_scalars + 12, flags, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-      return;
-    }
     // Two 512-thread workgroups per CU, 4K-record sub-tiles (81 VGPRs keep a 1024-thread
     // workgroup alone on its CU, idle at every barrier): RMAT-26 9.18 -> 8.92 ms.  Up to
     // 4096 buckets (vertex ids below 2^27), the scan's limit for 512 threads.
