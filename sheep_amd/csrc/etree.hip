@@ -948,6 +948,153 @@ __global__ __launch_bounds__(WAVE) void k_fin_heavy(const uint64_t *__restrict__
   }
 }
 
+// The last B levels of a block as the same divide and conquer, inside ONE workgroup:
+// its union-find, component tops, right-half minima and claims in LDS (B <= 13: 112 KB),
+// its list in global scratch as local (lo | hi << 16) words, ping-ponged between two
+// buffers over the block's own range.  Per level s: (1) hook the light edges (both ends in
+// the left half: CAS on the LDS roots, root = smaller id), (2) top[root] = max hi over
+// the light edges and mt[root] = min hi over the cross edges, (3) parent(top(r)) = m_r for
+// every root with a cross edge, and the next list = the entries that stay plus the
+// contractions (m_r, b) with b != m_r, first-seen (m, b) per b kept (the claim rule of
+// k_cross_apply).  Unlike Liu's sweep (k_fin_heavy: one step per hi), the work of a level
+// spreads over the workgroup, so blocks can be large enough to take the last global
+// levels too.  Workgroups take blocks from a ticket (largest lists need not come first:
+// the blocks are short against the grid).
+constexpr int FDC_T = 1024;
+__device__ __forceinline__ uint32_t dc_find(uint32_t *uf, uint32_t x) {
+  for (;;) {   // path halving (pointers only move toward the root: safe beside other threads)
+    const uint32_t p = uf[x];
+    if (p == x) return x;
+    const uint32_t g = uf[p];
+    if (g == p) return p;
+    uf[x] = g;
+    x = g;
+  }
+}
+template <int B>
+__global__ __launch_bounds__(FDC_T) void k_fin_dc(const uint64_t *__restrict__ fin, const uint64_t *__restrict__ eb,
+                                                  const uint32_t *__restrict__ vb, const uint32_t *__restrict__ blocks,
+                                                  const unsigned long long *__restrict__ n_blocks, uint32_t clo,
+                                                  uint32_t *__restrict__ buf, uint64_t cap,
+                                                  unsigned long long *__restrict__ ticket, uint32_t *__restrict__ parent) {
+  constexpr uint32_t NV = 1u << B, MASK = NV - 1;
+  __shared__ uint32_t uf[NV], top[NV], mt[NV];
+  __shared__ uint16_t claim[NV];
+  __shared__ unsigned s_cnt[3];   // [0], [1]: the levels' next lists by parity; [2]: the block's load
+  __shared__ uint64_t s_w;
+  const unsigned long long nbk = *n_blocks;
+  const uint32_t lane = threadIdx.x & 63;
+  for (;;) {
+    if (threadIdx.x == 0) s_w = atomicAdd(ticket, 1ull);
+    __syncthreads();
+    const uint64_t w = s_w;
+    if (w >= nbk) break;   // (uniform)
+    const uint32_t b = blocks[w];
+    const uint32_t v0 = vb[b], cnt = vb[b + 1] - v0;
+    const uint64_t e0 = eb[b], e1 = eb[b + 1];
+    const uint32_t yb0 = (uint32_t)(((uint64_t)b) << B);
+    auto ly = [&](uint32_t x) { return spread(v0 + x, clo) - yb0; };   // offset inside the block
+    uint32_t *cur = buf + e0, *nxt = buf + cap + e0;
+    uint32_t n = 0;
+    {   // the block's entries (lo << 32 | hi, swapped by k_fin_gather) as local words
+      if (threadIdx.x == 0) s_cnt[2] = 0;
+      __syncthreads();
+      const uint32_t ne = (uint32_t)(e1 - e0);
+      for (uint32_t i0 = 0; i0 < ne; i0 += FDC_T) {
+        const uint32_t i = i0 + threadIdx.x;
+        uint32_t word = 0;
+        bool keep = false;
+        if (i < ne) {
+          const uint64_t e = fin[e0 + i];
+          const uint32_t l = (uint32_t)(e >> 32) - v0, h = (uint32_t)e - v0;
+          keep = e != DEAD && l < cnt && h < cnt && l < h;   // both ends lie in the block (the D&C invariant)
+          word = l | (h << 16);
+        }
+        const uint64_t km = __ballot(keep);
+        uint32_t base = 0;
+        if (km && lane == (uint32_t)(__ffsll((unsigned long long)km) - 1)) base = atomicAdd(&s_cnt[2], (unsigned)__popcll(km));
+        base = __shfl(base, __ffsll((unsigned long long)(km ? km : 1)) - 1, 64);
+        if (keep) cur[base + __popcll(km & lanemask_lt())] = word;
+      }
+      __syncthreads();
+      n = s_cnt[2];
+    }
+    for (int s = B - 1; s >= 0 && n; --s) {
+      const int par = s & 1;
+      for (uint32_t x = threadIdx.x; x < cnt; x += FDC_T) {
+        uf[x] = x;
+        top[x] = x;
+        mt[x] = INVALID;
+        claim[x] = 0xFFFF;
+      }
+      if (threadIdx.x == 0) s_cnt[par] = 0;
+      __syncthreads();
+      for (uint32_t i = threadIdx.x; i < n; i += FDC_T) {   // (1) light edges
+        const uint32_t u = cur[i], l = u & 0xFFFF, h = u >> 16;
+        const uint32_t ya = ly(l), yb = ly(h);
+        if (((ya ^ yb) >> s) != 0 || ((yb >> s) & 1)) continue;
+        uint32_t a = l, c2 = h;
+        for (;;) {
+          a = dc_find(uf, a);
+          c2 = dc_find(uf, c2);
+          if (a == c2) break;
+          const uint32_t lo = a < c2 ? a : c2, hi = a < c2 ? c2 : a;
+          if (atomicCAS(&uf[hi], hi, lo) == hi) break;
+        }
+      }
+      __syncthreads();
+      for (uint32_t i = threadIdx.x; i < n; i += FDC_T) {   // (2) tops and minima
+        const uint32_t u = cur[i], l = u & 0xFFFF, h = u >> 16;
+        const uint32_t ya = ly(l), yb = ly(h), d = (ya ^ yb) >> s;
+        if (d == 0 && ((yb >> s) & 1)) continue;   // right half: untouched
+        const uint32_t r = dc_find(uf, l);
+        if (d == 0) {
+          if (h > top[r]) atomicMax(&top[r], h);
+        } else if (h < mt[r]) {
+          atomicMin(&mt[r], h);
+        }
+      }
+      __syncthreads();
+      for (uint32_t x = threadIdx.x; x < cnt; x += FDC_T)   // (3) adoption
+        if (mt[x] != INVALID) parent[v0 + top[x]] = v0 + mt[x];
+      for (uint32_t i0 = 0; i0 < n; i0 += FDC_T) {   // (3) the next list (wave-uniform trips: ballots)
+        const uint32_t i = i0 + threadIdx.x;
+        bool keep = false;
+        uint32_t word = 0;
+        if (i < n) {
+          const uint32_t u = cur[i], l = u & 0xFFFF, h = u >> 16;
+          const uint32_t ya = ly(l), yb = ly(h), d = (ya ^ yb) >> s;
+          if (d == 0) {
+            keep = true;
+            word = u;
+          } else {
+            const uint32_t m = mt[dc_find(uf, l)];
+            if (h != m) {
+              const uint32_t cl = claim[h];
+              if (cl != m) {
+                keep = true;
+                word = m | (h << 16);
+                if (cl == 0xFFFF) claim[h] = (uint16_t)m;   // first seen: a plain store (k_cross_apply's rule)
+              }
+            }
+          }
+        }
+        const uint64_t km = __ballot(keep);
+        uint32_t base = 0;
+        if (km && lane == (uint32_t)(__ffsll((unsigned long long)km) - 1)) base = atomicAdd(&s_cnt[par], (unsigned)__popcll(km));
+        base = __shfl(base, __ffsll((unsigned long long)(km ? km : 1)) - 1, 64);
+        if (keep) nxt[base + __popcll(km & lanemask_lt())] = word;
+      }
+      __syncthreads();
+      n = s_cnt[par];
+      uint32_t *t = cur;
+      cur = nxt;
+      nxt = t;
+    }
+    __syncthreads();   // LDS and s_w are reused by the next block
+  }
+}
+
 // ---- merge input ------------------------------------------------------------------
 // K trees: tree 0 at t0, tree k >= 1 at t1 + (k - 1) * stride (two separate trees, or K
 // stacked ones).  Node i contributes its DISTINCT parents over the K trees as edges
@@ -1636,6 +1783,8 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   const unsigned gt = grid_tiles(m), gt2 = grid_for(lcap + m, SPLIT_TILE), gf = grid_for(m, BLOCK * XK), gn = grid_for(n);
   const int FINB = fin_bits < 0 ? 0 : fin_bits > FIN_BITS_MAX ? FIN_BITS_MAX : fin_bits;   // levels s < FINB: Liu per block (0: none)
   const int nglobal = L > FINB ? L - FINB : 0;
+  static const int g_fin_dc = getenv("SHEEP_FIN_DC") ? atoi(getenv("SHEEP_FIN_DC")) : 0;   // (A/B runs)
+  const bool fin_dc = g_fin_dc && FINB >= 8;
   // the per-level state starts clean; tagged words need no restore between levels,
   // untagged ones are restored at each level's end (k_level_clean)
   const bool tagged = n < TAG_MAX_N;
@@ -1809,10 +1958,20 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       unsigned long long *n_lh = (unsigned long long *)(n_fin + 1);   // light, heavy counts (zeroed with stats)
       hipLaunchKernelGGL(k_fin_bounds, dim3(grid_for(nb > n ? nb + 1 : n + 1)), dim3(BLOCK), 0, c.stream,
                          (const uint64_t *)fin, (const uint64_t *)n_fin, clo, FINB, nb, n, eb, vb, light, heavy, n_lh,
-                         FINB <= FIN_LANE_BITS ? FIN_HEAVY : 0);
+                         fin_dc ? 0 : FINB <= FIN_LANE_BITS ? FIN_HEAVY : 0);
       LAUNCH_CHECK();
       const unsigned gl = (unsigned)((nb + WAVE - 1) / WAVE), gh = (unsigned)(nb < 8192 ? nb : 8192);
-      switch (FINB) {
+      if (fin_dc) {   // every non-empty block on the heavy list: one workgroup each, from a ticket
+        uint32_t *dbuf = c.get_as<uint32_t>("et_fin_dc", 2 * cap);
+        unsigned long long *ticket = (unsigned long long *)(n_fin + 3);   // (zeroed with stats)
+        const unsigned gd = (unsigned)(nb < 1024 ? nb : 1024);
+        switch (FINB) {
+#define SHEEP_FIN_DC(B)                                                                                            case B:                                                                                                            hipLaunchKernelGGL(k_fin_dc<B>, dim3(gd), dim3(FDC_T), 0, c.stream, (const uint64_t *)fin, (const uint64_t *)eb,                        (const uint32_t *)vb, (const uint32_t *)heavy, (const unsigned long long *)(n_lh + 1), clo, dbuf,                        cap, ticket, parent);                                                                         LAUNCH_CHECK();                                                                                                  break;
+          SHEEP_FIN_DC(8) SHEEP_FIN_DC(9) SHEEP_FIN_DC(10) SHEEP_FIN_DC(11) SHEEP_FIN_DC(12) SHEEP_FIN_DC(13)
+#undef SHEEP_FIN_DC
+          default: throw Error(SHEEP_ERR_ARG, "etree: bad finishing block size");
+        }
+      } else switch (FINB) {
 #define SHEEP_FIN_LANES(B)                                                                                       \
     hipLaunchKernelGGL(k_fin_lanes<B>, dim3(gl), dim3(WAVE), 0, c.stream, (const uint64_t *)fin, (const uint64_t *)eb, \
                        (const uint32_t *)vb, (const uint32_t *)light, (const unsigned long long *)n_lh, parent);  \
@@ -2020,7 +2179,8 @@ static void merge_set(Ctx &c, const TreeSet &ts, uint32_t K, uint64_t n, sheep_j
   uint64_t lo = 0, hi = n;
   if (n >= 2) spread_params(n, &L, &clo);
   // only as many parts as global levels (below them the per-block finish runs whole)
-  const int nglobal = L > FIN_MERGE ? L - FIN_MERGE : 0;
+  static const int fin_merge = getenv("SHEEP_FIN_MERGE") ? atoi(getenv("SHEEP_FIN_MERGE")) : FIN_MERGE;   // (A/B runs)
+  const int nglobal = L > fin_merge ? L - fin_merge : 0;
   if (nparts > 1 && (l >= nglobal || L > 31)) l = 0;   // too small a tree to split: every part runs it all
   uint32_t ylo = 0, yhi = 0;
   if (l > 0) {
@@ -2039,7 +2199,7 @@ static void merge_set(Ctx &c, const TreeSet &ts, uint32_t K, uint64_t n, sheep_j
     TimedRegion tr(c, "merge", 8 * (uint64_t)K * n);   // the K trees
     // groups activated at levels >= l are b < L - l
     const uint64_t m = merge_edges(c, ts, K, n, pst, &edges, &seg, &L, l > 0 ? L - l : 0, lo, hi);
-    etree_from_edges(c, edges, m, n, parent, seg, FIN_MERGE, l > 0 ? l : -1, ylo, yhi);
+    etree_from_edges(c, edges, m, n, parent, seg, fin_merge, l > 0 ? l : -1, ylo, yhi);
   }
   hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);
   LAUNCH_CHECK();
