@@ -971,6 +971,11 @@ __device__ __forceinline__ uint32_t dc_find(uint32_t *uf, uint32_t x) {
     x = g;
   }
 }
+// blocks whose list fits run it from LDS: the budget keeps two workgroups per CU up to
+// B = 12 (14 B of state per position) and one above
+template <int B> constexpr uint32_t fdc_lcap() {
+  return (uint32_t)(((B >= 13 ? 160 * 1024 - 1024 : 80 * 1024 - 512) - 14 * (1 << B)) / 8);
+}
 template <int B>
 __global__ __launch_bounds__(FDC_T) void k_fin_dc(const uint64_t *__restrict__ fin, const uint64_t *__restrict__ eb,
                                                   const uint32_t *__restrict__ vb, const uint32_t *__restrict__ blocks,
@@ -980,6 +985,8 @@ __global__ __launch_bounds__(FDC_T) void k_fin_dc(const uint64_t *__restrict__ f
   constexpr uint32_t NV = 1u << B, MASK = NV - 1;
   __shared__ uint32_t uf[NV], top[NV], mt[NV];
   __shared__ uint16_t claim[NV];
+  constexpr uint32_t LCAP = fdc_lcap<B>();
+  __shared__ uint32_t lbuf[2][LCAP];
   __shared__ unsigned s_cnt[3];   // [0], [1]: the levels' next lists by parity; [2]: the block's load
   __shared__ uint64_t s_w;
   const unsigned long long nbk = *n_blocks;
@@ -994,7 +1001,8 @@ __global__ __launch_bounds__(FDC_T) void k_fin_dc(const uint64_t *__restrict__ f
     const uint64_t e0 = eb[b], e1 = eb[b + 1];
     const uint32_t yb0 = (uint32_t)(((uint64_t)b) << B);
     auto ly = [&](uint32_t x) { return spread(v0 + x, clo) - yb0; };   // offset inside the block
-    uint32_t *cur = buf + e0, *nxt = buf + cap + e0;
+    const bool in_lds = e1 - e0 <= LCAP;   // (a level's list never outgrows its input)
+    uint32_t *cur = in_lds ? lbuf[0] : buf + e0, *nxt = in_lds ? lbuf[1] : buf + cap + e0;
     uint32_t n = 0;
     {   // the block's entries (lo << 32 | hi, swapped by k_fin_gather) as local words
       if (threadIdx.x == 0) s_cnt[2] = 0;
@@ -1616,7 +1624,7 @@ static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
 // Hub blocks go to whole waves (k_fin_heavy).  A merge's edges spread evenly over the
 // blocks, so its finish takes 11 bits (RMAT-26, 8 shard trees: K-way merge 19.5 -> 17.9
 // ms; 10: 18.1, 12: 18.2).
-constexpr int FIN_MERGE = 11, FIN_MAP = 10;
+constexpr int FIN_MERGE = 12, FIN_MAP = 12;
 
 // spread(x) = floor(x * c / 2^32), c = floor(2^(32+L) / n) in [2^32, 2^33), L = ceil(log2 n):
 // monotone, injective on [0,n), image in [0, 2^L).  clo = c - 2^32.
@@ -1783,7 +1791,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   const unsigned gt = grid_tiles(m), gt2 = grid_for(lcap + m, SPLIT_TILE), gf = grid_for(m, BLOCK * XK), gn = grid_for(n);
   const int FINB = fin_bits < 0 ? 0 : fin_bits > FIN_BITS_MAX ? FIN_BITS_MAX : fin_bits;   // levels s < FINB: Liu per block (0: none)
   const int nglobal = L > FINB ? L - FINB : 0;
-  static const int g_fin_dc = getenv("SHEEP_FIN_DC") ? atoi(getenv("SHEEP_FIN_DC")) : 0;   // (A/B runs)
+  static const int g_fin_dc = getenv("SHEEP_FIN_DC") ? atoi(getenv("SHEEP_FIN_DC")) : 1;   // (0: Liu per block, A/B runs)
   const bool fin_dc = g_fin_dc && FINB >= 8;
   // the per-level state starts clean; tagged words need no restore between levels,
   // untagged ones are restored at each level's end (k_level_clean)
