@@ -960,7 +960,7 @@ __global__ __launch_bounds__(WAVE) void k_fin_heavy(const uint64_t *__restrict__
 // spreads over the workgroup, so blocks can be large enough to take the last global
 // levels too.  Workgroups take blocks from a ticket (largest lists need not come first:
 // the blocks are short against the grid).
-constexpr int FDC_T = 1024;
+constexpr int FDC_T = 1024, FDC_U = 4;
 __device__ __forceinline__ uint32_t dc_find(uint32_t *uf, uint32_t x) {
   for (;;) {   // path halving (pointers only move toward the root: safe beside other threads)
     const uint32_t p = uf[x];
@@ -973,30 +973,32 @@ __device__ __forceinline__ uint32_t dc_find(uint32_t *uf, uint32_t x) {
 }
 // blocks whose list fits run it from LDS: the budget keeps two workgroups per CU up to
 // B = 12 (14 B of state per position) and one above
-template <int B> constexpr uint32_t fdc_lcap() {
+constexpr uint32_t fdc_lcap(int B) {
   return (uint32_t)(((B >= 13 ? 160 * 1024 - 1024 : 80 * 1024 - 512) - 14 * (1 << B)) / 8);
 }
 template <int B>
 __global__ __launch_bounds__(FDC_T) void k_fin_dc(const uint64_t *__restrict__ fin, const uint64_t *__restrict__ eb,
                                                   const uint32_t *__restrict__ vb, const uint32_t *__restrict__ blocks,
-                                                  const unsigned long long *__restrict__ n_blocks, uint32_t clo,
+                                                  const unsigned long long *__restrict__ n_blocks,
+                                                  const uint32_t *__restrict__ blocks2,
+                                                  const unsigned long long *__restrict__ n_blocks2, uint32_t clo,
                                                   uint32_t *__restrict__ buf, uint64_t cap,
                                                   unsigned long long *__restrict__ ticket, uint32_t *__restrict__ parent) {
   constexpr uint32_t NV = 1u << B, MASK = NV - 1;
   __shared__ uint32_t uf[NV], top[NV], mt[NV];
   __shared__ uint16_t claim[NV];
-  constexpr uint32_t LCAP = fdc_lcap<B>();
+  constexpr uint32_t LCAP = fdc_lcap(B);
   __shared__ uint32_t lbuf[2][LCAP];
   __shared__ unsigned s_cnt[3];   // [0], [1]: the levels' next lists by parity; [2]: the block's load
   __shared__ uint64_t s_w;
-  const unsigned long long nbk = *n_blocks;
+  const unsigned long long nbk = *n_blocks, nbk2 = *n_blocks2;   // the long lists first, then the short ones
   const uint32_t lane = threadIdx.x & 63;
   for (;;) {
     if (threadIdx.x == 0) s_w = atomicAdd(ticket, 1ull);
     __syncthreads();
     const uint64_t w = s_w;
-    if (w >= nbk) break;   // (uniform)
-    const uint32_t b = blocks[w];
+    if (w >= nbk + nbk2) break;   // (uniform)
+    const uint32_t b = w < nbk ? blocks[w] : blocks2[w - nbk];
     const uint32_t v0 = vb[b], cnt = vb[b + 1] - v0;
     const uint64_t e0 = eb[b], e1 = eb[b + 1];
     const uint32_t yb0 = (uint32_t)(((uint64_t)b) << B);
@@ -1037,10 +1039,22 @@ __global__ __launch_bounds__(FDC_T) void k_fin_dc(const uint64_t *__restrict__ f
       }
       if (threadIdx.x == 0) s_cnt[par] = 0;
       __syncthreads();
-      for (uint32_t i = threadIdx.x; i < n; i += FDC_T) {   // (1) light edges
-        const uint32_t u = cur[i], l = u & 0xFFFF, h = u >> 16;
+      // the list's words FDC_U per thread in flight before any is used (a long block's
+      // list is in HBM: one latency per word would serialise its passes)
+      auto each = [&](auto &&f) {
+        for (uint32_t i0 = threadIdx.x; i0 < n; i0 += FDC_U * FDC_T) {
+          uint32_t u[FDC_U];
+#pragma unroll
+          for (int j = 0; j < FDC_U; ++j) u[j] = i0 + j * FDC_T < n ? cur[i0 + j * FDC_T] : 0xFFFFFFFFu;
+#pragma unroll
+          for (int j = 0; j < FDC_U; ++j)
+            if (u[j] != 0xFFFFFFFFu) f(u[j]);
+        }
+      };
+      each([&](uint32_t u) {   // (1) light edges
+        const uint32_t l = u & 0xFFFF, h = u >> 16;
         const uint32_t ya = ly(l), yb = ly(h);
-        if (((ya ^ yb) >> s) != 0 || ((yb >> s) & 1)) continue;
+        if (((ya ^ yb) >> s) != 0 || ((yb >> s) & 1)) return;
         uint32_t a = l, c2 = h;
         for (;;) {
           a = dc_find(uf, a);
@@ -1049,49 +1063,57 @@ __global__ __launch_bounds__(FDC_T) void k_fin_dc(const uint64_t *__restrict__ f
           const uint32_t lo = a < c2 ? a : c2, hi = a < c2 ? c2 : a;
           if (atomicCAS(&uf[hi], hi, lo) == hi) break;
         }
-      }
+      });
       __syncthreads();
-      for (uint32_t i = threadIdx.x; i < n; i += FDC_T) {   // (2) tops and minima
-        const uint32_t u = cur[i], l = u & 0xFFFF, h = u >> 16;
+      each([&](uint32_t u) {   // (2) tops and minima
+        const uint32_t l = u & 0xFFFF, h = u >> 16;
         const uint32_t ya = ly(l), yb = ly(h), d = (ya ^ yb) >> s;
-        if (d == 0 && ((yb >> s) & 1)) continue;   // right half: untouched
+        if (d == 0 && ((yb >> s) & 1)) return;   // right half: untouched
         const uint32_t r = dc_find(uf, l);
         if (d == 0) {
           if (h > top[r]) atomicMax(&top[r], h);
         } else if (h < mt[r]) {
           atomicMin(&mt[r], h);
         }
-      }
+      });
       __syncthreads();
       for (uint32_t x = threadIdx.x; x < cnt; x += FDC_T)   // (3) adoption
         if (mt[x] != INVALID) parent[v0 + top[x]] = v0 + mt[x];
-      for (uint32_t i0 = 0; i0 < n; i0 += FDC_T) {   // (3) the next list (wave-uniform trips: ballots)
-        const uint32_t i = i0 + threadIdx.x;
-        bool keep = false;
-        uint32_t word = 0;
-        if (i < n) {
-          const uint32_t u = cur[i], l = u & 0xFFFF, h = u >> 16;
-          const uint32_t ya = ly(l), yb = ly(h), d = (ya ^ yb) >> s;
-          if (d == 0) {
-            keep = true;
-            word = u;
-          } else {
-            const uint32_t m = mt[dc_find(uf, l)];
-            if (h != m) {
-              const uint32_t cl = claim[h];
-              if (cl != m) {
-                keep = true;
-                word = m | (h << 16);
-                if (cl == 0xFFFF) claim[h] = (uint16_t)m;   // first seen: a plain store (k_cross_apply's rule)
+      for (uint32_t i0 = 0; i0 < n; i0 += FDC_U * FDC_T) {   // (3) the next list (wave-uniform trips: ballots)
+        uint32_t u[FDC_U];
+#pragma unroll
+        for (int j = 0; j < FDC_U; ++j) {
+          const uint32_t i = i0 + j * FDC_T + threadIdx.x;
+          u[j] = i < n ? cur[i] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int j = 0; j < FDC_U; ++j) {
+          bool keep = false;
+          uint32_t word = 0;
+          if (u[j] != 0xFFFFFFFFu) {
+            const uint32_t l = u[j] & 0xFFFF, h = u[j] >> 16;
+            const uint32_t ya = ly(l), yb = ly(h), d = (ya ^ yb) >> s;
+            if (d == 0) {
+              keep = true;
+              word = u[j];
+            } else {
+              const uint32_t m = mt[dc_find(uf, l)];
+              if (h != m) {
+                const uint32_t cl = claim[h];
+                if (cl != m) {
+                  keep = true;
+                  word = m | (h << 16);
+                  if (cl == 0xFFFF) claim[h] = (uint16_t)m;   // first seen: a plain store (k_cross_apply's rule)
+                }
               }
             }
           }
+          const uint64_t km = __ballot(keep);
+          uint32_t base = 0;
+          if (km && lane == (uint32_t)(__ffsll((unsigned long long)km) - 1)) base = atomicAdd(&s_cnt[par], (unsigned)__popcll(km));
+          base = __shfl(base, __ffsll((unsigned long long)(km ? km : 1)) - 1, 64);
+          if (keep) nxt[base + __popcll(km & lanemask_lt())] = word;
         }
-        const uint64_t km = __ballot(keep);
-        uint32_t base = 0;
-        if (km && lane == (uint32_t)(__ffsll((unsigned long long)km) - 1)) base = atomicAdd(&s_cnt[par], (unsigned)__popcll(km));
-        base = __shfl(base, __ffsll((unsigned long long)(km ? km : 1)) - 1, 64);
-        if (keep) nxt[base + __popcll(km & lanemask_lt())] = word;
       }
       __syncthreads();
       n = s_cnt[par];
@@ -1966,15 +1988,16 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       unsigned long long *n_lh = (unsigned long long *)(n_fin + 1);   // light, heavy counts (zeroed with stats)
       hipLaunchKernelGGL(k_fin_bounds, dim3(grid_for(nb > n ? nb + 1 : n + 1)), dim3(BLOCK), 0, c.stream,
                          (const uint64_t *)fin, (const uint64_t *)n_fin, clo, FINB, nb, n, eb, vb, light, heavy, n_lh,
-                         fin_dc ? 0 : FINB <= FIN_LANE_BITS ? FIN_HEAVY : 0);
+                         fin_dc ? fdc_lcap(FINB) : FINB <= FIN_LANE_BITS ? FIN_HEAVY : 0);
       LAUNCH_CHECK();
       const unsigned gl = (unsigned)((nb + WAVE - 1) / WAVE), gh = (unsigned)(nb < 8192 ? nb : 8192);
-      if (fin_dc) {   // every non-empty block on the heavy list: one workgroup each, from a ticket
+      if (fin_dc) {   // every non-empty block, one workgroup each from a ticket: lists past LDS first
         uint32_t *dbuf = c.get_as<uint32_t>("et_fin_dc", 2 * cap);
         unsigned long long *ticket = (unsigned long long *)(n_fin + 3);   // (zeroed with stats)
         const unsigned gd = (unsigned)(nb < 1024 ? nb : 1024);
         switch (FINB) {
-#define SHEEP_FIN_DC(B)                                                                                            case B:                                                                                                            hipLaunchKernelGGL(k_fin_dc<B>, dim3(gd), dim3(FDC_T), 0, c.stream, (const uint64_t *)fin, (const uint64_t *)eb,                        (const uint32_t *)vb, (const uint32_t *)heavy, (const unsigned long long *)(n_lh + 1), clo, dbuf,                        cap, ticket, parent);                                                                         LAUNCH_CHECK();                                                                                                  break;
+#define SHEEP_FIN_DC(B)                                                                                            case B:                                                                                                            hipLaunchKernelGGL(k_fin_dc<B>, dim3(gd), dim3(FDC_T), 0, c.stream, (const uint64_t *)fin, (const uint64_t *)eb,                        (const uint32_t *)vb, (const uint32_t *)heavy, (const unsigned long long *)(n_lh + 1),                \
+                       (const uint32_t *)light, (const unsigned long long *)n_lh, clo, dbuf,                        cap, ticket, parent);                                                                         LAUNCH_CHECK();                                                                                                  break;
           SHEEP_FIN_DC(8) SHEEP_FIN_DC(9) SHEEP_FIN_DC(10) SHEEP_FIN_DC(11) SHEEP_FIN_DC(12) SHEEP_FIN_DC(13)
 #undef SHEEP_FIN_DC
           default: throw Error(SHEEP_ERR_ARG, "etree: bad finishing block size");
