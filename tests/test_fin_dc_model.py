@@ -1,0 +1,88 @@
+"""CPU model of the per-block D&C finish (sheep_amd/csrc/etree.hip k_fin_dc): the level
+rules it runs inside one workgroup — hook the light edges, tops and right-half minima,
+parent(top(r)) = m_r, the next list = entries that stay plus the first-seen contractions
+(m_r, b) — restated in Python over one block of 2^B positions and checked against Liu's
+sequential elimination tree (the reference's JTree sweep, jtree.cpp:66-110) on random
+multigraphs, with the list shuffled between levels (the kernel's list order is arbitrary).
+The GPU kernel itself is pinned by the parity tests (tests/test_gpu_parity.py)."""
+import random
+
+
+def liu(n, edges):
+    parent, anc = [-1] * n, list(range(n))
+
+    def find(x):
+        while anc[x] != x:
+            anc[x] = anc[anc[x]]
+            x = anc[x]
+        return x
+
+    lower = [[] for _ in range(n)]
+    for lo, hi in edges:
+        lower[hi].append(lo)
+    for v in range(n):
+        for a in lower[v]:
+            r = find(a)
+            if r != v:
+                parent[r] = v
+                anc[r] = v
+    return parent
+
+
+def block_dc(n, edges, B, rng):
+    parent = [-1] * n
+    cur = list(edges)
+    for s in range(B - 1, -1, -1):
+        rng.shuffle(cur)
+        uf, top, mt, claim = list(range(n)), list(range(n)), [None] * n, [None] * n
+
+        def find(x):
+            while uf[x] != x:
+                x = uf[x]
+            return x
+
+        for lo, hi in cur:   # (1) light edges: both ends in the left half
+            if ((lo ^ hi) >> s) == 0 and not (hi >> s) & 1:
+                a, b = find(lo), find(hi)
+                if a != b:
+                    uf[max(a, b)] = min(a, b)
+        for lo, hi in cur:   # (2) tops and right-half minima
+            d = (lo ^ hi) >> s
+            if d == 0 and (hi >> s) & 1:
+                continue
+            r = find(lo)
+            if d == 0:
+                top[r] = max(top[r], hi)
+            else:
+                mt[r] = hi if mt[r] is None else min(mt[r], hi)
+        for x in range(n):   # (3) adoption
+            if mt[x] is not None:
+                parent[top[x]] = mt[x]
+        nxt = []
+        for lo, hi in cur:   # (3) the next list
+            if ((lo ^ hi) >> s) == 0:
+                nxt.append((lo, hi))
+                continue
+            m = mt[find(lo)]
+            if hi == m or claim[hi] == m:
+                continue
+            if claim[hi] is None:
+                claim[hi] = m
+            nxt.append((m, hi))
+        cur = nxt
+    return parent
+
+
+def test_block_dc_equals_liu_on_random_multigraphs():
+    rng = random.Random(2026)
+    for _ in range(300):
+        B = rng.randint(1, 7)
+        n = 1 << B
+        pairs = set()
+        for _ in range(rng.randint(0, 4 * n)):
+            a, b = rng.randrange(n), rng.randrange(n)
+            if a != b:
+                pairs.add((min(a, b), max(a, b)))
+        edges = sorted(pairs)
+        edges += rng.sample(edges, min(len(edges), 5))   # repeated edges, as contractions produce
+        assert block_dc(n, edges, B, rng) == liu(n, edges)
