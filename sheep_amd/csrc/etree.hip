@@ -990,6 +990,7 @@ __global__ __launch_bounds__(FDC_T) void k_fin_dc(const uint64_t *__restrict__ f
   constexpr uint32_t LCAP = fdc_lcap(B);
   __shared__ uint32_t lbuf[2][LCAP];
   __shared__ unsigned s_cnt[3];   // [0], [1]: the levels' next lists by parity; [2]: the block's load
+  __shared__ unsigned s_roots;
   __shared__ uint64_t s_w;
   const unsigned long long nbk = *n_blocks, nbk2 = *n_blocks2;   // the long lists first, then the short ones
   const uint32_t lane = threadIdx.x & 63;
@@ -1006,7 +1007,65 @@ __global__ __launch_bounds__(FDC_T) void k_fin_dc(const uint64_t *__restrict__ f
     const bool in_lds = e1 - e0 <= LCAP;   // (a level's list never outgrows its input)
     uint32_t *cur = in_lds ? lbuf[0] : buf + e0, *nxt = in_lds ? lbuf[1] : buf + cap + e0;
     uint32_t n = 0;
-    {   // the block's entries (lo << 32 | hi, swapped by k_fin_gather) as local words
+    bool loaded = false;
+    if (!in_lds) {
+      // A list past LDS (a dense block): round 0 of Borůvka first, as for the top block —
+      // every position's lowest lower neighbour (mt) and a has-upper-neighbour flag (top);
+      // when at most one root has an edge the block is one tree and its edges become its
+      // minimum spanning forest {(minlo(x), x)} (etree(G) = etree(MSF(G))): <= cnt - 1 words.
+      for (uint32_t x = threadIdx.x; x < cnt; x += FDC_T) {
+        mt[x] = INVALID;
+        top[x] = 0;
+      }
+      if (threadIdx.x == 0) s_cnt[2] = s_roots = 0;
+      __syncthreads();
+      const uint32_t ne = (uint32_t)(e1 - e0);
+      for (uint32_t i0 = threadIdx.x; i0 < ne; i0 += FDC_U * FDC_T) {
+        uint64_t ev[FDC_U];
+#pragma unroll
+        for (int j = 0; j < FDC_U; ++j) ev[j] = i0 + j * FDC_T < ne ? fin[e0 + i0 + j * FDC_T] : DEAD;
+#pragma unroll
+        for (int j = 0; j < FDC_U; ++j) {
+          if (ev[j] == DEAD) continue;
+          const uint32_t l = (uint32_t)(ev[j] >> 32) - v0, h = (uint32_t)ev[j] - v0;
+          if (l >= cnt || h >= cnt || l >= h) continue;
+          if (l < mt[h]) atomicMin(&mt[h], l);
+          if (!top[l]) top[l] = 1;
+        }
+      }
+      __syncthreads();
+      for (uint32_t x0 = 0; x0 < cnt; x0 += FDC_T) {   // non-roots, and roots with an edge (wave-counted)
+        const uint32_t x = x0 + threadIdx.x;
+        const bool nonroot = x < cnt && mt[x] != INVALID, eroot = x < cnt && !nonroot && top[x];
+        const uint64_t ma = __ballot(nonroot), mb = __ballot(eroot);
+        if (lane == 0 && ma) atomicAdd(&s_cnt[2], (unsigned)__popcll(ma));
+        if (lane == 0 && mb) atomicAdd(&s_roots, (unsigned)__popcll(mb));
+      }
+      __syncthreads();
+      if (s_roots <= 1) {   // (uniform)
+        if (s_cnt[2] <= LCAP) {
+          cur = lbuf[0];
+          nxt = lbuf[1];
+        }
+        __syncthreads();   // s_cnt[2] read by all
+        if (threadIdx.x == 0) s_cnt[2] = 0;
+        __syncthreads();
+        for (uint32_t x0 = 0; x0 < cnt; x0 += FDC_T) {
+          const uint32_t x = x0 + threadIdx.x;
+          const bool keep = x < cnt && mt[x] != INVALID;
+          const uint32_t word = keep ? mt[x] | (x << 16) : 0;
+          const uint64_t km = __ballot(keep);
+          uint32_t base = 0;
+          if (km && lane == (uint32_t)(__ffsll((unsigned long long)km) - 1)) base = atomicAdd(&s_cnt[2], (unsigned)__popcll(km));
+          base = __shfl(base, __ffsll((unsigned long long)(km ? km : 1)) - 1, 64);
+          if (keep) cur[base + __popcll(km & lanemask_lt())] = word;
+        }
+        __syncthreads();
+        n = s_cnt[2];
+        loaded = true;
+      }
+    }
+    if (!loaded) {   // the block's entries (lo << 32 | hi, swapped by k_fin_gather) as local words
       if (threadIdx.x == 0) s_cnt[2] = 0;
       __syncthreads();
       const uint32_t ne = (uint32_t)(e1 - e0);

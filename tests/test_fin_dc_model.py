@@ -29,9 +29,24 @@ def liu(n, edges):
     return parent
 
 
-def block_dc(n, edges, B, rng):
+def one_tree_msf(n, edges):
+    """Round 0 of Borůvka as k_fin_dc runs it on a long list: every vertex's lowest lower
+    neighbour; when at most one root has an edge the picks {(minlo(x), x)} are the minimum
+    spanning forest under (hi, lo) (else None: the block keeps its list)."""
+    minlo, up = [None] * n, [False] * n
+    for lo, hi in edges:
+        minlo[hi] = lo if minlo[hi] is None else min(minlo[hi], lo)
+        up[lo] = True
+    if sum(1 for x in range(n) if minlo[x] is None and up[x]) > 1:
+        return None
+    return [(minlo[x], x) for x in range(n) if minlo[x] is not None]
+
+
+def block_dc(n, edges, B, rng, msf=False):
     parent = [-1] * n
     cur = list(edges)
+    if msf and one_tree_msf(n, cur) is not None:
+        cur = one_tree_msf(n, cur)
     for s in range(B - 1, -1, -1):
         rng.shuffle(cur)
         uf, top, mt, claim = list(range(n)), list(range(n)), [None] * n, [None] * n
@@ -86,3 +101,4 @@ def test_block_dc_equals_liu_on_random_multigraphs():
         edges = sorted(pairs)
         edges += rng.sample(edges, min(len(edges), 5))   # repeated edges, as contractions produce
         assert block_dc(n, edges, B, rng) == liu(n, edges)
+        assert block_dc(n, edges, B, rng, msf=True) == liu(n, edges)
