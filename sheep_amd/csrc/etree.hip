@@ -1695,17 +1695,13 @@ __global__ void k_dbg_blocks(const uint64_t *__restrict__ a, const uint64_t *__r
 void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
 
 static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
-// Finishing block size (log2 positions) of the per-block Liu pass.  The last levels of a
-// map keep ~5M list entries each at RMAT-26 (0.6 ms per level for a dozen launches);
-// one sort + the per-block pass replaces the last 8 (RMAT-26: 49.7 -> 45.9 ms; B = 7:
-// 46.4; B = 10: 42.7 against 39.9, B = 12: 82.5 — hub blocks serialise on one wave).
-// With the dense top blocks cut to their MSFs (below) the hub blocks are gone and 10 bits
-// pay (RMAT-26, 4 blocks cut: etree 33.8 ms at B = 10 against 34.1 at B = 8 and 33.6 at 11;
-// no cut, B = 10: 37.4 — the finish alone 5.2 ms).
-// Hub blocks go to whole waves (k_fin_heavy).  A merge's edges spread evenly over the
-// blocks, so its finish takes 11 bits (RMAT-26, 8 shard trees: K-way merge 19.5 -> 17.9
-// ms; 10: 18.1, 12: 18.2).
-constexpr int FIN_MERGE = 12, FIN_MAP = 12;
+// Finishing block size (log2 positions).  Liu's sweep per block (SHEEP_FIN_DC=0) takes one
+// step per hi, so 10 bits were its best for maps (RMAT-26 etree 32.0-32.2 ms) and 11 for
+// merges.  The per-block D&C (k_fin_dc) spreads a level over a workgroup and cuts long
+// block lists to their MSF first: RMAT-26 etree 31.0 / 30.5 / 30.0 ms at 11 / 12 / 13 bits
+// (13: one workgroup per CU, 112 KB of LDS state); 8 shard maps 76.3 -> 71.2 ms and the
+// 8-tree merge 15.4 -> 14.1 ms at 12 bits.
+constexpr int FIN_MERGE = 12, FIN_MAP = 13;
 
 // spread(x) = floor(x * c / 2^32), c = floor(2^(32+L) / n) in [2^32, 2^33), L = ceil(log2 n):
 // monotone, injective on [0,n), image in [0, 2^L).  clo = c - 2^32.
