@@ -159,6 +159,39 @@ def test_relabel_layout_reuse_and_stale(gpu_ctx):
     assert np.array_equal(p, op) and np.array_equal(w, ow)
 
 
+def test_relabel_records_in_any_order(gpu_ctx):
+    """Records in no order (the degree pass's probe sees descents) take the three-pass
+    relabel (head buckets, then tail buckets, hist.hip k_relabel_mid): self-loops and
+    repeated records leave holes in the tail regions.  The tree and pst must be the
+    oracle's; a layout made stale in place (tails moved to other buckets) falls back to the
+    two-pass form with a recount, same tree."""
+    import sheep_amd
+    import torch
+    d = sheep_amd.rmat(16, 16, 31)
+    loops = d[:4000].clone()
+    loops[:, 1] = loops[:, 0]                            # self-loops
+    d = torch.cat([d, loops, d[:2000]])                  # and repeated records
+    g = torch.Generator(device=d.device)
+    g.manual_seed(9)
+    d = d[torch.randperm(d.shape[0], device=d.device, generator=g)].contiguous()
+    sw = d[::2, 0].clone()
+    d[::2, 0] = d[::2, 1]
+    d[::2, 1] = sw
+    h = sheep_amd.to_numpy_u32(d).reshape(-1, 3)
+    t_, h_ = h[:, 0].copy(), h[:, 1].copy()
+    s = sheep_amd.degree_sequence(d)
+    seq = oracle.sequence(t_, h_)
+    assert np.array_equal(s.numpy(), seq)
+    op, ow = oracle.build_tree(t_, h_, seq)
+    p, w = _tree_np(sheep_amd.build_tree(d, s))
+    assert np.array_equal(p, op) and np.array_equal(w, ow)
+    sw = d[::3, 0].clone()
+    d[::3, 0] = d[::3, 1]
+    d[::3, 1] = sw                                      # stale layouts: same ptr, same nrec
+    p, w = _tree_np(sheep_amd.build_tree(d, s))
+    assert np.array_equal(p, op) and np.array_equal(w, ow)
+
+
 def test_shards_merge_to_whole_tree(gpu_ctx):
     """Shard independence: 4 contiguous shards, pairwise merges == the whole tree."""
     import sheep_amd
