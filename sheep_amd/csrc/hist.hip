@@ -720,9 +720,11 @@ __global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restr
 // the chunk is walked one output tile at a time with the tile's counts in LDS after the
 // pos slice, flushed with one atomicAdd per non-zero bucket (a tile can span two chunks).
 template <bool COUNT>
-__global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restrict__ pairs, const Chunk *__restrict__ chunks,
+// (pairs may be edges itself: each slot is read, then written, by the same thread — the
+// three-pass form relabels in place, so neither pointer is __restrict__)
+__global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *pairs, const Chunk *__restrict__ chunks,
                                                        const uint32_t *__restrict__ pos, uint64_t pos_size,
-                                                       uint32_t *__restrict__ pst, uint64_t *__restrict__ edges,
+                                                       uint32_t *__restrict__ pst, uint64_t *edges,
                                                        unsigned long long *__restrict__ flags, EdgeLoPadded lk,
                                                        uint32_t lnb, uint32_t *__restrict__ tile_hist, uint64_t ntiles,
                                                        uint64_t n_tree) {
@@ -1080,7 +1082,7 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
       ((size_t)W + 2 * nb) * 4 <= 160 * 1024 && getenv("SHEEP_RELABEL_2PASS") == nullptr) {
     scatter(true);
     const uint64_t m3 = hl.tstart[nb];
-    uint64_t *pairs2 = c.get_as<uint64_t>("rl_pairs2", m3 ? m3 : 1);
+    uint64_t *pairs2 = edges;   // the tail-bucketed pairs, relabelled in place by the gather (capacity nrec)
     const uint32_t *ts = c.get_as<uint32_t>("tail_starts", nb + 1);
     unsigned *tcur = c.get_as<unsigned>("rl_tcur", nb);
     HIP_CHECK(hipMemcpyAsync(tcur, ts, nb * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
