@@ -82,14 +82,7 @@ struct Ctx {
   // Bucket layout of the last degree_count's head histogram (LLAMA mode): the scanned
   // (bucket, tile) offsets live in ws["head_offsets"]; relabel_bucketed reuses them when
   // it sees the same records and key range (and verifies every region's count in-kernel).
-  // (tstart: the tail buckets' region starts over all records, from the endpoint count of
-  // records in any order; the relabel's three-pass form for such records)
-  struct HeadLayout {
-    const void *rec = nullptr;
-    uint64_t nrec = 0, K = 0;
-    std::vector<uint32_t> bstart, tstart;
-    bool valid = false, tail_valid = false;
-  };
+  struct HeadLayout { const void *rec = nullptr; uint64_t nrec = 0, K = 0; std::vector<uint32_t> bstart; bool valid = false; };
   HeadLayout head_layout;
   // the degree pass's sortedness probe of the last record buffer (sequence.hip)
   struct SortedProbe { const void *rec = nullptr; uint64_t nrec = 0; bool sorted = true; };

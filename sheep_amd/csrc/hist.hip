@@ -646,7 +646,7 @@ struct RelabelKeys {
 // (stale offsets: the host recounts; a stale run's writes stay in bounds and are
 // discarded) — one random LDS read per record fewer than a per-region bound.  flags[0]: a
 // sequenced endpoint's neighbour >= pos_size.
-template <int PER, int NT = HB, bool RAW = false>   // RAW: carry the tail itself, not pos[tail]
+template <int PER, int NT = HB>
 __global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restrict__ rec, uint64_t n,
                                                         const uint32_t *__restrict__ pos, uint64_t pos_size, uint32_t nb,
                                                         const uint32_t *__restrict__ offsets, uint64_t ntiles,
@@ -680,7 +680,7 @@ __global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restr
       x[j] = NO_PAIR;
       if (hd[j] == INVALID && pt[j] == INVALID) continue;
       const uint32_t t = pt[j], h = hd[j];
-      const uint32_t ptm = RAW && h < pos_size ? t : t < pos_size ? pos[t] : PT_OOR;
+      const uint32_t ptm = t < pos_size ? pos[t] : PT_OOR;
       if (h >= pos_size) {
         if (ptm < PT_OOR) bad = true;   // index.at(head) throws (jtree.cpp:75)
         continue;
@@ -720,11 +720,9 @@ __global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restr
 // the chunk is walked one output tile at a time with the tile's counts in LDS after the
 // pos slice, flushed with one atomicAdd per non-zero bucket (a tile can span two chunks).
 template <bool COUNT>
-// (pairs may be edges itself: each slot is read, then written, by the same thread — the
-// three-pass form relabels in place, so neither pointer is __restrict__)
-__global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *pairs, const Chunk *__restrict__ chunks,
+__global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restrict__ pairs, const Chunk *__restrict__ chunks,
                                                        const uint32_t *__restrict__ pos, uint64_t pos_size,
-                                                       uint32_t *__restrict__ pst, uint64_t *edges,
+                                                       uint32_t *__restrict__ pst, uint64_t *__restrict__ edges,
                                                        unsigned long long *__restrict__ flags, EdgeLoPadded lk,
                                                        uint32_t lnb, uint32_t *__restrict__ tile_hist, uint64_t ntiles,
                                                        uint64_t n_tree) {
@@ -751,10 +749,6 @@ __global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *pairs, co
       for (int j = 0; j < 8; ++j) {
         const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
         if (i >= s1) continue;
-        if (x[j] == NO_PAIR) {   // a hole of the three-pass form's tail regions
-          edges[i] = ~0ull;
-          continue;
-        }
         const uint32_t ptm = (uint32_t)(x[j] >> 32), ph = lds[(uint32_t)x[j] & (W - 1)];
         uint64_t e = ~0ull;   // DEAD
         // (ptm is a position < n_tree, INVALID or PT_OOR; anything else is a stale region
@@ -782,82 +776,6 @@ __global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *pairs, co
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(&flags[0], 1ull);
 }
 
-// ---- the relabel for records in any order: three passes, no random gather ------------
-// Tail-sorted records make pass A's pos[tail] gather near-sequential; in any other order it
-// is random over the whole index (RMAT-26 shuffled: relabel 30.7 ms against 14.3).  Records
-// in any order therefore go: A' (k_relabel_scatter<RAW>) the raw (tail, head) pairs into
-// the head buckets; B' (k_relabel_mid) per head-bucket slice, pos[head] from the slice in
-// LDS, the pairs (pos[head], tail) into the TAIL buckets — regions sized by the endpoint
-// count's tail columns (all records: a self-loop or an out-of-range record leaves a hole,
-// filled with NO_PAIR by k_fill_holes), each slice's runs reserved with one atomic per tail
-// bucket and written from an LDS cursor; then k_relabel_gather unchanged over the tail
-// buckets (pos[tail] from the slice; the roles of the two ends are symmetric).
-template <int U = 8>
-__global__ __launch_bounds__(HB) void k_relabel_mid(const uint64_t *__restrict__ pairs, const Chunk *__restrict__ chunks,
-                                                    const uint32_t *__restrict__ pos, uint64_t pos_size, uint32_t ntb,
-                                                    unsigned *__restrict__ tcur, const uint32_t *__restrict__ tstart,
-                                                    uint64_t *__restrict__ out, unsigned long long *__restrict__ flags) {
-  extern __shared__ uint32_t lds[];
-  uint32_t *const lcnt = lds + W, *const lbase = lcnt + ntb;
-  const Chunk ch = chunks[blockIdx.x];
-  const uint64_t v0 = (uint64_t)ch.bucket << WBITS;
-  for (uint32_t i = threadIdx.x; i < W; i += HB) lds[i] = v0 + i < pos_size ? pos[v0 + i] : INVALID;
-  for (uint32_t b = threadIdx.x; b < ntb; b += HB) lcnt[b] = 0;
-  lds_barrier();
-  for (uint64_t i0 = ch.beg + threadIdx.x; i0 < ch.end; i0 += (uint64_t)U * HB) {   // the slice's tail buckets
-    uint32_t t[U];
-#pragma unroll
-    for (int j = 0; j < U; ++j) t[j] = i0 + (uint64_t)j * HB < ch.end ? (uint32_t)(pairs[i0 + (uint64_t)j * HB] >> 32) : INVALID;
-#pragma unroll
-    for (int j = 0; j < U; ++j)
-      if (t[j] < pos_size) atomicAdd(&lcnt[t[j] >> WBITS], 1u);
-  }
-  lds_barrier();
-  for (uint32_t b = threadIdx.x; b < ntb; b += HB) {
-    const uint32_t cnt = lcnt[b];
-    lbase[b] = cnt ? atomicAdd(&tcur[b], cnt) : 0;
-    lcnt[b] = 0;
-  }
-  lds_barrier();
-  bool bad = false, lost = false;
-  for (uint64_t i0 = ch.beg + threadIdx.x; i0 < ch.end; i0 += (uint64_t)U * HB) {
-    uint64_t x[U];
-#pragma unroll
-    for (int j = 0; j < U; ++j) x[j] = i0 + (uint64_t)j * HB < ch.end ? pairs[i0 + (uint64_t)j * HB] : NO_PAIR;
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      if (x[j] == NO_PAIR) continue;
-      const uint32_t t = (uint32_t)(x[j] >> 32), ph = lds[(uint32_t)x[j] & (W - 1)];
-      if (t >= pos_size) {   // index.at(tail) throws when the head is sequenced (jtree.cpp:75)
-        if (ph != INVALID) bad = true;
-        continue;
-      }
-      const uint32_t tb = t >> WBITS, dst = lbase[tb] + atomicAdd(&lcnt[tb], 1u);
-      if (dst < tstart[tb + 1]) out[dst] = ((uint64_t)ph << 32) | t;
-      else lost = true;   // (a stale layout: the host falls back)
-    }
-  }
-  if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(&flags[0], 1ull);
-  if (__any(lost) && (threadIdx.x & 63) == 0) atomicAdd(&flags[1], 1ull);
-}
-
-// out[tcur[b], tstart[b + 1]) = NO_PAIR: the tail regions' unused ends
-__global__ __launch_bounds__(BLOCK) void k_fill_holes(const unsigned *__restrict__ tcur, const uint32_t *__restrict__ tstart,
-                                                      uint64_t *__restrict__ out) {
-  const uint32_t b = blockIdx.x, e = tstart[b + 1];
-  for (uint32_t i = tcur[b] + threadIdx.x; i < e; i += BLOCK) out[i] = NO_PAIR;
-}
-
-// tot[b] = the tail columns' sum of bucket b's endpoint count row (one workgroup per bucket)
-__global__ __launch_bounds__(BLOCK) void k_tail_totals(const uint32_t *__restrict__ tile_hist, uint64_t nt,
-                                                       uint32_t *__restrict__ tot) {
-  const uint32_t *row = tile_hist + (uint64_t)blockIdx.x * 2 * nt;
-  uint64_t sum = 0;
-  for (uint64_t t = threadIdx.x; t < nt; t += BLOCK) sum += row[t];
-  const uint64_t r = block_reduce_u64(sum, false);
-  if (threadIdx.x == 0) tot[blockIdx.x] = (uint32_t)r;
-}
-
 // seg[i] = position of bucket sb[i] in the grouped array (sb: bucket indices)
 __global__ void k_seg_from_buckets(const uint32_t *__restrict__ bstart, const uint64_t *__restrict__ sb, int L,
                                    uint64_t *__restrict__ seg) {
@@ -879,9 +797,8 @@ bool degree_fused(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_
 
 void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt, bool counted) {
   Ctx::HeadLayout &hl = c.head_layout;
-  hl.valid = hl.tail_valid = false;
+  hl.valid = false;
   hl.bstart.clear();
-  hl.tstart.clear();
   const uint64_t nb = (K + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
   if (!llama || nb == 0 || nb > 8192 || ntiles * nb + 1 >= (1ull << 32)) {
     histogram_add(c, HeadKeys{rec, llama}, nrec, K, cnt, nullptr, nullptr, nullptr, nullptr, nullptr, counted);
@@ -909,9 +826,8 @@ bool degree_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uin
 void histogram_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt,
                          bool counted) {
   Ctx::HeadLayout &hl = c.head_layout;
-  hl.valid = hl.tail_valid = false;
+  hl.valid = false;
   hl.bstart.clear();
-  hl.tstart.clear();
   if (!counted) {   // the relabel counts its own head layout
     histogram_add(c, EndpointKeys{rec, nrec, llama}, 2 * nrec, K, cnt);
     return;
@@ -931,15 +847,6 @@ void histogram_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama,
     hipLaunchKernelGGL(k_bucket_starts, dim3(grid_for(nb + 1)), dim3(BLOCK), 0, c.stream, (const uint32_t *)off, nt,
                        (uint32_t)nb, (const uint32_t *)(off + nt * nb), bs_dev);
     LAUNCH_CHECK();
-    const bool tails = nrec < (1ull << 32);   // the tail regions of the three-pass relabel (relabel_bucketed)
-    if (tails) {
-      uint32_t *ts = c.get_as<uint32_t>("tail_starts", nb + 1);
-      hipLaunchKernelGGL(k_tail_totals, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, tile_hist, nt, ts);
-      LAUNCH_CHECK();
-      scan_exclusive_u32(c, ts, ts, nb, ts + nb);
-      hl.tstart.assign(nb + 1, 0);
-      HIP_CHECK(hipMemcpyAsync(hl.tstart.data(), ts, (nb + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
-    }
     hl.bstart.assign(nb + 1, 0);
     HIP_CHECK(hipMemcpyAsync(hl.bstart.data(), bs_dev, (nb + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
     c.sync();
@@ -947,7 +854,6 @@ void histogram_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama,
     hl.nrec = nrec;
     hl.K = K;
     hl.valid = true;
-    hl.tail_valid = tails;
   }
   histogram_add(c, EndpointKeysP{rec, nrec, nt * TKEYS, llama}, nt * TKEYS + nrec, K, cnt, nullptr, nullptr, nullptr,
                 nullptr, nullptr, true);
@@ -960,9 +866,8 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   const uint64_t nb = (pos_size + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
   if (nrec == 0 || nb == 0 || nb > 8192 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return UINT64_MAX;
   for (const void *f : {(const void *)k_relabel_scatter<8>, (const void *)k_relabel_scatter<4>,
-                        (const void *)k_relabel_scatter<8, 512>, (const void *)k_relabel_scatter<8, 512, true>,
-                        (const void *)k_relabel_gather<false>, (const void *)k_relabel_gather<true>,
-                        (const void *)k_relabel_mid<>})
+                        (const void *)k_relabel_scatter<8, 512>,
+                        (const void *)k_relabel_gather<false>, (const void *)k_relabel_gather<true>})
     allow_full_lds(f);
   Ctx::HeadLayout &hl = c.head_layout;
   unsigned long long *flags = c.get_as<unsigned long long>("rl_flags", 2);
@@ -990,16 +895,8 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   const uint64_t total = hl.bstart[nb];
   uint64_t *pairs = c.get_as<uint64_t>("rl_pairs", total ? total : 1);
   const size_t fixed = ((2 * nb + HB / WAVE + 1) & ~1ull) * 4;
-  auto scatter = [&](bool raw = false) {
+  auto scatter = [&]() {
     HIP_CHECK(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c.stream));
-    if (raw) {   // (three-pass form: 512 x 8 only; the caller checked the bucket count)
-      constexpr int NT = 512, P = 8;
-      const size_t lds = ((2 * nb + NT / WAVE + 1) & ~1ull) * 4 + (size_t)P * NT * 8;
-      hipLaunchKernelGGL((k_relabel_scatter<P, NT, true>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec, nrec, pos,
-                         pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
-      LAUNCH_CHECK();
-      return;
-    }
     // Two 512-thread workgroups per CU, 4K-record sub-tiles (81 VGPRs keep a 1024-thread
     // workgroup alone on its CU, idle at every barrier): RMAT-26 9.18 -> 8.92 ms.  Up to
     // 4096 buckets (vertex ids below 2^27), the scan's limit for 512 threads.
@@ -1035,23 +932,11 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   // run's writes stay in bounds (the gather checks every tail position against n) and its
   // pst / error counts are cleared.
   const uint64_t ntiles_e_max = (total + TKEYS - 1) >> TLOG;
-  // chunks (bucket, slice) of the regions `st` (st[b] .. st[b + 1]) into pinned host memory
-  // and the device (`tag` names the buffers); returns the count
-  auto chunks_of = [&](const std::vector<uint32_t> &st, const char *tag) -> std::pair<uint64_t, Chunk *> {
-    const uint64_t m = st[nb], chunk = chunk_for(m);
+  auto gather = [&]() -> bool {
+    const uint64_t m = hl.bstart[nb];
+    const uint64_t chunk = chunk_for(m);
     uint64_t nch = 0;
-    for (uint32_t b = 0; b < nb; ++b) nch += (st[b + 1] - st[b] + chunk - 1) / chunk;
-    if (!nch) return {0, nullptr};
-    Chunk *hch = (Chunk *)c.get_pinned(std::string("rl_chunks_host_") + tag, nch * sizeof(Chunk));
-    uint64_t j = 0;
-    for (uint32_t b = 0; b < nb; ++b)
-      for (uint64_t x = st[b]; x < st[b + 1]; x += chunk) hch[j++] = {x, x + chunk < st[b + 1] ? x + chunk : st[b + 1], b, 0};
-    Chunk *dch = c.get_as<Chunk>(std::string("rl_chunks_") + tag, nch);
-    HIP_CHECK(hipMemcpyAsync(dch, hch, nch * sizeof(Chunk), hipMemcpyHostToDevice, c.stream));
-    return {nch, dch};
-  };
-  auto gather = [&](const std::vector<uint32_t> &st, const uint64_t *src) -> bool {
-    const uint64_t m = st[nb];
+    for (uint32_t b = 0; b < nb; ++b) nch += (hl.bstart[b + 1] - hl.bstart[b] + chunk - 1) / chunk;
     // the grouping's count pass fused in when its bucket counters fit beside the pos slice
     const uint64_t ntiles_e = (m + TKEYS - 1) >> TLOG;
     const bool count = lg && m && lg->nb && ((size_t)W + lg->nb) * 4 <= 160 * 1024 &&
@@ -1061,63 +946,29 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
       tile_hist = c.get_as<uint32_t>("hist_tiles", std::max(ntiles_e, ntiles_e_max) * lg->nb + 1);
       HIP_CHECK(hipMemsetAsync(tile_hist, 0, ntiles_e * lg->nb * sizeof(uint32_t), c.stream));
     }
-    const auto [nch, dch] = chunks_of(st, "g");
     if (!nch) return count;
+    Chunk *hch = (Chunk *)c.get_pinned("rl_chunks_host", nch * sizeof(Chunk));
+    uint64_t j = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+      const uint64_t beg = hl.bstart[b], end = hl.bstart[b + 1];
+      for (uint64_t x = beg; x < end; x += chunk) hch[j++] = {x, x + chunk < end ? x + chunk : end, b, 0};
+    }
+    Chunk *dch = c.get_as<Chunk>("rl_chunks", nch);
+    HIP_CHECK(hipMemcpyAsync(dch, hch, nch * sizeof(Chunk), hipMemcpyHostToDevice, c.stream));
     const EdgeLoPadded lk{edges, lg ? lg->d_pad : nullptr, lg ? lg->clo : 0, lg ? lg->mask : 0};
     if (count)
       hipLaunchKernelGGL(k_relabel_gather<true>, dim3((unsigned)nch), dim3(HB), (W + lg->nb) * 4, c.stream,
-                         src, (const Chunk *)dch, pos, pos_size, pst, edges, err, lk, lg->nb,
+                         (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err, lk, lg->nb,
                          tile_hist, ntiles_e, n_tree);
     else
       hipLaunchKernelGGL(k_relabel_gather<false>, dim3((unsigned)nch), dim3(HB), W * 4, c.stream,
-                         src, (const Chunk *)dch, pos, pos_size, pst, edges, err, lk, 0u,
+                         (const uint64_t *)pairs, (const Chunk *)dch, pos, pos_size, pst, edges, err, lk, 0u,
                          (uint32_t *)nullptr, (uint64_t)0, n_tree);
     LAUNCH_CHECK();
     return count;
   };
-  // records in any order (the degree pass's probe) with the endpoint count's tail regions:
-  // the three-pass form (k_relabel_mid above)
-  const bool any_order = c.sorted_probe.rec == rec && c.sorted_probe.nrec == nrec && !c.sorted_probe.sorted;
-  if (any_order && cached && hl.tail_valid && hl.tstart.size() == nb + 1 && hl.tstart[nb] <= nrec && nb <= 8 * 512 &&
-      ((size_t)W + 2 * nb) * 4 <= 160 * 1024 && getenv("SHEEP_RELABEL_2PASS") == nullptr) {
-    scatter(true);
-    const uint64_t m3 = hl.tstart[nb];
-    uint64_t *pairs2 = edges;   // the tail-bucketed pairs, relabelled in place by the gather (capacity nrec)
-    const uint32_t *ts = c.get_as<uint32_t>("tail_starts", nb + 1);
-    unsigned *tcur = c.get_as<unsigned>("rl_tcur", nb);
-    HIP_CHECK(hipMemcpyAsync(tcur, ts, nb * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
-    const auto [nh, dh] = chunks_of(hl.bstart, "h");
-    if (nh) {
-      hipLaunchKernelGGL(k_relabel_mid<>, dim3((unsigned)nh), dim3(HB), ((size_t)W + 2 * nb) * 4, c.stream,
-                         (const uint64_t *)pairs, (const Chunk *)dh, pos, pos_size, (uint32_t)nb, tcur, ts, pairs2, flags);
-      LAUNCH_CHECK();
-    }
-    hipLaunchKernelGGL(k_fill_holes, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, (const unsigned *)tcur, ts, pairs2);
-    LAUNCH_CHECK();
-    HIP_CHECK(hipMemcpyAsync(c.h_scalars + 12, flags, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-    const bool count3 = gather(hl.tstart, pairs2);
-    c.sync();
-    if (!c.h_scalars[13]) {
-      if (c.h_scalars[12]) HIP_CHECK(hipMemsetAsync(err, 0xFF, 1, c.stream));   // range error (reported by the caller)
-      if (counted) *counted = count3;
-      return m3;
-    }
-    // a stale layout: clear what ran and take the two-pass form with a recount
-    HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned long long), c.stream));
-    if (n_tree) HIP_CHECK(hipMemsetAsync(pst, 0, n_tree * sizeof(uint32_t), c.stream));
-    hl.tail_valid = false;
-    off = recount();
-    if (hl.bstart[nb] > total) pairs = c.get_as<uint64_t>("rl_pairs", hl.bstart[nb]);
-    scatter();
-    const bool count2 = gather(hl.bstart, pairs);
-    c.sync();
-    if (c.h_scalars[13]) throw Error(SHEEP_ERR_HIP, "relabel: bucket layout inconsistent with its own count");
-    if (c.h_scalars[12]) HIP_CHECK(hipMemsetAsync(err, 0xFF, 1, c.stream));
-    if (counted) *counted = count2;
-    return hl.bstart[nb];
-  }
   scatter();
-  bool count = gather(hl.bstart, pairs);
+  bool count = gather();
   c.sync();
   if (c.h_scalars[13]) {   // offsets did not match these records: recount, run both passes again
     if (!cached) throw Error(SHEEP_ERR_HIP, "relabel: bucket layout inconsistent with its own count");
@@ -1126,7 +977,7 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
     off = recount();
     if (hl.bstart[nb] > total) pairs = c.get_as<uint64_t>("rl_pairs", hl.bstart[nb]);
     scatter();
-    count = gather(hl.bstart, pairs);
+    count = gather();
     c.sync();
     if (c.h_scalars[13]) throw Error(SHEEP_ERR_HIP, "relabel: bucket layout inconsistent with its own count");
   }

@@ -160,11 +160,10 @@ def test_relabel_layout_reuse_and_stale(gpu_ctx):
 
 
 def test_relabel_records_in_any_order(gpu_ctx):
-    """Records in no order (the degree pass's probe sees descents) take the three-pass
-    relabel (head buckets, then tail buckets, hist.hip k_relabel_mid): self-loops and
-    repeated records leave holes in the tail regions.  The tree and pst must be the
-    oracle's; a layout made stale in place (tails moved to other buckets) falls back to the
-    two-pass form with a recount, same tree."""
+    """Records in no order (the degree pass's probe sees descents: both endpoints are
+    bucketed, and the endpoint count's head columns are the relabel's head layout), with
+    self-loops and repeated records: the tree and pst must be the oracle's; a layout made
+    stale in place (heads moved to other buckets) is detected and recounted, same tree."""
     import sheep_amd
     import torch
     d = sheep_amd.rmat(16, 16, 31)
