@@ -646,7 +646,7 @@ struct RelabelKeys {
 // (stale offsets: the host recounts; a stale run's writes stay in bounds and are
 // discarded) — one random LDS read per record fewer than a per-region bound.  flags[0]: a
 // sequenced endpoint's neighbour >= pos_size.
-template <int PER, int NT = HB>
+template <int PER, int NT = HB, bool PL = false>   // PL: the staged pairs as two u32 planes
 __global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restrict__ rec, uint64_t n,
                                                         const uint32_t *__restrict__ pos, uint64_t pos_size, uint32_t nb,
                                                         const uint32_t *__restrict__ offsets, uint64_t ntiles,
@@ -655,6 +655,7 @@ __global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restr
   extern __shared__ uint32_t lds[];
   uint32_t *cur = lds, *gb = lds + nb, *wsum = lds + 2 * nb;
   uint64_t *stage = (uint64_t *)(lds + ((2 * nb + NT / WAVE + 1) & ~1u));
+  uint32_t *const slo = (uint32_t *)stage, *const shi = slo + SUB;
   const uint64_t tile = xcd_tile();
   const uint32_t cap = offsets[(uint64_t)nb * ntiles];   // the scanned total: the output's length
   for (uint32_t b = threadIdx.x; b < nb; b += NT) gb[b] = offsets[(uint64_t)b * ntiles + tile];
@@ -694,10 +695,18 @@ __global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restr
     lds_barrier();
 #pragma unroll
     for (int j = 0; j < PER; ++j)
-      if (x[j] != NO_PAIR) stage[cur[(uint32_t)x[j] >> WBITS] + rk[j]] = x[j];
+      if (x[j] != NO_PAIR) {
+        const uint32_t at = cur[(uint32_t)x[j] >> WBITS] + rk[j];
+        if (PL) {
+          slo[at] = (uint32_t)x[j];
+          shi[at] = (uint32_t)(x[j] >> 32);
+        } else {
+          stage[at] = x[j];
+        }
+      }
     lds_barrier();
     for (uint32_t j = threadIdx.x; j < total; j += NT) {
-      const uint64_t v = stage[j];
+      const uint64_t v = PL ? ((uint64_t)shi[j] << 32) | slo[j] : stage[j];
       const uint32_t b = (uint32_t)v >> WBITS, dst = gb[b] + j;
       if (dst < cap) out[dst] = v;
       else lost = true;
@@ -866,7 +875,7 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   const uint64_t nb = (pos_size + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
   if (nrec == 0 || nb == 0 || nb > 8192 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return UINT64_MAX;
   for (const void *f : {(const void *)k_relabel_scatter<8>, (const void *)k_relabel_scatter<4>,
-                        (const void *)k_relabel_scatter<8, 512>,
+                        (const void *)k_relabel_scatter<8, 512>, (const void *)k_relabel_scatter<8, 512, true>,
                         (const void *)k_relabel_gather<false>, (const void *)k_relabel_gather<true>})
     allow_full_lds(f);
   Ctx::HeadLayout &hl = c.head_layout;
@@ -903,9 +912,14 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
     {
       constexpr int NT = 512, P = 8;
       const size_t fx = ((2 * nb + NT / WAVE + 1) & ~1ull) * 4, lds = fx + (size_t)P * NT * 8;
+      static const bool planes = getenv("SHEEP_RELABEL_PLANES") != nullptr;   // (A/B runs)
       if (nb <= 8 * (uint64_t)NT && lds <= 160 * 1024) {
-        hipLaunchKernelGGL((k_relabel_scatter<P, NT>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec, nrec, pos,
-                           pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
+        if (planes)
+          hipLaunchKernelGGL((k_relabel_scatter<P, NT, true>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec, nrec,
+                             pos, pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
+        else
+          hipLaunchKernelGGL((k_relabel_scatter<P, NT>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec, nrec, pos,
+                             pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
         LAUNCH_CHECK();
         HIP_CHECK(hipMemcpyAsync(c.h_scalars + 12, flags, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
         return;
