@@ -1677,6 +1677,90 @@ __global__ __launch_bounds__(TOPB) void k_top_hook(TopSet t) {
   top_relabel(ts, par, cid, C, false);
 }
 
+// ---- the top subproblem at an early level: its MSF when round 0 leaves one tree ------
+// The same identity one level band higher: after the level that splits at s = BIG_BITS the
+// top 2^BIG_BITS positions are a subproblem of their own (groups 0..BIG_BITS-1 and the
+// list entries there; RMAT-26, BIG_BITS = 19: ~380 M edges on ~256 K vertices), and the
+// levels below spend most of their time in it.  Its labels do not fit LDS, so only round 0
+// runs: every vertex's lowest lower neighbour — in LDS for the block's top BIG_HOT
+// positions, where power-law edges mostly end, read-checked device atomics below — and a
+// has-upper-neighbour bit.  When at most one root has an edge the block is one tree and
+// its MSF is {(minlo(x), x)}; otherwise nothing is cut (the 2^TOP_BITS cut runs later).
+constexpr int BIG_BITS = 19;
+constexpr uint32_t BIG_HOT = 1u << 15;
+struct BigState {
+  uint32_t *minlo;                  // per vertex: the lowest lower neighbour (block-local)
+  unsigned *hasup;                  // per vertex a bit: it has an upper neighbour
+  unsigned long long *cnt;          // [0] vertices with a lower neighbour, [1] roots with an edge
+  uint64_t *st;                     // the cut level's stats row
+  uint64_t *out;                    // the MSF goes behind the level's list (st[ST_EXTRA])
+  uint32_t v0, V;
+};
+
+__global__ __launch_bounds__(BLOCK) void k_big_init(BigState b) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < b.V; v += stride) {
+    b.minlo[v] = INVALID;
+    if (v % 32 == 0) b.hasup[v / 32] = 0;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 2) b.cnt[threadIdx.x] = 0;
+}
+
+__global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, const uint64_t *__restrict__ st) {
+  extern __shared__ uint32_t lmin[];   // the hot window's minima
+  __shared__ uint64_t s_pre[NSHARD + 1];
+  const uint32_t V = b.V, v0 = b.v0, hot0 = V > BIG_HOT ? V - BIG_HOT : 0, HW = V - hot0;
+  for (uint32_t v = threadIdx.x; v < HW; v += TOPB) lmin[v] = INVALID;
+  top_prefix(te, s_pre);
+  __syncthreads();
+  const uint64_t total = s_pre[NSHARD] + (te.g1 - te.g0);
+  const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < total ? b0 + per : total;
+  uint32_t *const gmin = b.minlo;
+  unsigned *const up = b.hasup;
+  top_edges(te, s_pre, st[ST_TOPNT], b0 < b1 ? b0 : b1, b1, threadIdx.x, TOPB, [&](uint64_t e) {
+    if (e == DEAD) return;
+    const uint32_t l = (uint32_t)e - v0, h = (uint32_t)(e >> 32) - v0;
+    if (h >= hot0) {
+      if (l < lmin[h - hot0]) atomicMin(&lmin[h - hot0], l);
+    } else if (l < gmin[h]) {
+      atomicMin(&gmin[h], l);
+    }
+    const unsigned bit = 1u << (l & 31);
+    if (!(up[l >> 5] & bit)) atomicOr(&up[l >> 5], bit);
+  });
+  __syncthreads();
+  for (uint32_t v = threadIdx.x; v < HW; v += TOPB) {
+    const uint32_t x = lmin[v];
+    if (x != INVALID && x < gmin[hot0 + v]) atomicMin(&gmin[hot0 + v], x);
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_big_roots(BigState b) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  uint64_t nonroot = 0, eroot = 0;
+  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < b.V; v += stride) {
+    if (b.minlo[v] != INVALID) ++nonroot;
+    else if ((b.hasup[v >> 5] >> (v & 31)) & 1) ++eroot;
+  }
+  block_atomic_add(&b.cnt[0], nonroot);
+  block_atomic_add(&b.cnt[1], eroot);
+}
+
+// the MSF {(minlo(x), x)} appended behind the level's list (st[ST_EXTRA] counts them)
+__global__ __launch_bounds__(BLOCK) void k_big_emit(BigState b) {
+  const uint64_t base = b.st[ST_KEPT] + b.st[ST_CONTR];
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  const uint64_t iters = (b.V + stride - 1) / stride;
+  uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (uint64_t it = 0; it < iters; ++it, v += stride) {   // wave-uniform (appends)
+    const uint32_t ml = v < b.V ? b.minlo[v] : INVALID;
+    const bool has = ml != INVALID;
+    const uint64_t slot = wave_append(has, (unsigned long long *)&b.st[ST_EXTRA]);
+    if (has) b.out[base + slot] = ((uint64_t)(b.v0 + v) << 32) | (b.v0 + ml);
+  }
+}
+
 // Debug statistic (SHEEP_DEBUG_ETREE): live entries per block of 2^s spread positions
 // after a level (its next list plus the groups not yet activated).
 __global__ void k_dbg_blocks(const uint64_t *__restrict__ a, const uint64_t *__restrict__ st, const uint64_t *__restrict__ b,
@@ -1838,6 +1922,60 @@ static uint32_t top_blocks(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t 
   return nb;
 }
 
+// The top 2^bits positions after the level that splits at s = bits: round 0 of Borůvka
+// (k_big_*); when it leaves one tree the block's edges become its MSF behind `next`
+// (st[ST_EXTRA]) and st[ST_CUT] = cut0 drops its list entries at the next split.  One sync
+// for the list length, one for the counts.  Returns whether the block was cut.
+static bool big_cut(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, uint64_t g0, uint64_t g1, uint32_t cut0,
+                    int bits, uint32_t clo, uint64_t n) {
+  uint64_t hrow[ST_ROW];
+  HIP_CHECK(hipMemcpyAsync(hrow, st, sizeof hrow, hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  const uint64_t nl = hrow[ST_KEPT] + hrow[ST_CONTR];
+  const uint64_t tcap = (nl + TILE - 1) / TILE * TILE + TILE;
+  uint64_t *tl = c.get_as<uint64_t>("et_top_list", tcap);
+  unsigned long long *tcnt = c.get_as<unsigned long long>("et_top_cnt", TOP_CSET + TOP_NB_MAX);
+  HIP_CHECK(hipMemsetAsync(tcnt, 0, TOP_CSET * sizeof(unsigned long long), c.stream));
+  hipLaunchKernelGGL(k_top_extract_multi, dim3(grid_tiles(nl)), dim3(BLOCK), 0, c.stream, (const uint64_t *)next, st, cut0,
+                     bits, 1u, clo, tl, tcap, tcnt);
+  LAUNCH_CHECK();
+  uint64_t a = 0, z = n;   // the block's first vertex: min x with spread(x) >= cut0
+  while (a < z) {
+    const uint64_t x = (a + z) / 2;
+    if (x + ((x * (uint64_t)clo) >> 32) >= cut0) z = x; else a = x + 1;
+  }
+  BigState b;
+  b.v0 = (uint32_t)a;
+  b.V = (uint32_t)(n - a);
+  b.minlo = c.get_as<uint32_t>("et_big_minlo", b.V ? b.V : 1);
+  b.hasup = c.get_as<unsigned>("et_big_hasup", b.V / 32 + 1);
+  b.cnt = c.get_as<unsigned long long>("et_big_cnt", 2);
+  b.st = st;
+  b.out = next;
+  const TopEdges te{tl, tcnt, r0, g0, g1};
+  const size_t lds = BIG_HOT * sizeof(uint32_t);
+  allow_lds((const void *)k_big_min0, (int)lds);
+  hipLaunchKernelGGL(k_big_init, dim3(grid_for(b.V)), dim3(BLOCK), 0, c.stream, b);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_big_min0, dim3(TOP_WG), dim3(TOPB), lds, c.stream, te, b, (const uint64_t *)st);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_big_roots, dim3(grid_for(b.V)), dim3(BLOCK), 0, c.stream, b);
+  LAUNCH_CHECK();
+  unsigned long long h[2];
+  HIP_CHECK(hipMemcpyAsync(h, b.cnt, sizeof h, hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  if (g_debug_etree)
+    fprintf(stderr, "etree big cut after s %d: vertices %u group edges %lu list entries scanned %lu: non-roots %llu, "
+                    "roots with an edge %llu -> %s\n", bits, b.V, (unsigned long)(g1 - g0), (unsigned long)nl, h[0], h[1],
+            h[1] <= 1 ? "cut" : "kept");
+  if (h[1] > 1) return false;
+  hipLaunchKernelGGL(k_big_emit, dim3(grid_for(b.V)), dim3(BLOCK), 0, c.stream, b);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, c.stream, st + ST_CUT, (uint64_t)cut0);
+  LAUNCH_CHECK();
+  return true;
+}
+
 void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
                       int fin_bits, int filt_lvl, uint32_t ylo, uint32_t yhi, int top_bits) {
   fill_u32(c, parent, n, INVALID);
@@ -1900,6 +2038,27 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       gcut = top_bits;
     }
   }
+  // the early cut of the top subproblem (SHEEP_BIG_BITS; 0: off), tried when dense
+  static const int big_bits = getenv("SHEEP_BIG_BITS") ? atoi(getenv("SHEEP_BIG_BITS")) : BIG_BITS;
+  int big_lvl = -1;
+  uint64_t big_g0 = 0, big_g1 = 0;
+  uint32_t big_cut0 = 0;
+  if (top_lvl >= 0 && big_bits > top_bits && big_bits <= L - 1) {
+    std::vector<uint64_t> hs(2 * (size_t)L);
+    HIP_CHECK(hipMemcpyAsync(hs.data(), seg, hs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+    big_cut0 = (uint32_t)((1ull << L) - (1ull << big_bits));
+    uint64_t a = 0, z = n;
+    while (a < z) {
+      const uint64_t x = (a + z) / 2;
+      if (x + ((x * (uint64_t)clo) >> 32) >= big_cut0) z = x; else a = x + 1;
+    }
+    big_g0 = hs[big_bits - 1];
+    big_g1 = hs[L];
+    if (n - a >= 2 && big_g1 - big_g0 >= TOP_DENSE * (n - a)) big_lvl = L - 1 - big_bits;
+  }
+  int cut_lvl = -1;           // the level whose split follows a cut (its list entries dropped)
+  uint32_t cut_val = 0;
   // a split reads at most the list plus a bucket: (lcap + m) entries, in SPLIT_TILE tiles
   const uint64_t cstride = (lcap + m + SPLIT_TILE - 1) / SPLIT_TILE + 1;
   uint64_t *tcnt = c.get_as<uint64_t>("et_tilecnt", 3 * cstride + 1);
@@ -1915,7 +2074,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       // the previous level's clean first (its counters, adoptions and resets)
       const LevelClean clean = lvl ? LevelClean{lbuf, xbuf, xtop, prev, uf, mt, top, claim, n, tagged, lvl - 1, parent, csets}
                                    : LevelClean{};
-      const bool after_cut = top_lvl >= 0 && lvl == top_lvl + 1;
+      const bool after_cut = cut_lvl >= 0 && lvl == cut_lvl + 1;
       hipLaunchKernelGGL(after_cut ? k_split_count<true> : k_split_count<false>, dim3(gt2), dim3(BLOCK), 0, c.stream,
                          (const uint64_t *)cur, prev, st, s, clo, yr,
                          (const uint64_t *)r0, (const uint64_t *)seg, L, gcut, tcnt, clean);
@@ -1958,7 +2117,18 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       LAUNCH_CHECK();
       pack_shards<uint64_t>(c, alt, next, st + ST_NX, cset(CSET_APPLY), st + ST_CONTR, nullptr, nullptr, st + ST_KEPT);
     }
+    if (lvl == big_lvl) {
+      TimedRegion tr(c, "etree_top");
+      if (big_cut(c, next, st, r0, big_g0, big_g1, big_cut0, big_bits, clo, n)) {
+        gcut = big_bits;   // groups below are never activated; the 2^TOP_BITS cut has nothing left to do
+        top_lvl = -1;
+        cut_lvl = lvl;
+        cut_val = big_cut0;
+      }
+    }
     if (lvl == top_lvl) {
+      cut_lvl = lvl;
+      cut_val = top_cut;
       TimedRegion tr(c, "etree_top");
       static const int top_nb = getenv("SHEEP_TOP_BLOCKS") ? atoi(getenv("SHEEP_TOP_BLOCKS")) : TOP_NB;
       const uint32_t nbc = top_blocks(c, next, st, r0, top_g0, top_g1, top_cut, top_bits, (uint32_t)top_nb, clo, n, lcap);
@@ -1985,7 +2155,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       HIP_CHECK(hipMemsetAsync(cnt, 0, nblk * sizeof(unsigned), c.stream));
       c.sync();
       hipLaunchKernelGGL(k_dbg_blocks, dim3(1024), dim3(BLOCK), 0, c.stream, (const uint64_t *)next, (const uint64_t *)st,
-                         r0 + hs[0], hs[1] - hs[0], s, clo, cnt, lvl > top_lvl && top_lvl >= 0 ? top_cut : 0u);
+                         r0 + hs[0], hs[1] - hs[0], s, clo, cnt, cut_lvl >= 0 && lvl > cut_lvl ? cut_val : 0u);
       LAUNCH_CHECK();
       std::vector<unsigned> h(nblk);
       HIP_CHECK(hipMemcpyAsync(h.data(), cnt, nblk * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));

@@ -912,7 +912,9 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
     {
       constexpr int NT = 512, P = 8;
       const size_t fx = ((2 * nb + NT / WAVE + 1) & ~1ull) * 4, lds = fx + (size_t)P * NT * 8;
-      static const bool planes = getenv("SHEEP_RELABEL_PLANES") != nullptr;   // (A/B runs)
+      // the staged pairs as two u32 planes (RMAT-26 relabel 13.56 / 13.85 ms against 14.56 /
+      // 13.80 with one u64 array, two runs each: within box noise, not worse)
+      static const bool planes = getenv("SHEEP_RELABEL_U64") == nullptr;   // (A/B runs)
       if (nb <= 8 * (uint64_t)NT && lds <= 160 * 1024) {
         if (planes)
           hipLaunchKernelGGL((k_relabel_scatter<P, NT, true>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec, nrec,
