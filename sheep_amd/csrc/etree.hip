@@ -1718,8 +1718,14 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
   const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < total ? b0 + per : total;
   uint32_t *const gmin = b.minlo;
   unsigned *const up = b.hasup;
-  top_edges(te, s_pre, st[ST_TOPNT], b0 < b1 ? b0 : b1, b1, threadIdx.x, TOPB, [&](uint64_t e) {
-    if (e == DEAD) return;
+  // the list part one entry at a time; the group part TOP_U edges per thread, and their
+  // read checks (the minima below the window, the has-upper words) all issued before any
+  // atomic: a check that waits for the previous edge's turn serialises eight latencies per
+  // step, and a stale read only costs a redundant atomic (the minima only fall)
+  const uint64_t nl = s_pre[NSHARD], ntiles = st[ST_TOPNT];
+  for (uint64_t i = b0 + threadIdx.x; i < (b1 < nl ? b1 : nl); i += TOPB) {
+    const uint64_t e = top_list_at(te, s_pre, ntiles, i);
+    if (e == DEAD) continue;
     const uint32_t l = (uint32_t)e - v0, h = (uint32_t)(e >> 32) - v0;
     if (h >= hot0) {
       if (l < lmin[h - hot0]) atomicMin(&lmin[h - hot0], l);
@@ -1728,7 +1734,35 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
     }
     const unsigned bit = 1u << (l & 31);
     if (!(up[l >> 5] & bit)) atomicOr(&up[l >> 5], bit);
-  });
+  }
+  const uint64_t g0 = (b0 > nl ? b0 : nl) - nl, g1 = b1 > nl ? b1 - nl : 0;
+  const uint64_t *r = te.r0 + te.g0;
+  for (uint64_t i0 = g0 + threadIdx.x; i0 < g1; i0 += (uint64_t)TOP_U * TOPB) {
+    uint32_t l[TOP_U], h[TOP_U], gv[TOP_U], uv[TOP_U];
+#pragma unroll
+    for (int j = 0; j < TOP_U; ++j) {
+      const uint64_t i = i0 + (uint64_t)j * TOPB;
+      const uint64_t e = i < g1 ? __builtin_nontemporal_load(r + i) : DEAD;
+      l[j] = e == DEAD ? INVALID : (uint32_t)e - v0;
+      h[j] = e == DEAD ? 0 : (uint32_t)(e >> 32) - v0;
+    }
+#pragma unroll
+    for (int j = 0; j < TOP_U; ++j) {
+      gv[j] = l[j] != INVALID && h[j] < hot0 ? gmin[h[j]] : 0;
+      uv[j] = l[j] != INVALID ? up[l[j] >> 5] : ~0u;
+    }
+#pragma unroll
+    for (int j = 0; j < TOP_U; ++j) {
+      if (l[j] == INVALID) continue;
+      if (h[j] >= hot0) {
+        if (l[j] < lmin[h[j] - hot0]) atomicMin(&lmin[h[j] - hot0], l[j]);
+      } else if (l[j] < gv[j]) {
+        atomicMin(&gmin[h[j]], l[j]);
+      }
+      const unsigned bit = 1u << (l[j] & 31);
+      if (!(uv[j] & bit)) atomicOr(&up[l[j] >> 5], bit);
+    }
+  }
   __syncthreads();
   for (uint32_t v = threadIdx.x; v < HW; v += TOPB) {
     const uint32_t x = lmin[v];
