@@ -1686,8 +1686,9 @@ __global__ __launch_bounds__(TOPB) void k_top_hook(TopSet t) {
 // positions, where power-law edges mostly end, read-checked device atomics below — and a
 // has-upper-neighbour bit.  When at most one root has an edge the block is one tree and
 // its MSF is {(minlo(x), x)}; otherwise nothing is cut (the 2^TOP_BITS cut runs later).
-constexpr int BIG_BITS = 19;
+constexpr int BIG_BITS = 20;
 constexpr uint32_t BIG_HOT = 1u << 15;
+constexpr uint64_t BIG_DENSE = 256;
 struct BigState {
   uint32_t *minlo;                  // per vertex: the lowest lower neighbour (block-local)
   unsigned *hasup;                  // per vertex a bit: it has an upper neighbour
@@ -1706,16 +1707,30 @@ __global__ __launch_bounds__(BLOCK) void k_big_init(BigState b) {
   if (blockIdx.x == 0 && threadIdx.x < 2) b.cnt[threadIdx.x] = 0;
 }
 
+constexpr uint32_t BIG_UPW = 1u << 16;   // has-upper bits kept in LDS per workgroup: a window of lo
 __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, const uint64_t *__restrict__ st) {
   extern __shared__ uint32_t lmin[];   // the hot window's minima
+  __shared__ unsigned lup[BIG_UPW / 32];
   __shared__ uint64_t s_pre[NSHARD + 1];
+  __shared__ uint32_t s_w0;
   const uint32_t V = b.V, v0 = b.v0, hot0 = V > BIG_HOT ? V - BIG_HOT : 0, HW = V - hot0;
   for (uint32_t v = threadIdx.x; v < HW; v += TOPB) lmin[v] = INVALID;
+  for (uint32_t w = threadIdx.x; w < BIG_UPW / 32; w += TOPB) lup[w] = 0;
   top_prefix(te, s_pre);
   __syncthreads();
   const uint64_t total = s_pre[NSHARD] + (te.g1 - te.g0);
   const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
   const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < total ? b0 + per : total;
+  // the group part comes in lo buckets, so a chunk's lo values crowd into a narrow range:
+  // their has-upper bits go to an LDS window from the chunk's first lo (others: device atomics)
+  if (threadIdx.x == 0) {
+    const uint64_t nl0 = s_pre[NSHARD];
+    const uint64_t gi = (b0 > nl0 ? b0 : nl0) - nl0;
+    const uint64_t e = gi < te.g1 - te.g0 && b0 < b1 ? te.r0[te.g0 + gi] : DEAD;
+    s_w0 = e == DEAD ? 0u : (((uint32_t)e - v0) & ~31u);
+  }
+  __syncthreads();
+  const uint32_t w0 = s_w0;
   uint32_t *const gmin = b.minlo;
   unsigned *const up = b.hasup;
   // the list part one entry at a time; the group part TOP_U edges per thread, and their
@@ -1749,7 +1764,7 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
 #pragma unroll
     for (int j = 0; j < TOP_U; ++j) {
       gv[j] = l[j] != INVALID && h[j] < hot0 ? gmin[h[j]] : 0;
-      uv[j] = l[j] != INVALID ? up[l[j] >> 5] : ~0u;
+      uv[j] = l[j] != INVALID && l[j] - w0 >= BIG_UPW ? up[l[j] >> 5] : ~0u;
     }
 #pragma unroll
     for (int j = 0; j < TOP_U; ++j) {
@@ -1760,13 +1775,22 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
         atomicMin(&gmin[h[j]], l[j]);
       }
       const unsigned bit = 1u << (l[j] & 31);
-      if (!(uv[j] & bit)) atomicOr(&up[l[j] >> 5], bit);
+      const uint32_t d = l[j] - w0;
+      if (d < BIG_UPW) {
+        if (!(lup[d >> 5] & bit)) atomicOr(&lup[d >> 5], bit);
+      } else if (!(uv[j] & bit)) {
+        atomicOr(&up[l[j] >> 5], bit);
+      }
     }
   }
   __syncthreads();
   for (uint32_t v = threadIdx.x; v < HW; v += TOPB) {
     const uint32_t x = lmin[v];
     if (x != INVALID && x < gmin[hot0 + v]) atomicMin(&gmin[hot0 + v], x);
+  }
+  for (uint32_t w = threadIdx.x; w < BIG_UPW / 32 && w0 / 32 + w <= (V - 1) / 32; w += TOPB) {
+    const unsigned x = lup[w];
+    if (x && (x & ~up[w0 / 32 + w])) atomicOr(&up[w0 / 32 + w], x);
   }
 }
 
@@ -2089,7 +2113,10 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     }
     big_g0 = hs[big_bits - 1];
     big_g1 = hs[L];
-    if (n - a >= 2 && big_g1 - big_g0 >= TOP_DENSE * (n - a)) big_lvl = L - 1 - big_bits;
+    // only where the block is far denser than the top block's rule asks (RMAT-26: ~740 group
+    // edges per vertex at 2^19, ~540 at 2^20; a 1/8 edge shard's ~90 did not pay for the
+    // cut: 8 shard maps 70.2 -> 76.9 ms)
+    if (n - a >= 2 && big_g1 - big_g0 >= BIG_DENSE * (n - a)) big_lvl = L - 1 - big_bits;
   }
   int cut_lvl = -1;           // the level whose split follows a cut (its list entries dropped)
   uint32_t cut_val = 0;
