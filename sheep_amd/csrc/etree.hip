@@ -1696,6 +1696,7 @@ struct BigState {
   uint64_t *st;                     // the cut level's stats row
   uint64_t *out;                    // the MSF goes behind the level's list (st[ST_EXTRA])
   uint32_t v0, V;
+  uint32_t hot;                     // the LDS window: the block's top `hot` positions (<= BIG_HOT)
 };
 
 __global__ __launch_bounds__(BLOCK) void k_big_init(BigState b) {
@@ -1713,7 +1714,7 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
   __shared__ unsigned lup[BIG_UPW / 32];
   __shared__ uint64_t s_pre[NSHARD + 1];
   __shared__ uint32_t s_w0;
-  const uint32_t V = b.V, v0 = b.v0, hot0 = V > BIG_HOT ? V - BIG_HOT : 0, HW = V - hot0;
+  const uint32_t V = b.V, v0 = b.v0, hot0 = V > b.hot ? V - b.hot : 0, HW = V - hot0;
   for (uint32_t v = threadIdx.x; v < HW; v += TOPB) lmin[v] = INVALID;
   for (uint32_t w = threadIdx.x; w < BIG_UPW / 32; w += TOPB) lup[w] = 0;
   top_prefix(te, s_pre);
@@ -2011,8 +2012,11 @@ static bool big_cut(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, ui
   b.st = st;
   b.out = next;
   const TopEdges te{tl, tcnt, r0, g0, g1};
-  const size_t lds = BIG_HOT * sizeof(uint32_t);
-  allow_lds((const void *)k_big_min0, (int)lds);
+  // (SHEEP_BIG_HOT_BITS: a smaller window leaves LDS for two workgroups per CU)
+  static const int hot_bits = getenv("SHEEP_BIG_HOT_BITS") ? atoi(getenv("SHEEP_BIG_HOT_BITS")) : 15;
+  b.hot = std::min<uint32_t>(1u << std::max(10, std::min(15, hot_bits)), BIG_HOT);
+  const size_t lds = b.hot * sizeof(uint32_t);
+  allow_lds((const void *)k_big_min0, (int)(BIG_HOT * sizeof(uint32_t)));
   hipLaunchKernelGGL(k_big_init, dim3(grid_for(b.V)), dim3(BLOCK), 0, c.stream, b);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_big_min0, dim3(TOP_WG), dim3(TOPB), lds, c.stream, te, b, (const uint64_t *)st);
