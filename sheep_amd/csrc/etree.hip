@@ -1682,15 +1682,20 @@ __global__ __launch_bounds__(TOPB) void k_top_hook(TopSet t) {
 // top 2^BIG_BITS positions are a subproblem of their own (groups 0..BIG_BITS-1 and the
 // list entries there; RMAT-26, BIG_BITS = 19: ~380 M edges on ~256 K vertices), and the
 // levels below spend most of their time in it.  Its labels do not fit LDS, so only round 0
-// runs: every vertex's lowest lower neighbour — in LDS for the block's top BIG_HOT
-// positions, where power-law edges mostly end, read-checked device atomics below — and a
-// has-upper-neighbour bit.  When at most one root has an edge the block is one tree and
-// its MSF is {(minlo(x), x)}; otherwise nothing is cut (the 2^TOP_BITS cut runs later).
+// runs, and it picks ANY lower neighbour per vertex (plain stores, first writer seen wins:
+// in LDS for the block's top BIG_HOT positions, where power-law edges mostly end, in HBM
+// below) plus a has-upper-neighbour bit.  Under the weight hi alone the edges (v, l), l < v,
+// tie, and Kruskal with each v's pick first takes every pick (v is a singleton when its
+// weight comes up), so the picks lie in SOME minimum spanning forest; when at most one root
+// has an edge they span the block as one tree and ARE that forest — and etree(G) is the
+// elimination tree of every MSF under hi, whatever the tie order (the components of each
+// threshold graph G_t are every MSF's).  Otherwise nothing is cut (the 2^TOP_BITS cut runs
+// later).  (Lowest lower neighbours by read-checked atomicMin cost 6.1 ms at 2^20.)
 constexpr int BIG_BITS = 20;
 constexpr uint32_t BIG_HOT = 1u << 15;
 constexpr uint64_t BIG_DENSE = 256;
 struct BigState {
-  uint32_t *minlo;                  // per vertex: the lowest lower neighbour (block-local)
+  uint32_t *minlo;                  // per vertex: a lower neighbour (block-local), the round-0 pick
   unsigned *hasup;                  // per vertex a bit: it has an upper neighbour
   unsigned long long *cnt;          // [0] vertices with a lower neighbour, [1] roots with an edge
   uint64_t *st;                     // the cut level's stats row
@@ -1744,9 +1749,9 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
     if (e == DEAD) continue;
     const uint32_t l = (uint32_t)e - v0, h = (uint32_t)(e >> 32) - v0;
     if (h >= hot0) {
-      if (l < lmin[h - hot0]) atomicMin(&lmin[h - hot0], l);
-    } else if (l < gmin[h]) {
-      atomicMin(&gmin[h], l);
+      if (lmin[h - hot0] == INVALID) lmin[h - hot0] = l;
+    } else if (gmin[h] == INVALID) {
+      gmin[h] = l;
     }
     const unsigned bit = 1u << (l & 31);
     if (!(up[l >> 5] & bit)) atomicOr(&up[l >> 5], bit);
@@ -1764,16 +1769,16 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
     }
 #pragma unroll
     for (int j = 0; j < TOP_U; ++j) {
-      gv[j] = l[j] != INVALID && h[j] < hot0 ? gmin[h[j]] : 0;
+      gv[j] = l[j] != INVALID && h[j] < hot0 ? gmin[h[j]] : 0u;
       uv[j] = l[j] != INVALID && l[j] - w0 >= BIG_UPW ? up[l[j] >> 5] : ~0u;
     }
 #pragma unroll
     for (int j = 0; j < TOP_U; ++j) {
       if (l[j] == INVALID) continue;
       if (h[j] >= hot0) {
-        if (l[j] < lmin[h[j] - hot0]) atomicMin(&lmin[h[j] - hot0], l[j]);
-      } else if (l[j] < gv[j]) {
-        atomicMin(&gmin[h[j]], l[j]);
+        if (lmin[h[j] - hot0] == INVALID) lmin[h[j] - hot0] = l[j];
+      } else if (gv[j] == INVALID) {
+        gmin[h[j]] = l[j];
       }
       const unsigned bit = 1u << (l[j] & 31);
       const uint32_t d = l[j] - w0;
@@ -1787,7 +1792,7 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
   __syncthreads();
   for (uint32_t v = threadIdx.x; v < HW; v += TOPB) {
     const uint32_t x = lmin[v];
-    if (x != INVALID && x < gmin[hot0 + v]) atomicMin(&gmin[hot0 + v], x);
+    if (x != INVALID && gmin[hot0 + v] == INVALID) gmin[hot0 + v] = x;
   }
   for (uint32_t w = threadIdx.x; w < BIG_UPW / 32 && w0 / 32 + w <= (V - 1) / 32; w += TOPB) {
     const unsigned x = lup[w];

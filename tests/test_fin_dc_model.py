@@ -102,3 +102,31 @@ def test_block_dc_equals_liu_on_random_multigraphs():
         edges += rng.sample(edges, min(len(edges), 5))   # repeated edges, as contractions produce
         assert block_dc(n, edges, B, rng) == liu(n, edges)
         assert block_dc(n, edges, B, rng, msf=True) == liu(n, edges)
+
+
+def test_any_lower_neighbour_picks_that_form_one_tree_keep_the_etree():
+    """The early cut of the top subproblem (etree.hip k_big_min0 / k_big_emit) keeps, per
+    vertex, ANY lower neighbour (the first one a racing store leaves), not the lowest: under
+    the weight hi the picks lie in some minimum spanning forest, so when at most one root
+    has an edge they are one and the elimination tree is Liu's of the whole edge set."""
+    rng = random.Random(77)
+    cut = 0
+    for _ in range(400):
+        n = rng.randint(2, 64)
+        pairs = set()
+        for _ in range(rng.randint(n, 8 * n)):
+            a, b = rng.randrange(n), rng.randrange(n)
+            if a != b:
+                pairs.add((min(a, b), max(a, b)))
+        edges = sorted(pairs)
+        lower = [[] for _ in range(n)]
+        up = [False] * n
+        for lo, hi in edges:
+            lower[hi].append(lo)
+            up[lo] = True
+        picks = [(rng.choice(lower[x]), x) for x in range(n) if lower[x]]
+        if sum(1 for x in range(n) if not lower[x] and up[x]) > 1:
+            continue
+        cut += 1
+        assert liu(n, picks) == liu(n, edges)
+    assert cut > 100
