@@ -111,7 +111,7 @@ def test_any_lower_neighbour_picks_that_form_one_tree_keep_the_etree():
     has an edge they are one and the elimination tree is Liu's of the whole edge set."""
     rng = random.Random(77)
     cut = 0
-    for _ in range(400):
+    for _ in range(1500):
         n = rng.randint(2, 64)
         pairs = set()
         for _ in range(rng.randint(n, 8 * n)):
@@ -129,4 +129,4 @@ def test_any_lower_neighbour_picks_that_form_one_tree_keep_the_etree():
             continue
         cut += 1
         assert liu(n, picks) == liu(n, edges)
-    assert cut > 100
+    assert cut > 100   # (one-tree blocks: about one case in eight here)
