@@ -1697,6 +1697,7 @@ constexpr uint64_t BIG_DENSE = 256;
 struct BigState {
   uint32_t *minlo;                  // per vertex: a lower neighbour (block-local), the round-0 pick
   unsigned *hasup;                  // per vertex a bit: it has an upper neighbour
+  unsigned *picked;                 // per vertex a bit: minlo holds a pick (a 32x smaller read check)
   unsigned long long *cnt;          // [0] vertices with a lower neighbour, [1] roots with an edge
   uint64_t *st;                     // the cut level's stats row
   uint64_t *out;                    // the MSF goes behind the level's list (st[ST_EXTRA])
@@ -1708,7 +1709,7 @@ __global__ __launch_bounds__(BLOCK) void k_big_init(BigState b) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < b.V; v += stride) {
     b.minlo[v] = INVALID;
-    if (v % 32 == 0) b.hasup[v / 32] = 0;
+    if (v % 32 == 0) b.hasup[v / 32] = b.picked[v / 32] = 0;
   }
   if (blockIdx.x == 0 && threadIdx.x < 2) b.cnt[threadIdx.x] = 0;
 }
@@ -1738,7 +1739,7 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
   __syncthreads();
   const uint32_t w0 = s_w0;
   uint32_t *const gmin = b.minlo;
-  unsigned *const up = b.hasup;
+  unsigned *const up = b.hasup, *const pk = b.picked;
   // the list part one entry at a time; the group part TOP_U edges per thread, and their
   // read checks (the minima below the window, the has-upper words) all issued before any
   // atomic: a check that waits for the previous edge's turn serialises eight latencies per
@@ -1750,8 +1751,9 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
     const uint32_t l = (uint32_t)e - v0, h = (uint32_t)(e >> 32) - v0;
     if (h >= hot0) {
       if (lmin[h - hot0] == INVALID) lmin[h - hot0] = l;
-    } else if (gmin[h] == INVALID) {
+    } else if (!((pk[h >> 5] >> (h & 31)) & 1)) {
       gmin[h] = l;
+      atomicOr(&pk[h >> 5], 1u << (h & 31));
     }
     const unsigned bit = 1u << (l & 31);
     if (!(up[l >> 5] & bit)) atomicOr(&up[l >> 5], bit);
@@ -1769,7 +1771,7 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
     }
 #pragma unroll
     for (int j = 0; j < TOP_U; ++j) {
-      gv[j] = l[j] != INVALID && h[j] < hot0 ? gmin[h[j]] : 0u;
+      gv[j] = l[j] != INVALID && h[j] < hot0 ? pk[h[j] >> 5] : ~0u;
       uv[j] = l[j] != INVALID && l[j] - w0 >= BIG_UPW ? up[l[j] >> 5] : ~0u;
     }
 #pragma unroll
@@ -1777,8 +1779,9 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
       if (l[j] == INVALID) continue;
       if (h[j] >= hot0) {
         if (lmin[h[j] - hot0] == INVALID) lmin[h[j] - hot0] = l[j];
-      } else if (gv[j] == INVALID) {
+      } else if (!((gv[j] >> (h[j] & 31)) & 1)) {
         gmin[h[j]] = l[j];
+        atomicOr(&pk[h[j] >> 5], 1u << (h[j] & 31));
       }
       const unsigned bit = 1u << (l[j] & 31);
       const uint32_t d = l[j] - w0;
@@ -1792,7 +1795,10 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
   __syncthreads();
   for (uint32_t v = threadIdx.x; v < HW; v += TOPB) {
     const uint32_t x = lmin[v];
-    if (x != INVALID && gmin[hot0 + v] == INVALID) gmin[hot0 + v] = x;
+    if (x != INVALID && !((pk[(hot0 + v) >> 5] >> ((hot0 + v) & 31)) & 1)) {
+      gmin[hot0 + v] = x;
+      atomicOr(&pk[(hot0 + v) >> 5], 1u << ((hot0 + v) & 31));
+    }
   }
   for (uint32_t w = threadIdx.x; w < BIG_UPW / 32 && w0 / 32 + w <= (V - 1) / 32; w += TOPB) {
     const unsigned x = lup[w];
@@ -2013,6 +2019,7 @@ static bool big_cut(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, ui
   b.V = (uint32_t)(n - a);
   b.minlo = c.get_as<uint32_t>("et_big_minlo", b.V ? b.V : 1);
   b.hasup = c.get_as<unsigned>("et_big_hasup", b.V / 32 + 1);
+  b.picked = c.get_as<unsigned>("et_big_picked", b.V / 32 + 1);
   b.cnt = c.get_as<unsigned long long>("et_big_cnt", 2);
   b.st = st;
   b.out = next;
