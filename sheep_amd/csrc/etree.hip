@@ -2132,7 +2132,9 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     // only where the block is far denser than the top block's rule asks (RMAT-26: ~740 group
     // edges per vertex at 2^19, ~540 at 2^20; a 1/8 edge shard's ~90 did not pay for the
     // cut: 8 shard maps 70.2 -> 76.9 ms)
-    if (n - a >= 2 && big_g1 - big_g0 >= BIG_DENSE * (n - a)) big_lvl = L - 1 - big_bits;
+    static const uint64_t big_dense = getenv("SHEEP_BIG_DENSE") ? strtoull(getenv("SHEEP_BIG_DENSE"), nullptr, 10)
+                                                                 : BIG_DENSE;   // (A/B runs)
+    if (n - a >= 2 && big_g1 - big_g0 >= big_dense * (n - a)) big_lvl = L - 1 - big_bits;
   }
   int cut_lvl = -1;           // the level whose split follows a cut (its list entries dropped)
   uint32_t cut_val = 0;
