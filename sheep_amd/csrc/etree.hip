@@ -1715,13 +1715,33 @@ __global__ __launch_bounds__(BLOCK) void k_big_init(BigState b) {
 }
 
 constexpr uint32_t BIG_UPW = 1u << 16;   // has-upper bits kept in LDS per workgroup: a window of lo
+// H16: the window is the top 2^16 positions with each pick as a u16 distance h - l (0:
+// none); a hot vertex whose lower neighbours seen so far all lie 2^16 or more below takes
+// the device path
+template <bool H16>
 __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, const uint64_t *__restrict__ st) {
-  extern __shared__ uint32_t lmin[];   // the hot window's minima
+  extern __shared__ uint32_t lmin[];   // the hot window's picks
+  uint16_t *const ld = (uint16_t *)lmin;
   __shared__ unsigned lup[BIG_UPW / 32];
   __shared__ uint64_t s_pre[NSHARD + 1];
   __shared__ uint32_t s_w0;
-  const uint32_t V = b.V, v0 = b.v0, hot0 = V > b.hot ? V - b.hot : 0, HW = V - hot0;
-  for (uint32_t v = threadIdx.x; v < HW; v += TOPB) lmin[v] = INVALID;
+  const uint32_t hotn = H16 ? (1u << 16) : b.hot;
+  const uint32_t V = b.V, v0 = b.v0, hot0 = V > hotn ? V - hotn : 0, HW = V - hot0;
+  for (uint32_t v = threadIdx.x; v < HW; v += TOPB) {
+    if (H16) ld[v] = 0;
+    else lmin[v] = INVALID;
+  }
+  // a hot vertex's pick in LDS; false: the edge takes the device path
+  auto hot_pick = [&](uint32_t l, uint32_t h) -> bool {
+    if (H16) {
+      if (ld[h - hot0]) return true;
+      if (h - l >= (1u << 16)) return false;
+      ld[h - hot0] = (uint16_t)(h - l);
+      return true;
+    }
+    if (lmin[h - hot0] == INVALID) lmin[h - hot0] = l;
+    return true;
+  };
   for (uint32_t w = threadIdx.x; w < BIG_UPW / 32; w += TOPB) lup[w] = 0;
   top_prefix(te, s_pre);
   __syncthreads();
@@ -1749,8 +1769,7 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
     const uint64_t e = top_list_at(te, s_pre, ntiles, i);
     if (e == DEAD) continue;
     const uint32_t l = (uint32_t)e - v0, h = (uint32_t)(e >> 32) - v0;
-    if (h >= hot0) {
-      if (lmin[h - hot0] == INVALID) lmin[h - hot0] = l;
+    if (h >= hot0 && hot_pick(l, h)) {
     } else if (!((pk[h >> 5] >> (h & 31)) & 1)) {
       gmin[h] = l;
       atomicOr(&pk[h >> 5], 1u << (h & 31));
@@ -1778,7 +1797,10 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
     for (int j = 0; j < TOP_U; ++j) {
       if (l[j] == INVALID) continue;
       if (h[j] >= hot0) {
-        if (lmin[h[j] - hot0] == INVALID) lmin[h[j] - hot0] = l[j];
+        if (!hot_pick(l[j], h[j]) && !((pk[h[j] >> 5] >> (h[j] & 31)) & 1)) {   // (H16: a far pick)
+          gmin[h[j]] = l[j];
+          atomicOr(&pk[h[j] >> 5], 1u << (h[j] & 31));
+        }
       } else if (!((gv[j] >> (h[j] & 31)) & 1)) {
         gmin[h[j]] = l[j];
         atomicOr(&pk[h[j] >> 5], 1u << (h[j] & 31));
@@ -1794,7 +1816,7 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
   }
   __syncthreads();
   for (uint32_t v = threadIdx.x; v < HW; v += TOPB) {
-    const uint32_t x = lmin[v];
+    const uint32_t x = H16 ? (ld[v] ? hot0 + v - ld[v] : INVALID) : lmin[v];
     if (x != INVALID && !((pk[(hot0 + v) >> 5] >> ((hot0 + v) & 31)) & 1)) {
       gmin[hot0 + v] = x;
       atomicOr(&pk[(hot0 + v) >> 5], 1u << ((hot0 + v) & 31));
@@ -2028,10 +2050,16 @@ static bool big_cut(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, ui
   static const int hot_bits = getenv("SHEEP_BIG_HOT_BITS") ? atoi(getenv("SHEEP_BIG_HOT_BITS")) : 15;
   b.hot = std::min<uint32_t>(1u << std::max(10, std::min(15, hot_bits)), BIG_HOT);
   const size_t lds = b.hot * sizeof(uint32_t);
-  allow_lds((const void *)k_big_min0, (int)(BIG_HOT * sizeof(uint32_t)));
+  allow_lds((const void *)k_big_min0<false>, (int)(BIG_HOT * sizeof(uint32_t)));
+  allow_lds((const void *)k_big_min0<true>, (int)(BIG_HOT * sizeof(uint32_t)));
+  static const bool hot16 = getenv("SHEEP_BIG_HOT16") != nullptr;   // (A/B runs)
   hipLaunchKernelGGL(k_big_init, dim3(grid_for(b.V)), dim3(BLOCK), 0, c.stream, b);
   LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_big_min0, dim3(TOP_WG), dim3(TOPB), lds, c.stream, te, b, (const uint64_t *)st);
+  if (hot16)
+    hipLaunchKernelGGL(k_big_min0<true>, dim3(TOP_WG), dim3(TOPB), BIG_HOT * sizeof(uint32_t), c.stream, te, b,
+                       (const uint64_t *)st);
+  else
+    hipLaunchKernelGGL(k_big_min0<false>, dim3(TOP_WG), dim3(TOPB), lds, c.stream, te, b, (const uint64_t *)st);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_big_roots, dim3(grid_for(b.V)), dim3(BLOCK), 0, c.stream, b);
   LAUNCH_CHECK();
