@@ -1691,7 +1691,7 @@ __global__ __launch_bounds__(TOPB) void k_top_hook(TopSet t) {
 // elimination tree of every MSF under hi, whatever the tie order (the components of each
 // threshold graph G_t are every MSF's).  Otherwise nothing is cut (the 2^TOP_BITS cut runs
 // later).  (Lowest lower neighbours by read-checked atomicMin cost 6.1 ms at 2^20.)
-constexpr int BIG_BITS = 21;   // (RMAT-26 etree: 2^20 27.7, 2^21 26.9 ms; 2^22 misses the density rule)
+constexpr int BIG_BITS = 21;   // (RMAT-26 etree: 2^20 27.7, 2^21 26.9 ms; at 2^22 round 0 leaves 15 K trees)
 constexpr uint32_t BIG_HOT = 1u << 15;
 constexpr uint64_t BIG_DENSE = 256;
 struct BigState {
