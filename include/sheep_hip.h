@@ -125,6 +125,30 @@ int sheep_timer_reset(sheep_ctx *ctx);
 /* Names of every region timed since the last reset, comma-separated, into buf[cap]. */
 int sheep_timer_names(sheep_ctx *ctx, char *buf, size_t cap);
 
+/* ---- tuning -----------------------------------------------------------------------
+ * The algorithm's variants, one options struct per context (no reference analogue: the
+ * reference has one sequential algorithm).  Every variant computes the same bit-exact
+ * result; only time and device memory differ.  The defaults are the measured best
+ * (DESIGN.md §3); A/B runs (bench.py --tune) and the branch-forcing parity tests set the
+ * others.  A field equal to SHEEP_TUNE_DEFAULT keeps its default.  sheep_ctx_set_tuning
+ * checks every field's range (SHEEP_ERR_ARG) and NULL restores the defaults. */
+#define SHEEP_TUNE_DEFAULT (-1)
+typedef struct sheep_tuning {
+  int32_t fin_map_bits;    /* map: levels below this many position bits finish per block, 8..13 */
+  int32_t fin_merge_bits;  /* merge: the same, 8..13 */
+  int32_t fin_dc;          /* 1: per-block divide and conquer (k_fin_dc), 0: Liu's sweep per block */
+  int32_t top_bits;        /* dense top-block MSF cut: 0 off, else its size in position bits, 9..16 */
+  int32_t top_blocks;      /* blocks cut there (the top one included), 1..9 */
+  int32_t big_bits;        /* early MSF cut of the top subproblem: 0 off, else 17..30 position bits */
+  int64_t big_dense;       /* the early cut needs >= this many group edges per vertex, >= 1 */
+  int32_t big_hot_bits;    /* early cut: LDS window of picks, 10..15 position bits */
+  int32_t big_hot16;       /* early cut: 1 = u16-distance window over 2^16 positions */
+  int32_t relabel_planes;  /* relabel scatter: 1 = stage pairs as two u32 planes, 0 = one u64 array */
+} sheep_tuning;
+int sheep_tuning_default(sheep_tuning *out);
+int sheep_ctx_set_tuning(sheep_ctx *ctx, const sheep_tuning *t);
+int sheep_ctx_get_tuning(sheep_ctx *ctx, sheep_tuning *out);
+
 /* ---- degree sequence --------------------------------------------------------------
  * Adds this shard's degrees into deg_dev[0, deg_cap) (caller zeroes it once; shards
  * accumulate, or are summed with an all-reduce).  *max_slot_out (host, synchronises)
@@ -286,6 +310,8 @@ sheep_ctx *sheep_group_ctx(sheep_group *g, int local);
 int sheep_group_uses_rccl(const sheep_group *g);
 int sheep_group_barrier(sheep_group *g);
 int sheep_group_allreduce_max_u64(sheep_group *g, uint64_t *value);
+/* sheep_ctx_set_tuning on every context of this process's ranks */
+int sheep_group_set_tuning(sheep_group *g, const sheep_tuning *t);
 int sheep_group_sequence(sheep_group *g, const sheep_xs1 *const *rec_dev, const uint64_t *nrec,
                          uint32_t *const *deg_dev, uint64_t cap, uint32_t *const *seq_dev,
                          uint32_t *const *pos_dev, uint64_t *n_out, uint64_t *vs_out);

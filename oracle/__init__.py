@@ -115,6 +115,17 @@ def facts_text(parent, pst):
     return buf.value.decode()
 
 
+def print_text(parent, pst, seq):
+    """JTree::print (jtree.h:60-66) -> JNodeTable::print(id) (jnode.h:263-267) on the
+    default path: jnid -> vid through the sequence (get_sequence, jtree.h:50-57), width =
+    1 + pst (jnode.h:258-260, no junction data), pre_weight 0 (USE_PRE_WEIGHT off,
+    defs.h:62).  Pure Python: small trees only."""
+    out = []
+    for i, (par, w) in enumerate(zip(np.asarray(parent, np.uint32).tolist(), np.asarray(pst, np.uint32).tolist())):
+        out.append("%4d:%-8d%6d:w%6d:pre%6d:pst        ->[%4d]\n" % (i, int(seq[i]), 1 + w, 0, w, par))
+    return "".join(out)
+
+
 class Kids:
     """Persistent kid table for one tree (partition_tree keeps it across k)."""
 

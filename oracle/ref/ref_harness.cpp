@@ -140,6 +140,7 @@ static int usage() {
   fprintf(stderr,
           "ref_harness seq G OUT_SEQ                      degreeSequence (LLAMA degrees)\n"
           "ref_harness tree G SEQ|- OUT_TRE [p/k]         JTree (+ partial load), TREEFAQS\n"
+          "ref_harness print G SEQ|- [p/k]                JTree (+ partial load), JTree::print (graph2tree -t)\n"
           "ref_harness part G SEQ|- TREE PARTS_PREFIX k.. partition_tree -f -g flow + parts dumps\n"
           "ref_harness write G SEQ|- TREE k PREFIX        Partition + graph-based writePartitionedGraph\n"
           "ref_harness writefile G SEQ|- TREE k PREFIX    Partition + file-based writePartitionedGraph\n"
@@ -172,6 +173,15 @@ int main(int argc, char **argv) {
     JTree tree(g, seq);
     tree.jnodes.save(argv[4]);
     tree.jnodes.getFacts().print();
+    return 0;
+  }
+  if (cmd == "print" && (argc == 4 || argc == 5)) {   // graph2tree -t (graph2tree.cpp:229-230)
+    size_t part = 0, num_parts = 0;
+    if (argc == 5) sscanf(argv[4], "%zu/%zu", &part, &num_parts);
+    HarnessGraph g(argv[2], part, num_parts);
+    std::vector<vid_t> seq = strcmp(argv[3], "-") == 0 ? degreeSequence(g) : readSequence(argv[3]);
+    JTree tree(g, seq);
+    tree.print();   // jtree.h:60-66 -> jnode.h:263-267
     return 0;
   }
   if (cmd == "part" && argc >= 7) {

@@ -64,6 +64,29 @@ class _Facts(ctypes.Structure):
         "width", "root_cnt", "vert_height", "edge_height", "vert_cnt", "edge_cnt", "halo_id", "core_id", "fill")]
 
 
+class Tuning(ctypes.Structure):
+    """sheep_tuning (include/sheep_hip.h): the algorithm variants of one context; -1 keeps
+    a field's default.  Every variant gives the same bit-exact result."""
+    _fields_ = [("fin_map_bits", ctypes.c_int32), ("fin_merge_bits", ctypes.c_int32), ("fin_dc", ctypes.c_int32),
+                ("top_bits", ctypes.c_int32), ("top_blocks", ctypes.c_int32), ("big_bits", ctypes.c_int32),
+                ("big_dense", ctypes.c_int64), ("big_hot_bits", ctypes.c_int32), ("big_hot16", ctypes.c_int32),
+                ("relabel_planes", ctypes.c_int32)]
+
+    @classmethod
+    def of(cls, **kw):
+        """The defaults (-1 everywhere) with the named fields set; unknown names raise."""
+        t = cls(*([-1] * len(cls._fields_)))
+        names = {f for f, _ in cls._fields_}
+        for k, v in kw.items():
+            if k not in names:
+                raise KeyError(f"no tuning field {k!r} (fields: {sorted(names)})")
+            setattr(t, k, int(v))
+        return t
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
 _lib = None
 
 
@@ -91,6 +114,10 @@ def lib() -> ctypes.CDLL:
         "sheep_timer_get": ([P, ctypes.c_char_p, ctypes.POINTER(D), ctypes.POINTER(U64), ctypes.POINTER(U64)], I32),
         "sheep_timer_reset": ([P], I32),
         "sheep_timer_names": ([P, ctypes.c_char_p, ctypes.c_size_t], I32),
+        "sheep_tuning_default": ([ctypes.POINTER(Tuning)], I32),
+        "sheep_ctx_set_tuning": ([P, ctypes.POINTER(Tuning)], I32),
+        "sheep_ctx_get_tuning": ([P, ctypes.POINTER(Tuning)], I32),
+        "sheep_group_set_tuning": ([P, ctypes.POINTER(Tuning)], I32),
         "sheep_degree_count": ([P, P, U64, I32, P, U64, ctypes.POINTER(U64)], I32),
         "sheep_sequence_from_degrees": ([P, P, U64, P, P, ctypes.POINTER(U64)], I32),
         "sheep_positions": ([P, P, U64, P, U64], I32),
@@ -199,6 +226,16 @@ class Context:
 
     def timer_reset(self):
         _check(lib().sheep_timer_reset(self.handle))
+
+    def set_tuning(self, **kw):
+        """sheep_ctx_set_tuning: the named fields of Tuning set, the rest at their defaults
+        (no arguments: every default)."""
+        _check(lib().sheep_ctx_set_tuning(self.handle, ctypes.byref(Tuning.of(**kw))))
+
+    def tuning(self) -> dict:
+        t = Tuning()
+        _check(lib().sheep_ctx_get_tuning(self.handle, ctypes.byref(t)))
+        return t.as_dict()
 
 
 _default_ctx: Context | None = None
@@ -648,6 +685,10 @@ class Group:
 
     def barrier(self):
         _check(lib().sheep_group_barrier(self.handle))
+
+    def set_tuning(self, **kw):
+        """sheep_group_set_tuning: Context.set_tuning on every local rank's context."""
+        _check(lib().sheep_group_set_tuning(self.handle, ctypes.byref(Tuning.of(**kw))))
 
     def allreduce_max(self, v: int) -> int:
         x = ctypes.c_uint64(int(v))

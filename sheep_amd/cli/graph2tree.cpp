@@ -1,7 +1,7 @@
 // graph2tree — drop-in for chan150/sheep graph2tree.cpp (same getopt string, same
 // stdout lines, same .seq/.tre files) over libsheep_hip.so.
 //
-//   graph2tree input_graph [-s SEQ] [-o OUT] [-p K] [-l n/k] [-i] [-r] [-f] [-c] [-v]
+//   graph2tree input_graph [-s SEQ] [-o OUT] [-p K] [-l n/k] [-i] [-r] [-f] [-t] [-c] [-v]
 //
 // Phases (graph2tree.cpp:161-218): load the records into HBM, degree sequence (or -s
 // read), map (JTree on the GPU), [reduce], [partition], [TREEFAQS].  -i / -r select the
@@ -10,8 +10,9 @@
 // driving the ranks of SHEEP_DEVICES — edge shards, an RCCL all-reduce of the degrees,
 // per-GPU partial trees, the merge on rank 0, the parts broadcast and per-rank partition
 // files, with the reference's file names (include/sheep_hip.h sheep_group_*).  With one
-// rank the single-GPU path runs.  Flags of the junction-tree experiments (-e -j -m -w -x)
-// and -t are rejected with a message.
+// rank the single-GPU path runs.  -t prints every node (JTree::print, jtree.h:60-66) on
+// every rank.  Flags of the junction-tree experiments (-e -j -m -w -x) are rejected with a
+// message.
 #include <unistd.h>
 
 #include <cassert>
@@ -41,7 +42,8 @@ static bool tree_valid(const std::vector<sheep_jnode> &nodes, uint64_t n, uint64
 // w.local() of the w.size() ranks (all of them without a launcher, one under mpiexec).
 static int run_world(World &w, const char *graph_filename, bool use_mpi_sort, bool use_mpi_reduce,
                      size_t partitions, const char *sequence_filename, const char *output_filename, bool verbose,
-                     bool do_faqs, bool do_validate, std::chrono::steady_clock::time_point start_point) {
+                     bool do_faqs, bool do_print, bool do_validate,
+                     std::chrono::steady_clock::time_point start_point) {
   const int P = w.size(), L = w.local();
   if (!use_mpi_sort && strcmp(sequence_filename, "") == 0) {
     printf("graph2tree: -r needs -i or -s SEQ (every rank must use the same sequence).\n");
@@ -178,16 +180,26 @@ static int run_world(World &w, const char *graph_filename, bool use_mpi_sort, bo
   }
   w.barrier();   // MPI_Finalize
   if (verbose) printf("Built in: %f seconds\n", seconds_since(start_point));
-  // every rank prints its own tree's facts (rank 0's is the merged one); a process holding
-  // several ranks prints its first one's
-  if (do_faqs || do_validate) {
-    Facts f;
-    check(sheep_facts(w.ctx(0), rk[0].tree.get(), n, &f.f));
-    if (do_faqs) f.print();
-    if (do_validate) {
-      std::vector<sheep_jnode> h(n);
-      if (n) rk[0].tree.download(h.data(), n);
-      printf(tree_valid(h, n, f.f.vert_cnt) ? "Tree is valid.\n" : "ERROR: Tree is not valid.\n");
+  // graph2tree.cpp:227-236 are not leader-gated: every rank prints its own tree's facts,
+  // nodes and check (rank 0's tree is the merged one with -r, the others' their shard's);
+  // a process holding several ranks prints them one rank after another
+  if (do_faqs || do_print || do_validate) {
+    std::vector<vid_t> seq_host;
+    if (do_print) {
+      seq_host.resize(n);
+      if (n) rk[0].seq.download(seq_host.data(), n);
+    }
+    for (int i = 0; i < L; ++i) {
+      Facts f;
+      check(sheep_facts(w.ctx(i), rk[i].tree.get(), n, &f.f));
+      if (do_faqs) f.print();
+      std::vector<sheep_jnode> h;
+      if (do_print || do_validate) {
+        h.resize(n);
+        if (n) rk[i].tree.download(h.data(), n);
+      }
+      if (do_print) JTree::printTree(h, (jnid_t)n, seq_host);
+      if (do_validate) printf(tree_valid(h, n, f.f.vert_cnt) ? "Tree is valid.\n" : "ERROR: Tree is not valid.\n");
     }
   }
   if (verbose) printf("Finished in: %f seconds\n", seconds_since(start_point));
@@ -199,7 +211,7 @@ int main(int argc, char *argv[]) {
   size_t part = 0, num_parts = 0, partitions = 0;
   const char *sequence_filename = "";
   const char *output_filename = "";
-  bool verbose = false, do_faqs = false, do_validate = false;
+  bool verbose = false, do_faqs = false, do_print = false, do_validate = false;
 
   opterr = 0;
   int opt;
@@ -218,9 +230,10 @@ int main(int argc, char *argv[]) {
       case 'k': break;   // make_kids: the kid table is always built on demand
       case 'd': break;
       case 'f': do_faqs = !do_faqs; break;
+      case 't': do_print = !do_print; break;
       case 'c': do_validate = !do_validate; break;
-      case 'e': case 'j': case 'm': case 'w': case 'x': case 't':
-        printf("Option -%c (junction-tree / width / print experiments) is not supported by this build.\n", opt);
+      case 'e': case 'j': case 'm': case 'w': case 'x':
+        printf("Option -%c (junction-tree / width experiments) is not supported by this build.\n", opt);
         return 1;
       case '?':
         if (optopt == 's' || optopt == 'o')
@@ -245,7 +258,7 @@ int main(int argc, char *argv[]) {
       std::unique_ptr<World> w = World::from_env();
       if (w->size() > 1)
         return run_world(*w, graph_filename, use_mpi_sort, use_mpi_reduce, partitions, sequence_filename,
-                         output_filename, verbose, do_faqs, do_validate, start_point);
+                         output_filename, verbose, do_faqs, do_print, do_validate, start_point);
     } catch (const std::out_of_range &e) {
       fprintf(stderr, "terminate called after throwing an instance of 'std::out_of_range'\n  what():  %s\n", e.what());
       return 134;
@@ -307,6 +320,7 @@ int main(int argc, char *argv[]) {
 
     if (verbose) printf("Built in: %f seconds\n", seconds_since(start_point));
     if (do_faqs) tree.jnodes.getFacts().print();
+    if (do_print) tree.print(seq.host());   // graph2tree.cpp:229-230
     if (do_validate) {
       const Facts f = tree.jnodes.getFacts();
       printf(tree_valid(tree.jnodes.nodes(), tree.size(), f.f.vert_cnt) && f.f.vert_cnt == seq.n

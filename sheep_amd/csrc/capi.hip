@@ -12,7 +12,7 @@ namespace sheep {
 static thread_local std::string g_last_error;
 void set_error(const char *msg) { g_last_error = msg; }
 bool trace_launches() {
-  static const bool on = getenv("SHEEP_TRACE_LAUNCHES") != nullptr;
+  static const bool on = debug_on("launches");
   return on;
 }
 void trace_launch(const char *file, int line) {
@@ -224,6 +224,49 @@ int sheep_timer_names(sheep_ctx *ctx, char *buf, size_t cap) {
   for (auto &kv : ctx->c.timers) { if (!s.empty()) s += ','; s += kv.first; }
   NEED(s.size() < cap, "buffer too small");
   memcpy(buf, s.c_str(), s.size() + 1);
+  API_END
+}
+
+int sheep_tuning_default(sheep_tuning *out) {
+  API_BEGIN
+  NEED(out, "null argument");
+  *out = sheep::default_tuning();
+  API_END
+}
+
+// The defaults filled in for SHEEP_TUNE_DEFAULT fields, every field range-checked.
+static sheep_tuning resolve_tuning(const sheep_tuning *t) {
+  const sheep_tuning d = sheep::default_tuning();
+  if (!t) return d;
+  sheep_tuning r = *t;
+#define SHEEP_TUNE(f, ok)                                                                  \
+  if (r.f == SHEEP_TUNE_DEFAULT) r.f = d.f;                                                \
+  else if (!(ok)) throw sheep::Error(SHEEP_ERR_ARG, "sheep_tuning: " #f " out of range");
+  SHEEP_TUNE(fin_map_bits, r.fin_map_bits >= 1 && r.fin_map_bits <= 13)
+  SHEEP_TUNE(fin_merge_bits, r.fin_merge_bits >= 1 && r.fin_merge_bits <= 13)
+  SHEEP_TUNE(fin_dc, r.fin_dc == 0 || r.fin_dc == 1)
+  SHEEP_TUNE(top_bits, r.top_bits == 0 || (r.top_bits >= 9 && r.top_bits <= 16))
+  SHEEP_TUNE(top_blocks, r.top_blocks >= 1 && r.top_blocks <= 9)
+  SHEEP_TUNE(big_bits, r.big_bits == 0 || (r.big_bits >= 17 && r.big_bits <= 30))
+  SHEEP_TUNE(big_dense, r.big_dense >= 1)
+  SHEEP_TUNE(big_hot_bits, r.big_hot_bits >= 10 && r.big_hot_bits <= 15)
+  SHEEP_TUNE(big_hot16, r.big_hot16 == 0 || r.big_hot16 == 1)
+  SHEEP_TUNE(relabel_planes, r.relabel_planes == 0 || r.relabel_planes == 1)
+#undef SHEEP_TUNE
+  return r;
+}
+
+int sheep_ctx_set_tuning(sheep_ctx *ctx, const sheep_tuning *t) {
+  API_BEGIN
+  NEED(ctx, "null ctx");
+  ctx->c.tune = resolve_tuning(t);
+  API_END
+}
+
+int sheep_ctx_get_tuning(sheep_ctx *ctx, sheep_tuning *out) {
+  API_BEGIN
+  NEED(ctx && out, "null argument");
+  *out = ctx->c.tune;
   API_END
 }
 

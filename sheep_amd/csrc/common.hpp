@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <set>
@@ -32,7 +33,7 @@ struct Error : std::runtime_error {
                            std::string(#expr) + ": " + hipGetErrorString(_e));            \
   } while (0)
 
-// SHEEP_TRACE_LAUNCHES=1 (debugging): every launch is followed by a device-wide wait and a
+// SHEEP_DEBUG=launches (debugging): every launch is followed by a device-wide wait and a
 // stderr line naming its source line, so a kernel that never finishes names itself.
 bool trace_launches();
 void trace_launch(const char *file, int line);
@@ -53,20 +54,49 @@ inline unsigned grid_for(uint64_t items, unsigned per_block = BLOCK, unsigned ca
 // device): the attribute belongs to the device that is current when it is set.
 // allow_lds: the same for a kernel that also has static LDS (the limit is then the dynamic
 // part it launches with: static + dynamic <= 160 KiB).
+// The size granted so far is kept per (kernel, device): a later, larger request raises it.
 inline void allow_lds(const void *kernel, int bytes) {
   static std::mutex m;
-  static std::set<std::pair<const void *, int>> done;
+  static std::map<std::pair<const void *, int>, int> granted;
   int dev = 0;
   HIP_CHECK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> g(m);
-  if (done.insert({kernel, dev}).second)
+  int &have = granted[{kernel, dev}];
+  if (bytes > have) {
     HIP_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    have = bytes;
+  }
 }
 inline void allow_full_lds(const void *kernel) { allow_lds(kernel, 160 * 1024); }
+
+// The one debug variable the library reads: SHEEP_DEBUG=flag[,flag...] with flags
+// "launches" (sync + time every launch), "etree" (level / block statistics to stderr),
+// "part" (partition event timings to stderr).
+inline bool debug_on(const char *flag) {
+  static const std::string v = getenv("SHEEP_DEBUG") ? std::string(",") + getenv("SHEEP_DEBUG") + "," : "";
+  return !v.empty() && v.find(std::string(",") + flag + ",") != std::string::npos;
+}
+
+// The algorithm variants' defaults (include/sheep_hip.h sheep_tuning; measured).
+inline sheep_tuning default_tuning() {
+  sheep_tuning t;
+  t.fin_map_bits = 13;     // RMAT-26 etree 31.0 / 30.5 / 30.0 ms at 11 / 12 / 13 bits
+  t.fin_merge_bits = 12;   // 8-tree merge 15.4 -> 14.1 ms at 12 bits
+  t.fin_dc = 1;
+  t.top_bits = 16;         // RMAT-26 etree: 2^15 32.59, 2^16 32.15 ms
+  t.top_blocks = 4;        // no cut 34.5; 1 block 34.1; 4 blocks 33.8; 8 blocks 33.8
+  t.big_bits = 21;         // RMAT-26 etree: 2^20 27.7, 2^21 26.9 ms; 2^22 leaves 15 K trees
+  t.big_dense = 256;       // a 1/8 edge shard's ~90 group edges per vertex did not pay
+  t.big_hot_bits = 15;
+  t.big_hot16 = 0;
+  t.relabel_planes = 1;
+  return t;
+}
 
 // Per-context state: device, stream, grow-only named workspaces, pinned scalars, timers.
 struct Ctx {
   int device = 0;
+  sheep_tuning tune = default_tuning();
   hipStream_t stream = nullptr;
   bool own_stream = false;
 

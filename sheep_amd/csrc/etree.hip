@@ -988,6 +988,8 @@ __global__ __launch_bounds__(FDC_T) void k_fin_dc(const uint64_t *__restrict__ f
   __shared__ uint32_t uf[NV], top[NV], mt[NV];
   __shared__ uint16_t claim[NV];
   constexpr uint32_t LCAP = fdc_lcap(B);
+  // static LDS: 14 B of state per position, the two list buffers and the scalars below
+  static_assert(14u * NV + 8u * LCAP + 64u <= 160u * 1024u, "k_fin_dc's LDS exceeds 160 KiB");
   __shared__ uint32_t lbuf[2][LCAP];
   __shared__ unsigned s_cnt[3];   // [0], [1]: the levels' next lists by parity; [2]: the block's load
   __shared__ unsigned s_roots;
@@ -1290,12 +1292,10 @@ __global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t 
 // converge in a few rounds (RMAT-22's top 2^15: 3); every round at least halves the
 // components that have an outgoing edge, so TB + 1 rounds always finish.
 // the map's cut: blocks of 2^16 positions (RMAT-26 k=64, etree ms: 2^15 32.59 with the cut
-// 0.55; 2^16 32.15 / 0.81; 8 shard maps 77.0 -> 76.6).  SHEEP_TOP_BITS for A/B runs.
-constexpr int TOP_BITS = 16;
+// 0.55; 2^16 32.15 / 0.81; 8 shard maps 77.0 -> 76.6): sheep_tuning top_bits (default 16).
 constexpr int TOP_BITS_MAX = 16;            // u16 labels: <= 65536 vertices
-// the top block and the dense blocks right below it, at most TOP_NB in all (RMAT-26 k=64, etree
+// the top block and the dense blocks right below it, at most top_blocks in all (RMAT-26 k=64, etree
 // ms: no cut 34.5; 1 block 34.1; 4 blocks 33.8; 8 blocks 33.8 — with the 10-bit finish below)
-constexpr int TOP_NB = 4;
 constexpr int TOPB = 1024;                  // threads per workgroup of the top-block kernels
 constexpr int TOP_WG = 256;                 // workgroups per block of the LDS edge passes (one per CU)
 constexpr uint32_t TOP_HOOK_LDS = 1u << 15; // hooks: par and cid in LDS up to this many components (par alone
@@ -1444,7 +1444,7 @@ __global__ void k_set_u64(uint64_t *p, uint64_t v) { *p = v; }
 // needs no round (k_top_hook0).  Each workgroup (one per CU, a contiguous chunk of the
 // edges) keeps its minima and hasup bits in LDS and flushes them with one read-checked
 // atomic per vertex (the minima only fall).
-// Up to 2^15 vertices the minima are u32 (atomicMin); up to 2^16 (SHEEP_TOP_BITS = 16) u16
+// Up to 2^15 vertices the minima are u32 (atomicMin); up to 2^16 (top_bits = 16) u16
 // pairs updated by a 32-bit CAS (0xFFFF = none: a lower neighbour is at most V - 2).
 __device__ __forceinline__ void lds_min_u16(uint32_t *w2, uint32_t i, uint32_t v) {
   uint32_t *w = w2 + (i >> 1);
@@ -1678,9 +1678,9 @@ __global__ __launch_bounds__(TOPB) void k_top_hook(TopSet t) {
 }
 
 // ---- the top subproblem at an early level: its MSF when round 0 leaves one tree ------
-// The same identity one level band higher: after the level that splits at s = BIG_BITS the
-// top 2^BIG_BITS positions are a subproblem of their own (groups 0..BIG_BITS-1 and the
-// list entries there; RMAT-26, BIG_BITS = 19: ~380 M edges on ~256 K vertices), and the
+// The same identity one level band higher: after the level that splits at s = big_bits the
+// top 2^big_bits positions are a subproblem of their own (groups 0..BIG_BITS-1 and the
+// list entries there; RMAT-26, big_bits = 19: ~380 M edges on ~256 K vertices), and the
 // levels below spend most of their time in it.  Its labels do not fit LDS, so only round 0
 // runs, and it picks ANY lower neighbour per vertex (plain stores, first writer seen wins:
 // in LDS for the block's top BIG_HOT positions, where power-law edges mostly end, in HBM
@@ -1689,11 +1689,11 @@ __global__ __launch_bounds__(TOPB) void k_top_hook(TopSet t) {
 // weight comes up), so the picks lie in SOME minimum spanning forest; when at most one root
 // has an edge they span the block as one tree and ARE that forest — and etree(G) is the
 // elimination tree of every MSF under hi, whatever the tie order (the components of each
-// threshold graph G_t are every MSF's).  Otherwise nothing is cut (the 2^TOP_BITS cut runs
+// threshold graph G_t are every MSF's).  Otherwise nothing is cut (the 2^top_bits cut runs
 // later).  (Lowest lower neighbours by read-checked atomicMin cost 6.1 ms at 2^20.)
-constexpr int BIG_BITS = 21;   // (RMAT-26 etree: 2^20 27.7, 2^21 26.9 ms; at 2^22 round 0 leaves 15 K trees)
+// sheep_tuning big_bits (default 21: RMAT-26 etree 2^20 27.7, 2^21 26.9 ms; at 2^22 round 0
+// leaves 15 K trees) and big_dense (default 256 group edges per vertex).
 constexpr uint32_t BIG_HOT = 1u << 15;
-constexpr uint64_t BIG_DENSE = 256;
 struct BigState {
   uint32_t *minlo;                  // per vertex: a lower neighbour (block-local), the round-0 pick
   unsigned *hasup;                  // per vertex a bit: it has an upper neighbour
@@ -1853,7 +1853,7 @@ __global__ __launch_bounds__(BLOCK) void k_big_emit(BigState b) {
   }
 }
 
-// Debug statistic (SHEEP_DEBUG_ETREE): live entries per block of 2^s spread positions
+// Debug statistic (SHEEP_DEBUG=etree): live entries per block of 2^s spread positions
 // after a level (its next list plus the groups not yet activated).
 __global__ void k_dbg_blocks(const uint64_t *__restrict__ a, const uint64_t *__restrict__ st, const uint64_t *__restrict__ b,
                              uint64_t nb_edges, int s, uint32_t clo, unsigned *__restrict__ cnt, uint32_t cut) {
@@ -1870,14 +1870,13 @@ __global__ void k_dbg_blocks(const uint64_t *__restrict__ a, const uint64_t *__r
 
 void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
 
-static const bool g_debug_etree = getenv("SHEEP_DEBUG_ETREE") != nullptr;
-// Finishing block size (log2 positions).  Liu's sweep per block (SHEEP_FIN_DC=0) takes one
-// step per hi, so 10 bits were its best for maps (RMAT-26 etree 32.0-32.2 ms) and 11 for
-// merges.  The per-block D&C (k_fin_dc) spreads a level over a workgroup and cuts long
-// block lists to their MSF first: RMAT-26 etree 31.0 / 30.5 / 30.0 ms at 11 / 12 / 13 bits
-// (13: one workgroup per CU, 112 KB of LDS state); 8 shard maps 76.3 -> 71.2 ms and the
-// 8-tree merge 15.4 -> 14.1 ms at 12 bits.
-constexpr int FIN_MERGE = 12, FIN_MAP = 13;
+static const bool g_debug_etree = debug_on("etree");
+// Finishing block size (log2 positions; sheep_tuning fin_map_bits / fin_merge_bits).
+// Liu's sweep per block (fin_dc = 0) takes one step per hi, so 10 bits were its best for
+// maps (RMAT-26 etree 32.0-32.2 ms) and 11 for merges.  The per-block D&C (k_fin_dc)
+// spreads a level over a workgroup and cuts long block lists to their MSF first: RMAT-26
+// etree 31.0 / 30.5 / 30.0 ms at 11 / 12 / 13 bits (13: one workgroup per CU, 112 KB of
+// LDS state); 8 shard maps 76.3 -> 71.2 ms and the 8-tree merge 15.4 -> 14.1 ms at 12 bits.
 
 // spread(x) = floor(x * c / 2^32), c = floor(2^(32+L) / n) in [2^32, 2^33), L = ceil(log2 n):
 // monotone, injective on [0,n), image in [0, 2^L).  clo = c - 2^32.
@@ -1902,7 +1901,7 @@ static uint64_t list_capacity(uint64_t m) { return 2 * m + TILE; }
 // k_top_hook).  Block 0 is the top block [cut0, 2^L) (its list entries plus groups [g0, g1)
 // of r0), block j >= 1 the 2^bits positions below block j - 1 (list entries only); the
 // blocks below the top are cut while they are dense (up to nb_max - 1 of them,
-// SHEEP_TOP_BLOCKS).  The MSF edges are appended to `next` behind the cut level's
+// sheep_tuning top_blocks).  The MSF edges are appended to `next` behind the cut level's
 // contractions (st[ST_EXTRA]); st[ST_CUT] (the lowest cut block's start) makes the next split
 // drop the blocks' list entries, and the caller stops activating the top block's groups.
 // One host sync for the blocks' sizes, one to skip the idle Borůvka rounds.  Returns the
@@ -1918,6 +1917,14 @@ static uint32_t top_blocks(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t 
   const uint64_t tcap = (nl + TILE - 1) / TILE * TILE + TILE;
   nb_max = std::min<uint32_t>(std::max<uint32_t>(nb_max, 1), TOP_NB_MAX);
   while (nb_max > 1 && ((uint64_t)nb_max << bits) > cut0 + (1ull << bits)) --nb_max;   // blocks must lie above 0
+  {   // every block's region holds the whole list: as many blocks as half the free HBM takes
+    // (top_blocks = 8 with the 11-bit finish ran out of memory at RMAT-26)
+    size_t free_b = 0, total_b = 0;
+    HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+    const auto it = c.ws.find("et_top_list");
+    const size_t have = it == c.ws.end() ? 0 : it->second.bytes;
+    while (nb_max > 1 && (size_t)nb_max * tcap * sizeof(uint64_t) * 9 / 8 > have + free_b / 2) --nb_max;
+  }
   uint64_t *tl = c.get_as<uint64_t>("et_top_list", nb_max * tcap);
   unsigned long long *tcnt = c.get_as<unsigned long long>("et_top_cnt", nb_max * TOP_CSET + TOP_NB_MAX);
   unsigned long long *bcnt = tcnt + nb_max * TOP_CSET;
@@ -1954,7 +1961,7 @@ static uint32_t top_blocks(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t 
   uint16_t *comp = c.get_as<uint16_t>("et_top_comp", nb * VMAX);
   unsigned long long *best = c.get_as<unsigned long long>("et_top_best", nb * VMAX);
   unsigned *scal = c.get_as<unsigned>("et_top_scal", 4 * nb);
-  const bool big = VMAX > TOP_HOOK_LDS;   // (SHEEP_TOP_BITS = 16: the hooks keep cid in HBM)
+  const bool big = VMAX > TOP_HOOK_LDS;   // (top_bits = 16: the hooks keep cid in HBM)
   uint16_t *gcid = big ? c.get_as<uint16_t>("et_top_gcid", nb * VMAX) : nullptr;
   TopSet set{};
   uint32_t vmax = 0;
@@ -2046,13 +2053,13 @@ static bool big_cut(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, ui
   b.st = st;
   b.out = next;
   const TopEdges te{tl, tcnt, r0, g0, g1};
-  // (SHEEP_BIG_HOT_BITS: a smaller window leaves LDS for two workgroups per CU)
-  static const int hot_bits = getenv("SHEEP_BIG_HOT_BITS") ? atoi(getenv("SHEEP_BIG_HOT_BITS")) : 15;
+  // (big_hot_bits: a smaller window leaves LDS for two workgroups per CU)
+  const int hot_bits = c.tune.big_hot_bits;
   b.hot = std::min<uint32_t>(1u << std::max(10, std::min(15, hot_bits)), BIG_HOT);
   const size_t lds = b.hot * sizeof(uint32_t);
   allow_lds((const void *)k_big_min0<false>, (int)(BIG_HOT * sizeof(uint32_t)));
   allow_lds((const void *)k_big_min0<true>, (int)(BIG_HOT * sizeof(uint32_t)));
-  static const bool hot16 = getenv("SHEEP_BIG_HOT16") != nullptr;   // (A/B runs)
+  const bool hot16 = c.tune.big_hot16 != 0;
   hipLaunchKernelGGL(k_big_init, dim3(grid_for(b.V)), dim3(BLOCK), 0, c.stream, b);
   LAUNCH_CHECK();
   if (hot16)
@@ -2108,8 +2115,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   const unsigned gt = grid_tiles(m), gt2 = grid_for(lcap + m, SPLIT_TILE), gf = grid_for(m, BLOCK * XK), gn = grid_for(n);
   const int FINB = fin_bits < 0 ? 0 : fin_bits > FIN_BITS_MAX ? FIN_BITS_MAX : fin_bits;   // levels s < FINB: Liu per block (0: none)
   const int nglobal = L > FINB ? L - FINB : 0;
-  static const int g_fin_dc = getenv("SHEEP_FIN_DC") ? atoi(getenv("SHEEP_FIN_DC")) : 1;   // (0: Liu per block, A/B runs)
-  const bool fin_dc = g_fin_dc && FINB >= 8;
+  const bool fin_dc = c.tune.fin_dc && FINB >= 8;   // (0: Liu's sweep per block)
   // the per-level state starts clean; tagged words need no restore between levels,
   // untagged ones are restored at each level's end (k_level_clean)
   const bool tagged = n < TAG_MAX_N;
@@ -2121,7 +2127,6 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   int top_lvl = -1, gcut = 0;
   uint64_t top_g0 = 0, top_g1 = 0;
   uint32_t top_V = 0, top_cut = 0;
-  if (getenv("SHEEP_TOP_BITS") && top_bits) top_bits = atoi(getenv("SHEEP_TOP_BITS"));   // (A/B runs)
   if (top_bits > FINB && top_bits <= L - 1 && top_bits <= TOP_BITS_MAX) {
     std::vector<uint64_t> hs(2 * (size_t)L);
     HIP_CHECK(hipMemcpyAsync(hs.data(), seg, hs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
@@ -2135,13 +2140,13 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     top_V = (uint32_t)(n - a);
     top_g0 = hs[top_bits - 1];
     top_g1 = hs[L];
-    if (top_V >= 2 && top_g1 - top_g0 >= TOP_DENSE * top_V && getenv("SHEEP_NO_TOP") == nullptr) {
+    if (top_V >= 2 && top_g1 - top_g0 >= TOP_DENSE * top_V) {
       top_lvl = L - 1 - top_bits;
       gcut = top_bits;
     }
   }
-  // the early cut of the top subproblem (SHEEP_BIG_BITS; 0: off), tried when dense
-  static const int big_bits = getenv("SHEEP_BIG_BITS") ? atoi(getenv("SHEEP_BIG_BITS")) : BIG_BITS;
+  // the early cut of the top subproblem (sheep_tuning big_bits; 0: off), tried when dense
+  const int big_bits = top_bits ? c.tune.big_bits : 0;
   int big_lvl = -1;
   uint64_t big_g0 = 0, big_g1 = 0;
   uint32_t big_cut0 = 0;
@@ -2160,8 +2165,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     // only where the block is far denser than the top block's rule asks (RMAT-26: ~740 group
     // edges per vertex at 2^19, ~540 at 2^20; a 1/8 edge shard's ~90 did not pay for the
     // cut: 8 shard maps 70.2 -> 76.9 ms)
-    static const uint64_t big_dense = getenv("SHEEP_BIG_DENSE") ? strtoull(getenv("SHEEP_BIG_DENSE"), nullptr, 10)
-                                                                 : BIG_DENSE;   // (A/B runs)
+    const uint64_t big_dense = (uint64_t)c.tune.big_dense;
     if (n - a >= 2 && big_g1 - big_g0 >= big_dense * (n - a)) big_lvl = L - 1 - big_bits;
   }
   int cut_lvl = -1;           // the level whose split follows a cut (its list entries dropped)
@@ -2227,7 +2231,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     if (lvl == big_lvl) {
       TimedRegion tr(c, "etree_top");
       if (big_cut(c, next, st, r0, big_g0, big_g1, big_cut0, big_bits, clo, n)) {
-        gcut = big_bits;   // groups below are never activated; the 2^TOP_BITS cut has nothing left to do
+        gcut = big_bits;   // groups below are never activated; the 2^top_bits cut has nothing left to do
         top_lvl = -1;
         cut_lvl = lvl;
         cut_val = big_cut0;
@@ -2237,7 +2241,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       cut_lvl = lvl;
       cut_val = top_cut;
       TimedRegion tr(c, "etree_top");
-      static const int top_nb = getenv("SHEEP_TOP_BLOCKS") ? atoi(getenv("SHEEP_TOP_BLOCKS")) : TOP_NB;
+      const int top_nb = c.tune.top_blocks;
       const uint32_t nbc = top_blocks(c, next, st, r0, top_g0, top_g1, top_cut, top_bits, (uint32_t)top_nb, clo, n, lcap);
       if (g_debug_etree) {
         uint64_t h[ST_ROW];
@@ -2328,8 +2332,14 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
         unsigned long long *ticket = (unsigned long long *)(n_fin + 3);   // (zeroed with stats)
         const unsigned gd = (unsigned)(nb < 1024 ? nb : 1024);
         switch (FINB) {
-#define SHEEP_FIN_DC(B)                                                                                            case B:                                                                                                            hipLaunchKernelGGL(k_fin_dc<B>, dim3(gd), dim3(FDC_T), 0, c.stream, (const uint64_t *)fin, (const uint64_t *)eb,                        (const uint32_t *)vb, (const uint32_t *)heavy, (const unsigned long long *)(n_lh + 1),                \
-                       (const uint32_t *)light, (const unsigned long long *)n_lh, clo, dbuf,                        cap, ticket, parent);                                                                         LAUNCH_CHECK();                                                                                                  break;
+#define SHEEP_FIN_DC(B)                                                                                    \
+  case B:                                                                                                  \
+    hipLaunchKernelGGL(k_fin_dc<B>, dim3(gd), dim3(FDC_T), 0, c.stream, (const uint64_t *)fin,             \
+                       (const uint64_t *)eb, (const uint32_t *)vb, (const uint32_t *)heavy,                \
+                       (const unsigned long long *)(n_lh + 1), (const uint32_t *)light,                    \
+                       (const unsigned long long *)n_lh, clo, dbuf, cap, ticket, parent);                  \
+    LAUNCH_CHECK();                                                                                        \
+    break;
           SHEEP_FIN_DC(8) SHEEP_FIN_DC(9) SHEEP_FIN_DC(10) SHEEP_FIN_DC(11) SHEEP_FIN_DC(12) SHEEP_FIN_DC(13)
 #undef SHEEP_FIN_DC
           default: throw Error(SHEEP_ERR_ARG, "etree: bad finishing block size");
@@ -2436,8 +2446,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
       group_edges_by_lo(c, edges, m, lg, pst, r0, seg, counted);
     }
     TimedRegion tr(c, "etree", 8 * m);
-    static const int fin_map = getenv("SHEEP_FIN_MAP") ? atoi(getenv("SHEEP_FIN_MAP")) : FIN_MAP;   // (A/B runs)
-    etree_from_edges(c, r0, m, n, parent, seg, fin_map, -1, 0, 0, TOP_BITS);
+    etree_from_edges(c, r0, m, n, parent, seg, c.tune.fin_map_bits, -1, 0, 0, c.tune.top_bits);
   } else {
     fill_u32(c, parent, n, INVALID);
   }
@@ -2542,7 +2551,7 @@ static void merge_set(Ctx &c, const TreeSet &ts, uint32_t K, uint64_t n, sheep_j
   uint64_t lo = 0, hi = n;
   if (n >= 2) spread_params(n, &L, &clo);
   // only as many parts as global levels (below them the per-block finish runs whole)
-  static const int fin_merge = getenv("SHEEP_FIN_MERGE") ? atoi(getenv("SHEEP_FIN_MERGE")) : FIN_MERGE;   // (A/B runs)
+  const int fin_merge = c.tune.fin_merge_bits;
   const int nglobal = L > fin_merge ? L - fin_merge : 0;
   if (nparts > 1 && (l >= nglobal || L > 31)) l = 0;   // too small a tree to split: every part runs it all
   uint32_t ylo = 0, yhi = 0;

@@ -348,6 +348,7 @@ int sheep_group_join(int device, int rank, int world, const char *host, int port
     g->ctx.push_back(c);
     g->dev.push_back(device);
     g->rank.push_back(rank);
+    // (a run-time setting, not a debug knob: how long the ranks wait for each other)
     const int timeout = getenv("SHEEP_JOIN_TIMEOUT") ? atoi(getenv("SHEEP_JOIN_TIMEOUT")) : 300;
     g->mesh.reset(new sheep::Mesh(rank, world, host, port, sheep::bus_id(device), timeout));
     bool distinct = true;
@@ -406,6 +407,16 @@ int sheep_group_allreduce_max_u64(sheep_group *g, uint64_t *v) {
   GAPI_BEGIN
   GNEED(g && v, "null argument");
   if (g->mesh) *v = g->mesh->allreduce_max(*v);
+  GAPI_END
+}
+
+int sheep_group_set_tuning(sheep_group *g, const sheep_tuning *t) {
+  GAPI_BEGIN
+  GNEED(g, "null argument");
+  for (sheep_ctx *c : g->ctx) {
+    const int rc = sheep_ctx_set_tuning(c, t);
+    if (rc != SHEEP_OK) return rc;
+  }
   GAPI_END
 }
 

@@ -914,7 +914,7 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
       const size_t fx = ((2 * nb + NT / WAVE + 1) & ~1ull) * 4, lds = fx + (size_t)P * NT * 8;
       // the staged pairs as two u32 planes (RMAT-26 relabel 13.56 / 13.85 ms against 14.56 /
       // 13.80 with one u64 array, two runs each: within box noise, not worse)
-      static const bool planes = getenv("SHEEP_RELABEL_U64") == nullptr;   // (A/B runs)
+      const bool planes = c.tune.relabel_planes != 0;
       if (nb <= 8 * (uint64_t)NT && lds <= 160 * 1024) {
         if (planes)
           hipLaunchKernelGGL((k_relabel_scatter<P, NT, true>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec, nrec,

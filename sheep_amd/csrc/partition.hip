@@ -839,7 +839,7 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   HIP_CHECK(hipMemsetAsync(evprev, 0xFF, sizeof(uint64_t), c.stream));
   HIP_CHECK(hipMemsetAsync(done_ctr, 0, sizeof(uint64_t), c.stream));
   HIP_CHECK(hipMemsetAsync(found, 0xFF, sizeof(uint64_t), c.stream));   // k_event resets it after each event
-  static const bool dbg = getenv("SHEEP_DEBUG_PART") != nullptr;
+  static const bool dbg = debug_on("part");
   double dbg_tab = 0, dbg_search = 0, dbg_stage = 0, dbg_wait = 0, dbg_host = 0;
   uint64_t dbg_kids[4] = {0, 0, 0, 0}, dbg_kids_max = 0;   // packing nodes with <= 16 / 256 / 4096 / more kids
   uint8_t *stage = (uint8_t *)c.get_pinned("pt_event", 64 + (size_t)EV_STAGE * 12);

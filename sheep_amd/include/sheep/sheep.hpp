@@ -342,6 +342,7 @@ class JNodeTable {
   jnid_t parent(jnid_t id) const { return nodes_.at(id).parent; }
   esize_t pst_weight(jnid_t id) const { return nodes_.at(id).pst_weight; }
   std::vector<sheep_jnode> &nodes() { return nodes_; }
+  const std::vector<sheep_jnode> &nodes() const { return nodes_; }
 
   void save(const char *filename) const {   // jnode.cpp:164-168
     FILE *f = fopen(filename, "wb");
@@ -390,6 +391,15 @@ class JNodeTable {
     return x;
   }
 
+  // JNodeTable::print(id) (jnode.h:263-267) on the default path: no junction data, so
+  // width = 1 + pst (jnode.h:258-260), and pre_weight is 0 without USE_PRE_WEIGHT
+  // (defs.h:62, jnode.h:139-153).
+  void print(jnid_t id) const { printNode(nodes_.at(id)); }
+  static void printNode(const sheep_jnode &x) {
+    printf("%6zu:w%6zu:pre%6zu:pst        ->[%4zu]\n", (size_t)1 + x.pst_weight, (size_t)0, (size_t)x.pst_weight,
+           (size_t)x.parent);
+  }
+
  private:
   std::vector<sheep_jnode> nodes_;
   jnid_t end_id_ = 0;
@@ -407,6 +417,16 @@ class JTree {
     jnodes.assign_from_device(t, (jnid_t)seq.n, (jnid_t)seq.n);
   }
   jnid_t size() const { return jnodes.size(); }
+  // JTree::print (jtree.h:60-66): one line per jnid, "id:vid" and the node's print(id).
+  // The jnid->vid map is the sequence itself (get_sequence, jtree.h:50-57: every vid of
+  // the sequence holds a jnid, make_pad being the default, jtree.h:88).
+  void print(const std::vector<vid_t> &seq) const { printTree(jnodes.nodes(), size(), seq); }
+  static void printTree(const std::vector<sheep_jnode> &nodes, jnid_t n, const std::vector<vid_t> &seq) {
+    for (jnid_t id = 0; id != n; ++id) {
+      printf("%4zu:%-8zu", (size_t)id, (size_t)seq.at(id));
+      JNodeTable::printNode(nodes.at(id));
+    }
+  }
 };
 
 // The text files of writePartitionedGraph (partition.cpp:588-670): one SNAP text file per

@@ -77,6 +77,20 @@ def golden_part_text(name):
     return facts, blocks
 
 
+PRINT_GRAPHS = ["hep", "rmat10", "rmat12", "edge"]
+
+
+def check_print(text, name, tag="print"):
+    """graph2tree -t output against the reference's JTree::print run (make_golden.py):
+    the committed file where there is one, else its md5 and line count."""
+    entry = manifest()["_print"][f"{name}.{tag}.txt"]
+    path = os.path.join(GOLDEN, f"{name}.{tag}.txt")
+    if os.path.exists(path):
+        assert text == open(path).read(), f"{name}.{tag}"
+    assert text.count("\n") == entry["lines"], f"{name}.{tag}"
+    assert hashlib.md5(text.encode()).hexdigest() == entry["md5"], f"{name}.{tag}"
+
+
 def ks(name):
     return manifest()["_ks"][name]
 

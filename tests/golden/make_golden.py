@@ -23,6 +23,12 @@ Outputs per graph G (see MANIFEST.json for md5s):
   G.k<K>.parts     vid-indexed int16 parts per k (same run, so kid order persists)
   G.k<K>.g%04d     writePartitionedGraph(graph, seq, prefix) files (graph2tree -p K -o)
   G.k<K>.f%04d     writePartitionedGraph(filename, seq, prefix) files (partition_tree -o)
+  G.print.txt, G.h1.print.txt, G.h2.print.txt
+                   ref_harness print: JTree::print (graph2tree -t) of the whole tree and of
+                   the halves' partial trees; committed for PRINT_FILES, md5 only (in
+                   MANIFEST.json "_print") for the others
+
+`make_golden.py --print` regenerates only the print fixtures (and their manifest entries).
 """
 import hashlib
 import json
@@ -42,6 +48,9 @@ KS = {"hep": [2, 3, 4, 16, 64], "rmat10": [2, 16], "rmat12": [4, 16, 64], "rmat1
 # partition files (writePartitionedGraph): graph order (graph2tree -p -o) -> G.k<K>.g%04d,
 # input-file order (partition_tree -g G -o) -> G.k<K>.f%04d
 WRITE_K = {"hep": 4, "rmat10": 16, "edge": 2}
+# graph2tree -t dumps: committed as files for these, md5 + line count only for the rest
+PRINT_FILES = ("edge", "rmat10")
+PRINT_GRAPHS = ("hep", "rmat10", "rmat12", "edge")
 
 
 def run(*args, **kw):
@@ -63,9 +72,44 @@ def edge_graph():
     return t, h
 
 
+def make_prints(manifest):
+    """JTree::print of the whole tree and of the two halves' partial trees (graph2tree -t,
+    -l 1/2 and 2/2 with the golden sequence)."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    from conftest import golden_records   # the committed input, or the md5-checked regenerated one
+    H = os.path.join(REF, "ref_harness")
+    out = {}
+    tmp = os.path.join(HERE, "_tmp_print")
+    os.makedirs(tmp, exist_ok=True)
+    for name in PRINT_GRAPHS:
+        dat = os.path.join(HERE, f"{name}.dat")
+        if not os.path.exists(dat):
+            dat = os.path.join(tmp, f"{name}.dat")
+            golden_records(name).tofile(dat)
+        seq = os.path.join(HERE, f"{name}.seq")
+        for tag, extra in (("print", ()), ("h1.print", ("1/2",)), ("h2.print", ("2/2",))):
+            text = run(H, "print", dat, seq, *extra)
+            fname = f"{name}.{tag}.txt"
+            out[fname] = {"md5": hashlib.md5(text.encode()).hexdigest(), "lines": text.count("\n")}
+            if name in PRINT_FILES:
+                open(os.path.join(HERE, fname), "w").write(text)
+    shutil.rmtree(tmp)
+    manifest["_print"] = out
+
+
 def main():
     if not os.path.exists(os.path.join(REF, "ref_harness")):
         sys.exit("build oracle/_ref first: make ref")
+    if sys.argv[1:] == ["--print"]:
+        path = os.path.join(HERE, "MANIFEST.json")
+        manifest = json.load(open(path))
+        make_prints(manifest)
+        for f in sorted(os.listdir(HERE)):
+            if f.endswith(".print.txt"):
+                manifest[f] = hashlib.md5(open(os.path.join(HERE, f), "rb").read()).hexdigest()
+        json.dump(manifest, open(path, "w"), indent=1, sort_keys=True)
+        print(f"wrote {len(manifest['_print'])} print digests")
+        return
     import sheep_amd
     graphs = {}
     hep = np.fromfile("/root/reference/data/hep-th.dat", dtype=[("tail", "<u4"), ("head", "<u4"), ("weight", "<f4")])
@@ -114,6 +158,7 @@ def main():
     # against this manifest) instead of being committed
     for big in ("rmat12.dat", "rmat14.dat"):
         os.remove(os.path.join(HERE, big))
+    make_prints(manifest)
     manifest["_ks"] = KS
     manifest["_write_k"] = WRITE_K
     manifest["_rmat"] = {"rmat10": [10, 16, 10], "rmat12": [12, 16, 12], "rmat14": [14, 16, 14]}

@@ -66,3 +66,26 @@ def test_host_generator_matches_golden_inputs(name):
     assert np.all(rec["tail"] > rec["head"])
     key = rec["tail"].astype(np.uint64) << 32 | rec["head"]
     assert np.all(np.diff(key.astype(np.int64)) > 0)
+
+
+def test_tuning_defaults_without_a_device():
+    """sheep_tuning_default needs no device; the defaults are the documented ones."""
+    import sheep_amd
+    lib()
+    t = sheep_amd.Tuning()
+    assert sheep_amd.lib().sheep_tuning_default(ctypes.byref(t)) == 0
+    assert t.as_dict() == {"fin_map_bits": 13, "fin_merge_bits": 12, "fin_dc": 1, "top_bits": 16, "top_blocks": 4,
+                           "big_bits": 21, "big_dense": 256, "big_hot_bits": 15, "big_hot16": 0, "relabel_planes": 1}
+    with pytest.raises(KeyError):
+        sheep_amd.Tuning.of(no_such_field=1)
+
+
+def test_library_reads_one_debug_variable():
+    """The algorithm variants are per-context options (sheep_tuning), not environment
+    variables: the sources read SHEEP_DEBUG (debugging) and SHEEP_JOIN_TIMEOUT (how long
+    joined ranks wait for each other) and nothing else."""
+    csrc = os.path.join(ROOT, "sheep_amd", "csrc")
+    names = set()
+    for f in os.listdir(csrc):
+        names |= set(re.findall(r'getenv\("(\w+)"\)', open(os.path.join(csrc, f)).read()))
+    assert names == {"SHEEP_DEBUG", "SHEEP_JOIN_TIMEOUT"}, names

@@ -8,7 +8,7 @@ import subprocess
 
 import pytest
 
-from conftest import GOLDEN, ROOT, golden_records, ks
+from conftest import GOLDEN, ROOT, check_print, golden_records, ks, manifest
 
 BIN = os.path.join(ROOT, "sheep_amd", "bin")
 CLIS = ("graph2tree", "partition_tree", "merge_trees", "degree_sequence")
@@ -95,6 +95,23 @@ def test_degree_sequence_cli(gpu_ctx, tmp_path, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["hep", "rmat10", "rmat12", "edge"])
+def test_graph2tree_print(gpu_ctx, tmp_path, name):
+    """graph2tree G -f -t (graph2tree.cpp:107-108, 227-230): TREEFAQS, then JTree::print
+    (jtree.h:60-66) of every node, byte-exact with the reference's print; and the partial
+    trees of -l 1/2 and 2/2 with the sequence file."""
+    dat = dat_path(name, tmp_path)
+    p = run(os.path.join(BIN, "graph2tree"), dat, "-f", "-t")
+    facts = open(os.path.join(GOLDEN, f"{name}.facts")).read()
+    text = strip_timing(p.stdout)
+    assert text.startswith(facts)
+    check_print(text[len(facts):], name, "print")
+    for part, tag in ((1, "h1.print"), (2, "h2.print")):
+        p = run(os.path.join(BIN, "graph2tree"), dat, "-l", f"{part}/2", "-s", os.path.join(GOLDEN, f"{name}.seq"), "-t")
+        check_print(strip_timing(p.stdout), name, tag)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["hep", "rmat12", "edge"])
 def test_partition_tree_cli(gpu_ctx, tmp_path, name):
     """partition_tree -v -f -g G SEQ TREE k1 k2 ... (-v turns the timing lines off):
@@ -169,12 +186,46 @@ def test_graph2tree_world_ir(gpu_ctx, tmp_path, name, ranks, launch):
     assert filecmp.cmp(seq, os.path.join(GOLDEN, f"{name}.seq"), shallow=False)
     assert filecmp.cmp(out, os.path.join(GOLDEN, f"{name}.tre"), shallow=False)
     facts = open(os.path.join(GOLDEN, f"{name}.facts")).read()
-    if launch == "devices":
-        assert strip_timing(p.stdout) == facts
+    if launch == "devices":   # the ranks print one after another, rank 0 (the merged tree) first
+        assert strip_timing(p.stdout).startswith(facts)
     else:
         assert facts in strip_timing(p.stdout)
-        assert strip_timing(p.stdout).count("TREEFAQS") == ranks
+    assert strip_timing(p.stdout).count("TREEFAQS") == ranks
     assert p.stdout.count("Reduced in:") == 1 and p.stdout.count("Mapped in:") == 1
+
+
+def _print_blocks(text, name, tags):
+    """Split a world's -t output into one block per rank (each the tree's line count)."""
+    lines = text.splitlines(keepends=True)
+    blocks, at = [], 0
+    for tag in tags:
+        n = manifest()["_print"][f"{name}.{tag}.txt"]["lines"]
+        blocks.append("".join(lines[at:at + n]))
+        at += n
+    assert at == len(lines)
+    return blocks
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,launch", [("edge", "devices"), ("edge", "mpiexec"), ("rmat10", "devices"),
+                                         ("hep", "devices")])
+def test_graph2tree_world_print(gpu_ctx, tmp_path, name, launch):
+    """graph2tree G -s SEQ -ir -t over 2 ranks: tree.print() is not leader-gated
+    (graph2tree.cpp:229-230), so rank 0 prints the merged tree (== the whole graph's) and
+    rank 1 its own shard's partial tree (mpi_merge leaves the senders' nodes as they were,
+    jnode.cpp:241); with -i alone both ranks print their partial trees (-l 1/2, 2/2)."""
+    dat = dat_path(name, tmp_path)
+    for flags, tags in ((("-i", "-r"), ("print", "h2.print")), (("-i",), ("h1.print", "h2.print"))):
+        p = world_run(launch, 2, dat, "-s", seq_copy(tmp_path, name), *flags, "-t")
+        text = strip_timing(p.stdout)
+        if launch == "mpiexec":   # two processes: either may flush first (each < one pipe write)
+            first = manifest()["_print"][f"{name}.{tags[0]}.txt"]["md5"]
+            import hashlib
+            head = "".join(text.splitlines(keepends=True)[:manifest()["_print"][f"{name}.{tags[0]}.txt"]["lines"]])
+            if hashlib.md5(head.encode()).hexdigest() != first:
+                tags = tags[::-1]
+        for block, tag in zip(_print_blocks(text, name, tags), tags):
+            check_print(block, name, tag)
 
 
 @pytest.mark.gpu

@@ -6,7 +6,8 @@ import numpy as np
 import pytest
 
 import oracle
-from conftest import (GRAPHS, ROOT, golden_part_text, golden_parts, golden_records, golden_seq, golden_tree, ks)
+from conftest import (GRAPHS, PRINT_GRAPHS, ROOT, check_print, golden_part_text, golden_parts, golden_records,
+                      golden_seq, golden_tree, ks)
 
 
 @pytest.mark.parametrize("name", GRAPHS)
@@ -46,6 +47,15 @@ def test_partial_trees_and_merge(name):
     # merge == the tree of the whole graph (SURVEY §0 invariant 3)
     tp, tw = golden_tree(name)
     assert np.array_equal(p, tp) and np.array_equal(w, tw)
+
+
+@pytest.mark.parametrize("name", PRINT_GRAPHS)
+def test_print_restatement_matches_reference(name):
+    """graph2tree -t: JTree::print restated (oracle.print_text) over the golden whole and
+    half trees equals the reference's own print of the same trees."""
+    seq = golden_seq(name)
+    for which, tag in (("tre", "print"), ("h1.tre", "h1.print"), ("h2.tre", "h2.print")):
+        check_print(oracle.print_text(*golden_tree(name, which), seq), name, tag)
 
 
 @pytest.mark.parametrize("name", GRAPHS)
