@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--reduce", default="kway", choices=("kway", "binomial"),
                     help="kway: gather the partial trees to rank 0 and merge them in one pass; "
                          "binomial: ceil(log2 N) send/recv hops with a pairwise merge each (mpi_merge's schedule)")
+    ap.add_argument("--tune", nargs="+", default=[], metavar="FIELD=VALUE",
+                    help="algorithm variants for A/B runs (include/sheep_hip.h sheep_tuning, e.g. fin_map_bits=12); "
+                         "every variant gives the same bit-exact result")
     ap.add_argument("--no-verify", dest="verify", action="store_false",
                     help="skip the after-timing check of the merged tree (N > 1: against the whole-graph tree; "
                          "--shards: against the binomial pairwise merges of the same shard trees)")
@@ -190,6 +193,9 @@ def main():
         ctx = group.ctx[0]
     else:
         ctx = sheep_amd.Context(local)
+    tune = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in a.tune}
+    if tune:
+        (group or ctx).set_tuning(**tune)
     rec, vs_cap, workload = make_records(a, seed, ctx)          # whole graph, identical on every rank
     if a.shards > 1:
         workload += f", {a.shards} shards on 1 GPU"
@@ -268,6 +274,10 @@ def main():
         s, tree, res = step()
     barrier()
     t = sdist.max_over_ranks(time.perf_counter() - t0) if world > 1 else time.perf_counter() - t0
+    # device memory in use after the timed steps: the library's workspaces only grow and
+    # torch's caching allocator keeps its blocks, so this is the step's high-water mark
+    free_b, total_b = torch.cuda.mem_get_info(local)
+    hbm_used = total_b - free_b
 
     # per-region device timings (HIP events on the context stream), timed steps only
     phases = {}
@@ -339,6 +349,7 @@ def main():
             "config": {"workload": workload, "records": R, "vertex_slots": s.pos_size,
                        "tree_nodes": n, "k": a.k, "created": res.created, "packing_nodes": res.packing_nodes,
                        "heavy_nodes": res.heavy_nodes, "seed": seed, "shuffled": a.shuffle, "shards": a.shards,
+                       "tuning": ctx.tuning() if tune else "defaults",
                        "parallelism": f"edge-shards x{world}" + (
                            f", {a.reduce} reduce, sheep_group over {'RCCL' if group.rccl else 'host TCP (one device)'}"
                            if world > 1 else "")},
@@ -346,6 +357,9 @@ def main():
             "path_roofline": path,
             "evaluator": evaluator,
             "phases": phases,
+            "hbm_peak_bytes": hbm_used,
+            "hbm_peak_note": "device memory in use after the timed steps (hipMemGetInfo: total - free); the "
+                             "library's workspaces only grow, so this is the step's high-water mark",
         }
         if per_rank is not None:
             out["per_rank"] = per_rank

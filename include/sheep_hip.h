@@ -213,6 +213,14 @@ int sheep_partition(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n,
                     const uint32_t *seq_dev, uint64_t seq_n, uint64_t pos_size, sheep_kids *kids, int16_t k,
                     double balance, int vtx_weight, int pst_weight, int16_t *parts_vid_dev,
                     sheep_partition_info *info);
+/* The same with the sequence's vid -> jnid index pos_dev[0, pos_size) (sheep_positions /
+ * sheep_sequence_from_degrees; pos[seq[j]] = j, SHEEP_INVALID_ID elsewhere): the parts
+ * reach their vid slots by one streaming gather over pos instead of a scattered 2-B store
+ * per jnid.  Same results as sheep_partition for the same sequence. */
+int sheep_partition_pos(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n,
+                        const uint32_t *seq_dev, uint64_t seq_n, const uint32_t *pos_dev, uint64_t pos_size,
+                        sheep_kids *kids, int16_t k, double balance, int vtx_weight, int pst_weight,
+                        int16_t *parts_vid_dev, sheep_partition_info *info);
 
 /* ---- evaluators: both partition.cpp evaluators over one graph (all records) -------
  * what: bitmask SHEEP_EVAL_GRAPH (edges cut, Vcom vol, vertex balance, ECV(hash) +

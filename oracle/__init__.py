@@ -10,7 +10,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libsheep_oracle.so")
+# SHEEP_ORACLE_LIB: another build of the same restatement (`make asan`: AddressSanitizer +
+# UBSan, oracle/lib/asan/)
+LIB_PATH = os.environ.get("SHEEP_ORACLE_LIB") or os.path.join(_HERE, "lib", "libsheep_oracle.so")
 INVALID = 0xFFFFFFFF
 _lib = None
 

@@ -129,6 +129,7 @@ def lib() -> ctypes.CDLL:
         "sheep_kids_create": ([P, P, U64, ctypes.POINTER(P)], I32),
         "sheep_kids_destroy": ([P], I32),
         "sheep_partition": ([P, P, U64, P, U64, U64, P, I16, D, I32, I32, P, ctypes.POINTER(_PartInfo)], I32),
+        "sheep_partition_pos": ([P, P, U64, P, U64, P, U64, P, I16, D, I32, I32, P, ctypes.POINTER(_PartInfo)], I32),
         "sheep_evaluate": ([P, P, U64, P, U64, P, I32, ctypes.POINTER(_Eval)], I32),
         "sheep_facts": ([P, P, U64, ctypes.POINTER(_Facts)], I32),
         "sheep_eval_sizes": ([I32, I32, U64, ctypes.POINTER(U64), ctypes.POINTER(U64)], I32),
@@ -452,17 +453,25 @@ class PartitionResult:
 
 
 def partition(seq: Sequence, tree, k: int, balance: float = 1.03, vtx_weight: bool = False,
-              pst_weight: bool = True, kids: KidTable | None = None, ctx: Context | None = None) -> PartitionResult:
-    """Partition(seq, jnodes, k, balance, vtx, pst, pre=false) + forwardPartition."""
+              pst_weight: bool = True, kids: KidTable | None = None, ctx: Context | None = None,
+              use_pos: bool = True) -> PartitionResult:
+    """Partition(seq, jnodes, k, balance, vtx, pst, pre=false) + forwardPartition.
+    use_pos: the parts reach their vid slots through the sequence's index (sheep_partition_pos);
+    False: by the per-jnid scatter of sheep_partition (the same result)."""
     ctx = ctx or default_context()
     t = _torch()
     kids = kids or KidTable(tree, ctx)
     pos_size = seq.pos_size
     parts = t.empty(max(pos_size, 1), dtype=t.int16, device=_dev(ctx))
     info = _PartInfo()
-    _check(lib().sheep_partition(ctx.handle, _ptr(tree), tree.shape[0], _ptr(seq.seq), seq.n, pos_size, kids.handle,
-                                 int(k), float(balance), int(vtx_weight), int(pst_weight), _ptr(parts),
-                                 ctypes.byref(info)))
+    if use_pos:
+        _check(lib().sheep_partition_pos(ctx.handle, _ptr(tree), tree.shape[0], _ptr(seq.seq), seq.n, _ptr(seq.pos),
+                                         pos_size, kids.handle, int(k), float(balance), int(vtx_weight),
+                                         int(pst_weight), _ptr(parts), ctypes.byref(info)))
+    else:
+        _check(lib().sheep_partition(ctx.handle, _ptr(tree), tree.shape[0], _ptr(seq.seq), seq.n, pos_size,
+                                     kids.handle, int(k), float(balance), int(vtx_weight), int(pst_weight),
+                                     _ptr(parts), ctypes.byref(info)))
     return PartitionResult(parts[:pos_size], int(k), info.created, info.first_size, info.second_size,
                            info.max_component, info.total_weight, info.packing_nodes, info.heavy_nodes)
 

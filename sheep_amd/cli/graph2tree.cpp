@@ -146,8 +146,8 @@ static int run_world(World &w, const char *graph_filename, bool use_mpi_sort, bo
       sheep_kids *kids = nullptr;
       check(sheep_kids_create(w.ctx(i), rk[i].tree.get(), n, &kids));
       sheep_partition_info inf{};
-      const int rc = sheep_partition(w.ctx(i), rk[i].tree.get(), n, rk[i].seq.get(), n, pos_size, kids,
-                                     (int16_t)partitions, 1.03, 0, 1, rk[i].parts.get(), &inf);
+      const int rc = sheep_partition_pos(w.ctx(i), rk[i].tree.get(), n, rk[i].seq.get(), n, rk[i].pos.get(), pos_size,
+                                         kids, (int16_t)partitions, 1.03, 0, 1, rk[i].parts.get(), &inf);
       sheep_kids_destroy(kids);
       check(rc);
       if (rk[i].rank == 0) info = inf;

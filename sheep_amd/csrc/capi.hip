@@ -33,7 +33,7 @@ void merge_trees_part(Ctx &c, const sheep_jnode *trees, uint32_t k, uint64_t n, 
                       sheep_jnode *out, uint64_t *v_lo, uint64_t *v_hi);
 void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t *seq, uint64_t seq_n, uint64_t pos_size,
                     sheep_kids *k, int16_t np, double balance, int vtx, int pstw, int16_t *parts_vid,
-                    sheep_partition_info *info);
+                    sheep_partition_info *info, const uint32_t *pos = nullptr);
 void evaluate(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
               const int16_t *parts, int what, sheep_eval *out);
 void eval_sizes(int what, int nparts, uint64_t pos_size, uint64_t *bits_words, uint64_t *acc_words);
@@ -377,6 +377,17 @@ int sheep_partition(sheep_ctx *ctx, const sheep_jnode *tree, uint64_t n, const u
   DeviceGuard dg(ctx);
   NEED(ctx && kids && info && (tree || !n) && (seq || !seq_n) && (parts_vid || !pos_size), "null argument");
   sheep::partition_tree(ctx->c, tree, n, seq, seq_n, pos_size, kids, k, balance, vtx_weight, pst_weight, parts_vid, info);
+  API_END
+}
+
+int sheep_partition_pos(sheep_ctx *ctx, const sheep_jnode *tree, uint64_t n, const uint32_t *seq, uint64_t seq_n,
+                        const uint32_t *pos, uint64_t pos_size, sheep_kids *kids, int16_t k, double balance, int vtx_weight,
+                        int pst_weight, int16_t *parts_vid, sheep_partition_info *info) {
+  API_BEGIN
+  DeviceGuard dg(ctx);
+  NEED(ctx && kids && info && (tree || !n) && (seq || !seq_n) && ((parts_vid && pos) || !pos_size), "null argument");
+  sheep::partition_tree(ctx->c, tree, n, seq, seq_n, pos_size, kids, k, balance, vtx_weight, pst_weight, parts_vid, info,
+                        pos);
   API_END
 }
 

@@ -196,6 +196,40 @@ __global__ void k_parts_to_vid(const uint32_t *__restrict__ seq, uint64_t seq_n,
   block_atomic_max(&cnt[2], mx);
 }
 
+// The same by a gather over the vid slots through pos (the sequence's inverse): pv is
+// written once, in order, INVALID_PART included, and the jnid-indexed parts (2 B per node,
+// L2-resident) are read at random instead of stored at random (the scatter above wrote
+// ~24 B per 2-B value: 805 MB for 66 MB at RMAT-26).  A slot whose jnid is >= seq_n (a
+// sequence shorter than the tree's index) is not converted, as above.
+__global__ void k_parts_from_pos(const uint32_t *__restrict__ pos, uint64_t pos_size, uint64_t seq_n,
+                                 const int16_t *__restrict__ parts, int16_t *__restrict__ pv,
+                                 unsigned long long *__restrict__ cnt) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK * 4;
+  uint64_t c0 = 0, c1 = 0, mx = 0;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * BLOCK * 4 + threadIdx.x; i0 < pos_size; i0 += stride) {
+    uint32_t j[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t v = i0 + (uint64_t)k * BLOCK;
+      j[k] = v < pos_size ? pos[v] : INVALID;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t v = i0 + (uint64_t)k * BLOCK;
+      if (v >= pos_size) continue;
+      const int16_t p = j[k] < seq_n ? parts[j[k]] : SHEEP_INVALID_PART;
+      pv[v] = p;
+      if (j[k] >= seq_n) continue;
+      c0 += p == 0;
+      c1 += p == 1;
+      mx = (uint64_t)(p + 1) > mx ? (uint64_t)(p + 1) : mx;
+    }
+  }
+  block_atomic_add(&cnt[0], c0);
+  block_atomic_add(&cnt[1], c1);
+  block_atomic_max(&cnt[2], mx);
+}
+
 // ---- raking: exact subtree sums of the light fringe -------------------------------
 // Round r finishes every node whose kids are all finished and whose accumulated weight
 // acc (own weight + finished kids' sums) is <= max_component: acc is then its subtree sum
@@ -712,12 +746,12 @@ void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);
 
 void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t *seq, uint64_t seq_n, uint64_t pos_size,
                     sheep_kids *k, int16_t np, double balance, int vtx, int pstw, int16_t *parts_vid,
-                    sheep_partition_info *info) {
+                    sheep_partition_info *info, const uint32_t *pos) {
   if (np <= 0) throw Error(SHEEP_ERR_ARG, "number of parts must be positive");
   if (!k || k->n != n) throw Error(SHEEP_ERR_ARG, "kid table does not belong to this tree");
   if (seq_n > n) throw Error(SHEEP_ERR_RANGE, "vector::_M_range_check: the sequence is longer than the tree (partition.cpp:65 parts.at)");
   *info = sheep_partition_info();
-  if (pos_size) {
+  if (pos_size && (!pos || n == 0)) {   // (the gather below writes every slot itself)
     hipLaunchKernelGGL(k_fill_i16, dim3(grid_for(pos_size)), dim3(BLOCK), 0, c.stream, parts_vid, pos_size,
                        SHEEP_INVALID_PART);
     LAUNCH_CHECK();
@@ -1128,7 +1162,11 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   }
   // 6. jnid -> vid (:62-66) and print counts (partition.h:138-139)
   unsigned long long *cnt = (unsigned long long *)c.d_scalars + 37;
-  if (seq_n) {
+  if (pos && pos_size) {
+    hipLaunchKernelGGL(k_parts_from_pos, dim3(grid_for(pos_size, BLOCK * 4)), dim3(BLOCK), 0, c.stream, pos, pos_size,
+                       seq_n, (const int16_t *)parts, parts_vid, cnt);
+    LAUNCH_CHECK();
+  } else if (seq_n) {
     hipLaunchKernelGGL(k_parts_to_vid, dim3(grid_for(seq_n)), dim3(BLOCK), 0, c.stream, seq, seq_n, parts, parts_vid, cnt);
     LAUNCH_CHECK();
   }

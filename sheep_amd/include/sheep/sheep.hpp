@@ -493,8 +493,8 @@ class Partition {
       : num_parts_(np) {
     if (pre_weight) throw std::invalid_argument("pre_weight (-u) is outside this build's scope");
     parts_ = DeviceArray<int16_t>(seq.pos_size);
-    check(sheep_partition(ctx(), jnodes.device(), jnodes.size(), seq.seq.get(), seq.n, seq.pos_size, jnodes.kids(), np,
-                          balance_factor, vtx_weight, pst_weight, parts_.get(), &info_));
+    check(sheep_partition_pos(ctx(), jnodes.device(), jnodes.size(), seq.seq.get(), seq.n, seq.pos.get(), seq.pos_size,
+                              jnodes.kids(), np, balance_factor, vtx_weight, pst_weight, parts_.get(), &info_));
   }
   const sheep_partition_info &info() const { return info_; }
   const int16_t *device() const { return parts_.get(); }

@@ -10,7 +10,7 @@ import pytest
 
 from conftest import GOLDEN, ROOT, check_print, golden_records, ks, manifest
 
-BIN = os.path.join(ROOT, "sheep_amd", "bin")
+BIN = os.environ.get("SHEEP_BIN_DIR") or os.path.join(ROOT, "sheep_amd", "bin")   # (make asan: sheep_amd/bin/asan)
 CLIS = ("graph2tree", "partition_tree", "merge_trees", "degree_sequence")
 TIMING = ("Loaded graph in:", "Sorted in:", "Mapped in:", "Reduced in:", "Loaded tree in:", "Partitioning took:",
           "Finished in:", "Built in:", "Loaded in:")

@@ -92,10 +92,12 @@ def test_partial_trees_and_merge(gpu_ctx, name):
     assert np.array_equal(p, gp) and np.array_equal(w, gw)
 
 
+@pytest.mark.parametrize("use_pos", [True, False])
 @pytest.mark.parametrize("name", GRAPHS)
-def test_partition_evaluate_facts(gpu_ctx, name):
+def test_partition_evaluate_facts(gpu_ctx, name, use_pos):
     """partition_tree -f -g SEQ TREE k1 k2 ...: one kid table for all k (the FFD sort
-    order persists across k), printed lines byte-exact."""
+    order persists across k), printed lines byte-exact; the parts reach their vid slots
+    through the sequence's index (sheep_partition_pos) or by the per-jnid scatter."""
     import sheep_amd
     rec = golden_records(name)
     s = sheep_amd.sequence_from_host(golden_seq(name))
@@ -106,7 +108,7 @@ def test_partition_evaluate_facts(gpu_ctx, name):
     kids = sheep_amd.KidTable(tree)
     d = _dev_records(rec)
     for k, block in zip(ks(name), blocks):
-        res = sheep_amd.partition(s, tree, k, kids=kids)
+        res = sheep_amd.partition(s, tree, k, kids=kids, use_pos=use_pos)
         assert np.array_equal(res.numpy(), golden_parts(name, k)), f"k={k}"
         ev = sheep_amd.evaluate(d, s, res.parts)
         assert res.print_text() + ev.text(k) == block, f"k={k}"
@@ -392,7 +394,8 @@ def test_evaluate_wide_parts(gpu_ctx):
     assert sheep_amd.evaluate(d, s, res.parts).__dict__ == oracle.evaluate(h[:, 0], h[:, 1], s.numpy(), res.numpy())
 
 
-def test_partition_sequence_length(gpu_ctx):
+@pytest.mark.parametrize("use_pos", [True, False])
+def test_partition_sequence_length(gpu_ctx, use_pos):
     """Partition(seq, jnodes, k) (partition.cpp:62-66): a sequence longer than the tree is
     the reference's parts.at() throw; a shorter one converts only its own entries, and
     the printed counts come from the vid-indexed vector (partition.h:135-143)."""
@@ -402,9 +405,9 @@ def test_partition_sequence_length(gpu_ctx):
     tree = sheep_amd.tree_to_device(p, w)
     longer = sheep_amd.sequence_from_host(np.append(seq, np.uint32(seq.max() + 1)))
     with pytest.raises(IndexError):
-        sheep_amd.partition(longer, tree, 4)
+        sheep_amd.partition(longer, tree, 4, use_pos=use_pos)
     short = seq[:-100]
-    res = sheep_amd.partition(sheep_amd.sequence_from_host(short), tree, 4)
+    res = sheep_amd.partition(sheep_amd.sequence_from_host(short), tree, 4, use_pos=use_pos)
     oparts, oinfo = oracle.partition(p, w, short, 4)
     assert np.array_equal(res.numpy(), oparts)
     assert res.created == oinfo["created"]

@@ -24,6 +24,9 @@ def main():
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     K = int(sys.argv[3]) if len(sys.argv) > 3 else 8
     ctx = sheep_amd.Context(0)
+    tune = dict(kv.split("=") for kv in os.environ.get("SHEEP_TUNE", "").split())
+    if tune:
+        ctx.set_tuning(**{k: int(v) for k, v in tune.items()})
     rec = sheep_amd.rmat(scale, 16, scale, ctx=ctx)
     s = sheep_amd.degree_sequence(rec, ctx=ctx)
     R = rec.shape[0]
@@ -41,8 +44,9 @@ def main():
     for _ in range(reps):
         _, ms = timed(lambda: sheep_amd.build_tree(rec[:R // K], s, ctx=ctx))
         maps.append(ms)
-    stacked = torch.stack([sheep_amd.build_tree(rec[i * R // K:(i + 1) * R // K], s, ctx=ctx) for i in range(K)])
-    whole = sheep_amd.build_tree(rec, s, ctx=ctx)
+    stacked = torch.stack([timed(lambda i=i: sheep_amd.build_tree(rec[i * R // K:(i + 1) * R // K], s, ctx=ctx))[0]
+                           for i in range(K)])
+    whole, _ = timed(lambda: sheep_amd.build_tree(rec, s, ctx=ctx))
     del rec
     merges = []
     for _ in range(reps):
