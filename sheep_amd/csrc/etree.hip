@@ -470,7 +470,8 @@ __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict
 // 1.16 ms; from level 2 on the light components have merged, fewer roots fall inside the
 // window and the coarse chunks leave CUs idle: 1.60 -> 1.74 ms, later levels ~1.5x slower).
 // A 2^14 window: 1.07 / 1.58 ms.
-constexpr int XW_BITS = 15, XWB = 1024, XW_ITEMS = 8, XW_LEVELS = 2;
+// (sheep_tuning cross_win_levels: how many levels, default 2)
+constexpr int XW_BITS = 15, XWB = 1024, XW_ITEMS = 8;
 constexpr uint32_t XW = 1u << XW_BITS;
 constexpr uint64_t XW_STEP = (uint64_t)XWB * XW_ITEMS, XW_CH = XW_STEP * 8;
 __global__ __launch_bounds__(XWB) void k_cross_find_win(const uint64_t *__restrict__ xbuf, const uint64_t *__restrict__ n_x,
@@ -2007,6 +2008,10 @@ static uint32_t top_blocks(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t 
       c.sync();
       bool any = false;
       for (uint32_t b = 0; b < nb; ++b) any |= h[4 * b + 2] == 0;
+      if (g_debug_etree)
+        for (uint32_t b = 0; b < nb; ++b)
+          fprintf(stderr, "etree top round %d block %u: components %u done %u (minima %s)\n", r, b, h[4 * b],
+                  h[4 * b + 2], h[4 * b] <= (TOP_ROUND_LDS - ((set.s[b].V + 3) & ~3u) * 2) / 8 ? "lds" : "hbm");
       if (!any) break;
     }
     hipLaunchKernelGGL(k_top_round, dim3(TOP_WG, nb), dim3(TOPB), ldsr, c.stream, set, (const uint64_t *)st);
@@ -2211,7 +2216,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     }
     {
       TimedRegion tr(c, "etree_cross");
-      if (lvl < XW_LEVELS)
+      if (lvl < c.tune.cross_win_levels)
         hipLaunchKernelGGL(k_cross_find_win, dim3(grid_for(mcap, XW_STEP, 1024)), dim3(XWB),
                            (XW + XWB / WAVE) * 4, c.stream, (const uint64_t *)xbuf, (const uint64_t *)(st + ST_NX), uf,
                            mt, xtop, g);

@@ -668,10 +668,11 @@ __global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restr
     uint32_t pt[PER], hd[PER], rk[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {   // all record loads, then all pos[tail] loads in flight
-      const uint64_t i = base + s0 + (uint64_t)j * NT + threadIdx.x;
+      const uint32_t in_tile = s0 + (uint32_t)j * NT + threadIdx.x;   // (SUB need not divide the tile)
+      const uint64_t i = base + in_tile;
       hd[j] = INVALID;
       pt[j] = INVALID;
-      if (i < n) {
+      if (i < n && in_tile < TKEYS) {
         const uint32_t t = rec[i].tail, h = rec[i].head;
         if (t != h) { hd[j] = h; pt[j] = t; }
       }
@@ -876,6 +877,7 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   if (nrec == 0 || nb == 0 || nb > 8192 || nrec >= (1ull << 32) || ntiles * nb + 1 >= (1ull << 32)) return UINT64_MAX;
   for (const void *f : {(const void *)k_relabel_scatter<8>, (const void *)k_relabel_scatter<4>,
                         (const void *)k_relabel_scatter<8, 512>, (const void *)k_relabel_scatter<8, 512, true>,
+                        (const void *)k_relabel_scatter<12, 512, true>, (const void *)k_relabel_scatter<15, 512, true>,
                         (const void *)k_relabel_gather<false>, (const void *)k_relabel_gather<true>})
     allow_full_lds(f);
   Ctx::HeadLayout &hl = c.head_layout;
@@ -910,17 +912,25 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
     // workgroup alone on its CU, idle at every barrier): RMAT-26 9.18 -> 8.92 ms.  Up to
     // 4096 buckets (vertex ids below 2^27), the scan's limit for 512 threads.
     {
-      constexpr int NT = 512, P = 8;
-      const size_t fx = ((2 * nb + NT / WAVE + 1) & ~1ull) * 4, lds = fx + (size_t)P * NT * 8;
+      constexpr int NT = 512;
       // the staged pairs as two u32 planes (RMAT-26 relabel 13.56 / 13.85 ms against 14.56 /
-      // 13.80 with one u64 array, two runs each: within box noise, not worse)
+      // 13.80 with one u64 array, two runs each: within box noise, not worse); relabel_per
+      // records per thread per sub-tile (longer runs per bucket region, fewer flushes)
       const bool planes = c.tune.relabel_planes != 0;
+      const int P = planes ? c.tune.relabel_per : 8;
+      const size_t fx = ((2 * nb + NT / WAVE + 1) & ~1ull) * 4, lds = fx + (size_t)P * NT * 8;
       if (nb <= 8 * (uint64_t)NT && lds <= 160 * 1024) {
-        if (planes)
-          hipLaunchKernelGGL((k_relabel_scatter<P, NT, true>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec, nrec,
-                             pos, pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
+        if (planes && P == 15)
+          hipLaunchKernelGGL((k_relabel_scatter<15, NT, true>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec,
+                             nrec, pos, pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
+        else if (planes && P == 12)
+          hipLaunchKernelGGL((k_relabel_scatter<12, NT, true>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec,
+                             nrec, pos, pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
+        else if (planes)
+          hipLaunchKernelGGL((k_relabel_scatter<8, NT, true>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec,
+                             nrec, pos, pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
         else
-          hipLaunchKernelGGL((k_relabel_scatter<P, NT>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec, nrec, pos,
+          hipLaunchKernelGGL((k_relabel_scatter<8, NT>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec, nrec, pos,
                              pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
         LAUNCH_CHECK();
         HIP_CHECK(hipMemcpyAsync(c.h_scalars + 12, flags, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));

@@ -7,8 +7,8 @@ HB=$!
 trap 'kill $HB' EXIT
 O=gpurun_out/r4res
 B="python -u bench.py --no-cpu-baseline --steps 10 --warmup 2 --eval-reps 0"
-SHEEP_FIN_MERGE=13 timeout -k 10 200 $B --shards 8 > $O/ab_s8_merge13.json 2> $O/ab_s8_merge13.err || exit 1
-SHEEP_FIN_MAP=12 timeout -k 10 200 $B --scale 22 --k 16 --steps 20 > $O/ab_b22_fin12.json 2> $O/ab_b22_fin12.err || exit 1
+timeout -k 10 200 $B --shards 8 --tune fin_merge_bits=13 > $O/ab_s8_merge13.json 2> $O/ab_s8_merge13.err || exit 1
+timeout -k 10 200 $B --scale 22 --k 16 --steps 20 --tune fin_map_bits=12 > $O/ab_b22_fin12.json 2> $O/ab_b22_fin12.err || exit 1
 timeout -k 10 400 python -u bench.py --shuffle --steps 5 --no-cpu-baseline > $O/bench_rmat26_k64_shuffled.json 2> $O/shuf.err || exit 1
 timeout -k 10 500 python -u bench.py --graph powerlaw --k 128 --steps 3 --no-cpu-baseline > $O/bench_c4_powerlaw_k128.json 2> $O/c4.err || exit 1
 timeout -k 10 600 python -u bench.py --scale 28 --k 256 --shards 8 --steps 2 --warmup 1 --no-cpu-baseline --eval-reps 1 \
