@@ -197,6 +197,7 @@ def main():
     if tune:
         (group or ctx).set_tuning(**tune)
     rec, vs_cap, workload = make_records(a, seed, ctx)          # whole graph, identical on every rank
+    ctx.trim()                                                  # the generator's sort buffers are not the path's
     if a.shards > 1:
         workload += f", {a.shards} shards on 1 GPU"
     R = rec.shape[0]
@@ -358,6 +359,7 @@ def main():
             "evaluator": evaluator,
             "phases": phases,
             "hbm_peak_bytes": hbm_used,
+            "hbm_workspace_top": dict(list(ctx.workspace().items())[:12]),
             "hbm_peak_note": "device memory in use after the timed steps (hipMemGetInfo: total - free); the "
                              "library's workspaces only grow, so this is the step's high-water mark",
         }

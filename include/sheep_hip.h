@@ -109,6 +109,9 @@ int sheep_ctx_destroy(sheep_ctx *ctx);
  * sized by the largest graph seen, and the spare kid-table buffers); the next call
  * allocates again.  Synchronises the context's stream. */
 int sheep_ctx_trim(sheep_ctx *ctx);
+/* The context's device workspaces as "name=bytes" pairs, comma-separated, largest first,
+ * into buf[cap] (what sheep_ctx_trim would free; for memory reports). */
+int sheep_ctx_workspace(sheep_ctx *ctx, char *buf, size_t cap);
 int sheep_ctx_sync(sheep_ctx *ctx);
 void *sheep_ctx_stream(sheep_ctx *ctx);
 int sheep_malloc(sheep_ctx *ctx, size_t bytes, void **dev_out);

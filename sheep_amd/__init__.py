@@ -105,6 +105,7 @@ def lib() -> ctypes.CDLL:
         "sheep_ctx_create": ([I32, P, ctypes.POINTER(P)], I32),
         "sheep_ctx_destroy": ([P], I32),
         "sheep_ctx_trim": ([P], I32),
+        "sheep_ctx_workspace": ([P, ctypes.c_char_p, ctypes.c_size_t], I32),
         "sheep_ctx_sync": ([P], I32),
         "sheep_ctx_stream": ([P], P),
         "sheep_malloc": ([P, ctypes.c_size_t, ctypes.POINTER(P)], I32),
@@ -210,6 +211,12 @@ class Context:
     def trim(self):
         """Free the context's device workspace (sheep_ctx_trim)."""
         _check(lib().sheep_ctx_trim(self.handle))
+
+    def workspace(self) -> dict:
+        """The device workspaces the context holds, name -> bytes (largest first)."""
+        buf = ctypes.create_string_buffer(1 << 16)
+        _check(lib().sheep_ctx_workspace(self.handle, buf, 1 << 16))
+        return {k: int(v) for k, v in (x.split("=") for x in buf.value.decode().split(",") if x)}
 
     # device-side kernel timers (HIP events on the context stream)
     def timing(self, on: bool = True):

@@ -1,6 +1,7 @@
 // capi.hip — the extern "C" boundary of libsheep_hip.so (declared in include/sheep_hip.h).
 // Exceptions never cross it: every entry point maps sheep::Error / std::exception to a
 // status code and a thread-local message.
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <string>
@@ -222,6 +223,19 @@ int sheep_timer_names(sheep_ctx *ctx, char *buf, size_t cap) {
   NEED(ctx && buf && cap, "null argument");
   std::string s;
   for (auto &kv : ctx->c.timers) { if (!s.empty()) s += ','; s += kv.first; }
+  NEED(s.size() < cap, "buffer too small");
+  memcpy(buf, s.c_str(), s.size() + 1);
+  API_END
+}
+
+int sheep_ctx_workspace(sheep_ctx *ctx, char *buf, size_t cap) {
+  API_BEGIN
+  NEED(ctx && buf && cap, "null argument");
+  std::vector<std::pair<size_t, std::string>> v;
+  for (auto &kv : ctx->c.ws) if (kv.second.p) v.push_back({kv.second.bytes, kv.first});
+  std::sort(v.begin(), v.end(), [](const auto &a, const auto &b) { return a.first > b.first; });
+  std::string s;
+  for (auto &x : v) s += (s.empty() ? "" : ",") + x.second + "=" + std::to_string(x.first);
   NEED(s.size() < cap, "buffer too small");
   memcpy(buf, s.c_str(), s.size() + 1);
   API_END

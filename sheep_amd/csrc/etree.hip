@@ -1889,9 +1889,11 @@ void spread_params(uint64_t n, int *L_out, uint32_t *clo_out) {
   *clo_out = (uint32_t)(cfull - (((unsigned __int128)1) << 32));
 }
 
-// A level's next list holds the entries that stayed (alive, <= m) plus the surviving
-// contractions (<= one per cross edge, <= m).
-static uint64_t list_capacity(uint64_t m) { return 2 * m + TILE; }
+// A level's next list holds the entries that stayed plus the surviving contractions: each
+// entry of the level's input (list + activated group) yields at most one of them (it stays,
+// or it is cross and contracts, or it dies), so a list never holds more than the groups
+// activated so far, m, plus the MSF edges of cut blocks (<= n: at most one per vertex).
+static uint64_t list_capacity(uint64_t m, uint64_t n) { return m + n + 2 * (uint64_t)TILE; }
 
 // Elimination tree of `m` edges ((hi<<32)|lo, lo < hi < n, DEAD holes allowed), grouped
 // by first active level: seg[s] / seg[L + s] (device) delimit group s.  The edges are
@@ -2105,7 +2107,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   uint32_t *claim = c.get_as<uint32_t>("et_claim", n);
   // every list is bounded by m; scratch regions of sharded appends need whole tiles
   const uint64_t mcap = (m + TILE - 1) / TILE * TILE;
-  const uint64_t lcap = list_capacity(m);
+  const uint64_t lcap = list_capacity(m, n);
   uint32_t *xtop = c.get_as<uint32_t>("et_xtop", mcap);
   uint64_t *xbuf = c.get_as<uint64_t>("et_cross", mcap);
   // the two list buffers (level l reads one and writes the other) and the bucketed input r0
@@ -2302,13 +2304,16 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     // Liu's algorithm per 2^B-position block
     TimedRegion tr(c, "etree_finish");
     const int sg = (L < FINB ? L : FINB) - 1;   // highest group left
-    uint64_t hseg[2];
+    uint64_t hseg[2], hrow[ST_ROW] = {};
+    const uint64_t *prev = nglobal ? stats + (uint64_t)(nglobal - 1) * ST_ROW : nullptr;
     HIP_CHECK(hipMemcpyAsync(&hseg[0], seg + sg, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
     HIP_CHECK(hipMemcpyAsync(&hseg[1], seg + L, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+    if (prev) HIP_CHECK(hipMemcpyAsync(hrow, prev, sizeof hrow, hipMemcpyDeviceToHost, c.stream));
     c.sync();
     if (gcut > sg) hseg[0] = hseg[1];   // the top block's groups were replaced by its MSF
-    const uint64_t *prev = nglobal ? stats + (uint64_t)(nglobal - 1) * ST_ROW : nullptr;
-    const uint64_t cap = lcap + (hseg[1] - hseg[0]);
+    // the finish's input exactly: the last level's list plus the groups left (sized by the
+    // list's worst case, these three buffers took ~48 GB at RMAT-26)
+    const uint64_t cap = hrow[ST_KEPT] + hrow[ST_CONTR] + hrow[ST_EXTRA] + (hseg[1] - hseg[0]) + 1;
     uint64_t *fin = c.get_as<uint64_t>("et_fin", cap), *fin_alt = c.get_as<uint64_t>("et_fin_alt", cap);
     uint64_t *n_fin = stats + (uint64_t)L * ST_ROW;
     hipLaunchKernelGGL(k_fin_gather, dim3(grid_for(cap)), dim3(BLOCK), 0, c.stream, (const uint64_t *)lists[nglobal & 1],
@@ -2415,7 +2420,9 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   uint32_t *pst = c.get_as<uint32_t>("bt_pst", n ? n : 1);
   uint32_t *parent = c.get_as<uint32_t>("bt_parent", n ? n : 1);
   HIP_CHECK(hipMemsetAsync(pst, 0, n * sizeof(uint32_t), c.stream));
-  uint64_t *edges = c.get_as<uint64_t>("bt_edges", nrec ? nrec : 1);
+  // the relabelled edges die with the grouping below: their workspace is the elimination
+  // tree's second list buffer (et_list2), filled only by the levels
+  uint64_t *edges = c.get_as<uint64_t>("et_list2", nrec ? nrec : 1);
   unsigned long long *d = (unsigned long long *)c.d_scalars + 8;
   HIP_CHECK(hipMemsetAsync(d + 1, 0, sizeof(uint64_t), c.stream));
   uint64_t m = nrec;   // edges[i] per record, DEAD holes included (k_relabel)

@@ -904,7 +904,9 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   const bool cached = hl.valid && hl.rec == rec && hl.nrec == nrec && hl.K == pos_size && hl.bstart.size() == nb + 1;
   uint32_t *off = cached ? c.get_as<uint32_t>("head_offsets", ntiles * nb + 1) : recount();
   const uint64_t total = hl.bstart[nb];
-  uint64_t *pairs = c.get_as<uint64_t>("rl_pairs", total ? total : 1);
+  // (the pairs die with the gather: their workspace is the elimination tree's first list
+  // buffer, et_list1, which the levels fill only after the relabel)
+  uint64_t *pairs = c.get_as<uint64_t>("et_list1", total ? total : 1);
   const size_t fixed = ((2 * nb + HB / WAVE + 1) & ~1ull) * 4;
   auto scatter = [&]() {
     HIP_CHECK(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned long long), c.stream));
@@ -1001,7 +1003,7 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
     HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned long long), c.stream));
     if (n_tree) HIP_CHECK(hipMemsetAsync(pst, 0, n_tree * sizeof(uint32_t), c.stream));
     off = recount();
-    if (hl.bstart[nb] > total) pairs = c.get_as<uint64_t>("rl_pairs", hl.bstart[nb]);
+    if (hl.bstart[nb] > total) pairs = c.get_as<uint64_t>("et_list1", hl.bstart[nb]);
     scatter();
     count = gather();
     c.sync();
