@@ -266,8 +266,9 @@ static sheep_tuning resolve_tuning(const sheep_tuning *t) {
   SHEEP_TUNE(big_hot_bits, r.big_hot_bits >= 10 && r.big_hot_bits <= 15)
   SHEEP_TUNE(big_hot16, r.big_hot16 == 0 || r.big_hot16 == 1)
   SHEEP_TUNE(relabel_planes, r.relabel_planes == 0 || r.relabel_planes == 1)
-  SHEEP_TUNE(relabel_per, r.relabel_per == 8 || r.relabel_per == 12 || r.relabel_per == 15)
+  SHEEP_TUNE(relabel_per, r.relabel_per == 4 || r.relabel_per == 8 || r.relabel_per == 12 || r.relabel_per == 15)
   SHEEP_TUNE(cross_win_levels, r.cross_win_levels >= 0 && r.cross_win_levels <= 8)
+  SHEEP_TUNE(hook_batch, r.hook_batch >= 0 && r.hook_batch <= 2)
 #undef SHEEP_TUNE
   return r;
 }

@@ -92,6 +92,7 @@ inline sheep_tuning default_tuning() {
   t.relabel_planes = 1;
   t.relabel_per = 8;
   t.cross_win_levels = 2;   // RMAT-26: level 0/1 1.30/2.46 -> 0.77/1.16 ms; level 2 1.60 -> 1.74 ms
+  t.hook_batch = 0;
   return t;
 }
 
@@ -430,8 +431,11 @@ void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGroup 
 // subproblem of a split merge; the caller cuts the later groups to it).  top_bits > 0: the
 // block of the 2^top_bits highest positions is replaced by its minimum spanning forest when
 // dense (maps; etree.hip "the dense top block").
+// hook_batch: the hook rounds find all of a thread's edges' roots at once (merges: chains
+// of tree edges, little contention) instead of one edge after another (maps: hub pile-ups).
 void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
-                      int fin_bits, int filt_lvl = -1, uint32_t ylo = 0, uint32_t yhi = 0, int top_bits = 0);
+                      int fin_bits, int filt_lvl = -1, uint32_t ylo = 0, uint32_t yhi = 0, int top_bits = 0,
+                      bool hook_batch = false);
 void spread_params(uint64_t n, int *L, uint32_t *clo);
 // append.hip — sharded appends: counters (NSHARD * SHARD_STRIDE u64, zeroed).  The pack
 // step moves the shard regions of a producer that streamed *n_in items together in dst

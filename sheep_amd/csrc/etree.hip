@@ -345,6 +345,14 @@ __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict_
 // another round trip); rounds instead resolve such a pile-up in a few passes.
 // (Batched finds of all the thread's edges before any hook left more hooks to later
 // rounds: 21-22 ms against 10.8 ms at RMAT-26.)
+// BATCH (sheep_tuning hook_batch): the roots of all the thread's edges are found at once
+// (2 x TILE_ITEMS chains in flight, find_many) and then hooked.  A root found this way may
+// be stale by its turn — hook() then fails on the hi side and the edge goes to the next
+// round, or links hi under a lo that is no longer a root, which joins the same tree — so
+// the result is the same; it pays where the edges are chains (merges: one dependent load
+// after another, little contention) and not where a forming hub component takes every
+// hook (maps: more stale roots, more rounds).
+template <bool BATCH>
 __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict__ in, const uint64_t *__restrict__ n_in,
                                                       uint32_t *uf, Tg g, uint64_t *__restrict__ out,
                                                       unsigned long long *__restrict__ counter) {
@@ -358,14 +366,34 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
       const uint64_t i = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
       ev[j] = i < nin ? in[i] : DEAD;
     }
+    if (BATCH) {
+      uint32_t r[2 * TILE_ITEMS];
+      bool v[2 * TILE_ITEMS];
 #pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) {
-      if (ev[j] == DEAD) continue;
-      uint32_t a = (uint32_t)ev[j], b = (uint32_t)(ev[j] >> 32);
-      find2(uf, g, a, b);
-      if (a == b) continue;
-      const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-      if (!hook(uf, g, hi, lo)) keep |= 1u << j;
+      for (int j = 0; j < TILE_ITEMS; ++j) {
+        v[2 * j] = v[2 * j + 1] = ev[j] != DEAD;
+        r[2 * j] = ev[j] != DEAD ? (uint32_t)ev[j] : 0;
+        r[2 * j + 1] = ev[j] != DEAD ? (uint32_t)(ev[j] >> 32) : 0;
+      }
+      find_many<2 * TILE_ITEMS>(uf, g, r, v);
+#pragma unroll
+      for (int j = 0; j < TILE_ITEMS; ++j) {
+        if (ev[j] == DEAD) continue;
+        uint32_t a = r[2 * j], b = r[2 * j + 1];
+        if (a == b) continue;
+        const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+        if (!hook(uf, g, hi, lo)) keep |= 1u << j;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < TILE_ITEMS; ++j) {
+        if (ev[j] == DEAD) continue;
+        uint32_t a = (uint32_t)ev[j], b = (uint32_t)(ev[j] >> 32);
+        find2(uf, g, a, b);
+        if (a == b) continue;
+        const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+        if (!hook(uf, g, hi, lo)) keep |= 1u << j;
+      }
     }
     uint64_t slot = shard_reserve((uint32_t)__popc(keep), counter, tile, ntiles, 1);
 #pragma unroll
@@ -2093,7 +2121,7 @@ static bool big_cut(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, ui
 }
 
 void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
-                      int fin_bits, int filt_lvl, uint32_t ylo, uint32_t yhi, int top_bits) {
+                      int fin_bits, int filt_lvl, uint32_t ylo, uint32_t yhi, int top_bits, bool hook_batch) {
   fill_u32(c, parent, n, INVALID);
   if (n < 2 || m == 0) return;
   if (m >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "too many edges for one shard");
@@ -2206,8 +2234,8 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     {
       TimedRegion tr(c, "etree_union");
       static_assert(HOOK_ROUNDS == 1, "k_hook_finish reads the one round's shard regions");
-      hipLaunchKernelGGL(k_hook_round, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
-                         (const uint64_t *)(st + ST_NL), uf, g, alt, cset(CSET_HOOK));
+      hipLaunchKernelGGL(hook_batch ? k_hook_round<true> : k_hook_round<false>, dim3(gt), dim3(BLOCK), 0, c.stream,
+                         (const uint64_t *)lbuf, (const uint64_t *)(st + ST_NL), uf, g, alt, cset(CSET_HOOK));
       LAUNCH_CHECK();
       hipLaunchKernelGGL(k_hook_finish, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)alt,
                          (const uint64_t *)(st + ST_NL), (const unsigned long long *)cset(CSET_HOOK), uf, g, st + ST_HOOK);
@@ -2458,7 +2486,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
       group_edges_by_lo(c, edges, m, lg, pst, r0, seg, counted);
     }
     TimedRegion tr(c, "etree", 8 * m);
-    etree_from_edges(c, r0, m, n, parent, seg, c.tune.fin_map_bits, -1, 0, 0, c.tune.top_bits);
+    etree_from_edges(c, r0, m, n, parent, seg, c.tune.fin_map_bits, -1, 0, 0, c.tune.top_bits, c.tune.hook_batch >= 2);
   } else {
     fill_u32(c, parent, n, INVALID);
   }
@@ -2583,7 +2611,7 @@ static void merge_set(Ctx &c, const TreeSet &ts, uint32_t K, uint64_t n, sheep_j
     TimedRegion tr(c, "merge", 8 * (uint64_t)K * n);   // the K trees
     // groups activated at levels >= l are b < L - l
     const uint64_t m = merge_edges(c, ts, K, n, pst, &edges, &seg, &L, l > 0 ? L - l : 0, lo, hi);
-    etree_from_edges(c, edges, m, n, parent, seg, fin_merge, l > 0 ? l : -1, ylo, yhi);
+    etree_from_edges(c, edges, m, n, parent, seg, fin_merge, l > 0 ? l : -1, ylo, yhi, 0, c.tune.hook_batch >= 1);
   }
   hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);
   LAUNCH_CHECK();

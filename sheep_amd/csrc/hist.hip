@@ -878,6 +878,7 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   for (const void *f : {(const void *)k_relabel_scatter<8>, (const void *)k_relabel_scatter<4>,
                         (const void *)k_relabel_scatter<8, 512>, (const void *)k_relabel_scatter<8, 512, true>,
                         (const void *)k_relabel_scatter<12, 512, true>, (const void *)k_relabel_scatter<15, 512, true>,
+                        (const void *)k_relabel_scatter<4, 512, true>,
                         (const void *)k_relabel_gather<false>, (const void *)k_relabel_gather<true>})
     allow_full_lds(f);
   Ctx::HeadLayout &hl = c.head_layout;
@@ -924,6 +925,9 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
       if (nb <= 8 * (uint64_t)NT && lds <= 160 * 1024) {
         if (planes && P == 15)
           hipLaunchKernelGGL((k_relabel_scatter<15, NT, true>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec,
+                             nrec, pos, pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
+        else if (planes && P == 4)
+          hipLaunchKernelGGL((k_relabel_scatter<4, NT, true>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec,
                              nrec, pos, pos_size, (uint32_t)nb, (const uint32_t *)off, ntiles, pairs, flags);
         else if (planes && P == 12)
           hipLaunchKernelGGL((k_relabel_scatter<12, NT, true>), dim3((unsigned)ntiles), dim3(NT), lds, c.stream, rec,

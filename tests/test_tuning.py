@@ -71,6 +71,8 @@ CASES = {
         {"tune": {"relabel_per": 15}, "expect": []},
         {"tune": {"cross_win_levels": 0}, "merge": True, "expect": []},
         {"tune": {"cross_win_levels": 8}, "merge": True, "expect": []},
+        {"tune": {"hook_batch": 1}, "merge": True, "expect": []},
+        {"tune": {"hook_batch": 2}, "merge": True, "expect": []},
     ]),
     # four times denser: the blocks right below the top one pass the density rule too
     "rmat18ef64": (lambda: rmat_graph(18, 64, 18), [
