@@ -240,7 +240,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t *__restrict__ uf, uint
 // endpoints, cross roots and cross hi ends were written), else densely; the choice is
 // made on the device from the level's counts (no host round trip).
 struct LevelClean {   // what k_level_clean needs of the level it closes
-  const uint64_t *lbuf, *xbuf;
+  const uint64_t *lx;   // the level's light entries, then its cross entries (st[ST_NL] on)
   const uint32_t *xtop;
   const uint64_t *st;
   uint32_t *uf, *mt, *top, *claim;
@@ -251,7 +251,7 @@ struct LevelClean {   // what k_level_clean needs of the level it closes
   unsigned long long *csets;
 };
 __device__ void level_clean(const LevelClean &lc) {
-  const uint64_t *__restrict__ lbuf = lc.lbuf, *__restrict__ xbuf = lc.xbuf;
+  const uint64_t *__restrict__ lbuf = lc.lx, *__restrict__ xbuf = lc.lx + lc.st[ST_NL];
   const uint32_t *__restrict__ xtop = lc.xtop;
   uint32_t *__restrict__ uf = lc.uf, *__restrict__ mt = lc.mt, *__restrict__ top = lc.top, *__restrict__ claim = lc.claim;
   uint32_t *__restrict__ parent = lc.parent;
@@ -446,10 +446,11 @@ __global__ __launch_bounds__(BLOCK) void k_hook_finish(const uint64_t *__restric
 }
 
 // For every cross edge (a,b): r = root of a's light component; m_r = min b (atomicMin).
-__global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict__ xbuf, const uint64_t *__restrict__ n_x,
+__global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict__ lx, const uint64_t *__restrict__ st,
                                                       uint32_t *uf, uint32_t *__restrict__ mt, uint32_t *__restrict__ xtop,
                                                       Tg g) {
-  const uint64_t nx = *n_x;
+  const uint64_t nx = st[ST_NX];
+  const uint64_t *__restrict__ xbuf = lx + st[ST_NL];   // the cross entries follow the light ones
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK * XK;
   const uint64_t iters = (nx + stride - 1) / stride;
   uint64_t base = (uint64_t)blockIdx.x * BLOCK * XK + threadIdx.x;
@@ -502,12 +503,13 @@ __global__ __launch_bounds__(BLOCK) void k_cross_find(const uint64_t *__restrict
 constexpr int XW_BITS = 15, XWB = 1024, XW_ITEMS = 8;
 constexpr uint32_t XW = 1u << XW_BITS;
 constexpr uint64_t XW_STEP = (uint64_t)XWB * XW_ITEMS, XW_CH = XW_STEP * 8;
-__global__ __launch_bounds__(XWB) void k_cross_find_win(const uint64_t *__restrict__ xbuf, const uint64_t *__restrict__ n_x,
+__global__ __launch_bounds__(XWB) void k_cross_find_win(const uint64_t *__restrict__ lx, const uint64_t *__restrict__ st,
                                                         uint32_t *uf, uint32_t *__restrict__ mt,
                                                         uint32_t *__restrict__ xtop, Tg g) {
   extern __shared__ uint32_t lmin[];
   uint32_t *const s_red = lmin + XW;   // (dynamic only: allow_full_lds admits no static LDS)
-  const uint64_t nx = *n_x;
+  const uint64_t nx = st[ST_NX];
+  const uint64_t *__restrict__ xbuf = lx + st[ST_NL];
   // chunks of XW_STEP..XW_CH edges, so that even a short list spreads over the CUs
   // (RMAT-22's first levels: ~2M cross edges, 29 chunks of XW_CH)
   uint64_t ch = (nx / 1024 + XW_STEP - 1) / XW_STEP * XW_STEP;
@@ -588,13 +590,14 @@ __global__ __launch_bounds__(XWB) void k_cross_find_win(const uint64_t *__restri
 // kept entries, so the next level reads no dead slots (at RMAT-26 most contractions die
 // as duplicates: 80% of a level's list was dead slots).  Every gather stage is issued
 // for all of a thread's 8 edges before the next (xtop/xbuf, then mt, then claim).
-__global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restrict__ xbuf, const uint32_t *__restrict__ xtop,
+__global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restrict__ lx, const uint32_t *__restrict__ xtop,
                                                        const uint64_t *__restrict__ st, const uint32_t *__restrict__ mt,
                                                        const uint32_t *__restrict__ top, uint32_t *__restrict__ claim,
                                                        uint64_t *__restrict__ scratch,
                                                        unsigned long long *__restrict__ counters,
                                                        uint32_t *__restrict__ parent, Tg g) {
   const uint64_t nx = st[ST_NX];
+  const uint64_t *__restrict__ xbuf = lx + st[ST_NL];
   const uint64_t ntiles = (nx + TILE - 1) / TILE;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     uint32_t r[TILE_ITEMS], b[TILE_ITEMS], m[TILE_ITEMS], cl[TILE_ITEMS];
@@ -747,8 +750,7 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
                                                        uint64_t *__restrict__ st, int s, uint32_t clo, YRange yr,
                                                        const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
                                                        int L, int gcut, const uint64_t *__restrict__ cnt,
-                                                       uint64_t *__restrict__ next, uint64_t *__restrict__ lbuf,
-                                                       uint64_t *__restrict__ xbuf) {
+                                                       uint64_t *__restrict__ next, uint64_t *__restrict__ lx) {
   const SplitIn<CUT> in(list, prev, r0, seg, s, L, gcut, clo);
   const uint64_t ntiles = (in.m + SPLIT_TILE - 1) / SPLIT_TILE, cstride = ntiles;
   const uint64_t b0 = cnt[0], b1 = cnt[cstride], b2 = cnt[2 * cstride], b3 = cnt[3 * cstride];
@@ -785,7 +787,10 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
     __shared__ uint64_t stg[SPLIT_TILE];
     uint64_t tot = 0;
     for (int w = 0; w < BLOCK / WAVE; ++w) tot += s_w[w];
-    uint64_t *const outs[3] = {next, lbuf, xbuf};
+    // the stay run into `next`; the light and the cross runs into lx back to back: the one
+    // scan of the three rows already places cross after light (offsets from the light row's start)
+    uint64_t *const outs[3] = {next, lx, lx};
+    const uint64_t obase[3] = {b0, b1, b1};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       uint32_t r = (uint32_t)((ex >> (16 * k)) & 0xFFFF);
@@ -794,7 +799,7 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
         if ((cl[j] >> k) & 1) stg[r++] = ev[j];
       lds_barrier();
       const uint32_t n_k = (uint32_t)((tot >> (16 * k)) & 0xFFFF);
-      uint64_t *const o = outs[k] + (cnt[k * cstride + tile] - cnt[k * cstride]);
+      uint64_t *const o = outs[k] + (cnt[k * cstride + tile] - obase[k]);
       for (uint32_t i = threadIdx.x; i < n_k; i += BLOCK) o[i] = stg[i];
       lds_barrier();   // stg (and, after the last class, s_w) is rewritten next
     }
@@ -2137,11 +2142,13 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   const uint64_t mcap = (m + TILE - 1) / TILE * TILE;
   const uint64_t lcap = list_capacity(m, n);
   uint32_t *xtop = c.get_as<uint32_t>("et_xtop", mcap);
-  uint64_t *xbuf = c.get_as<uint64_t>("et_cross", mcap);
+  // a level's light entries and then its cross entries, back to back (light + cross <= the
+  // level's input, <= the list bound)
+  uint64_t *lx = c.get_as<uint64_t>("et_lx", lcap);
   // the two list buffers (level l reads one and writes the other) and the bucketed input r0
   uint64_t *lists[2] = {c.get_as<uint64_t>("et_list1", lcap), c.get_as<uint64_t>("et_list2", lcap)};
   const uint64_t *r0 = edges;
-  uint64_t *lbuf = c.get_as<uint64_t>("et_light", mcap);  // must outlive the level (its clean, next level)
+  // (lx must outlive the level: its clean runs at the next level's split)
   uint64_t *alt = c.get_as<uint64_t>("et_alt", mcap);     // shard scratch of the hook round and the contractions
   unsigned long long *csets = c.get_as<unsigned long long>("et_csets", NCSET * CSET_WORDS);
   uint64_t *stats = c.get_as<uint64_t>("et_stats", (uint64_t)(L + 1) * ST_ROW);
@@ -2218,7 +2225,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     {
       TimedRegion tr(c, "etree_split");
       // the previous level's clean first (its counters, adoptions and resets)
-      const LevelClean clean = lvl ? LevelClean{lbuf, xbuf, xtop, prev, uf, mt, top, claim, n, tagged, lvl - 1, parent, csets}
+      const LevelClean clean = lvl ? LevelClean{lx, xtop, prev, uf, mt, top, claim, n, tagged, lvl - 1, parent, csets}
                                    : LevelClean{};
       const bool after_cut = cut_lvl >= 0 && lvl == cut_lvl + 1;
       hipLaunchKernelGGL(after_cut ? k_split_count<true> : k_split_count<false>, dim3(gt2), dim3(BLOCK), 0, c.stream,
@@ -2228,19 +2235,19 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       scan_exclusive_u64_dev(c, tcnt, tcnt, 3 * cstride + 1, st + ST_SCANN);
       hipLaunchKernelGGL(after_cut ? k_split_write<true> : k_split_write<false>, dim3(gt2), dim3(BLOCK), 0, c.stream,
                          (const uint64_t *)cur, prev, st, s, clo, yr,
-                         (const uint64_t *)r0, (const uint64_t *)seg, L, gcut, (const uint64_t *)tcnt, next, lbuf, xbuf);
+                         (const uint64_t *)r0, (const uint64_t *)seg, L, gcut, (const uint64_t *)tcnt, next, lx);
       LAUNCH_CHECK();
     }
     {
       TimedRegion tr(c, "etree_union");
       static_assert(HOOK_ROUNDS == 1, "k_hook_finish reads the one round's shard regions");
       hipLaunchKernelGGL(hook_batch ? k_hook_round<true> : k_hook_round<false>, dim3(gt), dim3(BLOCK), 0, c.stream,
-                         (const uint64_t *)lbuf, (const uint64_t *)(st + ST_NL), uf, g, alt, cset(CSET_HOOK));
+                         (const uint64_t *)lx, (const uint64_t *)(st + ST_NL), uf, g, alt, cset(CSET_HOOK));
       LAUNCH_CHECK();
       hipLaunchKernelGGL(k_hook_finish, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)alt,
                          (const uint64_t *)(st + ST_NL), (const unsigned long long *)cset(CSET_HOOK), uf, g, st + ST_HOOK);
       LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_light_top, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)lbuf,
+      hipLaunchKernelGGL(k_light_top, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)lx,
                          (const uint64_t *)(st + ST_NL), uf, top, g);
       LAUNCH_CHECK();
     }
@@ -2248,16 +2255,16 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       TimedRegion tr(c, "etree_cross");
       if (lvl < c.tune.cross_win_levels)
         hipLaunchKernelGGL(k_cross_find_win, dim3(grid_for(mcap, XW_STEP, 1024)), dim3(XWB),
-                           (XW + XWB / WAVE) * 4, c.stream, (const uint64_t *)xbuf, (const uint64_t *)(st + ST_NX), uf,
+                           (XW + XWB / WAVE) * 4, c.stream, (const uint64_t *)lx, (const uint64_t *)st, uf,
                            mt, xtop, g);
       else
-        hipLaunchKernelGGL(k_cross_find, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)xbuf,
-                           (const uint64_t *)(st + ST_NX), uf, mt, xtop, g);
+        hipLaunchKernelGGL(k_cross_find, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)lx,
+                           (const uint64_t *)st, uf, mt, xtop, g);
       LAUNCH_CHECK();
     }
     {
       TimedRegion tr(c, "etree_apply");
-      hipLaunchKernelGGL(k_cross_apply, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)xbuf,
+      hipLaunchKernelGGL(k_cross_apply, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)lx,
                          (const uint32_t *)xtop, (const uint64_t *)st, (const uint32_t *)mt, (const uint32_t *)top, claim,
                          alt, cset(CSET_APPLY), parent, g);
       LAUNCH_CHECK();
@@ -2323,7 +2330,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   if (nglobal) {   // the last level's clean (the others ran in the next level's split)
     TimedRegion tr(c, "etree_apply");
     hipLaunchKernelGGL(k_level_clean, dim3(gf), dim3(BLOCK), 0, c.stream,
-                       LevelClean{lbuf, xbuf, xtop, stats + (uint64_t)(nglobal - 1) * ST_ROW, uf, mt, top, claim, n, tagged,
+                       LevelClean{lx, xtop, stats + (uint64_t)(nglobal - 1) * ST_ROW, uf, mt, top, claim, n, tagged,
                                   nglobal - 1, parent, csets});
     LAUNCH_CHECK();
   }

@@ -400,7 +400,9 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
                         (const void *)k_lo_scatter_staged<16>, (const void *)k_lo_scatter_staged<8>})
     allow_full_lds(f);
   uint32_t *tile_hist = c.get_as<uint32_t>("hist_tiles", ntiles * nb + 1);
-  uint16_t *keys = c.get_as<uint16_t>("hist_keys", n);
+  // (the keys live only inside a histogram pass; their workspace is the elimination tree's
+  // per-cross-entry root buffer, et_xtop, which the levels fill only after the relabel)
+  uint16_t *keys = c.get_as<uint16_t>("et_xtop", n);
   if (!counted) {   // (counted: degree_fused already wrote tile_hist, >= nb bucket rows)
     hipLaunchKernelGGL(k_hist_count<Src>, dim3((unsigned)ntiles), dim3(CB), nb * 4, c.stream, src, n, nb, tile_hist,
                        ntiles);
