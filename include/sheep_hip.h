@@ -150,6 +150,7 @@ typedef struct sheep_tuning {
   int32_t relabel_per;     /* relabel scatter: records per thread per staged sub-tile, 4, 8, 12 or 15 */
   int32_t cross_win_levels;/* etree: levels (from the first) whose cross pass keeps minima in an LDS window, 0..8 */
   int32_t hook_batch;      /* etree hook rounds find all of a thread's roots at once: 0 never, 1 merges, 2 all */
+  int32_t merge_cut_bits;  /* merges: the early MSF cut of the top 2^bits positions, whatever the density: 0 off, 14..30 */
 } sheep_tuning;
 int sheep_tuning_default(sheep_tuning *out);
 int sheep_ctx_set_tuning(sheep_ctx *ctx, const sheep_tuning *t);

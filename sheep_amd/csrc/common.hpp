@@ -92,7 +92,8 @@ inline sheep_tuning default_tuning() {
   t.relabel_planes = 1;
   t.relabel_per = 8;
   t.cross_win_levels = 2;   // RMAT-26: level 0/1 1.30/2.46 -> 0.77/1.16 ms; level 2 1.60 -> 1.74 ms
-  t.hook_batch = 0;
+  t.hook_batch = 0;        // merges 14.0 -> 18.0 ms, maps no better (RMAT-26, 8 shards)
+  t.merge_cut_bits = 0;
   return t;
 }
 
@@ -435,7 +436,7 @@ void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGroup 
 // of tree edges, little contention) instead of one edge after another (maps: hub pile-ups).
 void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
                       int fin_bits, int filt_lvl = -1, uint32_t ylo = 0, uint32_t yhi = 0, int top_bits = 0,
-                      bool hook_batch = false);
+                      bool hook_batch = false, int force_big_bits = 0);
 void spread_params(uint64_t n, int *L, uint32_t *clo);
 // append.hip — sharded appends: counters (NSHARD * SHARD_STRIDE u64, zeroed).  The pack
 // step moves the shard regions of a producer that streamed *n_in items together in dst

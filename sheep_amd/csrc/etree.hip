@@ -2126,7 +2126,8 @@ static bool big_cut(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, ui
 }
 
 void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
-                      int fin_bits, int filt_lvl, uint32_t ylo, uint32_t yhi, int top_bits, bool hook_batch) {
+                      int fin_bits, int filt_lvl, uint32_t ylo, uint32_t yhi, int top_bits, bool hook_batch,
+                      int force_big_bits) {
   fill_u32(c, parent, n, INVALID);
   if (n < 2 || m == 0) return;
   if (m >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "too many edges for one shard");
@@ -2187,12 +2188,14 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       gcut = top_bits;
     }
   }
-  // the early cut of the top subproblem (sheep_tuning big_bits; 0: off), tried when dense
-  const int big_bits = top_bits ? c.tune.big_bits : 0;
+  // the early cut of the top subproblem (sheep_tuning big_bits; 0: off), tried when dense;
+  // force_big_bits (merges, sheep_tuning merge_cut_bits): tried whatever the density
+  const bool forced = force_big_bits > FINB && force_big_bits <= L - 1 && filt_lvl < 0;
+  const int big_bits = forced ? force_big_bits : top_bits ? c.tune.big_bits : 0;
   int big_lvl = -1;
   uint64_t big_g0 = 0, big_g1 = 0;
   uint32_t big_cut0 = 0;
-  if (top_lvl >= 0 && big_bits > top_bits && big_bits <= L - 1) {
+  if (forced || (top_lvl >= 0 && big_bits > top_bits && big_bits <= L - 1)) {
     std::vector<uint64_t> hs(2 * (size_t)L);
     HIP_CHECK(hipMemcpyAsync(hs.data(), seg, hs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
     c.sync();
@@ -2208,7 +2211,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     // edges per vertex at 2^19, ~540 at 2^20; a 1/8 edge shard's ~90 did not pay for the
     // cut: 8 shard maps 70.2 -> 76.9 ms)
     const uint64_t big_dense = (uint64_t)c.tune.big_dense;
-    if (n - a >= 2 && big_g1 - big_g0 >= big_dense * (n - a)) big_lvl = L - 1 - big_bits;
+    if (n - a >= 2 && (forced || big_g1 - big_g0 >= big_dense * (n - a))) big_lvl = L - 1 - big_bits;
   }
   int cut_lvl = -1;           // the level whose split follows a cut (its list entries dropped)
   uint32_t cut_val = 0;
@@ -2618,7 +2621,8 @@ static void merge_set(Ctx &c, const TreeSet &ts, uint32_t K, uint64_t n, sheep_j
     TimedRegion tr(c, "merge", 8 * (uint64_t)K * n);   // the K trees
     // groups activated at levels >= l are b < L - l
     const uint64_t m = merge_edges(c, ts, K, n, pst, &edges, &seg, &L, l > 0 ? L - l : 0, lo, hi);
-    etree_from_edges(c, edges, m, n, parent, seg, fin_merge, l > 0 ? l : -1, ylo, yhi, 0, c.tune.hook_batch >= 1);
+    etree_from_edges(c, edges, m, n, parent, seg, fin_merge, l > 0 ? l : -1, ylo, yhi, 0, c.tune.hook_batch >= 1,
+                     c.tune.merge_cut_bits);
   }
   hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);
   LAUNCH_CHECK();
