@@ -1730,8 +1730,12 @@ __global__ __launch_bounds__(TOPB) void k_top_hook(TopSet t) {
 constexpr uint32_t BIG_HOT = 1u << 15;
 struct BigState {
   uint32_t *minlo;                  // per vertex: a lower neighbour (block-local), the round-0 pick
-  unsigned *hasup;                  // per vertex a bit: it has an upper neighbour
-  unsigned *picked;                 // per vertex a bit: minlo holds a pick (a 32x smaller read check)
+  // Per vertex a BYTE (plain stores, no read-modify-write): a bit map's atomicOr runs at the
+  // memory side, and 64 lanes on 64 lines took ~17x a coalesced one (MI355X_MICROARCH.md,
+  // atomics) — these atomics were most of k_big_min0's 7 ms at RMAT-26.  A stale read of
+  // a byte another XCD just set only costs a redundant store of the same value.
+  uint8_t *hasup;                   // per vertex: it has an upper neighbour
+  uint8_t *picked;                  // per vertex: minlo holds a pick (a 4x smaller read check)
   unsigned long long *cnt;          // [0] vertices with a lower neighbour, [1] roots with an edge
   uint64_t *st;                     // the cut level's stats row
   uint64_t *out;                    // the MSF goes behind the level's list (st[ST_EXTRA])
@@ -1743,7 +1747,7 @@ __global__ __launch_bounds__(BLOCK) void k_big_init(BigState b) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < b.V; v += stride) {
     b.minlo[v] = INVALID;
-    if (v % 32 == 0) b.hasup[v / 32] = b.picked[v / 32] = 0;
+    b.hasup[v] = b.picked[v] = 0;
   }
   if (blockIdx.x == 0 && threadIdx.x < 2) b.cnt[threadIdx.x] = 0;
 }
@@ -1793,7 +1797,7 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
   __syncthreads();
   const uint32_t w0 = s_w0;
   uint32_t *const gmin = b.minlo;
-  unsigned *const up = b.hasup, *const pk = b.picked;
+  uint8_t *const up = b.hasup, *const pk = b.picked;
   // the list part one entry at a time; the group part TOP_U edges per thread, and their
   // read checks (the minima below the window, the has-upper words) all issued before any
   // atomic: a check that waits for the previous edge's turn serialises eight latencies per
@@ -1804,12 +1808,11 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
     if (e == DEAD) continue;
     const uint32_t l = (uint32_t)e - v0, h = (uint32_t)(e >> 32) - v0;
     if (h >= hot0 && hot_pick(l, h)) {
-    } else if (!((pk[h >> 5] >> (h & 31)) & 1)) {
+    } else if (!pk[h]) {
       gmin[h] = l;
-      atomicOr(&pk[h >> 5], 1u << (h & 31));
+      pk[h] = 1;
     }
-    const unsigned bit = 1u << (l & 31);
-    if (!(up[l >> 5] & bit)) atomicOr(&up[l >> 5], bit);
+    if (!up[l]) up[l] = 1;
   }
   const uint64_t g0 = (b0 > nl ? b0 : nl) - nl, g1 = b1 > nl ? b1 - nl : 0;
   const uint64_t *r = te.r0 + te.g0;
@@ -1824,42 +1827,40 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
     }
 #pragma unroll
     for (int j = 0; j < TOP_U; ++j) {
-      gv[j] = l[j] != INVALID && h[j] < hot0 ? pk[h[j] >> 5] : ~0u;
-      uv[j] = l[j] != INVALID && l[j] - w0 >= BIG_UPW ? up[l[j] >> 5] : ~0u;
+      gv[j] = l[j] != INVALID && h[j] < hot0 ? pk[h[j]] : 1u;
+      uv[j] = l[j] != INVALID && l[j] - w0 >= BIG_UPW ? up[l[j]] : 1u;
     }
 #pragma unroll
     for (int j = 0; j < TOP_U; ++j) {
       if (l[j] == INVALID) continue;
       if (h[j] >= hot0) {
-        if (!hot_pick(l[j], h[j]) && !((pk[h[j] >> 5] >> (h[j] & 31)) & 1)) {   // (H16: a far pick)
+        if (!hot_pick(l[j], h[j]) && !pk[h[j]]) {   // (H16: a far pick)
           gmin[h[j]] = l[j];
-          atomicOr(&pk[h[j] >> 5], 1u << (h[j] & 31));
+          pk[h[j]] = 1;
         }
-      } else if (!((gv[j] >> (h[j] & 31)) & 1)) {
+      } else if (!gv[j]) {
         gmin[h[j]] = l[j];
-        atomicOr(&pk[h[j] >> 5], 1u << (h[j] & 31));
+        pk[h[j]] = 1;
       }
       const unsigned bit = 1u << (l[j] & 31);
       const uint32_t d = l[j] - w0;
       if (d < BIG_UPW) {
         if (!(lup[d >> 5] & bit)) atomicOr(&lup[d >> 5], bit);
-      } else if (!(uv[j] & bit)) {
-        atomicOr(&up[l[j] >> 5], bit);
+      } else if (!uv[j]) {
+        up[l[j]] = 1;
       }
     }
   }
   __syncthreads();
   for (uint32_t v = threadIdx.x; v < HW; v += TOPB) {
     const uint32_t x = H16 ? (ld[v] ? hot0 + v - ld[v] : INVALID) : lmin[v];
-    if (x != INVALID && !((pk[(hot0 + v) >> 5] >> ((hot0 + v) & 31)) & 1)) {
+    if (x != INVALID && !pk[hot0 + v]) {
       gmin[hot0 + v] = x;
-      atomicOr(&pk[(hot0 + v) >> 5], 1u << ((hot0 + v) & 31));
+      pk[hot0 + v] = 1;
     }
   }
-  for (uint32_t w = threadIdx.x; w < BIG_UPW / 32 && w0 / 32 + w <= (V - 1) / 32; w += TOPB) {
-    const unsigned x = lup[w];
-    if (x && (x & ~up[w0 / 32 + w])) atomicOr(&up[w0 / 32 + w], x);
-  }
+  for (uint32_t d = threadIdx.x; d < BIG_UPW && w0 + d < V; d += TOPB)   // the window's bits as bytes
+    if (((lup[d >> 5] >> (d & 31)) & 1) && !up[w0 + d]) up[w0 + d] = 1;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_big_roots(BigState b) {
@@ -1867,7 +1868,7 @@ __global__ __launch_bounds__(BLOCK) void k_big_roots(BigState b) {
   uint64_t nonroot = 0, eroot = 0;
   for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < b.V; v += stride) {
     if (b.minlo[v] != INVALID) ++nonroot;
-    else if ((b.hasup[v >> 5] >> (v & 31)) & 1) ++eroot;
+    else if (b.hasup[v]) ++eroot;
   }
   block_atomic_add(&b.cnt[0], nonroot);
   block_atomic_add(&b.cnt[1], eroot);
@@ -2087,8 +2088,8 @@ static bool big_cut(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, ui
   b.v0 = (uint32_t)a;
   b.V = (uint32_t)(n - a);
   b.minlo = c.get_as<uint32_t>("et_big_minlo", b.V ? b.V : 1);
-  b.hasup = c.get_as<unsigned>("et_big_hasup", b.V / 32 + 1);
-  b.picked = c.get_as<unsigned>("et_big_picked", b.V / 32 + 1);
+  b.hasup = c.get_as<uint8_t>("et_big_hasup", b.V ? b.V : 1);
+  b.picked = c.get_as<uint8_t>("et_big_picked", b.V ? b.V : 1);
   b.cnt = c.get_as<unsigned long long>("et_big_cnt", 2);
   b.st = st;
   b.out = next;
