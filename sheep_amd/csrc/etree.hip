@@ -1816,12 +1816,24 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
   }
   const uint64_t g0 = (b0 > nl ? b0 : nl) - nl, g1 = b1 > nl ? b1 - nl : 0;
   const uint64_t *r = te.r0 + te.g0;
-  for (uint64_t i0 = g0 + threadIdx.x; i0 < g1; i0 += (uint64_t)TOP_U * TOPB) {
-    uint32_t l[TOP_U], h[TOP_U], gv[TOP_U], uv[TOP_U];
+  // software-pipelined: the next TOP_U edges are loaded while this batch's read checks are
+  // in flight and its picks are made (the batch's loads, then its checks, then its LDS work
+  // left no edge load in flight for most of each step: ~1 TB/s)
+  constexpr uint64_t STEP = (uint64_t)TOP_U * TOPB;
+  uint64_t en[TOP_U];
+  auto load = [&](uint64_t i0) {
 #pragma unroll
     for (int j = 0; j < TOP_U; ++j) {
       const uint64_t i = i0 + (uint64_t)j * TOPB;
-      const uint64_t e = i < g1 ? __builtin_nontemporal_load(r + i) : DEAD;
+      en[j] = i < g1 ? __builtin_nontemporal_load(r + i) : DEAD;
+    }
+  };
+  if (g0 + threadIdx.x < g1) load(g0 + threadIdx.x);
+  for (uint64_t i0 = g0 + threadIdx.x; i0 < g1; i0 += STEP) {
+    uint32_t l[TOP_U], h[TOP_U], gv[TOP_U], uv[TOP_U];
+#pragma unroll
+    for (int j = 0; j < TOP_U; ++j) {
+      const uint64_t e = en[j];
       l[j] = e == DEAD ? INVALID : (uint32_t)e - v0;
       h[j] = e == DEAD ? 0 : (uint32_t)(e >> 32) - v0;
     }
@@ -1830,6 +1842,7 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
       gv[j] = l[j] != INVALID && h[j] < hot0 ? pk[h[j]] : 1u;
       uv[j] = l[j] != INVALID && l[j] - w0 >= BIG_UPW ? up[l[j]] : 1u;
     }
+    if (i0 + STEP < g1) load(i0 + STEP);
 #pragma unroll
     for (int j = 0; j < TOP_U; ++j) {
       if (l[j] == INVALID) continue;
