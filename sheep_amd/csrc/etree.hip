@@ -1396,7 +1396,17 @@ template <typename F>
 __device__ __forceinline__ void top_edges(const TopEdges &te, const uint64_t *s_pre, uint64_t ntiles, uint64_t b0,
                                           uint64_t b1, uint32_t t, uint32_t nt, F &&f) {
   const uint64_t nl = s_pre[NSHARD];
-  for (uint64_t i = b0 + t; i < (b1 < nl ? b1 : nl); i += nt) f(top_list_at(te, s_pre, ntiles, i));
+  const uint64_t le = b1 < nl ? b1 : nl;
+  for (uint64_t i0 = b0 + t; i0 < le; i0 += (uint64_t)TOP_U * nt) {   // TOP_U list entries in flight
+    uint64_t e[TOP_U];
+#pragma unroll
+    for (int j = 0; j < TOP_U; ++j) {
+      const uint64_t i = i0 + (uint64_t)j * nt;
+      e[j] = i < le ? top_list_at(te, s_pre, ntiles, i) : DEAD;
+    }
+#pragma unroll
+    for (int j = 0; j < TOP_U; ++j) f(e[j]);
+  }
   const uint64_t g0 = (b0 > nl ? b0 : nl) - nl, g1 = b1 > nl ? b1 - nl : 0;   // group-part range
   const uint64_t *r = te.r0 + te.g0;
   uint64_t i = g0 + t;
@@ -1783,42 +1793,50 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
   for (uint32_t w = threadIdx.x; w < BIG_UPW / 32; w += TOPB) lup[w] = 0;
   top_prefix(te, s_pre);
   __syncthreads();
-  const uint64_t total = s_pre[NSHARD] + (te.g1 - te.g0);
-  const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
-  const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < total ? b0 + per : total;
+  // The list part (the entries the extraction moved out, ~42 M at RMAT-26) strided over
+  // every workgroup, TOP_U entries per thread in flight; the group part in one contiguous
+  // chunk per workgroup.  (One chunk of list-then-groups per workgroup left the list to
+  // the first ~15 workgroups, one dependent load per entry: most of the kernel's 7 ms.)
+  const uint64_t nl = s_pre[NSHARD], ntiles = st[ST_TOPNT], G = te.g1 - te.g0;
+  const uint64_t per = (G + gridDim.x - 1) / gridDim.x;
+  const uint64_t g0 = (uint64_t)blockIdx.x * per < G ? (uint64_t)blockIdx.x * per : G;
+  const uint64_t g1 = g0 + per < G ? g0 + per : G;
   // the group part comes in lo buckets, so a chunk's lo values crowd into a narrow range:
-  // their has-upper bits go to an LDS window from the chunk's first lo (others: device atomics)
+  // their has-upper bits go to an LDS window from the chunk's first lo (others: byte stores)
   if (threadIdx.x == 0) {
-    const uint64_t nl0 = s_pre[NSHARD];
-    const uint64_t gi = (b0 > nl0 ? b0 : nl0) - nl0;
-    const uint64_t e = gi < te.g1 - te.g0 && b0 < b1 ? te.r0[te.g0 + gi] : DEAD;
+    const uint64_t e = g0 < g1 ? te.r0[te.g0 + g0] : DEAD;
     s_w0 = e == DEAD ? 0u : (((uint32_t)e - v0) & ~31u);
   }
   __syncthreads();
   const uint32_t w0 = s_w0;
   uint32_t *const gmin = b.minlo;
   uint8_t *const up = b.hasup, *const pk = b.picked;
-  // the list part one entry at a time; the group part TOP_U edges per thread, and their
-  // read checks (the minima below the window, the has-upper words) all issued before any
-  // atomic: a check that waits for the previous edge's turn serialises eight latencies per
-  // step, and a stale read only costs a redundant atomic (the minima only fall)
-  const uint64_t nl = s_pre[NSHARD], ntiles = st[ST_TOPNT];
-  for (uint64_t i = b0 + threadIdx.x; i < (b1 < nl ? b1 : nl); i += TOPB) {
-    const uint64_t e = top_list_at(te, s_pre, ntiles, i);
-    if (e == DEAD) continue;
-    const uint32_t l = (uint32_t)e - v0, h = (uint32_t)(e >> 32) - v0;
-    if (h >= hot0 && hot_pick(l, h)) {
-    } else if (!pk[h]) {
-      gmin[h] = l;
-      pk[h] = 1;
+  // the group part's read checks (the picks below the window, the has-upper bytes) are all
+  // issued before any store: a check that waits for the previous edge's turn serialises
+  // eight latencies per step, and a stale read only costs a redundant store
+  const uint64_t lstride = (uint64_t)gridDim.x * TOPB;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * TOPB + threadIdx.x; i0 < nl; i0 += (uint64_t)TOP_U * lstride) {
+    uint64_t e[TOP_U];
+#pragma unroll
+    for (int j = 0; j < TOP_U; ++j) {
+      const uint64_t i = i0 + (uint64_t)j * lstride;
+      e[j] = i < nl ? top_list_at(te, s_pre, ntiles, i) : DEAD;
     }
-    if (!up[l]) up[l] = 1;
+#pragma unroll
+    for (int j = 0; j < TOP_U; ++j) {
+      if (e[j] == DEAD) continue;
+      const uint32_t l = (uint32_t)e[j] - v0, h = (uint32_t)(e[j] >> 32) - v0;
+      if (h >= hot0 && hot_pick(l, h)) {
+      } else if (!pk[h]) {
+        gmin[h] = l;
+        pk[h] = 1;
+      }
+      if (!up[l]) up[l] = 1;
+    }
   }
-  const uint64_t g0 = (b0 > nl ? b0 : nl) - nl, g1 = b1 > nl ? b1 - nl : 0;
   const uint64_t *r = te.r0 + te.g0;
   // software-pipelined: the next TOP_U edges are loaded while this batch's read checks are
-  // in flight and its picks are made (the batch's loads, then its checks, then its LDS work
-  // left no edge load in flight for most of each step: ~1 TB/s)
+  // in flight and its picks are made
   constexpr uint64_t STEP = (uint64_t)TOP_U * TOPB;
   uint64_t en[TOP_U];
   auto load = [&](uint64_t i0) {

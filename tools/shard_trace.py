@@ -52,9 +52,24 @@ def main():
     for _ in range(reps):
         merged, ms = timed(lambda: sheep_amd.merge_trees_many(stacked, ctx=ctx))
         merges.append(ms)
+    # mpi_merge's binomial schedule (jnode.cpp:241, MPI_Reduce): ceil(log2 K) hops, each a
+    # pairwise merge per pair of ranks — on K GPUs a hop's merges run side by side, so a
+    # hop costs its slowest merge
+    hops, cur = [], [stacked[i] for i in range(K)]
+    while len(cur) > 1:
+        nxt, worst = [], 0.0
+        for i in range(0, len(cur) - 1, 2):
+            m, ms = timed(lambda a=cur[i], b=cur[i + 1]: sheep_amd.merge_trees(a, b, ctx=ctx))
+            nxt.append(m)
+            worst = max(worst, ms)
+        if len(cur) % 2:
+            nxt.append(cur[-1])
+        hops.append(worst)
+        cur = nxt
     torch.cuda.synchronize()
     time.sleep(gap)
     print(json.dumps({"scale": scale, "shards": K, "map_ms": maps, "merge_ms": merges,
+                      "binomial_hop_ms": hops, "binomial_equals_whole": bool(torch.equal(cur[0], whole)),
                       "merge_equals_whole": bool(torch.equal(merged, whole))}))
 
 
