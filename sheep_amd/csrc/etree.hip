@@ -1740,10 +1740,9 @@ __global__ __launch_bounds__(TOPB) void k_top_hook(TopSet t) {
 constexpr uint32_t BIG_HOT = 1u << 15;
 struct BigState {
   uint32_t *minlo;                  // per vertex: a lower neighbour (block-local), the round-0 pick
-  // Per vertex a BYTE (plain stores, no read-modify-write): a bit map's atomicOr runs at the
-  // memory side, and 64 lanes on 64 lines took ~17x a coalesced one (MI355X_MICROARCH.md,
-  // atomics) — these atomics were most of k_big_min0's 7 ms at RMAT-26.  A stale read of
-  // a byte another XCD just set only costs a redundant store of the same value.
+  // Per vertex a BYTE (plain stores, no read-modify-write, instead of bit maps and their
+  // memory-side atomicOrs; measured the same at RMAT-26).  A stale read of a byte another
+  // XCD just set only costs a redundant store of the same value.
   uint8_t *hasup;                   // per vertex: it has an upper neighbour
   uint8_t *picked;                  // per vertex: minlo holds a pick (a 4x smaller read check)
   unsigned long long *cnt;          // [0] vertices with a lower neighbour, [1] roots with an edge
@@ -2138,7 +2137,9 @@ static bool big_cut(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, ui
     hipLaunchKernelGGL(k_big_min0<true>, dim3(TOP_WG), dim3(TOPB), BIG_HOT * sizeof(uint32_t), c.stream, te, b,
                        (const uint64_t *)st);
   else
-    hipLaunchKernelGGL(k_big_min0<false>, dim3(TOP_WG), dim3(TOPB), lds, c.stream, te, b, (const uint64_t *)st);
+    // (a window of at most 2^14 positions leaves LDS for two workgroups per CU: twice the grid)
+    hipLaunchKernelGGL(k_big_min0<false>, dim3(b.hot <= (1u << 14) ? 2 * TOP_WG : TOP_WG), dim3(TOPB), lds, c.stream,
+                       te, b, (const uint64_t *)st);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_big_roots, dim3(grid_for(b.V)), dim3(BLOCK), 0, c.stream, b);
   LAUNCH_CHECK();
