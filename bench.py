@@ -349,7 +349,7 @@ def main():
                     + (", records shuffled and half of them reversed)" if a.shuffle else ", records (tail, head)-sorted)"),
             "config": {"workload": workload, "records": R, "vertex_slots": s.pos_size,
                        "tree_nodes": n, "k": a.k, "created": res.created, "packing_nodes": res.packing_nodes,
-                       "heavy_nodes": res.heavy_nodes, "seed": seed, "shuffled": a.shuffle, "shards": a.shards,
+                       "heavy_nodes": res.heavy_nodes, "event_launches": res.event_launches, "seed": seed, "shuffled": a.shuffle, "shards": a.shards,
                        "tuning": ctx.tuning() if tune else "defaults",
                        "parallelism": f"edge-shards x{world}" + (
                            f", {a.reduce} reduce, sheep_group over {'RCCL' if group.rccl else 'host TCP (one device)'}"

@@ -83,6 +83,7 @@ typedef struct {
   uint64_t total_weight;
   uint64_t packing_nodes;   /* nodes where first-fit-decreasing packing ran         */
   uint64_t heavy_nodes;     /* |{v : subtree weight > max_component}|               */
+  uint64_t event_launches;  /* packing-event kernel launches (sheep_tuning event_loop) */
 } sheep_partition_info;
 
 typedef struct {
@@ -151,6 +152,8 @@ typedef struct sheep_tuning {
   int32_t cross_win_levels;/* etree: levels (from the first) whose cross pass keeps minima in an LDS window, 0..8 */
   int32_t hook_batch;      /* etree hook rounds find all of a thread's roots at once: 0 never, 1 merges, 2 all */
   int32_t merge_cut_bits;  /* merges: the early MSF cut of the top 2^bits positions, whatever the density: 0 off, 14..30 */
+  int32_t event_loop;      /* partition packing events: 0 one launch per event, else one persistent launch while the
+                              event table fits this many entries (in LDS), 1..4096 */
 } sheep_tuning;
 int sheep_tuning_default(sheep_tuning *out);
 int sheep_ctx_set_tuning(sheep_ctx *ctx, const sheep_tuning *t);

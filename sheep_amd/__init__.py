@@ -50,7 +50,8 @@ class SheepError(RuntimeError):
 class _PartInfo(ctypes.Structure):
     _fields_ = [("created", ctypes.c_int32), ("first_size", ctypes.c_uint64), ("second_size", ctypes.c_uint64),
                 ("max_component", ctypes.c_uint64), ("total_weight", ctypes.c_uint64),
-                ("packing_nodes", ctypes.c_uint64), ("heavy_nodes", ctypes.c_uint64)]
+                ("packing_nodes", ctypes.c_uint64), ("heavy_nodes", ctypes.c_uint64),
+                ("event_launches", ctypes.c_uint64)]
 
 
 class _Eval(ctypes.Structure):
@@ -72,7 +73,7 @@ class Tuning(ctypes.Structure):
                 ("big_dense", ctypes.c_int64), ("big_hot_bits", ctypes.c_int32), ("big_hot16", ctypes.c_int32),
                 ("relabel_planes", ctypes.c_int32), ("relabel_per", ctypes.c_int32),
                 ("cross_win_levels", ctypes.c_int32), ("hook_batch", ctypes.c_int32),
-                ("merge_cut_bits", ctypes.c_int32)]
+                ("merge_cut_bits", ctypes.c_int32), ("event_loop", ctypes.c_int32)]
 
     @classmethod
     def of(cls, **kw):
@@ -452,6 +453,7 @@ class PartitionResult:
     total_weight: int
     packing_nodes: int
     heavy_nodes: int
+    event_launches: int = 0   # packing-event kernel launches (sheep_tuning event_loop)
 
     def print_text(self) -> str:   # partition.h:135-143
         return (f"Actually created {self.created} partitions.\n"
@@ -482,7 +484,8 @@ def partition(seq: Sequence, tree, k: int, balance: float = 1.03, vtx_weight: bo
                                      kids.handle, int(k), float(balance), int(vtx_weight), int(pst_weight),
                                      _ptr(parts), ctypes.byref(info)))
     return PartitionResult(parts[:pos_size], int(k), info.created, info.first_size, info.second_size,
-                           info.max_component, info.total_weight, info.packing_nodes, info.heavy_nodes)
+                           info.max_component, info.total_weight, info.packing_nodes, info.heavy_nodes,
+                           info.event_launches)
 
 
 @dataclass

@@ -94,6 +94,7 @@ inline sheep_tuning default_tuning() {
   t.cross_win_levels = 2;   // RMAT-26: level 0/1 1.30/2.46 -> 0.77/1.16 ms; level 2 1.60 -> 1.74 ms
   t.hook_batch = 0;        // merges 14.0 -> 18.0 ms, maps no better (RMAT-26, 8 shards)
   t.merge_cut_bits = 0;
+  t.event_loop = 4096;
   return t;
 }
 

@@ -388,6 +388,34 @@ struct EvView {
     const uint32_t i = lower(lo), j = hi == INVALID ? m : lower(hi + 1);
     return j > i ? pre[j] - pre[i] : 0;
   }
+  // the same for P intervals at once: branchless searches with the table-wide trip count,
+  // so the 2P searches' loads of one step are in flight together (one search at a time cost
+  // the persistent event kernel 7 us an event at 68 entries)
+  template <int P>
+  __device__ void removed_many(const uint32_t (&lo)[P], const uint32_t (&hi)[P], uint64_t (&out)[P]) const {
+    uint32_t bl[P], bh[P], xh[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      bl[j] = 0;
+      bh[j] = 0;
+      xh[j] = hi[j] == INVALID ? INVALID : hi[j] + 1;   // (pos < INVALID: lower(INVALID) = m)
+      out[j] = 0;
+    }
+    if (m == 0) return;
+    for (uint32_t n = m; n > 1; n -= n >> 1) {
+      const uint32_t half = n >> 1;
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        bl[j] = pos[bl[j] + half] < lo[j] ? bl[j] + half : bl[j];
+        bh[j] = pos[bh[j] + half] < xh[j] ? bh[j] + half : bh[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const uint32_t i = bl[j] + (pos[bl[j]] < lo[j]), k = bh[j] + (pos[bh[j]] < xh[j]);
+      out[j] = lo[j] != INVALID && k > i ? pre[k] - pre[i] : 0;
+    }
+  }
 };
 
 // Tables of up to EV_ARG events travel as a kernel argument (device-side kernarg memory):
@@ -419,18 +447,7 @@ __device__ __forceinline__ EvView load_table(const uint32_t *gpos, const uint64_
   return EvView{spos, spre, m};
 }
 
-// One packing event in one launch.  Every workgroup scans 2048-entry chunks of the heavy
-// set in index order for the lowest-index node after the last packing node whose
-// residual exceeds max_component, and stops once a hit below its chunk is known (an
-// event reads about the distance to the next packing node, not the whole heavy set).
-// The last workgroup to finish then knows the node and stages the event straight into
-// mapped host memory: hdr = {v, koff[v], #kids, R[v] lo, R[v] hi, tD(v) (INVALID for a
-// root), kids staged?}, the node's kids in their current order and their residuals (up
-// to EV_INLINE of them; larger kid lists go through k_event_kids).  It resets the
-// search state for the next event and raises hdr[7] = seq (system scope), which the
-// host polls instead of synchronising the stream.  The event table is read from mapped
-// host memory too (the host rewrites it between events), so an event is ONE launch.
-// 512-entry chunks: an event's scan reaches its hit in fewer dependent rounds per
+// The event search's chunks: 512 entries reach the hit in fewer dependent rounds per
 // workgroup (RMAT-26 / Chung-Lu events: 2048-entry chunks 2.2 / 4.6 ms, 512 2.0 / 3.9 ms)
 constexpr int EVI = 2, EV_CH = BLOCK * EVI;
 constexpr uint32_t EV_STAGE = 1u << 16;   // mapped staging area (kids)
@@ -448,88 +465,123 @@ __device__ __forceinline__ void stage_kids(const EvView &ev, uint32_t beg, uint3
   }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hids, uint64_t nh,
-                                                 const uint64_t *__restrict__ SH, const uint32_t *__restrict__ hst,
-                                                 const uint32_t *__restrict__ hen, const uint32_t *__restrict__ epos,
-                                                 const uint64_t *__restrict__ epre, uint32_t m, uint64_t maxc,
-                                                 uint64_t *__restrict__ evprev, unsigned long long *__restrict__ found,
-                                                 unsigned *__restrict__ done, const uint32_t *__restrict__ koff,
-                                                 const uint32_t *__restrict__ kids, const uint64_t *__restrict__ S,
-                                                 const uint32_t *__restrict__ cparent, const uint32_t *__restrict__ ckoff,
-                                                 const uint32_t *__restrict__ tD, const uint32_t *__restrict__ tU,
-                                                 const uint32_t *__restrict__ rst, const uint32_t *__restrict__ ren,
-                                                 uint32_t *__restrict__ hdr, uint32_t *__restrict__ kid_out,
-                                                 uint64_t *__restrict__ r_out, uint32_t seq, const EvArg arg) {
-  __shared__ uint32_t spos[EV_LDS];
-  __shared__ uint64_t spre[EV_LDS + 1];
-  __shared__ unsigned long long s_best[BLOCK / WAVE];
-  __shared__ unsigned long long s_word;   // one thread's atomic read, for the workgroup
-  __shared__ bool last;
-  uint64_t t_start = wall_clock64();
-  const EvView ev = epos ? load_table(epos, epre, m, spos, spre) : load_arg(arg, spos, spre);
-  uint64_t t_table = wall_clock64();
-  // The search state (evprev, found, done) is only ever touched by atomic read-modify-writes,
-  // which every XCD sees at one coherent point: a plain or atomic LOAD is served from the
-  // reading XCD's own L2 and can return a value an earlier event left there (a stale hit
-  // below every chunk made one search end empty: seen with 512-entry chunks on C4).
-  if (threadIdx.x == 0) s_word = atomicOr((unsigned long long *)evprev, 0ull);
+// One event's search by every workgroup: chunks of the heavy set in index order, from the
+// last packing node on, until a hit below the chunk is known; the last workgroup to
+// finish (event_done) then sees every other workgroup's atomicMin in `found`.
+// The search state (evprev, found, done) is only ever touched by atomic read-modify-writes,
+// which every XCD sees at one coherent point: a plain or atomic LOAD is served from the
+// reading XCD's own L2 and can return a value an earlier event left there (a stale hit
+// below every chunk made one search end empty: seen with 512-entry chunks on C4).
+struct EvShared {
+  unsigned long long best[BLOCK / WAVE];
+  unsigned long long word;   // one thread's atomic read, for the workgroup
+  bool last;
+};
+// the workgroup's least hit among P candidates per thread (loaded by the caller) into `found`
+// (thread 0: `dep` collects the atomic's return, which event_done's ticket waits for)
+template <int P>
+__device__ void event_hits(const EvView &ev, const uint32_t (&ca)[P], const uint32_t (&cs)[P], const uint32_t (&ce)[P],
+                           const uint64_t (&cr)[P], uint64_t base, uint32_t vlast, uint64_t maxc,
+                           unsigned long long *__restrict__ found, EvShared &sh, uint32_t &dep) {
+  unsigned long long best = ~0ull;
+  uint64_t rm[P];
+  ev.removed_many<P>(cs, ce, rm);
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const uint32_t a = ca[j];
+    if (a == INVALID || (vlast != INVALID && a <= vlast)) continue;
+    const uint64_t r = cr[j] - rm[j];
+    if (r > maxc) {
+      const unsigned long long key = ((unsigned long long)a << 32) | (base + (uint64_t)j * BLOCK + threadIdx.x);
+      best = key < best ? key : best;
+    }
+  }
+  best = wave_min(best);
+  if ((threadIdx.x & 63) == 0) sh.best[threadIdx.x >> 6] = best;
   __syncthreads();
-  const uint64_t prev = s_word;
-  __syncthreads();   // s_word is rewritten below
-  const uint64_t start = prev == ~0ull ? 0 : (uint32_t)prev;
-  const uint32_t vlast = prev == ~0ull ? INVALID : (uint32_t)(prev >> 32);
+  if (threadIdx.x == 0) {
+    unsigned long long b = sh.best[0];
+    for (int w = 1; w < BLOCK / WAVE; ++w) b = sh.best[w] < b ? sh.best[w] : b;
+    if (b != ~0ull) dep |= (uint32_t)atomicMin(found, b);
+  }
+  __syncthreads();
+}
+// every candidate's four words loaded before any is decoded (a load behind the id check
+// of the same candidate serialised two latencies per candidate: 24 us a scan)
+template <int P>
+__device__ __forceinline__ void event_load(const uint32_t *__restrict__ hids, const uint64_t *__restrict__ SH,
+                                           const uint32_t *__restrict__ hst, const uint32_t *__restrict__ hen,
+                                           uint64_t nh, uint64_t base, uint32_t (&ca)[P], uint32_t (&cs)[P],
+                                           uint32_t (&ce)[P], uint64_t (&cr)[P]) {
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const uint64_t h = base + (uint64_t)j * BLOCK + threadIdx.x;
+    const bool in = h < nh;
+    ca[j] = in ? hids[h] : INVALID;
+    cr[j] = in ? SH[h] : 0;
+    cs[j] = in ? hst[h] : INVALID;
+    ce[j] = in ? hen[h] : INVALID;
+  }
+}
+// the chunks from `from` on, workgroup-strided; `check_first`: a hit may already be known
+// (the first chunk of a fresh search is not checked: `found` was reset with the last event)
+__device__ void event_scan(const EvView &ev, const uint32_t *__restrict__ hids, uint64_t nh,
+                           const uint64_t *__restrict__ SH, const uint32_t *__restrict__ hst,
+                           const uint32_t *__restrict__ hen, uint64_t maxc, uint64_t from, uint32_t vlast,
+                           bool check_first, unsigned long long *__restrict__ found, EvShared &sh, uint32_t &dep) {
   for (uint64_t ch = blockIdx.x;; ch += gridDim.x) {
-    const uint64_t base = start + ch * EV_CH;
+    const uint64_t base = from + ch * EV_CH;
     if (base >= nh) break;
-    if (threadIdx.x == 0) s_word = atomicOr(found, 0ull);
-    __syncthreads();
-    const unsigned long long f = s_word;
-    if (f != ~0ull && (uint32_t)f < base) break;   // a hit below this chunk is known (uniform)
-    unsigned long long best = ~0ull;
-    // every candidate's four words loaded before any is decoded (a load behind the id
-    // check of the same candidate serialised two latencies per candidate: 24 us a scan)
+    if (check_first || ch != blockIdx.x) {
+      if (threadIdx.x == 0) sh.word = atomicOr(found, 0ull);
+      __syncthreads();
+      const unsigned long long f = sh.word;
+      __syncthreads();
+      if (f != ~0ull && (uint32_t)f < base) break;   // a hit below this chunk is known (uniform)
+    }
     uint32_t ca[EVI], cs[EVI], ce[EVI];
     uint64_t cr[EVI];
-#pragma unroll
-    for (int j = 0; j < EVI; ++j) {
-      const uint64_t h = base + (uint64_t)j * BLOCK + threadIdx.x;
-      const bool in = h < nh;
-      ca[j] = in ? hids[h] : INVALID;
-      cr[j] = in ? SH[h] : 0;
-      cs[j] = in ? hst[h] : INVALID;
-      ce[j] = in ? hen[h] : INVALID;
-    }
-#pragma unroll
-    for (int j = 0; j < EVI; ++j) {
-      const uint64_t h = base + (uint64_t)j * BLOCK + threadIdx.x;
-      const uint32_t a = ca[j];
-      if (a == INVALID || (vlast != INVALID && a <= vlast)) continue;
-      const uint64_t r = cr[j] - ev.removed(cs[j], ce[j]);
-      if (r > maxc) {
-        const unsigned long long key = ((unsigned long long)a << 32) | h;
-        best = key < best ? key : best;
-      }
-    }
-    best = wave_min(best);
-    if ((threadIdx.x & 63) == 0) s_best[threadIdx.x >> 6] = best;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned long long b = s_best[0];
-      for (int w = 1; w < BLOCK / WAVE; ++w) b = s_best[w] < b ? s_best[w] : b;
-      if (b != ~0ull) atomicMin(found, b);
-    }
-    __syncthreads();
+    event_load<EVI>(hids, SH, hst, hen, nh, base, ca, cs, ce, cr);
+    event_hits<EVI>(ev, ca, cs, ce, cr, base, vlast, maxc, found, sh, dep);
   }
-  // the last workgroup to finish sees every other workgroup's atomicMin
-  __threadfence();
+}
+// The ticket: issued only after this workgroup's atomicMins have RETURNED (`zero` is 0
+// computed from their results inside asm, as in scan.hip), so the last ticket sees them all;
+// a __threadfence() here wrote back the XCD's L2 in every workgroup (3.6 us an event).
+__device__ bool event_done(unsigned *__restrict__ done, EvShared &sh, uint32_t dep) {
   __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
+  if (threadIdx.x == 0) {
+    uint32_t zero;
+    asm volatile("v_and_b32 %0, 0, %1" : "=v"(zero) : "v"(dep));
+    sh.last = atomicAdd(done, 1u + zero) == gridDim.x - 1;
+  }
   __syncthreads();
-  if (!last) return;
-  const uint64_t t_search = wall_clock64();
-  if (threadIdx.x == 0) s_word = atomicOr(found, 0ull);
+  return sh.last;
+}
+// the last packing node (id << 32 | its index in the heavy set; ~0 before the first)
+__device__ uint64_t event_prev(uint64_t *__restrict__ evprev, EvShared &sh) {
+  if (threadIdx.x == 0) sh.word = atomicOr((unsigned long long *)evprev, 0ull);
   __syncthreads();
-  const unsigned long long e = s_word;
+  const uint64_t prev = sh.word;
+  __syncthreads();
+  return prev;
+}
+
+// The last workgroup's part: the event staged straight into mapped host memory (hdr =
+// {v, koff[v], #kids, R[v] lo, R[v] hi, tD(v) (INVALID for a root), kids staged?}, the
+// node's kids in their current order with their residuals, up to EV_INLINE of them), the
+// search state reset for the next event, then hdr[7] = seq raised (system scope).
+__device__ void event_stage(const EvView &ev, unsigned long long *__restrict__ found, uint64_t *__restrict__ evprev,
+                            unsigned *__restrict__ done, const uint32_t *__restrict__ koff,
+                            const uint32_t *__restrict__ kids, const uint64_t *__restrict__ S,
+                            const uint32_t *__restrict__ cparent, const uint32_t *__restrict__ ckoff,
+                            const uint32_t *__restrict__ tD, const uint32_t *__restrict__ tU,
+                            const uint32_t *__restrict__ rst, const uint32_t *__restrict__ ren,
+                            uint32_t *__restrict__ hdr, uint32_t *__restrict__ kid_out, uint64_t *__restrict__ r_out,
+                            uint32_t seq, EvShared &sh, uint64_t t_start, uint64_t t_table, uint64_t t_search) {
+  if (threadIdx.x == 0) sh.word = atomicOr(found, 0ull);
+  __syncthreads();
+  const unsigned long long e = sh.word;
   const uint32_t v = e == ~0ull ? INVALID : (uint32_t)(e >> 32);
   if (v != INVALID) {
     const uint32_t beg = koff[v], cnt = koff[v + 1] - beg;
@@ -558,8 +610,175 @@ __global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hi
     hdr[10] = (uint32_t)(t_stage - t_search);
     atomicExch(found, ~0ull);   // the next event's search starts clean
     atomicExch(done, 0u);
-    __threadfence_system();
-    __hip_atomic_store(&hdr[7], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&hdr[7], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);   // (orders the staged words)
+  }
+}
+
+// One packing event in one launch.  Every workgroup scans 512-entry chunks of the heavy
+// set (event_search: an event reads about the distance to the next packing node, not the
+// whole heavy set), the last one stages the event (event_stage) for the host, which polls
+// hdr[7] instead of synchronising the stream.  The event table is read from kernel
+// arguments or mapped host memory (the host rewrites it between events), so an event is
+// ONE launch.
+__global__ __launch_bounds__(BLOCK) void k_event(const uint32_t *__restrict__ hids, uint64_t nh,
+                                                 const uint64_t *__restrict__ SH, const uint32_t *__restrict__ hst,
+                                                 const uint32_t *__restrict__ hen, const uint32_t *__restrict__ epos,
+                                                 const uint64_t *__restrict__ epre, uint32_t m, uint64_t maxc,
+                                                 uint64_t *__restrict__ evprev, unsigned long long *__restrict__ found,
+                                                 unsigned *__restrict__ done, const uint32_t *__restrict__ koff,
+                                                 const uint32_t *__restrict__ kids, const uint64_t *__restrict__ S,
+                                                 const uint32_t *__restrict__ cparent, const uint32_t *__restrict__ ckoff,
+                                                 const uint32_t *__restrict__ tD, const uint32_t *__restrict__ tU,
+                                                 const uint32_t *__restrict__ rst, const uint32_t *__restrict__ ren,
+                                                 uint32_t *__restrict__ hdr, uint32_t *__restrict__ kid_out,
+                                                 uint64_t *__restrict__ r_out, uint32_t seq, const EvArg arg) {
+  __shared__ uint32_t spos[EV_LDS];
+  __shared__ uint64_t spre[EV_LDS + 1];
+  __shared__ EvShared sh;
+  const uint64_t t_start = wall_clock64();
+  const EvView ev = epos ? load_table(epos, epre, m, spos, spre) : load_arg(arg, spos, spre);
+  const uint64_t t_table = wall_clock64();
+  const uint64_t prev = event_prev(evprev, sh);
+  uint32_t dep = 0;
+  event_scan(ev, hids, nh, SH, hst, hen, maxc, prev == ~0ull ? 0 : (uint32_t)prev,
+             prev == ~0ull ? INVALID : (uint32_t)(prev >> 32), false, found, sh, dep);
+  if (!event_done(done, sh, dep)) return;
+  event_stage(ev, found, evprev, done, koff, kids, S, cparent, ckoff, tD, tU, rst, ren, hdr, kid_out, r_out, seq, sh,
+              t_start, t_table, wall_clock64());
+}
+
+// The persistent form: ONE launch runs event after event.  After staging an event the last
+// workgroup publishes it (go[5..7]) to the others, which prefetch the first EVP * BLOCK
+// candidates of their next search (the heavy set does not change, only the table does)
+// while it waits for the host's answer in mapped memory (EvReply: the host packs the kids
+// with std::sort + first-fit, as for k_event) and hands it on (go[0..4], device memory,
+// read-modify-write only, like the search state).  Every workgroup then inserts the event
+// into its own LDS copy of the table (double-buffered) and decodes its prefetched
+// candidates.  The host answers EV_STOP when the node's kids exceed EV_INLINE
+// (k_event_kids stages them after this kernel has ended) or the table would outgrow `cap`
+// entries; an empty search ends the kernel; either side gives up after `timeout` ticks.
+struct EvReply {
+  uint32_t seq, cmd, vpos, dlo, dhi;
+};
+constexpr uint32_t EV_CONT = 0, EV_STOP = 1;
+constexpr int EV_TIMEOUT_S = 30;   // either side of the event protocol gives up after this long
+constexpr int EVP = 8, EVP_CH = BLOCK * EVP;   // prefetched candidates per thread
+__device__ bool wait_word(unsigned *w, uint32_t want, uint64_t timeout) {   // (thread 0)
+  const uint64_t t0 = wall_clock64();
+  while (atomicOr(w, 0u) != want) {
+    __builtin_amdgcn_s_sleep(4);
+    if (wall_clock64() - t0 > timeout) return false;
+  }
+  return true;
+}
+__global__ __launch_bounds__(BLOCK) void k_event_loop(const uint32_t *__restrict__ hids, uint64_t nh,
+                                                      const uint64_t *__restrict__ SH, const uint32_t *__restrict__ hst,
+                                                      const uint32_t *__restrict__ hen, const uint32_t *__restrict__ epos,
+                                                      const uint64_t *__restrict__ epre, uint32_t m, uint64_t maxc,
+                                                      uint64_t *__restrict__ evprev, unsigned long long *__restrict__ found,
+                                                      unsigned *__restrict__ done, const uint32_t *__restrict__ koff,
+                                                      const uint32_t *__restrict__ kids, const uint64_t *__restrict__ S,
+                                                      const uint32_t *__restrict__ cparent,
+                                                      const uint32_t *__restrict__ ckoff, const uint32_t *__restrict__ tD,
+                                                      const uint32_t *__restrict__ tU, const uint32_t *__restrict__ rst,
+                                                      const uint32_t *__restrict__ ren, uint32_t *__restrict__ hdr,
+                                                      uint32_t *__restrict__ kid_out, uint64_t *__restrict__ r_out,
+                                                      uint32_t seq0, const EvArg arg, EvReply *reply,
+                                                      unsigned *__restrict__ go, uint64_t timeout) {
+  __shared__ uint32_t spos[2][EV_LDS];
+  __shared__ uint64_t spre[2][EV_LDS + 1];
+  __shared__ EvShared sh;
+  __shared__ uint32_t cmd[4];
+  int cur = 0;
+  if (epos) load_table(epos, epre, m, spos[0], spre[0]);   // (m <= cap <= EV_LDS: the LDS copy)
+  else load_arg(arg, spos[0], spre[0]);
+  uint64_t e = event_prev(evprev, sh);
+  bool was_last = false;
+  for (uint32_t seq = seq0 + 1;; ++seq) {
+    const uint64_t start = e == ~0ull ? 0 : (uint32_t)e;
+    const uint32_t vlast = e == ~0ull ? INVALID : (uint32_t)(e >> 32);
+    const uint64_t pbase = start + (uint64_t)blockIdx.x * EVP_CH;
+    uint32_t ca[EVP], cs[EVP], ce[EVP];
+    uint64_t cr[EVP];
+    event_load<EVP>(hids, SH, hst, hen, nh, pbase, ca, cs, ce, cr);
+    if (seq != seq0 + 1) {   // the previous event's answer
+      if (threadIdx.x == 0) {
+        uint32_t c[4] = {EV_STOP, INVALID, 0, 0};
+        if (was_last) {   // from the host, handed on to the other workgroups
+          const uint64_t t0 = wall_clock64();
+          bool ok = true;
+          while (__hip_atomic_load(&reply->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq - 1) {
+            __builtin_amdgcn_s_sleep(4);
+            if (wall_clock64() - t0 > timeout) { ok = false; break; }
+          }
+          if (ok) {
+            c[0] = __hip_atomic_load(&reply->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            c[1] = __hip_atomic_load(&reply->vpos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            c[2] = __hip_atomic_load(&reply->dlo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            c[3] = __hip_atomic_load(&reply->dhi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+          uint32_t d = 0, zero;   // go[0] after the four words' atomics returned (event_done's idiom)
+          for (int i = 0; i < 4; ++i) d |= atomicExch(&go[1 + i], c[i]);
+          asm volatile("v_and_b32 %0, 0, %1" : "=v"(zero) : "v"(d));
+          atomicExch(&go[0], seq - 1 + zero);
+        } else if (wait_word(&go[0], seq - 1, 2 * timeout)) {
+          for (int i = 0; i < 4; ++i) c[i] = atomicOr(&go[1 + i], 0u);
+        }
+        for (int i = 0; i < 4; ++i) cmd[i] = c[i];
+      }
+      __syncthreads();
+      if (cmd[0] != EV_CONT) return;
+      const uint32_t vpos = cmd[1];
+      if (vpos != INVALID) {   // insert (vpos, delta) behind every entry at or below vpos
+        const uint64_t d = (uint64_t)cmd[2] | ((uint64_t)cmd[3] << 32);
+        const uint32_t *p0 = spos[cur];
+        const uint64_t *q0 = spre[cur];
+        uint32_t *p1 = spos[cur ^ 1];
+        uint64_t *q1 = spre[cur ^ 1];
+        uint32_t lo = 0, hi = m;   // first entry above vpos
+        while (lo < hi) { const uint32_t c = (lo + hi) >> 1; if (p0[c] <= vpos) lo = c + 1; else hi = c; }
+        for (uint32_t j = threadIdx.x; j <= m + 1; j += BLOCK) {
+          if (j <= m) p1[j] = j < lo ? p0[j] : j == lo ? vpos : p0[j - 1];
+          q1[j] = j <= lo ? q0[j] : q0[j - 1] + d;
+        }
+        cur ^= 1;
+        ++m;
+        __syncthreads();
+      }
+    }
+    const uint64_t t_start = wall_clock64();
+    const EvView ev{spos[cur], spre[cur], m};
+    uint32_t dep = 0;
+    event_hits<EVP>(ev, ca, cs, ce, cr, pbase, vlast, maxc, found, sh, dep);
+    const uint64_t t_hits = wall_clock64();
+    event_scan(ev, hids, nh, SH, hst, hen, maxc, start + (uint64_t)gridDim.x * EVP_CH, vlast, true, found, sh, dep);
+    const uint64_t t_scan = wall_clock64();
+    was_last = event_done(done, sh, dep);
+    if (was_last) {
+      if (threadIdx.x == 0) {   // (SHEEP_DEBUG=part: the last workgroup's phases)
+        hdr[11] = (uint32_t)(t_hits - t_start);
+        hdr[12] = (uint32_t)(t_scan - t_hits);
+        hdr[13] = (uint32_t)(wall_clock64() - t_scan);
+        hdr[14] = (uint32_t)start;
+      }
+      event_stage(ev, found, evprev, done, koff, kids, S, cparent, ckoff, tD, tU, rst, ren, hdr, kid_out, r_out, seq,
+                  sh, t_start, t_start, wall_clock64());
+      if (threadIdx.x == 0) {   // the event to the other workgroups (sh.word: event_stage's read of found)
+        uint32_t zero;
+        const uint32_t d = atomicExch(&go[6], (uint32_t)sh.word) | atomicExch(&go[7], (uint32_t)(sh.word >> 32));
+        asm volatile("v_and_b32 %0, 0, %1" : "=v"(zero) : "v"(d));
+        atomicExch(&go[5], seq + zero);
+      }
+    } else if (threadIdx.x == 0) {
+      sh.word = ~0ull;
+      if (wait_word(&go[5], seq, 2 * timeout)) {
+        sh.word = (uint64_t)atomicOr(&go[6], 0u) | ((uint64_t)atomicOr(&go[7], 0u) << 32);
+      }
+    }
+    __syncthreads();
+    e = sh.word;
+    __syncthreads();
+    if (e == ~0ull) return;   // the search came back empty: the partition's events are over
   }
 }
 
@@ -928,11 +1147,32 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   std::vector<std::pair<uint32_t, uint64_t>> root_own;   // a root's own packing delta
   uint32_t seq_no = 0;
   // waits for the event kernels' completion flag (hdr[7]): a poll of mapped memory wakes
-  // the host sooner than a stream synchronisation
+  // the host sooner than a stream synchronisation (which would never return while
+  // k_event_loop waits for this thread's answer: the wait is bounded in time instead)
   auto wait_stage = [&](uint32_t want) {
+    const auto t0 = std::chrono::steady_clock::now();
     for (long spin = 0; hdr[7] != want; ++spin)
-      if (spin > (1l << 22)) { c.sync(); break; }
+      if ((spin & 4095) == 4095 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(EV_TIMEOUT_S))
+        throw Error(SHEEP_ERR_HIP, "partition: the packing event kernel did not report");
     std::atomic_thread_fence(std::memory_order_acquire);
+  };
+  // the persistent event kernel (sheep_tuning event_loop > 0) and its answer word
+  const uint32_t ev_cap = (uint32_t)c.tune.event_loop;
+  EvReply *rep = (EvReply *)c.get_pinned("pt_reply", sizeof(EvReply));
+  EvReply *d_rep;
+  HIP_CHECK(hipHostGetDevicePointer((void **)&d_rep, rep, 0));
+  unsigned *go = c.get_as<unsigned>("pt_go", 8);
+  HIP_CHECK(hipMemsetAsync(go, 0, 8 * sizeof(unsigned), c.stream));
+  __atomic_store_n(&rep->seq, 0u, __ATOMIC_RELEASE);   // (a word left by the last call could match a seq)
+  bool live = false;   // k_event_loop is running: it waits for an answer after each event
+  auto answer = [&](uint32_t cmd, uint32_t vpos, uint64_t d) {
+    volatile EvReply *r = rep;
+    r->cmd = cmd;
+    r->vpos = vpos;
+    r->dlo = (uint32_t)d;
+    r->dhi = (uint32_t)(d >> 32);
+    __atomic_store_n(&rep->seq, seq_no, __ATOMIC_RELEASE);
+    if (cmd != EV_CONT) live = false;
   };
   std::vector<uint64_t> part_size;
   std::vector<uint32_t> asg_ids;
@@ -951,21 +1191,40 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
                        (const uint32_t *)core.parent, (const uint32_t *)t.tD, (const uint32_t *)t.tU, d_hdr, o_kids, o_r,
                        beg_j, cap, done_ctr, seq_no);
     LAUNCH_CHECK();
+    info->event_launches++;
     wait_stage(seq_no);
   };
   {
     TimedRegion tr(c, "partition_events");
     hdr[7] = 0;
+    try {
     for (;;) {
+      if (!live) {   // k_event for this event, or k_event_loop from it on (both read the table as written now)
+        write_table(false);
+        const bool by_arg = m_ev <= EV_ARG;
+        if (ev_cap && m_ev <= ev_cap) {
+          hipLaunchKernelGGL(k_event_loop, dim3(gev), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh,
+                             (const uint64_t *)SH, (const uint32_t *)hst, (const uint32_t *)hen,
+                             by_arg ? nullptr : t_pos, by_arg ? nullptr : t_pre, m_ev, max_component, evprev, found,
+                             done_ctr, (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
+                             (const uint32_t *)core.parent, (const uint32_t *)core.koff, (const uint32_t *)t.tD,
+                             (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren, d_hdr, d_kids, d_r,
+                             seq_no, evarg, d_rep, go, (uint64_t)EV_TIMEOUT_S * 100000000ull);
+          live = true;
+          info->event_launches++;
+        } else {
+          hipLaunchKernelGGL(k_event, dim3(gev), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh,
+                             (const uint64_t *)SH, (const uint32_t *)hst, (const uint32_t *)hen,
+                             by_arg ? nullptr : t_pos, by_arg ? nullptr : t_pre, m_ev, max_component, evprev, found,
+                             done_ctr, (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
+                             (const uint32_t *)core.parent, (const uint32_t *)core.koff, (const uint32_t *)t.tD,
+                             (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren, d_hdr, d_kids, d_r,
+                             seq_no + 1, evarg);
+          info->event_launches++;
+        }
+        LAUNCH_CHECK();
+      }
       ++seq_no;
-      const bool by_arg = m_ev <= EV_ARG;
-      hipLaunchKernelGGL(k_event, dim3(gev), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh, (const uint64_t *)SH,
-                         (const uint32_t *)hst, (const uint32_t *)hen, by_arg ? nullptr : t_pos, by_arg ? nullptr : t_pre, m_ev, max_component, evprev, found,
-                         done_ctr, (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
-                         (const uint32_t *)core.parent, (const uint32_t *)core.koff, (const uint32_t *)t.tD,
-                         (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren, d_hdr, d_kids, d_r, seq_no,
-                         evarg);
-      LAUNCH_CHECK();
       const auto h0 = std::chrono::steady_clock::now();
       wait_stage(seq_no);
       const auto h1 = std::chrono::steady_clock::now();
@@ -976,11 +1235,22 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
         dbg_wait += std::chrono::duration<double, std::micro>(h1 - h0).count();
       }
       const uint32_t v = hdr[0];
-      if (v == INVALID) break;
+      if (dbg && live)
+        fprintf(stderr, "partition event %u: hits %.1f scan %.1f done %.1f stage %.1f us, from %u, wait %.1f us\n", seq_no,
+                hdr[11] / 100.0, hdr[12] / 100.0, hdr[13] / 100.0, hdr[10] / 100.0, hdr[14],
+                std::chrono::duration<double, std::micro>(h1 - h0).count());
+      if (v == INVALID) {
+        if (live) answer(EV_STOP, INVALID, 0);
+        break;
+      }
       info->packing_nodes++;
       const uint32_t beg = hdr[1], cnt = hdr[2], vpos = hdr[5];
       uint64_t cb = (uint64_t)hdr[3] | ((uint64_t)hdr[4] << 32);
-      if (!hdr[6]) stage_kids_of(0, EV_STAGE, d_kids, d_r);   // more kids than the event kernel stages
+      if (!hdr[6]) {   // more kids than the event kernel stages: k_event_kids, behind k_event_loop's end
+        if (live) answer(EV_STOP, INVALID, 0);
+        write_table(false);
+        stage_kids_of(0, EV_STAGE, d_kids, d_r);
+      }
       seg.assign(st_kids, st_kids + std::min(cnt, EV_STAGE));
       segR.assign(st_r, st_r + std::min(cnt, EV_STAGE));
       if (cnt > EV_STAGE) {   // a node with more kids than the staging area: fetch the rest
@@ -1037,8 +1307,15 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
         evs.insert(std::upper_bound(evs.begin(), evs.end(), std::make_pair(vpos, (uint64_t)~0ull)), {vpos, cb0 - cb});
       else
         root_own.push_back({v, cb0 - cb});
-      write_table(false);   // (no kernel reads the table now: the last one has finished)
+      if (live) {   // k_event_loop inserts the event into its own table copy, up to ev_cap entries
+        if (vpos != INVALID && evs.size() > ev_cap) answer(EV_STOP, INVALID, 0);
+        else answer(EV_CONT, vpos, cb0 - cb);
+      }
       if (dbg) dbg_host += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h1).count();
+    }
+    } catch (...) {   // k_event_loop must not wait for an answer that never comes
+      if (live) answer(EV_STOP, INVALID, 0);
+      throw;
     }
   }
   if (dbg)

@@ -414,6 +414,47 @@ def test_partition_sequence_length(gpu_ctx, use_pos):
     assert res.first_size == np.count_nonzero(oparts == 0) and res.second_size == np.count_nonzero(oparts == 1)
 
 
+def _star_plus_rmat(scale, seed, leaves):
+    """RMAT records plus a star of `leaves` degree-1 vertices on a new centre: the centre's
+    elimination-tree node has `leaves` kids (above the event kernel's 4096 staged inline)."""
+    import sheep_amd
+    r = sheep_amd.rmat_host(scale, 16, seed)
+    t, h = r[:, 0].astype(np.uint32), r[:, 1].astype(np.uint32)
+    c = np.uint32(1 << scale)
+    lv = np.arange(c + 1, c + 1 + leaves, dtype=np.uint32)
+    return np.concatenate([t, lv]), np.concatenate([h, np.full(leaves, c, np.uint32)])
+
+
+@pytest.mark.parametrize("event_loop", [0, 1, 3, 4096])
+def test_partition_event_loop_variants(gpu_ctx, event_loop):
+    """sheep_tuning event_loop: one k_event launch per packing event (0), the persistent
+    k_event_loop handing over to per-event launches once its table outgrows 1 or 3 entries,
+    and the default (one launch, relaunched only behind a node whose kids k_event_kids
+    stages), each against the oracle's forwardPartition (partition.cpp:86-157)."""
+    import sheep_amd
+    t, h = _star_plus_rmat(16, 9, 6000)
+    w = np.ones(len(t), np.float32)
+    d = sheep_amd.records_to_device(t, h, w)
+    seq = oracle.sequence(t, h)
+    s = sheep_amd.degree_sequence(d)
+    assert np.array_equal(s.numpy(), seq)
+    tree = sheep_amd.build_tree(d, s)
+    p, pw = _tree_np(tree)
+    gpu_ctx.set_tuning(event_loop=event_loop)
+    try:
+        for k in (4, 64, 512):
+            res = sheep_amd.partition(s, tree, k)
+            oparts, oinfo = oracle.partition(p, pw, seq, k)
+            assert np.array_equal(res.numpy(), oparts), f"k={k}"
+            assert res.created == oinfo["created"] and res.packing_nodes == oinfo["packing_nodes"], f"k={k}"
+            if event_loop == 0:   # one k_event per event and one for the empty search
+                assert res.event_launches >= res.packing_nodes + 1
+            elif event_loop == 4096:   # k_event_loop, k_event_kids for the star's centre, k_event_loop again
+                assert res.event_launches <= 3, res.event_launches
+    finally:
+        gpu_ctx.set_tuning()
+
+
 def test_context_on_another_device(gpu_ctx):
     """Calls run on the context's device whatever device the calling thread has current."""
     import torch
