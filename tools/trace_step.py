@@ -43,7 +43,7 @@ def main():
                 cur = defaultdict(float)
                 lv.append(cur)
             if cur is not None and b in ("k_split_count", "k_split_write", "k_hook_round", "k_hook_finish", "k_light_top",
-                                         "k_cross_find", "k_cross_apply", "k_level_clean", "k_pack", "k_apply", "k_reduce"):
+                                         "k_cross_find", "k_cross_find_win", "k_cross_apply", "k_level_clean", "k_pack", "k_apply", "k_reduce"):
                 cur[b] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
         for i, d in enumerate(lv):
             print(f"level {i:2d} {sum(d.values()):7.3f} ms  " + " ".join(f"{k[2:]}={v:.3f}" for k, v in sorted(d.items())))
