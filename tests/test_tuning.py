@@ -46,6 +46,28 @@ def pairs_graph():
     return t, h
 
 
+def with_sequence_path(t, h):
+    """The graph plus an edge between every two vertices adjacent in its degree sequence:
+    every degree grows by 2 (the ends' by 1), so the order barely moves and every vertex
+    but the first has a neighbour right below it."""
+    import oracle
+    seq = oracle.sequence(t, h)
+    a, b = seq[:-1], seq[1:]
+    return np.concatenate([t, np.maximum(a, b)]), np.concatenate([h, np.minimum(a, b)])
+
+
+def cliques_graph(scale, size=34):
+    """Disjoint cliques of `size` vertices over [0, 2^scale): every degree is size - 1, so
+    positions are vid order; 16.5 edges per vertex in every block of positions (dense enough
+    for the top-block cut), and no block is one tree."""
+    g = np.arange(0, (1 << scale) - size + 1, size, dtype=np.uint32)
+    t, h = [], []
+    for a in range(size):
+        for b in range(a + 1, size):
+            t.append(g + b), h.append(g + a)
+    return np.concatenate(t), np.concatenate(h)
+
+
 # (graph, configurations): each configuration's "expect" lists regexes its debug block
 # must match (the branch it forces)
 TOP = r"etree top blocks after s (\d+): (\d+) block"
@@ -81,12 +103,25 @@ CASES = {
          "expect": [r"etree top blocks after s 14: [2-9] block"]},
         {"tune": {"top_bits": 12, "top_blocks": 9, "fin_map_bits": 10},
          "expect": [r"etree top blocks after s 12: [2-9] block"]},
-        {"tune": {"top_bits": 14, "big_bits": 17, "big_dense": 1}, "expect": [r"etree big cut after s 17:"]},
+        {"tune": {"top_bits": 14, "big_bits": 17, "big_dense": 1}, "expect": [r"etree big cut after s 17: .*-> kept"]},
+    ]),
+    # the same with a path through the sequence: every vertex but the lowest then has a
+    # lower neighbour, so the early cut's round 0 leaves one tree and the cut is made (small
+    # RMAT graphs alone leave thousands of trees: the cut is abandoned, above)
+    "rmat18ef64path": (lambda: with_sequence_path(*rmat_graph(18, 64, 18)), [
+        {"tune": {"top_bits": 14, "big_bits": 17, "big_dense": 1}, "merge": True,
+         "expect": [r"etree top blocks after s 14:", r"etree big cut after s 17: .*-> cut"]},
     ]),
     "pairs": (pairs_graph, [
         {"tune": {"top_bits": 16, "top_blocks": 1}, "merge": True,
          "expect": [r"etree top blocks after s 16: 1 block",
                     r"etree top round 0 block 0: components 45536 done 0 \(minima hbm\)"]},
+    ]),
+    # the early cut over the top half: round 0 leaves ~3,900 separate cliques there, so the
+    # cut is abandoned and the levels run as without it
+    "cliques18": (lambda: cliques_graph(18), [
+        {"tune": {"top_bits": 14, "big_bits": 17, "big_dense": 1}, "merge": True,
+         "expect": [r"etree top blocks after s 14:", r"etree big cut after s 17: .*-> kept"]},
     ]),
 }
 
