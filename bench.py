@@ -44,7 +44,8 @@ REGION_KERNELS = {"degree": ["k_degree_fused"], "relabel": ["k_relabel_scatter",
                   "etree_cross": ["k_cross_find"], "etree_apply": ["k_cross_apply", "k_level_clean"],
                   "etree_top": ["k_top_extract_multi", "k_top_sum_counts", "k_top_init", "k_top_min0_lds", "k_top_hook0",
                                 "k_top_round", "k_top_hook"],
-                  "evaluate": ["k_pp", "k_eval_records", "k_eval_nodes"]}
+                  "evaluate": ["k_pp", "k_eval_records", "k_eval_nodes", "k_parts_jnid", "k_eval_edges", "k_eval_loops",
+                               "k_eval_nodes_j"]}
 # the newest round's profile of this workload (profiles/rNN/), collected by tools/gpu/gpuprof.sh
 PMC_DIRS = ("r5", "r4", "r3")
 PMC_FILE = os.path.join(ROOT, "profiles", "{round}", "pmc_traffic_rmat{scale}_k{k}.json")
@@ -69,6 +70,8 @@ def parse():
     ap.add_argument("--shuffle", action="store_true",
                     help="records in a random order, half with tail/head swapped (a generic edge list)")
     ap.add_argument("--eval-reps", type=int, default=3, help="timed evaluator runs (0: skip)")
+    ap.add_argument("--eval-records", action="store_true",
+                    help="one GPU: also time the record evaluator (sheep_evaluate) beside the step-edge one")
     ap.add_argument("--cpu-scale", type=int, default=None,
                     help="RMAT scale of the CPU-baseline sample (default: the bench's own RMAT scale up to 26, else 22)")
     ap.add_argument("--cpu-configs", nargs="+", default=["8x1", "16x1"],
@@ -426,8 +429,8 @@ def time_evaluator(a, ctx, group, shard, subs, s, res, rank, world, dev, barrier
     for _ in range(a.eval_reps):
         barrier()
         t0 = time.perf_counter()
-        if world == 1 and a.shards == 1:
-            ev = sheep_amd.evaluate(shard, s, res.parts, what=sheep_amd.EVAL_DOWN, ctx=ctx)
+        if world == 1 and a.shards == 1:   # from the position-space edges the step's map left in HBM
+            ev = sheep_amd.evaluate(shard, s, res.parts, what=sheep_amd.EVAL_DOWN, ctx=ctx, from_step=True)
         elif world == 1:                                         # the shards' bitsets, then one node pass
             e = sheep_amd.ShardedEvaluator(s, res.parts, sheep_amd.EVAL_DOWN, ctx=ctx)
             for sub in subs:
@@ -454,6 +457,18 @@ def time_evaluator(a, ctx, group, shard, subs, s, res, rank, world, dev, barrier
         ms, launches, _ = ctx.timer("evaluate")
         if launches:
             out["device_ms"] = round(ms / launches, 3)
+    if world == 1 and a.shards == 1:
+        out["source"] = "the step's position-space edges (sheep_evaluate_step)"
+        if a.eval_records:   # the record evaluator (sheep_evaluate) on the same parts, for comparison
+            rt = []
+            for _ in range(a.eval_reps):
+                barrier()
+                t0 = time.perf_counter()
+                er = sheep_amd.evaluate(shard, s, res.parts, what=sheep_amd.EVAL_DOWN, ctx=ctx)
+                barrier()
+                rt.append(time.perf_counter() - t0)
+            assert er == ev, (er, ev)
+            out["records_ms"] = round(1e3 * min(rt), 3)
     out.update(pmc_region(a, world, "evaluate", 1))
     return out
 

@@ -242,6 +242,16 @@ int sheep_partition_pos(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n,
 int sheep_evaluate(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec,
                    const uint32_t *pos_dev, uint64_t pos_size, const int16_t *parts_vid_dev,
                    int what, sheep_eval *out);
+/* The same counts from the position-space edges the context's last map
+ * (sheep_build_tree over rec_dev[0, nrec) with this sequence: seq_dev[0, seq_n) and its
+ * index pos_dev[0, pos_size)) left grouped in HBM: no pass over the records unless they
+ * hold self-loops, and the random side of every edge reads jnid-indexed state (parts: 2 B
+ * per node, owner bits: 8 B per node per metric for k <= 64) instead of vid-indexed rows.
+ * SHEEP_ERR_ARG when the context's last map ran on other records or another sequence (or
+ * the context was trimmed since); the records must be unchanged since that map. */
+int sheep_evaluate_step(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec,
+                        const uint32_t *seq_dev, uint64_t seq_n, const uint32_t *pos_dev, uint64_t pos_size,
+                        const int16_t *parts_vid_dev, int what, sheep_eval *out);
 /* The same evaluators over edge shards (the records of one graph
  * split over devices or passes):
  *   sheep_eval_sizes      u64 words of the bitset and accumulator state for (what,

@@ -135,6 +135,7 @@ def lib() -> ctypes.CDLL:
         "sheep_partition": ([P, P, U64, P, U64, U64, P, I16, D, I32, I32, P, ctypes.POINTER(_PartInfo)], I32),
         "sheep_partition_pos": ([P, P, U64, P, U64, P, U64, P, I16, D, I32, I32, P, ctypes.POINTER(_PartInfo)], I32),
         "sheep_evaluate": ([P, P, U64, P, U64, P, I32, ctypes.POINTER(_Eval)], I32),
+        "sheep_evaluate_step": ([P, P, U64, P, U64, P, U64, P, I32, ctypes.POINTER(_Eval)], I32),
         "sheep_facts": ([P, P, U64, ctypes.POINTER(_Facts)], I32),
         "sheep_eval_sizes": ([I32, I32, U64, ctypes.POINTER(U64), ctypes.POINTER(U64)], I32),
         "sheep_eval_num_parts": ([P, P, U64, ctypes.POINTER(ctypes.c_int32)], I32),
@@ -528,12 +529,19 @@ def _cfmt(a: int, b: int) -> str:
 
 
 def evaluate(records, seq: Sequence, parts, what: int = 0, nrec: int | None = None,
-             ctx: Context | None = None) -> EvalResult:
+             ctx: Context | None = None, from_step: bool = False) -> EvalResult:
+    """Partition::evaluate(graph, seq) / evaluate(graph).  from_step: the same counts from the
+    position-space edges the context's last build_tree over these records and this sequence
+    left in HBM (sheep_evaluate_step; an error if it ran on anything else)."""
     ctx = ctx or default_context()
     nrec = records.shape[0] if nrec is None else nrec
     out = _Eval()
-    _check(lib().sheep_evaluate(ctx.handle, _ptr(records), nrec, _ptr(seq.pos), seq.pos_size, _ptr(parts), what,
-                                ctypes.byref(out)))
+    if from_step:
+        _check(lib().sheep_evaluate_step(ctx.handle, _ptr(records), nrec, _ptr(seq.seq), seq.n, _ptr(seq.pos),
+                                         seq.pos_size, _ptr(parts), what, ctypes.byref(out)))
+    else:
+        _check(lib().sheep_evaluate(ctx.handle, _ptr(records), nrec, _ptr(seq.pos), seq.pos_size, _ptr(parts), what,
+                                    ctypes.byref(out)))
     return EvalResult(*[getattr(out, f) for f, _ in _Eval._fields_])
 
 

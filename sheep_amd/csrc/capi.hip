@@ -37,6 +37,8 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
                     sheep_partition_info *info, const uint32_t *pos = nullptr);
 void evaluate(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
               const int16_t *parts, int what, sheep_eval *out);
+void evaluate_step(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *seq, uint64_t n, const uint32_t *pos,
+                   uint64_t pos_size, const int16_t *parts, int what, sheep_eval *out);
 void eval_sizes(int what, int nparts, uint64_t pos_size, uint64_t *bits_words, uint64_t *acc_words);
 int eval_num_parts(Ctx &c, const int16_t *parts, uint64_t pos_size);
 void eval_shard(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
@@ -119,6 +121,7 @@ int sheep_ctx_trim(sheep_ctx *ctx) {
   for (auto &kv : c.ws) if (kv.second.p) HIP_CHECK(hipFree(kv.second.p));
   c.ws.clear();
   c.head_layout = sheep::Ctx::HeadLayout();   // its offsets lived in the workspace
+  c.step_edges = sheep::Ctx::StepEdges();     // and the last map's grouped edges
   if (c.kid_spare.parent) {
     hipFree(c.kid_spare.parent); hipFree(c.kid_spare.koff); hipFree(c.kid_spare.kids); hipFree(c.kid_spare.kpar);
   }
@@ -416,6 +419,15 @@ int sheep_evaluate(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, const ui
   DeviceGuard dg(ctx);
   NEED(ctx && out && (rec || !nrec) && ((pos && parts_vid) || !pos_size), "null argument");
   sheep::evaluate(ctx->c, rec, nrec, pos, pos_size, parts_vid, what, out);
+  API_END
+}
+
+int sheep_evaluate_step(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *seq, uint64_t seq_n,
+                        const uint32_t *pos, uint64_t pos_size, const int16_t *parts_vid, int what, sheep_eval *out) {
+  API_BEGIN
+  DeviceGuard dg(ctx);
+  NEED(ctx && out && (rec || !nrec) && (seq || !seq_n) && ((pos && parts_vid) || !pos_size), "null argument");
+  sheep::evaluate_step(ctx->c, rec, nrec, seq, seq_n, pos, pos_size, parts_vid, what, out);
   API_END
 }
 

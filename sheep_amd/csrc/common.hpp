@@ -127,6 +127,17 @@ struct Ctx {
   // (hipFree waits for the device), ~1 ms of idle GPU per step at RMAT-26.
   struct KidBufs { uint32_t *parent = nullptr, *koff = nullptr, *kids = nullptr, *kpar = nullptr; uint64_t cap = 0; };
   KidBufs kid_spare;
+  // The last map's position-space edges, grouped by lo in the workspace bt_grouped
+  // (sheep_evaluate_step reads them): m_pairs edges came out of the relabel (DEAD ones
+  // included), m_valid of them are grouped.  Valid until the next map or sheep_ctx_trim.
+  struct StepEdges {
+    const void *rec = nullptr;
+    const uint32_t *pos = nullptr;
+    const uint64_t *edges = nullptr;
+    uint64_t nrec = 0, pos_size = 0, n = 0, m_pairs = 0, m_valid = 0;
+    bool valid = false;
+  };
+  StepEdges step_edges;
 
   bool timing = false;
   struct Timer { std::vector<std::pair<hipEvent_t, hipEvent_t>> pending; double ms = 0; uint64_t launches = 0; uint64_t bytes = 0; };
@@ -426,8 +437,8 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
                           uint64_t n_tree, uint32_t *pst, uint64_t *edges, unsigned long long *err,
                           const LoGroup *lg = nullptr, bool *counted = nullptr);
 void histogram_edge_lo(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t K, uint32_t *cnt);
-void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGroup &g, uint32_t *pst, uint64_t *r0,
-                       uint64_t *seg, bool counted);
+uint64_t group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGroup &g, uint32_t *pst, uint64_t *r0,
+                           uint64_t *seg, bool counted);
 // etree.hip
 // filt_lvl >= 0: at that level only entries with spread(lo) in [ylo, yhi) are kept (one
 // subproblem of a split merge; the caller cuts the later groups to it).  top_bits > 0: the

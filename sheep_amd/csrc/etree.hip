@@ -2488,6 +2488,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
 
 void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
                       uint64_t n, sheep_jnode *tree) {
+  c.step_edges = Ctx::StepEdges();
   uint32_t *pst = c.get_as<uint32_t>("bt_pst", n ? n : 1);
   uint32_t *parent = c.get_as<uint32_t>("bt_parent", n ? n : 1);
   HIP_CHECK(hipMemsetAsync(pst, 0, n * sizeof(uint32_t), c.stream));
@@ -2497,6 +2498,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
   unsigned long long *d = (unsigned long long *)c.d_scalars + 8;
   HIP_CHECK(hipMemsetAsync(d + 1, 0, sizeof(uint64_t), c.stream));
   uint64_t m = nrec;   // edges[i] per record, DEAD holes included (k_relabel)
+  bool bucketed = false;   // (k_relabel's edges keep one slot per record: no step edges for the evaluator)
   int L = 0;
   uint32_t clo = 0;
   LoGroup lg;
@@ -2510,6 +2512,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
     // head-bucketed relabel (hist.hip) when the key range fits its LDS buckets; it also
     // counts the edges for the grouping below
     m = relabel_bucketed(c, rec, nrec, pos, pos_size, n, pst, edges, d + 1, n >= 2 ? &lg : nullptr, &counted);
+    bucketed = m != UINT64_MAX;
     if (m == UINT64_MAX) {
       m = nrec;
       hipLaunchKernelGGL(k_relabel, dim3(grid_tiles(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos, pos_size, pst,
@@ -2526,7 +2529,19 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
     {
       // pst = histogram of the edges' lo; the same passes group the edges by lo
       TimedRegion tr(c, "pst_group", 20 * m);
-      group_edges_by_lo(c, edges, m, lg, pst, r0, seg, counted);
+      const uint64_t grouped = group_edges_by_lo(c, edges, m, lg, pst, r0, seg, counted);
+      if (bucketed && grouped != UINT64_MAX) {   // (read by sheep_evaluate_step until the next map)
+        Ctx::StepEdges &se = c.step_edges;
+        se.rec = rec;
+        se.nrec = nrec;
+        se.pos = pos;
+        se.pos_size = pos_size;
+        se.n = n;
+        se.edges = r0;
+        se.m_pairs = m;
+        se.m_valid = grouped;
+        se.valid = true;
+      }
     }
     TimedRegion tr(c, "etree", 8 * m);
     etree_from_edges(c, r0, m, n, parent, seg, c.tune.fin_map_bits, -1, 0, 0, c.tune.top_bits, c.tune.hook_batch >= 2);

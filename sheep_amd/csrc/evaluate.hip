@@ -363,6 +363,228 @@ void evaluate(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, 
   }
 }
 
+namespace {
+
+// ---- the same counts from the map's position-space edges --------------------------------
+// A map (relabel_and_tree) leaves every non-loop record as a tree edge (hi << 32 | lo) of
+// positions, grouped by lo, in HBM (Ctx::step_edges).  In position space both evaluators'
+// owners come from the jnid-indexed parts pj (2 B per node: cache-resident) and, for the
+// hash owner, seq (the vids): down = part(lo), up = part(hi), hash = the part of the
+// endpoint with the smaller cormen hash, Vcom = the other endpoint's part.  The lo side's
+// bit words lie in the group's 2^15-position window; the hi side's are random over a
+// row array of n * M * W64 words (262 MB for one metric at RMAT-26, 1.07 GB for the record
+// evaluator's vid-indexed 16-B rows).  Self-loops are no edges: when the records hold any
+// (nrec != the relabel's pair count) one pass over the records adds each loop vertex's own
+// part to its sets and counts them; an endpoint without a position or a part is the
+// reference's pos.at() throw, as in k_eval_records.
+__global__ void k_parts_jnid(const uint32_t *__restrict__ seq, uint64_t n, const int16_t *__restrict__ parts_vid,
+                             uint64_t pos_size, int16_t *__restrict__ pj, unsigned long long *__restrict__ bad) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  bool b = false;
+  for (uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; x < n; x += stride) {
+    const uint32_t v = seq[x];
+    const int16_t p = v < pos_size ? parts_vid[v] : (int16_t)-1;
+    b |= p < 0;
+    pj[x] = p;
+  }
+  if (__any(b) && (threadIdx.x & 63) == 0) atomicAdd(bad, 1ull);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_eval_edges(const uint64_t *__restrict__ edges, uint64_t m,
+                                                      const int16_t *__restrict__ pj, const uint32_t *__restrict__ seq,
+                                                      int what, int M, uint32_t W64, int nparts,
+                                                      unsigned long long *__restrict__ bits,
+                                                      unsigned long long *__restrict__ acc) {
+  const uint32_t RW = (uint32_t)M * W64;
+  unsigned long long *const bal = acc + AC_SCAL;
+  __shared__ uint32_t lbal[3][LDS_PARTS];
+  const bool lds = nparts <= LDS_PARTS;
+  if (lds)
+    for (int i = threadIdx.x; i < 3 * LDS_PARTS; i += BLOCK) (&lbal[0][0])[i] = 0;
+  __syncthreads();
+  const int ad = (what & 2) ? 0 : -1;
+  const int au = (what & 4) ? ((what & 2) ? 1 : 0) : -1;
+  const int ah = (what & 1) ? M - 2 : -1, av = (what & 1) ? M - 1 : -1;
+  const bool need_hi = (what & 5) != 0;   // up, hash and Vcom read the hi end's part
+  uint64_t cut = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) {
+    const uint64_t e = edges[i];
+    const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
+    const int pl = pj[lo], ph = need_hi ? pj[hi] : 0;
+    int po = 0;
+    if (what & 1) {
+      po = cormen_hash(seq[lo]) < cormen_hash(seq[hi]) ? pl : ph;
+      cut += pl != ph;
+    }
+    if (ad >= 0) { if (lds) atomicAdd(&lbal[0][pl], 1u); else atomicAdd(&bal[pl], 1ull); }
+    if (au >= 0) { if (lds) atomicAdd(&lbal[1][ph], 1u); else atomicAdd(&bal[nparts + ph], 1ull); }
+    if (ah >= 0) { if (lds) atomicAdd(&lbal[2][po], 1u); else atomicAdd(&bal[2 * nparts + po], 1ull); }
+    const int own_lo[4] = {pl, ph, po, ph};   // down, up, hash, Vcom owner seen from lo
+    const int own_hi[4] = {pl, ph, po, pl};   // ... and from hi
+    const int arr[4] = {ad, au, ah, av};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (arr[q] < 0) continue;   // uniform
+      or_bits(bits, (uint64_t)lo * RW + arr[q] * W64 + (own_lo[q] >> 6), 1ull << (own_lo[q] & 63));
+      or_bits(bits, (uint64_t)hi * RW + arr[q] * W64 + (own_hi[q] >> 6), 1ull << (own_hi[q] & 63));
+    }
+  }
+  block_atomic_add(&acc[AC_CUT], cut);
+  __syncthreads();
+  if (lds)
+    for (int x = threadIdx.x; x < 3 * nparts; x += BLOCK) {
+      const uint32_t v = lbal[x / nparts][x % nparts];
+      if (v) atomicAdd(&bal[x], (unsigned long long)v);
+    }
+}
+
+// self-loops (own part into every requested set of the vertex) and the records the edges
+// do not account for: loops counted, an endpoint without a position is bad
+__global__ __launch_bounds__(BLOCK) void k_eval_loops(const sheep_xs1 *__restrict__ rec, uint64_t nrec,
+                                                      const uint32_t *__restrict__ pos, uint64_t pos_size,
+                                                      const int16_t *__restrict__ pj, int what, int M, uint32_t W64,
+                                                      unsigned long long *__restrict__ bits,
+                                                      unsigned long long *__restrict__ acc) {
+  const uint32_t RW = (uint32_t)M * W64;
+  uint64_t loops = 0, bad = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nrec; i += stride) {
+    const sheep_xs1 r = rec[i];
+    const uint32_t pt = r.tail < pos_size ? pos[r.tail] : INVALID, ph = r.head < pos_size ? pos[r.head] : INVALID;
+    if (pt == INVALID || ph == INVALID) { ++bad; continue; }
+    if (r.tail != r.head) continue;
+    ++loops;
+    const int p = pj[pt];
+    for (int a = 0; a < M; ++a) or_bits(bits, (uint64_t)pt * RW + a * W64 + (p >> 6), 1ull << (p & 63));
+  }
+  block_atomic_add(&acc[AC_LOOPS], loops);
+  block_atomic_add(&acc[AC_BAD], bad);
+}
+
+// per jnid: as k_eval_nodes over the jnid rows (no pp word), parts by jnid
+__global__ __launch_bounds__(BLOCK) void k_eval_nodes_j(uint64_t n, const int16_t *__restrict__ pj, int what, int M,
+                                                        uint32_t W64, int nparts,
+                                                        const unsigned long long *__restrict__ bits,
+                                                        unsigned long long *__restrict__ vbal,
+                                                        unsigned long long *__restrict__ out) {
+  __shared__ uint32_t lv[LDS_PARTS];
+  const bool lds = nparts <= LDS_PARTS;
+  if (lds)
+    for (int i = threadIdx.x; i < LDS_PARTS; i += BLOCK) lv[i] = 0;
+  __syncthreads();
+  const int ad = (what & 2) ? 0 : -1;
+  const int au = (what & 4) ? ((what & 2) ? 1 : 0) : -1;
+  const int ah = (what & 1) ? M - 2 : -1, av = (what & 1) ? M - 1 : -1;
+  uint64_t s[4] = {0, 0, 0, 0}, nodes = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; x < n; x += stride) {
+    const unsigned long long *b = bits + x * (uint64_t)M * W64;
+    bool node = false;
+    for (uint32_t w = 0; w < W64; ++w) node |= b[w] != 0;
+    if (!node) continue;
+    ++nodes;
+    const int p = pj[x];
+    const int arr[4] = {ad, au, ah, av};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (arr[q] < 0) continue;
+      uint32_t cnt = 0;
+      for (uint32_t w = 0; w < W64; ++w) {
+        uint64_t v = b[arr[q] * W64 + w];
+        if (q == 3 && (uint32_t)(p >> 6) == w) v |= 1ull << (p & 63);   // Vcom: own part
+        cnt += __popcll(v);
+      }
+      s[q] += cnt - 1;
+    }
+    if (av >= 0 && p < nparts) {
+      if (lds) atomicAdd(&lv[p], 1u); else atomicAdd(&vbal[p], 1ull);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) block_atomic_add(&out[q], s[q]);
+  block_atomic_add(&out[4], nodes);
+  __syncthreads();
+  if (lds)
+    for (int x = threadIdx.x; x < nparts; x += BLOCK)
+      if (lv[x]) atomicAdd(&vbal[x], (unsigned long long)lv[x]);
+}
+
+}  // namespace
+
+// sheep_evaluate's counts from the edges the context's last map left (Ctx::step_edges):
+// the records, sequence and index must be the ones that map ran on.
+void evaluate_step(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *seq, uint64_t n, const uint32_t *pos,
+                   uint64_t pos_size, const int16_t *parts, int what, sheep_eval *out) {
+  const Ctx::StepEdges se = c.step_edges;
+  if (!se.valid || se.rec != rec || se.nrec != nrec || se.pos != pos || se.pos_size != pos_size || se.n != n)
+    throw Error(SHEEP_ERR_ARG, "evaluate_step: the context's last map did not run on these records and this sequence");
+  uint64_t words = 0, aw = 0;
+  eval_sizes(what, 1, pos_size, &words, &aw);   // validates `what`
+  if (what == 0) what = 7;
+  const int nparts = eval_num_parts(c, parts, pos_size);
+  const int M = eval_arrays(what);
+  const uint32_t W64 = (uint32_t)((nparts + 63) / 64);
+  aw = AC_SCAL + 3 * (uint64_t)nparts;
+  words = n * (uint64_t)M * W64;
+  uint64_t *bits = c.get_as<uint64_t>("ev_bits", words ? words : 1);
+  uint64_t *acc = c.get_as<uint64_t>("ev_acc", aw);
+  int16_t *pj = c.get_as<int16_t>("ev_pj", n ? n : 1);
+  unsigned long long *vbal = c.get_as<unsigned long long>("ev_vbal", (uint64_t)nparts);
+  unsigned long long *res = (unsigned long long *)c.d_scalars + 48;   // ecv down, up, hash, vcom, nodes
+  unsigned long long *pbad = (unsigned long long *)c.d_scalars + 53;
+  *out = sheep_eval();
+  {
+    // B_eval as sheep_evaluate's (the evaluation's algorithmic bytes)
+    TimedRegion tr(c, "evaluate", 28 * nrec + 2 * (uint64_t)M * W64 * 8 * pos_size);
+    HIP_CHECK(hipMemsetAsync(bits, 0, words * sizeof(uint64_t), c.stream));
+    HIP_CHECK(hipMemsetAsync(acc, 0, aw * sizeof(uint64_t), c.stream));
+    HIP_CHECK(hipMemsetAsync(vbal, 0, (uint64_t)nparts * sizeof(uint64_t), c.stream));
+    HIP_CHECK(hipMemsetAsync(res, 0, 6 * sizeof(uint64_t), c.stream));
+    if (n) {
+      hipLaunchKernelGGL(k_parts_jnid, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, seq, n, parts, pos_size, pj, pbad);
+      LAUNCH_CHECK();
+    }
+    if (se.m_valid) {
+      hipLaunchKernelGGL(k_eval_edges, dim3(grid_for(se.m_valid)), dim3(BLOCK), 0, c.stream, se.edges, se.m_valid,
+                         (const int16_t *)pj, seq, what, M, W64, nparts, (unsigned long long *)bits,
+                         (unsigned long long *)acc);
+      LAUNCH_CHECK();
+    }
+    if (se.m_pairs != nrec) {   // self-loops or endpoints past the index: the records say which
+      hipLaunchKernelGGL(k_eval_loops, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, pos, pos_size,
+                         (const int16_t *)pj, what, M, W64, (unsigned long long *)bits, (unsigned long long *)acc);
+      LAUNCH_CHECK();
+    }
+    if (n) {
+      hipLaunchKernelGGL(k_eval_nodes_j, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, n, (const int16_t *)pj, what, M,
+                         W64, nparts, (const unsigned long long *)bits, vbal, res);
+      LAUNCH_CHECK();
+    }
+    std::vector<uint64_t> ha(aw), hv(nparts);
+    HIP_CHECK(hipMemcpyAsync(ha.data(), acc, aw * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipMemcpyAsync(hv.data(), vbal, (uint64_t)nparts * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipMemcpyAsync(c.h_scalars + 48, res, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+    // a DEAD edge (an endpoint without a position), a part < 0, or a bad record
+    if (se.m_valid != se.m_pairs || c.h_scalars[53] || ha[AC_BAD])
+      throw Error(SHEEP_ERR_RANGE, "evaluate: a vertex is unsequenced or unassigned");
+    auto mx = [&](const uint64_t *h) { uint64_t m = 0; for (int p = 0; p < nparts; ++p) m = h[p] > m ? h[p] : m; return m; };
+    const uint64_t *bal = ha.data() + AC_SCAL;
+    out->nodes = c.h_scalars[52];
+    out->edges = (2 * nrec - ha[AC_LOOPS]) / 2;
+    if (what & 2) { out->ecv_down = c.h_scalars[48]; out->max_down_bal = mx(bal); }
+    if (what & 4) { out->ecv_up = c.h_scalars[49]; out->max_up_bal = mx(bal + nparts); }
+    if (what & 1) {
+      out->ecv_hash = c.h_scalars[50];
+      out->vcom_vol = c.h_scalars[51];
+      out->edges_cut = ha[AC_CUT];
+      out->max_hash_bal = mx(bal + 2 * (uint64_t)nparts);
+      out->max_vertex_bal = mx(hv.data());
+    }
+  }
+}
+
 }  // namespace sheep
 
 // ---- partition files (partition.cpp:588-670 writePartitionedGraph) -----------------------

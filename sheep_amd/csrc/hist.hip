@@ -367,12 +367,13 @@ __global__ void k_bucket_starts(const uint32_t *__restrict__ off, uint64_t ntile
 // EdgeLoPadded, K its padded key range, kbase the counter index of each bucket's first
 // key, and the edges are also written to `grouped` in bucket order; bstart_out (nb + 1
 // entries, device) receives each bucket's first position there.
+// Returns the number of keys bucketed (UINT64_MAX on the one-atomic-per-key path).
 template <typename Src>
-void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint64_t *grouped = nullptr,
-                   const uint32_t *kbase = nullptr, uint32_t *bstart_out = nullptr,
-                   uint32_t *save_offsets = nullptr, std::vector<uint32_t> *save_bstart = nullptr,
-                   bool counted = false) {
-  if (n == 0 || K == 0) return;
+uint64_t histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint64_t *grouped = nullptr,
+                       const uint32_t *kbase = nullptr, uint32_t *bstart_out = nullptr,
+                       uint32_t *save_offsets = nullptr, std::vector<uint32_t> *save_bstart = nullptr,
+                       bool counted = false) {
+  if (n == 0 || K == 0) return 0;
   const uint32_t nb = (uint32_t)((K + W - 1) >> WBITS);
   const uint64_t ntiles = (n + TKEYS - 1) >> TLOG;
   const size_t lds_scatter = (2 * (size_t)nb + HB / WAVE + TKEYS) * 4;   // <= 160 KiB for nb <= 4087
@@ -389,7 +390,7 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
     } else {   // key ranges beyond the LDS buckets: one scattered atomic per key
       hipLaunchKernelGGL(k_count_atomic<Src>, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, src, n, cnt);
       LAUNCH_CHECK();
-      return;
+      return UINT64_MAX;
     }
   }
   for (const void *f : {(const void *)k_hist_scatter<HeadKeys>, (const void *)k_hist_scatter<EdgeLoKeys>,
@@ -448,7 +449,8 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
     std::copy(bstart, bstart + nb + 1, bs);
     HIP_CHECK(hipMemcpyAsync(bstart_out, bs, (nb + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
   }
-  if (!nch) return;
+  const uint64_t keys_total = bstart[nb];
+  if (!nch) return keys_total;
   Chunk *chunks = (Chunk *)c.get_pinned("hist_chunks_host", nch * sizeof(Chunk));
   uint64_t j = 0;
   for (uint32_t b = 0; b < nb; ++b) {
@@ -462,6 +464,7 @@ void histogram_add(Ctx &c, Src src, uint64_t n, uint64_t K, uint32_t *cnt, uint6
   hipLaunchKernelGGL(k_hist_final, dim3((unsigned)nch), dim3(HB), W * 4, c.stream, (const uint16_t *)keys,
                      (const Chunk *)dch, K, kbase, cnt);
   LAUNCH_CHECK();
+  return keys_total;
 }
 
 
@@ -1066,13 +1069,13 @@ void lo_group_prepare(Ctx &c, uint64_t n, int L, uint32_t clo, LoGroup &g) {
   c.sync();   // the layout's host vectors are the copies' sources
 }
 
-void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGroup &g, uint32_t *pst, uint64_t *r0,
-                       uint64_t *seg, bool counted) {
+uint64_t group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGroup &g, uint32_t *pst, uint64_t *r0,
+                           uint64_t *seg, bool counted) {
   const int L = g.L;
   uint32_t *d_bstart = c.get_as<uint32_t>("grp_bstart", g.nb + 1);
   HIP_CHECK(hipMemsetAsync(d_bstart, 0, (g.nb + 1) * sizeof(uint32_t), c.stream));
-  histogram_add(c, EdgeLoPadded{edges, g.d_pad, g.clo, g.mask}, m, g.K, pst, r0, g.d_kbase, d_bstart, nullptr, nullptr,
-                counted);
+  const uint64_t grouped = histogram_add(c, EdgeLoPadded{edges, g.d_pad, g.clo, g.mask}, m, g.K, pst, r0, g.d_kbase,
+                                         d_bstart, nullptr, nullptr, counted);
   // (pinned: no sync for the copy; histogram_add's sync above ordered any earlier use)
   uint64_t *hseg = (uint64_t *)c.get_pinned("grp_segb_host", 2 * (size_t)L * sizeof(uint64_t));
   for (int s = 0; s < L; ++s) { hseg[s] = g.pstart[s] / W; hseg[L + s] = (g.pstart[s] + g.plen[s]) / W; }
@@ -1081,6 +1084,7 @@ void group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGroup 
   hipLaunchKernelGGL(k_seg_from_buckets, dim3(1), dim3(64), 0, c.stream, (const uint32_t *)d_bstart,
                      (const uint64_t *)d_sb, L, seg);
   LAUNCH_CHECK();
+  return grouped;
 }
 
 }  // namespace sheep

@@ -414,6 +414,72 @@ def test_partition_sequence_length(gpu_ctx, use_pos):
     assert res.first_size == np.count_nonzero(oparts == 0) and res.second_size == np.count_nonzero(oparts == 1)
 
 
+@pytest.mark.parametrize("name", GRAPHS)
+def test_evaluate_from_step_edges(gpu_ctx, name):
+    """sheep_evaluate_step: every count from the map's position-space edges equals the record
+    evaluator's (and the golden stdout), for each metric set — the golden graphs include
+    self-loops, repeated records and isolated slots (`edge`)."""
+    import sheep_amd
+    rec = golden_records(name)
+    s = sheep_amd.sequence_from_host(golden_seq(name))
+    d = _dev_records(rec)
+    tree = sheep_amd.build_tree(d, s)
+    assert np.array_equal(_tree_np(tree)[0], golden_tree(name)[0])
+    kids = sheep_amd.KidTable(tree)
+    _, blocks = golden_part_text(name)
+    for k, block in zip(ks(name), blocks):
+        res = sheep_amd.partition(s, tree, k, kids=kids)
+        for what in (1, 2, 4, 6, 0):
+            a = sheep_amd.evaluate(d, s, res.parts, what=what)
+            b = sheep_amd.evaluate(d, s, res.parts, what=what, from_step=True)
+            assert a == b, (k, what, a, b)
+        assert res.print_text() + b.text(k) == block, f"k={k}"   # (b: every metric)
+
+
+def test_evaluate_from_step_edges_needs_that_map(gpu_ctx):
+    """The step edges belong to the last map over these records and this sequence: other
+    records, another sequence, or a trimmed context are an argument error, not a result."""
+    import sheep_amd
+    rec, rec2 = golden_records("rmat12"), golden_records("rmat14")
+    s, s2 = sheep_amd.sequence_from_host(golden_seq("rmat12")), sheep_amd.sequence_from_host(golden_seq("rmat14"))
+    d, d2 = _dev_records(rec), _dev_records(rec2)
+    tree = sheep_amd.build_tree(d, s)
+    res = sheep_amd.partition(s, tree, 4)
+    ok = sheep_amd.evaluate(d, s, res.parts, from_step=True)
+    assert ok == sheep_amd.evaluate(d, s, res.parts)
+    tree2 = sheep_amd.build_tree(d2, s2)   # the context's last map is now another graph's
+    with pytest.raises(ValueError):
+        sheep_amd.evaluate(d, s, res.parts, from_step=True)
+    res2 = sheep_amd.partition(s2, tree2, 4)
+    assert sheep_amd.evaluate(d2, s2, res2.parts, from_step=True) == sheep_amd.evaluate(d2, s2, res2.parts)
+    gpu_ctx.trim()
+    with pytest.raises(ValueError):
+        sheep_amd.evaluate(d2, s2, res2.parts, from_step=True)
+
+
+@pytest.mark.parametrize("scale,seed,k", [(16, 5, 16), (18, 7, 64)])
+def test_evaluate_from_step_edges_rmat(gpu_ctx, scale, seed, k):
+    """Larger RMAT graphs, with the records' self-loops and repeats added: the step-edge
+    evaluator against the record evaluator and the oracle's counts."""
+    import sheep_amd
+    h = sheep_amd.rmat_host(scale, 16, seed)
+    t_, h_ = h[:, 0].astype(np.uint32), h[:, 1].astype(np.uint32)
+    extra = np.arange(0, 1 << scale, 97, dtype=np.uint32)   # self-loops on some vertices with edges
+    extra = extra[np.isin(extra, np.concatenate([t_, h_]))]
+    t_ = np.concatenate([t_, extra, t_[:1000]])
+    h_ = np.concatenate([h_, extra, h_[:1000]])
+    d = sheep_amd.records_to_device(t_, h_, np.ones(len(t_), np.float32))
+    s = sheep_amd.degree_sequence(d)
+    tree = sheep_amd.build_tree(d, s)
+    res = sheep_amd.partition(s, tree, k)
+    a = sheep_amd.evaluate(d, s, res.parts)
+    b = sheep_amd.evaluate(d, s, res.parts, from_step=True)
+    assert a == b
+    o = oracle.evaluate(t_, h_, s.numpy(), res.numpy())
+    assert (b.edges_cut, b.vcom_vol, b.ecv_hash, b.ecv_down, b.ecv_up) == \
+        (o["edges_cut"], o["vcom_vol"], o["ecv_hash"], o["ecv_down"], o["ecv_up"])
+
+
 def _star_plus_rmat(scale, seed, leaves):
     """RMAT records plus a star of `leaves` degree-1 vertices on a new centre: the centre's
     elimination-tree node has `leaves` kids (above the event kernel's 4096 staged inline)."""

@@ -23,7 +23,8 @@ import csv
 import json
 from collections import defaultdict
 
-EVAL_KERNELS = ("k_pp", "k_eval_records", "k_eval_nodes", "k_max_part")
+EVAL_KERNELS = ("k_pp", "k_eval_records", "k_eval_nodes", "k_max_part", "k_parts_jnid", "k_eval_edges", "k_eval_loops",
+                "k_eval_nodes_j")
 
 
 def per_kernel(path):
