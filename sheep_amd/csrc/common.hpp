@@ -134,6 +134,7 @@ struct Ctx {
     const void *rec = nullptr;
     const uint32_t *pos = nullptr;
     const uint64_t *edges = nullptr;
+    const uint32_t *pst = nullptr;   // per jnid: edges with that lo (bt_pst; DEAD edges add to it too)
     uint64_t nrec = 0, pos_size = 0, n = 0, m_pairs = 0, m_valid = 0;
     bool valid = false;
   };

@@ -2538,6 +2538,7 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
         se.pos_size = pos_size;
         se.n = n;
         se.edges = r0;
+        se.pst = pst;
         se.m_pairs = m;
         se.m_valid = grouped;
         se.valid = true;

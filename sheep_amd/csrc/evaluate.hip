@@ -373,7 +373,11 @@ namespace {
 // endpoint with the smaller cormen hash, Vcom = the other endpoint's part.  The lo side's
 // bit words lie in the group's 2^15-position window; the hi side's are random over a
 // row array of n * M * W64 words (262 MB for one metric at RMAT-26, 1.07 GB for the record
-// evaluator's vid-indexed 16-B rows).  Self-loops are no edges: when the records hold any
+// evaluator's vid-indexed 16-B rows).  A vertex's OWN part enters two sets without any
+// per-edge bit: ECV(down) at lo iff the vertex is the lo end of an edge (pst > 0: the map's
+// lo histogram), ECV(up) at hi through a byte flag (a plain store, no atomic) — the per-edge
+// read-and-atomicOr of the lo's own down bit cost 7 of the 17.6 ms at RMAT-26, its lines
+// shared by the eight XCDs.  Self-loops are no edges: when the records hold any
 // (nrec != the relabel's pair count) one pass over the records adds each loop vertex's own
 // part to its sets and counts them; an endpoint without a position or a part is the
 // reference's pos.at() throw, as in k_eval_records.
@@ -394,6 +398,7 @@ __global__ __launch_bounds__(BLOCK) void k_eval_edges(const uint64_t *__restrict
                                                       const int16_t *__restrict__ pj, const uint32_t *__restrict__ seq,
                                                       int what, int M, uint32_t W64, int nparts,
                                                       unsigned long long *__restrict__ bits,
+                                                      uint8_t *__restrict__ up_own,
                                                       unsigned long long *__restrict__ acc) {
   const uint32_t RW = (uint32_t)M * W64;
   unsigned long long *const bal = acc + AC_SCAL;
@@ -426,9 +431,12 @@ __global__ __launch_bounds__(BLOCK) void k_eval_edges(const uint64_t *__restrict
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (arr[q] < 0) continue;   // uniform
-      or_bits(bits, (uint64_t)lo * RW + arr[q] * W64 + (own_lo[q] >> 6), 1ull << (own_lo[q] & 63));
-      or_bits(bits, (uint64_t)hi * RW + arr[q] * W64 + (own_hi[q] >> 6), 1ull << (own_hi[q] & 63));
+      if (q != 0)   // (down at lo: lo's own part, from pst in the node pass)
+        or_bits(bits, (uint64_t)lo * RW + arr[q] * W64 + (own_lo[q] >> 6), 1ull << (own_lo[q] & 63));
+      if (q != 1)   // (up at hi: hi's own part, flagged below)
+        or_bits(bits, (uint64_t)hi * RW + arr[q] * W64 + (own_hi[q] >> 6), 1ull << (own_hi[q] & 63));
     }
+    if (au >= 0) up_own[hi] = 1;
   }
   block_atomic_add(&acc[AC_CUT], cut);
   __syncthreads();
@@ -466,6 +474,8 @@ __global__ __launch_bounds__(BLOCK) void k_eval_loops(const sheep_xs1 *__restric
 __global__ __launch_bounds__(BLOCK) void k_eval_nodes_j(uint64_t n, const int16_t *__restrict__ pj, int what, int M,
                                                         uint32_t W64, int nparts,
                                                         const unsigned long long *__restrict__ bits,
+                                                        const uint32_t *__restrict__ pst,
+                                                        const uint8_t *__restrict__ up_own,
                                                         unsigned long long *__restrict__ vbal,
                                                         unsigned long long *__restrict__ out) {
   __shared__ uint32_t lv[LDS_PARTS];
@@ -480,11 +490,13 @@ __global__ __launch_bounds__(BLOCK) void k_eval_nodes_j(uint64_t n, const int16_
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; x < n; x += stride) {
     const unsigned long long *b = bits + x * (uint64_t)M * W64;
-    bool node = false;
+    const int p = pj[x];
+    // the own-part entries the edge pass left out: down (x is some edge's lo), up (flag)
+    const bool own[4] = {ad >= 0 && pst[x] != 0, au >= 0 && up_own[x] != 0, false, true};
+    bool node = own[ad >= 0 ? 0 : 1];   // (the first array: an own entry alone makes a node)
     for (uint32_t w = 0; w < W64; ++w) node |= b[w] != 0;
     if (!node) continue;
     ++nodes;
-    const int p = pj[x];
     const int arr[4] = {ad, au, ah, av};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -492,7 +504,7 @@ __global__ __launch_bounds__(BLOCK) void k_eval_nodes_j(uint64_t n, const int16_
       uint32_t cnt = 0;
       for (uint32_t w = 0; w < W64; ++w) {
         uint64_t v = b[arr[q] * W64 + w];
-        if (q == 3 && (uint32_t)(p >> 6) == w) v |= 1ull << (p & 63);   // Vcom: own part
+        if (own[q] && (uint32_t)(p >> 6) == w) v |= 1ull << (p & 63);   // Vcom: always; down / up: as flagged
         cnt += __popcll(v);
       }
       s[q] += cnt - 1;
@@ -530,6 +542,7 @@ void evaluate_step(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *
   uint64_t *bits = c.get_as<uint64_t>("ev_bits", words ? words : 1);
   uint64_t *acc = c.get_as<uint64_t>("ev_acc", aw);
   int16_t *pj = c.get_as<int16_t>("ev_pj", n ? n : 1);
+  uint8_t *up_own = c.get_as<uint8_t>("ev_upown", n ? n : 1);
   unsigned long long *vbal = c.get_as<unsigned long long>("ev_vbal", (uint64_t)nparts);
   unsigned long long *res = (unsigned long long *)c.d_scalars + 48;   // ecv down, up, hash, vcom, nodes
   unsigned long long *pbad = (unsigned long long *)c.d_scalars + 53;
@@ -541,13 +554,14 @@ void evaluate_step(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *
     HIP_CHECK(hipMemsetAsync(acc, 0, aw * sizeof(uint64_t), c.stream));
     HIP_CHECK(hipMemsetAsync(vbal, 0, (uint64_t)nparts * sizeof(uint64_t), c.stream));
     HIP_CHECK(hipMemsetAsync(res, 0, 6 * sizeof(uint64_t), c.stream));
+    if (what & 4) HIP_CHECK(hipMemsetAsync(up_own, 0, n, c.stream));
     if (n) {
       hipLaunchKernelGGL(k_parts_jnid, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, seq, n, parts, pos_size, pj, pbad);
       LAUNCH_CHECK();
     }
     if (se.m_valid) {
       hipLaunchKernelGGL(k_eval_edges, dim3(grid_for(se.m_valid)), dim3(BLOCK), 0, c.stream, se.edges, se.m_valid,
-                         (const int16_t *)pj, seq, what, M, W64, nparts, (unsigned long long *)bits,
+                         (const int16_t *)pj, seq, what, M, W64, nparts, (unsigned long long *)bits, up_own,
                          (unsigned long long *)acc);
       LAUNCH_CHECK();
     }
@@ -558,7 +572,7 @@ void evaluate_step(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *
     }
     if (n) {
       hipLaunchKernelGGL(k_eval_nodes_j, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, n, (const int16_t *)pj, what, M,
-                         W64, nparts, (const unsigned long long *)bits, vbal, res);
+                         W64, nparts, (const unsigned long long *)bits, se.pst, (const uint8_t *)up_own, vbal, res);
       LAUNCH_CHECK();
     }
     std::vector<uint64_t> ha(aw), hv(nparts);
