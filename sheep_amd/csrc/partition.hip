@@ -1198,121 +1198,121 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
     TimedRegion tr(c, "partition_events");
     hdr[7] = 0;
     try {
-    for (;;) {
-      if (!live) {   // k_event for this event, or k_event_loop from it on (both read the table as written now)
-        write_table(false);
-        const bool by_arg = m_ev <= EV_ARG;
-        if (ev_cap && m_ev <= ev_cap) {
-          hipLaunchKernelGGL(k_event_loop, dim3(gev), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh,
-                             (const uint64_t *)SH, (const uint32_t *)hst, (const uint32_t *)hen,
-                             by_arg ? nullptr : t_pos, by_arg ? nullptr : t_pre, m_ev, max_component, evprev, found,
-                             done_ctr, (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
-                             (const uint32_t *)core.parent, (const uint32_t *)core.koff, (const uint32_t *)t.tD,
-                             (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren, d_hdr, d_kids, d_r,
-                             seq_no, evarg, d_rep, go, (uint64_t)EV_TIMEOUT_S * 100000000ull);
-          live = true;
-          info->event_launches++;
-        } else {
-          hipLaunchKernelGGL(k_event, dim3(gev), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh,
-                             (const uint64_t *)SH, (const uint32_t *)hst, (const uint32_t *)hen,
-                             by_arg ? nullptr : t_pos, by_arg ? nullptr : t_pre, m_ev, max_component, evprev, found,
-                             done_ctr, (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
-                             (const uint32_t *)core.parent, (const uint32_t *)core.koff, (const uint32_t *)t.tD,
-                             (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren, d_hdr, d_kids, d_r,
-                             seq_no + 1, evarg);
-          info->event_launches++;
+      for (;;) {
+        if (!live) {   // k_event for this event, or k_event_loop from it on (both read the table as written now)
+          write_table(false);
+          const bool by_arg = m_ev <= EV_ARG;
+          if (ev_cap && m_ev <= ev_cap) {
+            hipLaunchKernelGGL(k_event_loop, dim3(gev), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh,
+                               (const uint64_t *)SH, (const uint32_t *)hst, (const uint32_t *)hen,
+                               by_arg ? nullptr : t_pos, by_arg ? nullptr : t_pre, m_ev, max_component, evprev, found,
+                               done_ctr, (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
+                               (const uint32_t *)core.parent, (const uint32_t *)core.koff, (const uint32_t *)t.tD,
+                               (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren, d_hdr, d_kids, d_r,
+                               seq_no, evarg, d_rep, go, (uint64_t)EV_TIMEOUT_S * 100000000ull);
+            live = true;
+            info->event_launches++;
+          } else {
+            hipLaunchKernelGGL(k_event, dim3(gev), dim3(BLOCK), 0, c.stream, (const uint32_t *)hids, nh,
+                               (const uint64_t *)SH, (const uint32_t *)hst, (const uint32_t *)hen,
+                               by_arg ? nullptr : t_pos, by_arg ? nullptr : t_pre, m_ev, max_component, evprev, found,
+                               done_ctr, (const uint32_t *)k->koff, (const uint32_t *)k->kids, (const uint64_t *)S,
+                               (const uint32_t *)core.parent, (const uint32_t *)core.koff, (const uint32_t *)t.tD,
+                               (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren, d_hdr, d_kids, d_r,
+                               seq_no + 1, evarg);
+            info->event_launches++;
+          }
+          LAUNCH_CHECK();
         }
-        LAUNCH_CHECK();
-      }
-      ++seq_no;
-      const auto h0 = std::chrono::steady_clock::now();
-      wait_stage(seq_no);
-      const auto h1 = std::chrono::steady_clock::now();
-      if (dbg) {
-        dbg_tab += hdr[8] / 100.0;   // wall_clock64: 100 MHz
-        dbg_search += hdr[9] / 100.0;
-        dbg_stage += hdr[10] / 100.0;
-        dbg_wait += std::chrono::duration<double, std::micro>(h1 - h0).count();
-      }
-      const uint32_t v = hdr[0];
-      if (dbg && live)
-        fprintf(stderr, "partition event %u: hits %.1f scan %.1f done %.1f stage %.1f us, from %u, wait %.1f us\n", seq_no,
-                hdr[11] / 100.0, hdr[12] / 100.0, hdr[13] / 100.0, hdr[10] / 100.0, hdr[14],
-                std::chrono::duration<double, std::micro>(h1 - h0).count());
-      if (v == INVALID) {
-        if (live) answer(EV_STOP, INVALID, 0);
-        break;
-      }
-      info->packing_nodes++;
-      const uint32_t beg = hdr[1], cnt = hdr[2], vpos = hdr[5];
-      uint64_t cb = (uint64_t)hdr[3] | ((uint64_t)hdr[4] << 32);
-      if (!hdr[6]) {   // more kids than the event kernel stages: k_event_kids, behind k_event_loop's end
-        if (live) answer(EV_STOP, INVALID, 0);
-        write_table(false);
-        stage_kids_of(0, EV_STAGE, d_kids, d_r);
-      }
-      seg.assign(st_kids, st_kids + std::min(cnt, EV_STAGE));
-      segR.assign(st_r, st_r + std::min(cnt, EV_STAGE));
-      if (cnt > EV_STAGE) {   // a node with more kids than the staging area: fetch the rest
-        seg.resize(cnt); segR.resize(cnt);
-        uint32_t *kk = c.get_as<uint32_t>("pt_kK", cnt);
-        uint64_t *kR = c.get_as<uint64_t>("pt_kR", cnt);
-        stage_kids_of(EV_STAGE, cnt - EV_STAGE, kk, kR);
-        d2h(c, seg.data() + EV_STAGE, (const uint32_t *)kk, cnt - EV_STAGE);
-        d2h(c, segR.data() + EV_STAGE, (const uint64_t *)kR, cnt - EV_STAGE);
-        c.sync();
-      }
-      if (dbg) {
-        dbg_kids[cnt <= 16 ? 0 : cnt <= 256 ? 1 : cnt <= 4096 ? 2 : 3]++;
-        dbg_kids_max = std::max<uint64_t>(dbg_kids_max, cnt);
-      }
-      const uint64_t cb0 = cb;
-      // std::sort on the current kid order with the reference comparator (:104-106);
-      // sorting positions with a comparator on their keys is the same sort.
-      order.resize(cnt);
-      for (uint32_t j = 0; j < cnt; ++j) order[j] = j;
-      std::sort(order.begin(), order.end(), [&segR](uint32_t a, uint32_t b) { return segR[a] > segR[b]; });
-      sorted.resize(cnt); scb.resize(cnt);
-      for (uint32_t j = 0; j < cnt; ++j) {
-        sorted[j] = seg[order[j]];
-        scb[j] = segR[order[j]];
-        if (j != order[j]) { upl_pos.push_back(beg + j); upl_ids.push_back(sorted[j]); }
-      }
-      done.assign(cnt, 0);
-      do {
-        for (uint32_t j = 0; cb > max_component && j < cnt; ++j) {
-          if (scb[j] > max_component) throw Error(SHEEP_ERR_PACK, "forwardPartition: kid exceeds max_component");
-          if (done[j]) continue;
-          for (size_t p = 0; p != part_size.size(); ++p) {
-            if (part_size[p] + scb[j] <= max_component) {
-              cb -= scb[j];
-              part_size[p] += scb[j];
-              done[j] = 1;
-              asg_ids.push_back(sorted[j]);
-              asg_part.push_back((int16_t)p);
-              break;
+        ++seq_no;
+        const auto h0 = std::chrono::steady_clock::now();
+        wait_stage(seq_no);
+        const auto h1 = std::chrono::steady_clock::now();
+        if (dbg) {
+          dbg_tab += hdr[8] / 100.0;   // wall_clock64: 100 MHz
+          dbg_search += hdr[9] / 100.0;
+          dbg_stage += hdr[10] / 100.0;
+          dbg_wait += std::chrono::duration<double, std::micro>(h1 - h0).count();
+        }
+        const uint32_t v = hdr[0];
+        if (dbg && live)
+          fprintf(stderr, "partition event %u: hits %.1f scan %.1f done %.1f stage %.1f us, from %u, wait %.1f us\n", seq_no,
+                  hdr[11] / 100.0, hdr[12] / 100.0, hdr[13] / 100.0, hdr[10] / 100.0, hdr[14],
+                  std::chrono::duration<double, std::micro>(h1 - h0).count());
+        if (v == INVALID) {
+          if (live) answer(EV_STOP, INVALID, 0);
+          break;
+        }
+        info->packing_nodes++;
+        const uint32_t beg = hdr[1], cnt = hdr[2], vpos = hdr[5];
+        uint64_t cb = (uint64_t)hdr[3] | ((uint64_t)hdr[4] << 32);
+        if (!hdr[6]) {   // more kids than the event kernel stages: k_event_kids, behind k_event_loop's end
+          if (live) answer(EV_STOP, INVALID, 0);
+          write_table(false);
+          stage_kids_of(0, EV_STAGE, d_kids, d_r);
+        }
+        seg.assign(st_kids, st_kids + std::min(cnt, EV_STAGE));
+        segR.assign(st_r, st_r + std::min(cnt, EV_STAGE));
+        if (cnt > EV_STAGE) {   // a node with more kids than the staging area: fetch the rest
+          seg.resize(cnt); segR.resize(cnt);
+          uint32_t *kk = c.get_as<uint32_t>("pt_kK", cnt);
+          uint64_t *kR = c.get_as<uint64_t>("pt_kR", cnt);
+          stage_kids_of(EV_STAGE, cnt - EV_STAGE, kk, kR);
+          d2h(c, seg.data() + EV_STAGE, (const uint32_t *)kk, cnt - EV_STAGE);
+          d2h(c, segR.data() + EV_STAGE, (const uint64_t *)kR, cnt - EV_STAGE);
+          c.sync();
+        }
+        if (dbg) {
+          dbg_kids[cnt <= 16 ? 0 : cnt <= 256 ? 1 : cnt <= 4096 ? 2 : 3]++;
+          dbg_kids_max = std::max<uint64_t>(dbg_kids_max, cnt);
+        }
+        const uint64_t cb0 = cb;
+        // std::sort on the current kid order with the reference comparator (:104-106);
+        // sorting positions with a comparator on their keys is the same sort.
+        order.resize(cnt);
+        for (uint32_t j = 0; j < cnt; ++j) order[j] = j;
+        std::sort(order.begin(), order.end(), [&segR](uint32_t a, uint32_t b) { return segR[a] > segR[b]; });
+        sorted.resize(cnt); scb.resize(cnt);
+        for (uint32_t j = 0; j < cnt; ++j) {
+          sorted[j] = seg[order[j]];
+          scb[j] = segR[order[j]];
+          if (j != order[j]) { upl_pos.push_back(beg + j); upl_ids.push_back(sorted[j]); }
+        }
+        done.assign(cnt, 0);
+        do {
+          for (uint32_t j = 0; cb > max_component && j < cnt; ++j) {
+            if (scb[j] > max_component) throw Error(SHEEP_ERR_PACK, "forwardPartition: kid exceeds max_component");
+            if (done[j]) continue;
+            for (size_t p = 0; p != part_size.size(); ++p) {
+              if (part_size[p] + scb[j] <= max_component) {
+                cb -= scb[j];
+                part_size[p] += scb[j];
+                done[j] = 1;
+                asg_ids.push_back(sorted[j]);
+                asg_part.push_back((int16_t)p);
+                break;
+              }
             }
           }
+          if (cb > max_component) {
+            bool any = false;
+            for (uint32_t j = 0; j < cnt; ++j) any |= !done[j];
+            if (!any || part_size.size() >= 32767)
+              throw Error(SHEEP_ERR_PACK, "forwardPartition: node weight exceeds max_component (reference loops forever)");
+            part_size.push_back(0);
+          }
+        } while (cb > max_component);
+        // the event into the table for the next scan (sorted by tD; a root keeps its own)
+        if (vpos != INVALID)
+          evs.insert(std::upper_bound(evs.begin(), evs.end(), std::make_pair(vpos, (uint64_t)~0ull)), {vpos, cb0 - cb});
+        else
+          root_own.push_back({v, cb0 - cb});
+        if (live) {   // k_event_loop inserts the event into its own table copy, up to ev_cap entries
+          if (vpos != INVALID && evs.size() > ev_cap) answer(EV_STOP, INVALID, 0);
+          else answer(EV_CONT, vpos, cb0 - cb);
         }
-        if (cb > max_component) {
-          bool any = false;
-          for (uint32_t j = 0; j < cnt; ++j) any |= !done[j];
-          if (!any || part_size.size() >= 32767)
-            throw Error(SHEEP_ERR_PACK, "forwardPartition: node weight exceeds max_component (reference loops forever)");
-          part_size.push_back(0);
-        }
-      } while (cb > max_component);
-      // the event into the table for the next scan (sorted by tD; a root keeps its own)
-      if (vpos != INVALID)
-        evs.insert(std::upper_bound(evs.begin(), evs.end(), std::make_pair(vpos, (uint64_t)~0ull)), {vpos, cb0 - cb});
-      else
-        root_own.push_back({v, cb0 - cb});
-      if (live) {   // k_event_loop inserts the event into its own table copy, up to ev_cap entries
-        if (vpos != INVALID && evs.size() > ev_cap) answer(EV_STOP, INVALID, 0);
-        else answer(EV_CONT, vpos, cb0 - cb);
+        if (dbg) dbg_host += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h1).count();
       }
-      if (dbg) dbg_host += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h1).count();
-    }
     } catch (...) {   // k_event_loop must not wait for an answer that never comes
       if (live) answer(EV_STOP, INVALID, 0);
       throw;
