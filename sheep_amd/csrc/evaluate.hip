@@ -414,7 +414,7 @@ __global__ __launch_bounds__(BLOCK) void k_eval_edges(const uint64_t *__restrict
   uint64_t cut = 0;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) {
-    const uint64_t e = edges[i];
+    const uint64_t e = __builtin_nontemporal_load(&edges[i]);   // (streamed once: keep the caches for the rows)
     const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
     const int pl = pj[lo], ph = need_hi ? pj[hi] : 0;
     int po = 0;
