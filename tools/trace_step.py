@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel time of the LAST path step in a rocprofv3 kernel trace (kernel_trace.csv of
 a bench.py run): the dispatches from the last k_degree_fused up to the evaluator's first
-kernel (k_pp) or the end.  Prints ms per kernel base name, calls, and the step span.
+kernel (k_max_part, k_pp or k_parts_jnid) or the end.  Prints ms per kernel base name, calls, and the step span.
 
     python tools/trace_step.py run_kernel_trace.csv [--levels] [--from KERNEL]
 
@@ -24,7 +24,7 @@ def main():
     first = sys.argv[sys.argv.index("--from") + 1] if "--from" in sys.argv else "k_degree_fused"
     starts = [i for i, r in enumerate(rows) if base(r["Kernel_Name"]) == first]
     step = rows[starts[-1]:]
-    ends = [i for i, r in enumerate(step) if base(r["Kernel_Name"]) == "k_pp"]
+    ends = [i for i, r in enumerate(step) if base(r["Kernel_Name"]) in ("k_pp", "k_max_part", "k_parts_jnid")]
     step = step[:ends[0]] if ends else step
     tot, cnt = defaultdict(float), Counter()
     for r in step:
