@@ -338,7 +338,8 @@ void build_tour(Ctx &c, sheep_kids *k, Tour &t) {
 
   uint32_t *rid = c.get_as<uint32_t>("tour_rid", 2 * n);
   // one arc in 32 is a ruler (1/32, 1/64, 1/128 measured 8.54 / 8.71 / 8.81 ms of partition
-  // at RMAT-26: shorter walks against more pointer-jumping work)
+  // at RMAT-26: shorter walks against more pointer-jumping work; round 5: 1/16 and 1/8 cut
+  // the walk 0.53 -> 0.44 / 0.40 ms, partition 6.46 / 6.47 / 6.60 ms: no better)
   constexpr uint32_t rmask = 31u;
   const uint64_t rcap = 2 * n * 4 / (rmask + 1) + 1024;   // expected 2n/(rmask + 1) hash-picked rulers
   uint32_t *rulers = c.get_as<uint32_t>("tour_rulers", rcap);
