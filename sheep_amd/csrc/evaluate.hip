@@ -71,6 +71,29 @@ __device__ __forceinline__ uint64_t run_or(uint32_t key, uint64_t m) {
   return start ? v : 0;
 }
 
+// +1 at c[key] for every live lane of the wave: one atomic per distinct key while the
+// keys repeat (the balance histograms' keys are parts: the lanes of a wave over lo-grouped
+// edges mostly share one), one per lane once a key turns out rare (C4's positions mix parts)
+__device__ __forceinline__ void wave_count(uint32_t *lc, unsigned long long *gc, int key, bool live) {
+  uint64_t todo = __ballot(live);
+  while (todo) {   // (uniform)
+    const int leader = __ffsll((long long)todo) - 1;
+    const int k = __shfl(key, leader, 64);
+    const uint64_t same = __ballot(live && key == k) & todo;
+    const uint32_t cnt = (uint32_t)__popcll(same);
+    if (cnt < 8) {   // rare: every lane left adds its own
+      if ((todo >> __lane_id()) & 1) {
+        if (lc) atomicAdd(&lc[key], 1u); else atomicAdd(&gc[key], 1ull);
+      }
+      break;
+    }
+    if ((int)__lane_id() == leader) {
+      if (lc) atomicAdd(&lc[k], cnt); else atomicAdd(&gc[k], (unsigned long long)cnt);
+    }
+    todo &= ~same;
+  }
+}
+
 __device__ __forceinline__ void or_bits(unsigned long long *bits, uint64_t idx, uint64_t m) {
   if (!m) return;
   if ((bits[idx] & m) != m) atomicOr(&bits[idx], (unsigned long long)m);
@@ -413,18 +436,22 @@ __global__ __launch_bounds__(BLOCK) void k_eval_edges(const uint64_t *__restrict
   const bool need_hi = (what & 5) != 0;   // up, hash and Vcom read the hi end's part
   uint64_t cut = 0;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < m; i += stride) {
-    const uint64_t e = __builtin_nontemporal_load(&edges[i]);   // (streamed once: keep the caches for the rows)
+  const uint64_t iters = (m + stride - 1) / stride;
+  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (uint64_t it = 0; it < iters; ++it, i += stride) {   // wave-uniform trip count (wave_count)
+    const bool live = i < m;
+    const uint64_t e = live ? __builtin_nontemporal_load(&edges[i]) : 0ull;   // (streamed once: caches kept for the rows)
     const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
-    const int pl = pj[lo], ph = need_hi ? pj[hi] : 0;
+    const int pl = live ? pj[lo] : 0, ph = live && need_hi ? pj[hi] : 0;
     int po = 0;
-    if (what & 1) {
+    if ((what & 1) && live) {
       po = cormen_hash(seq[lo]) < cormen_hash(seq[hi]) ? pl : ph;
       cut += pl != ph;
     }
-    if (ad >= 0) { if (lds) atomicAdd(&lbal[0][pl], 1u); else atomicAdd(&bal[pl], 1ull); }
-    if (au >= 0) { if (lds) atomicAdd(&lbal[1][ph], 1u); else atomicAdd(&bal[nparts + ph], 1ull); }
-    if (ah >= 0) { if (lds) atomicAdd(&lbal[2][po], 1u); else atomicAdd(&bal[2 * nparts + po], 1ull); }
+    if (ad >= 0) wave_count(lds ? lbal[0] : nullptr, bal, pl, live);
+    if (au >= 0) wave_count(lds ? lbal[1] : nullptr, bal + nparts, ph, live);
+    if (ah >= 0) wave_count(lds ? lbal[2] : nullptr, bal + 2 * nparts, po, live);
+    if (!live) continue;
     const int own_lo[4] = {pl, ph, po, ph};   // down, up, hash, Vcom owner seen from lo
     const int own_hi[4] = {pl, ph, po, pl};   // ... and from hi
     const int arr[4] = {ad, au, ah, av};
