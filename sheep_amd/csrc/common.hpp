@@ -246,6 +246,25 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 
+// +1 at c[key] for every live lane of the wave: one atomic per distinct key while the keys
+// repeat across the lanes (histograms of parts or of hub ids), one per lane once a key
+// turns out rare.  Every lane of the wave calls it (uniform control flow).
+template <typename C> __device__ __forceinline__ void wave_count(C *c, uint32_t key, bool live) {
+  uint64_t todo = __ballot(live);
+  while (todo) {   // (uniform)
+    const int leader = __ffsll((long long)todo) - 1;
+    const uint32_t k = __shfl(key, leader, 64);
+    const uint64_t same = __ballot(live && key == k) & todo;
+    const uint32_t cnt = (uint32_t)__popcll(same);
+    if (cnt < 8) {   // rare: every lane left adds its own
+      if ((todo >> __lane_id()) & 1) atomicAdd(&c[key], (C)1);
+      break;
+    }
+    if ((int)__lane_id() == leader) atomicAdd(&c[k], (C)cnt);
+    todo &= ~same;
+  }
+}
+
 // Adds w into cnt[key] for every lane whose key != INVALID, with one atomic per run of
 // equal keys in consecutive lanes (records sorted by tail, as generated and as many
 // edge lists are stored, make tail runs long; a hub's endpoints collapse too).

@@ -71,29 +71,6 @@ __device__ __forceinline__ uint64_t run_or(uint32_t key, uint64_t m) {
   return start ? v : 0;
 }
 
-// +1 at c[key] for every live lane of the wave: one atomic per distinct key while the
-// keys repeat (the balance histograms' keys are parts: the lanes of a wave over lo-grouped
-// edges mostly share one), one per lane once a key turns out rare (C4's positions mix parts)
-__device__ __forceinline__ void wave_count(uint32_t *lc, unsigned long long *gc, int key, bool live) {
-  uint64_t todo = __ballot(live);
-  while (todo) {   // (uniform)
-    const int leader = __ffsll((long long)todo) - 1;
-    const int k = __shfl(key, leader, 64);
-    const uint64_t same = __ballot(live && key == k) & todo;
-    const uint32_t cnt = (uint32_t)__popcll(same);
-    if (cnt < 8) {   // rare: every lane left adds its own
-      if ((todo >> __lane_id()) & 1) {
-        if (lc) atomicAdd(&lc[key], 1u); else atomicAdd(&gc[key], 1ull);
-      }
-      break;
-    }
-    if ((int)__lane_id() == leader) {
-      if (lc) atomicAdd(&lc[k], cnt); else atomicAdd(&gc[k], (unsigned long long)cnt);
-    }
-    todo &= ~same;
-  }
-}
-
 __device__ __forceinline__ void or_bits(unsigned long long *bits, uint64_t idx, uint64_t m) {
   if (!m) return;
   if ((bits[idx] & m) != m) atomicOr(&bits[idx], (unsigned long long)m);
@@ -448,9 +425,10 @@ __global__ __launch_bounds__(BLOCK) void k_eval_edges(const uint64_t *__restrict
       po = cormen_hash(seq[lo]) < cormen_hash(seq[hi]) ? pl : ph;
       cut += pl != ph;
     }
-    if (ad >= 0) wave_count(lds ? lbal[0] : nullptr, bal, pl, live);
-    if (au >= 0) wave_count(lds ? lbal[1] : nullptr, bal + nparts, ph, live);
-    if (ah >= 0) wave_count(lds ? lbal[2] : nullptr, bal + 2 * nparts, po, live);
+    // (per wave: the lanes mostly share a part; lds is uniform)
+    if (ad >= 0) { if (lds) wave_count(lbal[0], (uint32_t)pl, live); else wave_count(bal, (uint32_t)pl, live); }
+    if (au >= 0) { if (lds) wave_count(lbal[1], (uint32_t)ph, live); else wave_count(bal + nparts, (uint32_t)ph, live); }
+    if (ah >= 0) { if (lds) wave_count(lbal[2], (uint32_t)po, live); else wave_count(bal + 2 * nparts, (uint32_t)po, live); }
     if (!live) continue;
     const int own_lo[4] = {pl, ph, po, ph};   // down, up, hash, Vcom owner seen from lo
     const int own_hi[4] = {pl, ph, po, pl};   // ... and from hi
