@@ -47,53 +47,61 @@ __global__ __launch_bounds__(BLOCK) void k_hist(const K *__restrict__ keys, uint
   for (int d = threadIdx.x; d < RADIX; d += BLOCK) hist[(uint64_t)d * ntiles + blockIdx.x] = h[d];
 }
 
+// Per tile: every wave ranks a contiguous quarter of it (index order = wave, then item,
+// then lane), counting its digits in its own LDS row as it goes — LDS operations of one
+// wave execute in order, so an item sees the counts of the wave's earlier items without a
+// barrier; one barrier then turns the rows into per-wave digit offsets.  (Ranking the tile
+// item by item across the waves took three workgroup barriers per item.)
 template <typename K, bool VALS, int DB>
 __global__ __launch_bounds__(BLOCK) void k_scatter(const K *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                    K *__restrict__ kout, uint32_t *__restrict__ vout,
                                                    uint64_t n, int shift, uint32_t ntiles,
                                                    const uint32_t *__restrict__ offsets) {
   constexpr int RADIX = 1 << DB, DPT = RADIX > BLOCK ? RADIX / BLOCK : 1;   // digits per thread
+  constexpr int NW = BLOCK / WAVE, WCH = WAVE * R_ITEMS;                    // waves, keys per wave
   __shared__ uint32_t run[RADIX];
-  __shared__ uint32_t wcnt[BLOCK / WAVE][RADIX];
+  __shared__ uint32_t wcnt[NW][RADIX];   // a wave's digit counts, then its digit offsets in the tile
   __shared__ uint32_t dstart[RADIX];
-  __shared__ uint32_t wtot[BLOCK / WAVE];
+  __shared__ uint32_t wtot[NW];
   __shared__ K skeys[R_TILE];
   __shared__ uint32_t svals[VALS ? R_TILE : 1];
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  for (int d = t; d < RADIX; d += BLOCK) {
-    run[d] = 0;
-    for (int w = 0; w < BLOCK / WAVE; ++w) wcnt[w][d] = 0;
-  }
+  for (int d = t; d < RADIX; d += BLOCK)
+    for (int w = 0; w < NW; ++w) wcnt[w][d] = 0;
   lds_barrier();
 
-  const uint64_t base = (uint64_t)blockIdx.x * R_TILE;
+  const uint64_t tbase = (uint64_t)blockIdx.x * R_TILE, base = tbase + (uint64_t)wave * WCH;
   K key[R_ITEMS];
   uint32_t val[R_ITEMS];
   uint32_t rank[R_ITEMS];
-  for (int j = 0; j < R_ITEMS; ++j) {
-    uint64_t i = base + (uint64_t)j * BLOCK + t;
-    bool valid = i < n;
-    key[j] = valid ? kin[i] : K(0);
-    if (VALS) val[j] = valid ? vin[i] : 0u;
-    uint32_t d = (uint32_t)((key[j] >> shift) & (RADIX - 1));
-    uint64_t peers = digit_peers<DB>(valid, d);
-    uint32_t lrank = (uint32_t)__popcll(peers & lanemask_lt());
-    if (valid && lrank == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
-    lds_barrier();
-    if (valid) {
-      uint32_t before = run[d];
-      for (int w = 0; w < wave; ++w) before += wcnt[w][d];
-      rank[j] = before + lrank;
-    }
-    lds_barrier();
-    for (int dd = t; dd < RADIX; dd += BLOCK) {
-      uint32_t add = 0;
-      for (int w = 0; w < BLOCK / WAVE; ++w) { add += wcnt[w][dd]; wcnt[w][dd] = 0; }
-      run[dd] += add;
-    }
-    lds_barrier();
+#pragma unroll
+  for (int j = 0; j < R_ITEMS; ++j) {   // every load in flight before the ranking
+    const uint64_t i = base + (uint64_t)j * WAVE + lane;
+    key[j] = i < n ? kin[i] : K(0);
+    if (VALS) val[j] = i < n ? vin[i] : 0u;
   }
+  uint32_t *const mine = wcnt[wave];
+  for (int j = 0; j < R_ITEMS; ++j) {
+    const bool valid = base + (uint64_t)j * WAVE + lane < n;
+    const uint32_t d = (uint32_t)((key[j] >> shift) & (RADIX - 1));
+    const uint64_t peers = digit_peers<DB>(valid, d);
+    const uint32_t lrank = (uint32_t)__popcll(peers & lanemask_lt());
+    const uint32_t before = valid ? mine[d] : 0u;
+    rank[j] = before + lrank;
+    if (valid && lrank == 0) mine[d] = before + (uint32_t)__popcll(peers);
+  }
+  lds_barrier();
+  for (int d = t; d < RADIX; d += BLOCK) {   // per digit: the waves' offsets (exclusive, wave order), total
+    uint32_t s = 0;
+    for (int w = 0; w < NW; ++w) {
+      const uint32_t x = wcnt[w][d];
+      wcnt[w][d] = s;
+      s += x;
+    }
+    run[d] = s;
+  }
+  lds_barrier();
   // tile-local digit starts: exclusive scan of run[] (thread t owns digits t*DPT .. +DPT)
   uint32_t v = 0;
   if (t * DPT < RADIX)
@@ -113,16 +121,15 @@ __global__ __launch_bounds__(BLOCK) void k_scatter(const K *__restrict__ kin, co
   }
   lds_barrier();
   for (int j = 0; j < R_ITEMS; ++j) {
-    uint64_t i = base + (uint64_t)j * BLOCK + t;
-    if (i < n) {
-      uint32_t d = (uint32_t)((key[j] >> shift) & (RADIX - 1));
-      uint32_t lp = dstart[d] + rank[j];
+    if (base + (uint64_t)j * WAVE + lane < n) {
+      const uint32_t d = (uint32_t)((key[j] >> shift) & (RADIX - 1));
+      const uint32_t lp = dstart[d] + mine[d] + rank[j];
       skeys[lp] = key[j];
       if (VALS) svals[lp] = val[j];
     }
   }
   lds_barrier();
-  uint32_t cnt = (uint32_t)((n - base) < (uint64_t)R_TILE ? (n - base) : (uint64_t)R_TILE);
+  uint32_t cnt = (uint32_t)((n - tbase) < (uint64_t)R_TILE ? (n - tbase) : (uint64_t)R_TILE);
   for (uint32_t idx = t; idx < cnt; idx += BLOCK) {
     K k = skeys[idx];
     uint32_t d = (uint32_t)((k >> shift) & (RADIX - 1));
