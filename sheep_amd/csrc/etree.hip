@@ -599,12 +599,17 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restric
   const uint64_t nx = st[ST_NX];
   const uint64_t *__restrict__ xbuf = lx + st[ST_NL];
   const uint64_t ntiles = (nx + TILE - 1) / TILE;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t lt = lanemask_lt();
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     uint32_t r[TILE_ITEMS], b[TILE_ITEMS], m[TILE_ITEMS], cl[TILE_ITEMS];
     uint32_t keep = 0;
+    // each wave takes a contiguous share of the tile, so the survivors can be appended in
+    // input order (k_split_write: the next passes' gathers keep their locality)
+    const uint64_t w0 = tile * TILE + (uint64_t)wave * (TILE_ITEMS * WAVE) + lane;
 #pragma unroll
     for (int k = 0; k < TILE_ITEMS; ++k) {
-      const uint64_t j = tile * TILE + (uint64_t)k * BLOCK + threadIdx.x;
+      const uint64_t j = w0 + (uint64_t)k * WAVE;
       const bool live = j < nx;
       r[k] = live ? xtop[j] : INVALID;
       b[k] = live ? (uint32_t)(xbuf[j] >> 32) : 0;
@@ -630,10 +635,17 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restric
       keep |= 1u << k;
       if (c == INVALID) claim[b[k]] = g.enc(m[k]);   // first seen this level: a plain store
     }
-    uint64_t slot = shard_reserve((uint32_t)__popc(keep), counters, tile, ntiles, 1);
+    uint32_t run = 0, rk[TILE_ITEMS];   // ranks in the wave's share (run: wave-uniform)
+#pragma unroll
+    for (int k = 0; k < TILE_ITEMS; ++k) {
+      const uint64_t q = __ballot((keep >> k) & 1);
+      rk[k] = run + (uint32_t)__popcll(q & lt);
+      run += (uint32_t)__popcll(q);
+    }
+    const uint64_t wbase = __shfl(shard_reserve(lane == 0 ? run : 0u, counters, tile, ntiles, 1), 0, 64);
 #pragma unroll
     for (int k = 0; k < TILE_ITEMS; ++k)
-      if (keep & (1u << k)) scratch[slot++] = ((uint64_t)b[k] << 32) | m[k];
+      if (keep & (1u << k)) scratch[wbase + rk[k]] = ((uint64_t)b[k] << 32) | m[k];
   }
 }
 
@@ -743,14 +755,23 @@ __global__ __launch_bounds__(BLOCK) void k_split_count(const uint64_t *__restric
 
 // cnt: the three rows (stride ntiles, then a 0) scanned as ONE exclusive scan, so a
 // row's offsets are relative to its first entry; the row totals go to st.  Each class's
-// run of the tile is first placed in LDS at its thread-major rank, then copied out by
-// consecutive lanes (per-thread stores to the same positions: 16.6 against 12.2 ms).
+// run of the tile is placed in LDS in INPUT order, then copied out by consecutive lanes
+// (per-thread stores to the same positions: 16.6 against 12.2 ms).  Input order keeps a
+// wave's lanes on neighbouring lo in the next passes' gathers: the thread-major order it
+// replaced (a thread's 16 entries, 256 apart in the input, side by side) cost the hook
+// round, the cross pass and the contractions 0.8 ms per RMAT-26 step.  Each wave takes a
+// contiguous quarter of the tile and ranks it item by item with ballots (the running
+// counts are wave-uniform: no LDS, no barrier); one barrier adds the waves' offsets.  (A
+// rank over (item, wave) pairs, with the pairs' counts scanned in LDS: +0.28 ms.)
 template <bool CUT>
 __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
                                                        uint64_t *__restrict__ st, int s, uint32_t clo, YRange yr,
                                                        const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg,
                                                        int L, int gcut, const uint64_t *__restrict__ cnt,
                                                        uint64_t *__restrict__ next, uint64_t *__restrict__ lx) {
+  constexpr int NW = BLOCK / WAVE;
+  constexpr uint32_t WCH = SPLIT_ITEMS * WAVE;   // a wave's contiguous share of the tile
+  static_assert(WCH <= 1024, "10-bit ranks");
   const SplitIn<CUT> in(list, prev, r0, seg, s, L, gcut, clo);
   const uint64_t ntiles = (in.m + SPLIT_TILE - 1) / SPLIT_TILE, cstride = ntiles;
   const uint64_t b0 = cnt[0], b1 = cnt[cstride], b2 = cnt[2 * cstride], b3 = cnt[3 * cstride];
@@ -759,48 +780,54 @@ __global__ __launch_bounds__(BLOCK) void k_split_write(const uint64_t *__restric
     st[ST_NL] = b2 - b1;
     st[ST_NX] = b3 - b2;
   }
-  __shared__ uint64_t s_w[BLOCK / WAVE];
+  __shared__ uint32_t s_w[NW][3];
+  __shared__ uint64_t stg[SPLIT_TILE];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t lt = lanemask_lt();
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     uint64_t ev[SPLIT_ITEMS];
-    uint32_t cl[SPLIT_ITEMS];
-    uint64_t c3 = 0;
+    uint32_t cl[SPLIT_ITEMS], lr[SPLIT_ITEMS];   // class bits; the ranks in the wave's share, 3 x 10 bits
+    const uint64_t w0 = tile * SPLIT_TILE + (uint64_t)wave * WCH + lane;
 #pragma unroll
-    for (int j = 0; j < SPLIT_ITEMS; ++j) ev[j] = in[tile * SPLIT_TILE + (uint64_t)j * BLOCK + threadIdx.x];
+    for (int j = 0; j < SPLIT_ITEMS; ++j) ev[j] = in[w0 + (uint64_t)j * WAVE];
+    uint32_t run0 = 0, run1 = 0, run2 = 0;   // wave-uniform
 #pragma unroll
     for (int j = 0; j < SPLIT_ITEMS; ++j) {
       cl[j] = classify(ev[j], s, clo, yr);
-      c3 += pack3(cl[j]);
+      const uint64_t q0 = __ballot(cl[j] & 1), q1 = __ballot((cl[j] >> 1) & 1), q2 = __ballot((cl[j] >> 2) & 1);
+      lr[j] = (run0 + (uint32_t)__popcll(q0 & lt)) | (run1 + (uint32_t)__popcll(q1 & lt)) << 10 |
+              (run2 + (uint32_t)__popcll(q2 & lt)) << 20;
+      run0 += (uint32_t)__popcll(q0);
+      run1 += (uint32_t)__popcll(q1);
+      run2 += (uint32_t)__popcll(q2);
     }
-    // thread-major ranks inside the tile: exclusive scan of the packed counters
-    uint64_t inc = c3;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint64_t u = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += u;
+    if (lane == 0) {
+      s_w[wave][0] = run0;
+      s_w[wave][1] = run1;
+      s_w[wave][2] = run2;
     }
-    if (lane == 63) s_w[wave] = inc;
     lds_barrier();
-    uint64_t off = 0;
-    for (int w = 0; w < wave; ++w) off += s_w[w];
-    const uint64_t ex = off + inc - c3;
-    __shared__ uint64_t stg[SPLIT_TILE];
-    uint64_t tot = 0;
-    for (int w = 0; w < BLOCK / WAVE; ++w) tot += s_w[w];
+    uint32_t off[3] = {0, 0, 0}, tot[3] = {0, 0, 0};
+#pragma unroll
+    for (int w = 0; w < NW; ++w)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const uint32_t x = s_w[w][k];
+        if (w < wave) off[k] += x;
+        tot[k] += x;
+      }
     // the stay run into `next`; the light and the cross runs into lx back to back: the one
     // scan of the three rows already places cross after light (offsets from the light row's start)
     uint64_t *const outs[3] = {next, lx, lx};
     const uint64_t obase[3] = {b0, b1, b1};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      uint32_t r = (uint32_t)((ex >> (16 * k)) & 0xFFFF);
 #pragma unroll
       for (int j = 0; j < SPLIT_ITEMS; ++j)
-        if ((cl[j] >> k) & 1) stg[r++] = ev[j];
+        if ((cl[j] >> k) & 1) stg[off[k] + ((lr[j] >> (10 * k)) & 1023)] = ev[j];
       lds_barrier();
-      const uint32_t n_k = (uint32_t)((tot >> (16 * k)) & 0xFFFF);
       uint64_t *const o = outs[k] + (cnt[k * cstride + tile] - obase[k]);
-      for (uint32_t i = threadIdx.x; i < n_k; i += BLOCK) o[i] = stg[i];
+      for (uint32_t i = threadIdx.x; i < tot[k]; i += BLOCK) o[i] = stg[i];
       lds_barrier();   // stg (and, after the last class, s_w) is rewritten next
     }
   }
