@@ -2,9 +2,12 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <set>
@@ -139,11 +142,43 @@ struct Ctx {
     bool valid = false;
   };
   StepEdges step_edges;
+  // The first-activity group bounds the last grouping wrote to `dev`, on the host (taken,
+  // once, by the elimination tree that reads them next)
+  struct SegHost { const uint64_t *dev = nullptr; std::vector<uint64_t> v; };
+  SegHost seg_host;
 
   bool timing = false;
   struct Timer { std::vector<std::pair<hipEvent_t, hipEvent_t>> pending; double ms = 0; uint64_t launches = 0; uint64_t bytes = 0; };
   std::map<std::string, Timer> timers;
   std::vector<hipEvent_t> event_pool;
+  // Byte counts that need device-side results (the etree's per-level list sizes): the
+  // results are copied into a pinned buffer on the stream and counted when the timers are
+  // collected, so a timed run pays no host round trip for them.
+  struct Deferred { void *host; size_t bytes; std::function<void(const void *)> count; };
+  std::vector<Deferred> deferred;
+  std::vector<std::pair<void *, size_t>> deferred_pool;
+  void defer_bytes(const void *dev, size_t bytes, std::function<void(const void *)> count) {
+    void *h = nullptr;
+    for (size_t i = 0; i < deferred_pool.size(); ++i)
+      if (deferred_pool[i].second >= bytes) {
+        h = deferred_pool[i].first;
+        bytes = deferred_pool[i].second;
+        deferred_pool.erase(deferred_pool.begin() + (long)i);
+        break;
+      }
+    if (!h) {
+      if (deferred.size() >= 256) collect_timers();   // (bounded: a long timed run without reads)
+      for (size_t i = 0; !h && i < deferred_pool.size(); ++i)
+        if (deferred_pool[i].second >= bytes) {
+          h = deferred_pool[i].first;
+          bytes = deferred_pool[i].second;
+          deferred_pool.erase(deferred_pool.begin() + (long)i);
+        }
+      if (!h) HIP_CHECK(hipHostMalloc(&h, bytes, hipHostMallocDefault));
+    }
+    HIP_CHECK(hipMemcpyAsync(h, dev, bytes, hipMemcpyDeviceToHost, stream));
+    deferred.push_back({h, bytes, std::move(count)});
+  }
 
   void *get(const std::string &name, size_t bytes) {
     Buf &b = ws[name];
@@ -171,7 +206,46 @@ struct Ctx {
     }
     return b.p;
   }
-  void sync() { HIP_CHECK(hipStreamSynchronize(stream)); }
+  // Pinned staging for copies of pageable host vectors: a copy from or to pageable memory
+  // is synchronous (each one a host round trip, 30-50 us of idle GPU); staged, it is queued
+  // like any other copy.  Downloads land in their vectors at the next sync().
+  struct Stage { char *p = nullptr; size_t cap = 0, used = 0; };
+  Stage stage;
+  std::vector<char *> stage_old;
+  std::vector<std::function<void()>> after_sync;
+  void *stage_alloc(size_t bytes) {
+    bytes = (bytes + 255) & ~(size_t)255;
+    if (stage.used + bytes > stage.cap) {
+      if (stage.p) stage_old.push_back(stage.p);   // still read by queued copies: freed at sync()
+      const size_t cap = std::max(bytes, std::max(2 * stage.cap, (size_t)1 << 20));
+      HIP_CHECK(hipHostMalloc((void **)&stage.p, cap, hipHostMallocDefault));
+      stage.cap = cap;
+      stage.used = 0;
+    }
+    void *r = stage.p + stage.used;
+    stage.used += bytes;
+    return r;
+  }
+  template <typename T> void download(T *h, const T *d, uint64_t cnt) {
+    if (!cnt) return;
+    T *s = (T *)stage_alloc(cnt * sizeof(T));
+    HIP_CHECK(hipMemcpyAsync(s, d, cnt * sizeof(T), hipMemcpyDeviceToHost, stream));
+    after_sync.push_back([h, s, cnt]() { memcpy(h, s, cnt * sizeof(T)); });
+  }
+  template <typename T> void upload(T *d, const T *h, uint64_t cnt) {
+    if (!cnt) return;
+    T *s = (T *)stage_alloc(cnt * sizeof(T));
+    memcpy(s, h, cnt * sizeof(T));
+    HIP_CHECK(hipMemcpyAsync(d, s, cnt * sizeof(T), hipMemcpyHostToDevice, stream));
+  }
+  void sync() {
+    HIP_CHECK(hipStreamSynchronize(stream));
+    for (auto &f : after_sync) f();
+    after_sync.clear();
+    stage.used = 0;
+    for (char *p : stage_old) HIP_CHECK(hipHostFree(p));
+    stage_old.clear();
+  }
   // algorithmic bytes learned only after the launches (device-side counts)
   void add_bytes(const char *name, uint64_t bytes) { if (timing) timers[name].bytes += bytes; }
 
@@ -183,6 +257,14 @@ struct Ctx {
     hipEvent_t e; HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence)); return e;
   }
   void collect_timers() {
+    if (!deferred.empty()) {
+      sync();
+      for (auto &d : deferred) {
+        d.count(d.host);
+        deferred_pool.push_back({d.host, d.bytes});
+      }
+      deferred.clear();
+    }
     for (auto &kv : timers) {
       for (auto &p : kv.second.pending) {
         float ms = 0;

@@ -2230,10 +2230,25 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   int top_lvl = -1, gcut = 0;
   uint64_t top_g0 = 0, top_g1 = 0;
   uint32_t top_V = 0, top_cut = 0;
-  if (top_bits > FINB && top_bits <= L - 1 && top_bits <= TOP_BITS_MAX) {
-    std::vector<uint64_t> hs(2 * (size_t)L);
-    HIP_CHECK(hipMemcpyAsync(hs.data(), seg, hs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  std::vector<uint64_t> hs;   // the group bounds on the host, read once for both cuts
+  const bool seg_known = c.seg_host.dev == seg && c.seg_host.v.size() == 2 * (size_t)L;
+  c.seg_host.dev = nullptr;
+  if (seg_known && g_debug_etree) {   // the grouping's host bounds against the device's
+    std::vector<uint64_t> d(2 * (size_t)L);
+    HIP_CHECK(hipMemcpyAsync(d.data(), seg, d.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
     c.sync();
+    if (d != c.seg_host.v) throw Error(SHEEP_ERR_HIP, "etree: host group bounds differ from the device's");
+  }
+  auto host_seg = [&]() {
+    if (hs.empty() && seg_known) hs = c.seg_host.v;
+    if (hs.empty()) {
+      hs.resize(2 * (size_t)L);
+      HIP_CHECK(hipMemcpyAsync(hs.data(), seg, hs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+      c.sync();
+    }
+  };
+  if (top_bits > FINB && top_bits <= L - 1 && top_bits <= TOP_BITS_MAX) {
+    host_seg();
     top_cut = (uint32_t)((1ull << L) - (1ull << top_bits));
     uint64_t a = 0, z = n;   // the block's first vertex: min x with spread(x) >= cut
     while (a < z) {
@@ -2256,9 +2271,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
   uint64_t big_g0 = 0, big_g1 = 0;
   uint32_t big_cut0 = 0;
   if (forced || (top_lvl >= 0 && big_bits > top_bits && big_bits <= L - 1)) {
-    std::vector<uint64_t> hs(2 * (size_t)L);
-    HIP_CHECK(hipMemcpyAsync(hs.data(), seg, hs.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-    c.sync();
+    host_seg();
     big_cut0 = (uint32_t)((1ull << L) - (1ull << big_bits));
     uint64_t a = 0, z = n;
     while (a < z) {
@@ -2490,21 +2503,34 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     }
   }
   if (!c.timing && !g_debug_etree) return;
+  // algorithmic bytes: split reads the list and the bucket and writes the
+  // three lists; hooking reads each light edge once per round it takes part in; the
+  // cross pass reads the edge and writes its top; apply reads edge, top, m and claim
+  // and appends the contraction
+  // (the timers of the run that launched these levels: counted even if timing was switched
+  // off before they were read)
+  auto count = [&c, nglobal](const uint64_t *h) {
+    for (int lvl = 0; lvl < nglobal; ++lvl) {
+      const uint64_t *r = &h[(uint64_t)lvl * ST_ROW];
+      uint64_t hooked = r[ST_NL];
+      for (int k = 0; k < HOOK_ROUNDS - 1; ++k) hooked += r[ST_HOOK + k];
+      c.timers["etree_split"].bytes += 8 * (r[ST_LIVE] + r[ST_R0]) + 8 * (r[ST_KEPT] + r[ST_NL] + r[ST_NX]);
+      c.timers["etree_union"].bytes += 8 * hooked + 8 * r[ST_NL];
+      c.timers["etree_cross"].bytes += 12 * r[ST_NX];
+      c.timers["etree_apply"].bytes += 20 * r[ST_NX];
+    }
+  };
+  const size_t sbytes = (size_t)L * ST_ROW * sizeof(uint64_t);
+  if (!g_debug_etree) {   // counted when the timers are read: no round trip in a timed run
+    c.defer_bytes(stats, sbytes, [count](const void *h) { count((const uint64_t *)h); });
+    return;
+  }
   std::vector<uint64_t> h((uint64_t)L * ST_ROW);
-  HIP_CHECK(hipMemcpyAsync(h.data(), stats, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipMemcpyAsync(h.data(), stats, sbytes, hipMemcpyDeviceToHost, c.stream));
   c.sync();
+  if (c.timing) count(h.data());
   for (int lvl = 0; lvl < nglobal; ++lvl) {
     const uint64_t *r = &h[(uint64_t)lvl * ST_ROW];
-    uint64_t hooked = r[ST_NL];
-    for (int k = 0; k < HOOK_ROUNDS - 1; ++k) hooked += r[ST_HOOK + k];
-    // algorithmic bytes: split reads the list and the bucket and writes the
-    // three lists; hooking reads each light edge once per round it takes part in; the
-    // cross pass reads the edge and writes its top; apply reads edge, top, m and claim
-    // and appends the contraction
-    c.add_bytes("etree_split", 8 * (r[ST_LIVE] + r[ST_R0]) + 8 * (r[ST_KEPT] + r[ST_NL] + r[ST_NX]));
-    c.add_bytes("etree_union", 8 * hooked + 8 * r[ST_NL]);
-    c.add_bytes("etree_cross", 12 * r[ST_NX]);
-    c.add_bytes("etree_apply", 20 * r[ST_NX]);
     if (g_debug_etree)
       fprintf(stderr, "etree lvl %d s %d list %lu bucket %lu kept %lu light %lu cross %lu contractions %lu hook-left %lu %lu %lu\n",
               lvl, L - 1 - lvl, (unsigned long)r[ST_LIVE], (unsigned long)r[ST_R0], (unsigned long)r[ST_KEPT],

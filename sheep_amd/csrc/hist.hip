@@ -1074,11 +1074,19 @@ uint64_t group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGr
   const int L = g.L;
   uint32_t *d_bstart = c.get_as<uint32_t>("grp_bstart", g.nb + 1);
   HIP_CHECK(hipMemsetAsync(d_bstart, 0, (g.nb + 1) * sizeof(uint32_t), c.stream));
+  std::vector<uint32_t> bs;   // the bucket starts on the host (histogram_add has them after its sync)
   const uint64_t grouped = histogram_add(c, EdgeLoPadded{edges, g.d_pad, g.clo, g.mask}, m, g.K, pst, r0, g.d_kbase,
-                                         d_bstart, nullptr, nullptr, counted);
+                                         d_bstart, nullptr, &bs, counted);
   // (pinned: no sync for the copy; histogram_add's sync above ordered any earlier use)
   uint64_t *hseg = (uint64_t *)c.get_pinned("grp_segb_host", 2 * (size_t)L * sizeof(uint64_t));
   for (int s = 0; s < L; ++s) { hseg[s] = g.pstart[s] / W; hseg[L + s] = (g.pstart[s] + g.plen[s]) / W; }
+  // the same bounds for the host (the elimination tree's cut decisions read them: no copy back)
+  c.seg_host.dev = nullptr;
+  if (bs.size() == (size_t)g.nb + 1) {
+    c.seg_host.v.resize(2 * (size_t)L);
+    for (int i = 0; i < 2 * L; ++i) c.seg_host.v[i] = hseg[i] <= g.nb ? bs[hseg[i]] : 0;
+    c.seg_host.dev = seg;
+  }
   uint64_t *d_sb = c.get_as<uint64_t>("grp_segb", 2 * (size_t)L);
   HIP_CHECK(hipMemcpyAsync(d_sb, hseg, 2 * (size_t)L * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
   hipLaunchKernelGGL(k_seg_from_buckets, dim3(1), dim3(64), 0, c.stream, (const uint32_t *)d_bstart,

@@ -1258,8 +1258,8 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
           uint32_t *kk = c.get_as<uint32_t>("pt_kK", cnt);
           uint64_t *kR = c.get_as<uint64_t>("pt_kR", cnt);
           stage_kids_of(EV_STAGE, cnt - EV_STAGE, kk, kR);
-          d2h(c, seg.data() + EV_STAGE, (const uint32_t *)kk, cnt - EV_STAGE);
-          d2h(c, segR.data() + EV_STAGE, (const uint64_t *)kR, cnt - EV_STAGE);
+          c.download(seg.data() + EV_STAGE, (const uint32_t *)kk, cnt - EV_STAGE);
+          c.download(segR.data() + EV_STAGE, (const uint64_t *)kR, cnt - EV_STAGE);
           c.sync();
         }
         if (dbg) {
@@ -1328,8 +1328,8 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   if (!upl_pos.empty()) {   // persist the sorted kid orders (forwardPartition mutates kids, :104-106)
     const uint64_t mu = upl_pos.size();
     uint32_t *dp = c.get_as<uint32_t>("pt_uplpos", mu), *dv = c.get_as<uint32_t>("pt_uplids", mu);
-    h2d(c, dp, upl_pos.data(), mu);
-    h2d(c, dv, upl_ids.data(), mu);
+    c.upload(dp, upl_pos.data(), mu);
+    c.upload(dv, upl_ids.data(), mu);
     hipLaunchKernelGGL(k_scatter_u32, dim3(grid_for(mu)), dim3(BLOCK), 0, c.stream, (const uint32_t *)dp,
                        (const uint32_t *)dv, mu, k->kids);
     LAUNCH_CHECK();
@@ -1346,8 +1346,8 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
                        (const uint32_t *)t.tD, (const uint32_t *)t.tU, (const uint32_t *)rst, (const uint32_t *)ren,
                        (const uint32_t *)ev_pos, (const uint64_t *)ev_pre, m_ev, rR);
     LAUNCH_CHECK();
-    d2h(c, r_ids.data(), (const uint32_t *)rids, nroots);
-    d2h(c, r_cb.data(), (const uint64_t *)rR, nroots);
+    c.download(r_ids.data(), (const uint32_t *)rids, nroots);
+    c.download(r_cb.data(), (const uint64_t *)rR, nroots);
   }
   c.sync();   // the kid-order upload vectors die with this call
   for (const auto &ro : root_own) {   // a packed root's own removed weight
@@ -1387,8 +1387,8 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   {
     uint32_t *aid = c.get_as<uint32_t>("pt_aid", na);
     int16_t *ap = c.get_as<int16_t>("pt_ap", na);
-    h2d(c, aid, all_ids.data(), na);
-    h2d(c, ap, all_part.data(), na);
+    c.upload(aid, all_ids.data(), na);
+    c.upload(ap, all_part.data(), na);
     hipLaunchKernelGGL(k_scatter_parts, dim3(grid_for(na)), dim3(BLOCK), 0, c.stream, aid, ap, na, parts);
     LAUNCH_CHECK();
     uint32_t *st = c.get_as<uint32_t>("pt_ast", na), *en = c.get_as<uint32_t>("pt_aen", na);
@@ -1396,8 +1396,8 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
                        (const uint32_t *)rst, (const uint32_t *)ren, t.tD, t.tU, st, en);
     LAUNCH_CHECK();
     std::vector<uint32_t> hs(na), he(na);
-    d2h(c, hs.data(), st, na);
-    d2h(c, he.data(), en, na);
+    c.download(hs.data(), st, na);
+    c.download(he.data(), en, na);
     c.sync();
     std::vector<uint32_t> ord;
     ord.reserve(na);
@@ -1424,18 +1424,17 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
       uint32_t *dst_ = c.get_as<uint32_t>("pt_sst", m), *den = c.get_as<uint32_t>("pt_sen", m);
       uint32_t *dencl = c.get_as<uint32_t>("pt_encl", m);
       int16_t *dsp = c.get_as<int16_t>("pt_sp", m);
-      h2d(c, dst_, sst.data(), m);
-      h2d(c, den, sen.data(), m);
-      h2d(c, dencl, encl.data(), m);
-      h2d(c, dsp, sp.data(), m);
+      c.upload(dst_, sst.data(), m);
+      c.upload(den, sen.data(), m);
+      c.upload(dencl, encl.data(), m);
+      c.upload(dsp, sp.data(), m);
       hipLaunchKernelGGL(k_push_down, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, core.parent, t.tD, n, dst_, den, dsp,
                          dencl, m, parts, e);
       LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(k_push_fringe, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->parent,
                        (const uint8_t *)fin, n, parts, e, rake_rounds);
-    LAUNCH_CHECK();
-    c.sync();   // the staged host vectors die with this block
+    LAUNCH_CHECK();   // (the uploads were staged: the vectors may die with this block)
   }
   // 6. jnid -> vid (:62-66) and print counts (partition.h:138-139)
   unsigned long long *cnt = (unsigned long long *)c.d_scalars + 37;

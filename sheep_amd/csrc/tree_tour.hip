@@ -116,9 +116,10 @@ __global__ void k_rootnext(const uint32_t *__restrict__ rk, uint64_t nrk, const 
     rootnext[rk[i]] = i + 1 < nrk ? kids[koff[rk[i + 1]]] : INVALID;
 }
 
-__global__ void k_head(const uint32_t *__restrict__ rk, const uint32_t *__restrict__ koff,
+// (nrk: the count of roots with kids, on the device; none: no head)
+__global__ void k_head(const uint32_t *__restrict__ rk, const uint32_t *__restrict__ nrk, const uint32_t *__restrict__ koff,
                        const uint32_t *__restrict__ kids, uint32_t *__restrict__ head) {
-  if (threadIdx.x == 0) head[0] = kids[koff[rk[0]]];
+  if (threadIdx.x == 0) head[0] = *nrk ? kids[koff[rk[0]]] : INVALID;
 }
 
 __device__ __forceinline__ bool hash_ruler(uint32_t a, uint32_t mask) {
@@ -307,7 +308,14 @@ void build_tour(Ctx &c, sheep_kids *k, Tour &t) {
   uint32_t *rk = c.get_as<uint32_t>("tour_rk", n);
   hipLaunchKernelGGL(k_rk_write, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, k->parent, k->koff, n, bcnt, rk);
   LAUNCH_CHECK();
+  // head = down arc into the first kid of the first root with kids, found before the one
+  // sync that reads the count (a sync of its own cost a host round trip)
+  uint32_t *dhead = (uint32_t *)(c.d_scalars + 24);
+  hipLaunchKernelGGL(k_head, dim3(1), dim3(WAVE), 0, c.stream, (const uint32_t *)rk, (const uint32_t *)(d + 1),
+                     (const uint32_t *)k->koff, (const uint32_t *)k->kids, dhead);
+  LAUNCH_CHECK();
   HIP_CHECK(hipMemcpyAsync(c.h_scalars + 20, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 24, dhead, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
   c.sync();
   t.nroots = n - k->nkids;   // every non-root is one kid
   t.nrk = (uint32_t)c.h_scalars[21];
@@ -327,13 +335,6 @@ void build_tour(Ctx &c, sheep_kids *k, Tour &t) {
   hipLaunchKernelGGL(k_succ, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, k->parent, n, k->koff, k->kids, kidpos,
                      rootnext, succ);
   LAUNCH_CHECK();
-  // head = down arc into the first kid of the first root with kids
-  uint32_t *dhead = (uint32_t *)(c.d_scalars + 24);
-  hipLaunchKernelGGL(k_head, dim3(1), dim3(WAVE), 0, c.stream, (const uint32_t *)rk, (const uint32_t *)k->koff,
-                     (const uint32_t *)k->kids, dhead);
-  LAUNCH_CHECK();
-  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 24, dhead, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
-  c.sync();
   const uint32_t head = (uint32_t)c.h_scalars[24];
 
   uint32_t *rid = c.get_as<uint32_t>("tour_rid", 2 * n);
