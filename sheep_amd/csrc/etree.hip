@@ -1788,6 +1788,7 @@ __global__ __launch_bounds__(BLOCK) void k_big_init(BigState b) {
   if (blockIdx.x == 0 && threadIdx.x < 2) b.cnt[threadIdx.x] = 0;
 }
 
+constexpr int BIG_U = 16;   // edges per thread in flight in k_big_min0 (one 1024-thread workgroup per CU)
 constexpr uint32_t BIG_UPW = 1u << 16;   // has-upper bits kept in LDS per workgroup: a window of lo
 // H16: the window is the top 2^16 positions with each pick as a u16 distance h - l (0:
 // none); a hot vertex whose lower neighbours seen so far all lie 2^16 or more below takes
@@ -1820,7 +1821,7 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
   top_prefix(te, s_pre);
   __syncthreads();
   // The list part (the entries the extraction moved out, ~42 M at RMAT-26) strided over
-  // every workgroup, TOP_U entries per thread in flight; the group part in one contiguous
+  // every workgroup, BIG_U entries per thread in flight; the group part in one contiguous
   // chunk per workgroup.  (One chunk of list-then-groups per workgroup left the list to
   // the first ~15 workgroups, one dependent load per entry: most of the kernel's 7 ms.)
   const uint64_t nl = s_pre[NSHARD], ntiles = st[ST_TOPNT], G = te.g1 - te.g0;
@@ -1841,15 +1842,15 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
   // issued before any store: a check that waits for the previous edge's turn serialises
   // eight latencies per step, and a stale read only costs a redundant store
   const uint64_t lstride = (uint64_t)gridDim.x * TOPB;
-  for (uint64_t i0 = (uint64_t)blockIdx.x * TOPB + threadIdx.x; i0 < nl; i0 += (uint64_t)TOP_U * lstride) {
-    uint64_t e[TOP_U];
+  for (uint64_t i0 = (uint64_t)blockIdx.x * TOPB + threadIdx.x; i0 < nl; i0 += (uint64_t)BIG_U * lstride) {
+    uint64_t e[BIG_U];
 #pragma unroll
-    for (int j = 0; j < TOP_U; ++j) {
+    for (int j = 0; j < BIG_U; ++j) {
       const uint64_t i = i0 + (uint64_t)j * lstride;
       e[j] = i < nl ? top_list_at(te, s_pre, ntiles, i) : DEAD;
     }
 #pragma unroll
-    for (int j = 0; j < TOP_U; ++j) {
+    for (int j = 0; j < BIG_U; ++j) {
       if (e[j] == DEAD) continue;
       const uint32_t l = (uint32_t)e[j] - v0, h = (uint32_t)(e[j] >> 32) - v0;
       if (h >= hot0 && hot_pick(l, h)) {
@@ -1861,34 +1862,34 @@ __global__ __launch_bounds__(TOPB) void k_big_min0(TopEdges te, BigState b, cons
     }
   }
   const uint64_t *r = te.r0 + te.g0;
-  // software-pipelined: the next TOP_U edges are loaded while this batch's read checks are
+  // software-pipelined: the next BIG_U edges are loaded while this batch's read checks are
   // in flight and its picks are made
-  constexpr uint64_t STEP = (uint64_t)TOP_U * TOPB;
-  uint64_t en[TOP_U];
+  constexpr uint64_t STEP = (uint64_t)BIG_U * TOPB;
+  uint64_t en[BIG_U];
   auto load = [&](uint64_t i0) {
 #pragma unroll
-    for (int j = 0; j < TOP_U; ++j) {
+    for (int j = 0; j < BIG_U; ++j) {
       const uint64_t i = i0 + (uint64_t)j * TOPB;
       en[j] = i < g1 ? __builtin_nontemporal_load(r + i) : DEAD;
     }
   };
   if (g0 + threadIdx.x < g1) load(g0 + threadIdx.x);
   for (uint64_t i0 = g0 + threadIdx.x; i0 < g1; i0 += STEP) {
-    uint32_t l[TOP_U], h[TOP_U], gv[TOP_U], uv[TOP_U];
+    uint32_t l[BIG_U], h[BIG_U], gv[BIG_U], uv[BIG_U];
 #pragma unroll
-    for (int j = 0; j < TOP_U; ++j) {
+    for (int j = 0; j < BIG_U; ++j) {
       const uint64_t e = en[j];
       l[j] = e == DEAD ? INVALID : (uint32_t)e - v0;
       h[j] = e == DEAD ? 0 : (uint32_t)(e >> 32) - v0;
     }
 #pragma unroll
-    for (int j = 0; j < TOP_U; ++j) {
+    for (int j = 0; j < BIG_U; ++j) {
       gv[j] = l[j] != INVALID && h[j] < hot0 ? pk[h[j]] : 1u;
       uv[j] = l[j] != INVALID && l[j] - w0 >= BIG_UPW ? up[l[j]] : 1u;
     }
     if (i0 + STEP < g1) load(i0 + STEP);
 #pragma unroll
-    for (int j = 0; j < TOP_U; ++j) {
+    for (int j = 0; j < BIG_U; ++j) {
       if (l[j] == INVALID) continue;
       if (h[j] >= hot0) {
         if (!hot_pick(l[j], h[j]) && !pk[h[j]]) {   // (H16: a far pick)
