@@ -316,6 +316,7 @@ static uint64_t chunk_for(uint64_t total) {
   return (c + 8191) & ~8191ull;
 }
 
+constexpr int HF_U = 16;   // keys per thread in flight in k_hist_final (one workgroup per CU)
 __global__ __launch_bounds__(HB) void k_hist_final(const uint16_t *__restrict__ keys, const Chunk *__restrict__ chunks,
                                                    uint64_t K, const uint32_t *__restrict__ kbase,
                                                    uint32_t *__restrict__ cnt) {
@@ -323,15 +324,15 @@ __global__ __launch_bounds__(HB) void k_hist_final(const uint16_t *__restrict__ 
   const Chunk ch = chunks[blockIdx.x];
   for (uint32_t i = threadIdx.x; i < W; i += HB) lds[i] = 0;
   lds_barrier();
-  for (uint64_t i0 = ch.beg; i0 < ch.end; i0 += 8 * HB) {
-    uint32_t k[8];
+  for (uint64_t i0 = ch.beg; i0 < ch.end; i0 += HF_U * HB) {
+    uint32_t k[HF_U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < HF_U; ++j) {
       const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
       k[j] = i < ch.end ? keys[i] : NO_KEY;
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+    for (int j = 0; j < HF_U; ++j)
       if (k[j] != NO_KEY) atomicAdd(&lds[k[j]], 1u);
   }
   lds_barrier();
@@ -734,6 +735,7 @@ __global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restr
 // count pass (k_hist_count<EdgeLoPadded> over the same edges, which then does not run):
 // the chunk is walked one output tile at a time with the tile's counts in LDS after the
 // pos slice, flushed with one atomicAdd per non-zero bucket (a tile can span two chunks).
+constexpr int RG_U = 16;   // pairs per thread in flight (one 1024-thread workgroup per CU: the pos slice fills LDS)
 template <bool COUNT>
 __global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restrict__ pairs, const Chunk *__restrict__ chunks,
                                                        const uint32_t *__restrict__ pos, uint64_t pos_size,
@@ -753,15 +755,15 @@ __global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restric
     if (COUNT)
       for (uint32_t b = threadIdx.x; b < lnb; b += HB) lcnt[b] = 0;
     lds_barrier();
-    for (uint64_t i0 = t0; i0 < s1; i0 += 8 * HB) {
-      uint64_t x[8];
+    for (uint64_t i0 = t0; i0 < s1; i0 += RG_U * HB) {
+      uint64_t x[RG_U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < RG_U; ++j) {
         const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
         x[j] = i >= s1 ? NO_PAIR : pairs[i];
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < RG_U; ++j) {
         const uint64_t i = i0 + (uint64_t)j * HB + threadIdx.x;
         if (i >= s1) continue;
         const uint32_t ptm = (uint32_t)(x[j] >> 32), ph = lds[(uint32_t)x[j] & (W - 1)];
