@@ -316,7 +316,7 @@ static uint64_t chunk_for(uint64_t total) {
   return (c + 8191) & ~8191ull;
 }
 
-constexpr int HF_U = 16;   // keys per thread in flight in k_hist_final (one workgroup per CU)
+constexpr int HF_U = 32;   // keys per thread in flight in k_hist_final (one workgroup per CU)
 __global__ __launch_bounds__(HB) void k_hist_final(const uint16_t *__restrict__ keys, const Chunk *__restrict__ chunks,
                                                    uint64_t K, const uint32_t *__restrict__ kbase,
                                                    uint32_t *__restrict__ cnt) {
@@ -735,7 +735,7 @@ __global__ __launch_bounds__(NT) void k_relabel_scatter(const sheep_xs1 *__restr
 // count pass (k_hist_count<EdgeLoPadded> over the same edges, which then does not run):
 // the chunk is walked one output tile at a time with the tile's counts in LDS after the
 // pos slice, flushed with one atomicAdd per non-zero bucket (a tile can span two chunks).
-constexpr int RG_U = 16;   // pairs per thread in flight (one 1024-thread workgroup per CU: the pos slice fills LDS)
+constexpr int RG_U = 32;   // pairs per thread in flight (one 1024-thread workgroup per CU: the pos slice fills LDS)
 template <bool COUNT>
 __global__ __launch_bounds__(HB) void k_relabel_gather(const uint64_t *__restrict__ pairs, const Chunk *__restrict__ chunks,
                                                        const uint32_t *__restrict__ pos, uint64_t pos_size,
