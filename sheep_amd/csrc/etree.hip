@@ -1935,14 +1935,24 @@ __global__ __launch_bounds__(BLOCK) void k_big_roots(BigState b) {
 // the MSF {(minlo(x), x)} appended behind the level's list (st[ST_EXTRA] counts them)
 __global__ __launch_bounds__(BLOCK) void k_big_emit(BigState b) {
   const uint64_t base = b.st[ST_KEPT] + b.st[ST_CONTR];
+  // up to 32 strided vertices per thread per reservation: one atomic on the counter per
+  // workgroup call (a wave-aggregated append per wave serialised ~32 K atomics on it)
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   const uint64_t iters = (b.V + stride - 1) / stride;
-  uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  for (uint64_t it = 0; it < iters; ++it, v += stride) {   // wave-uniform (appends)
-    const uint32_t ml = v < b.V ? b.minlo[v] : INVALID;
-    const bool has = ml != INVALID;
-    const uint64_t slot = wave_append(has, (unsigned long long *)&b.st[ST_EXTRA]);
-    if (has) b.out[base + slot] = ((uint64_t)(b.v0 + v) << 32) | (b.v0 + ml);
+  const uint64_t v0 = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  for (uint64_t it0 = 0; it0 < iters; it0 += 32) {   // uniform over the workgroup (block_reserve)
+    const uint32_t ni = iters - it0 < 32 ? (uint32_t)(iters - it0) : 32u;
+    uint32_t has = 0;
+    for (uint32_t q = 0; q < ni; ++q) {
+      const uint64_t v = v0 + (it0 + q) * stride;
+      if (v < b.V && b.minlo[v] != INVALID) has |= 1u << q;
+    }
+    uint64_t slot = block_reserve((uint32_t)__popc(has), (unsigned long long *)&b.st[ST_EXTRA]);
+    for (uint32_t q = 0; q < ni; ++q)
+      if (has & (1u << q)) {
+        const uint64_t v = v0 + (it0 + q) * stride;
+        b.out[base + slot++] = ((uint64_t)(b.v0 + v) << 32) | (b.v0 + b.minlo[v]);
+      }
   }
 }
 

@@ -133,29 +133,40 @@ __device__ __forceinline__ bool hash_ruler(uint32_t a, uint32_t mask) {
 __global__ __launch_bounds__(BLOCK) void k_pick_rulers(const uint32_t *__restrict__ parent, uint64_t n, uint32_t head,
                                                        uint32_t *__restrict__ rid, uint32_t *__restrict__ rulers,
                                                        uint64_t cap, unsigned long long *__restrict__ counter, uint32_t rmask) {
+  // PR_T tiles per reservation: one atomic on the single counter per workgroup call, and
+  // that counter's serialised atomics (one per 2,048-arc tile) were the kernel's bound
+  constexpr int PR_T = 8;
   const uint64_t total = 2 * n;
-  const uint64_t ntiles = (total + TILE - 1) / TILE;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    uint32_t flags = 0;
+  const uint64_t ntiles = (total + TILE - 1) / TILE, nsup = (ntiles + PR_T - 1) / PR_T;
+  for (uint64_t sup = blockIdx.x; sup < nsup; sup += gridDim.x) {
+    uint32_t flags[PR_T], cnt = 0;
 #pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j) {
-      const uint64_t a = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
-      if (a < total) {
-        const uint32_t node = (uint32_t)(a < n ? a : a - n);
-        if (parent[node] != INVALID && (a == head || hash_ruler((uint32_t)a, rmask))) flags |= 1u << j;
-      }
-    }
-    uint64_t slot = block_reserve((uint32_t)__popc(flags), counter);
+    for (int t = 0; t < PR_T; ++t) {
+      flags[t] = 0;
+      const uint64_t tile = sup * PR_T + t;
 #pragma unroll
-    for (int j = 0; j < TILE_ITEMS; ++j)
-      if (flags & (1u << j)) {
-        const uint32_t a = (uint32_t)(tile * TILE + (uint64_t)j * BLOCK + threadIdx.x);
-        if (slot < cap) {   // overflow is reported by the host (counter > cap)
-          rid[a] = (uint32_t)slot;
-          rulers[slot] = a;
+      for (int j = 0; j < TILE_ITEMS; ++j) {
+        const uint64_t a = tile * TILE + (uint64_t)j * BLOCK + threadIdx.x;
+        if (a < total) {
+          const uint32_t node = (uint32_t)(a < n ? a : a - n);
+          if (parent[node] != INVALID && (a == head || hash_ruler((uint32_t)a, rmask))) flags[t] |= 1u << j;
         }
-        ++slot;
       }
+      cnt += (uint32_t)__popc(flags[t]);
+    }
+    uint64_t slot = block_reserve(cnt, counter);
+#pragma unroll
+    for (int t = 0; t < PR_T; ++t)
+#pragma unroll
+      for (int j = 0; j < TILE_ITEMS; ++j)
+        if (flags[t] & (1u << j)) {
+          const uint32_t a = (uint32_t)((sup * PR_T + t) * TILE + (uint64_t)j * BLOCK + threadIdx.x);
+          if (slot < cap) {   // overflow is reported by the host (counter > cap)
+            rid[a] = (uint32_t)slot;
+            rulers[slot] = a;
+          }
+          ++slot;
+        }
   }
 }
 
