@@ -68,17 +68,25 @@ constexpr int C_TILE = BLOCK * C_ITEMS;
 __global__ __launch_bounds__(BLOCK) void k_compact_count(const uint32_t *__restrict__ deg, uint64_t vs,
                                                          uint32_t *__restrict__ block_cnt,
                                                          unsigned long long *__restrict__ d_maxdeg) {
+  // tiles strided over a capped grid, the maximum reduced over all of a workgroup's tiles:
+  // one atomicMax per tile (32 K at RMAT-26, all on one word) was the kernel's bound
   __shared__ uint32_t s[BLOCK / WAVE];
-  uint64_t base = (uint64_t)blockIdx.x * C_TILE;
-  uint32_t cnt = 0, mx = 0;
-  for (int j = 0; j < C_ITEMS; ++j) {
-    uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
-    if (i < vs) { uint32_t d = deg[i]; cnt += d != 0; mx = d > mx ? d : mx; }
+  const uint64_t ntiles = (vs + C_TILE - 1) / C_TILE;
+  uint32_t mx = 0;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t base = tile * C_TILE;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int j = 0; j < C_ITEMS; ++j) {
+      const uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
+      if (i < vs) { const uint32_t d = deg[i]; cnt += d != 0; mx = d > mx ? d : mx; }
+    }
+    cnt = wave_sum(cnt);
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) block_cnt[tile] = s[0] + s[1] + s[2] + s[3];
+    __syncthreads();   // s is rewritten by the next tile
   }
-  cnt = wave_sum(cnt);
-  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = cnt;
-  __syncthreads();
-  if (threadIdx.x == 0) block_cnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
   block_atomic_max(d_maxdeg, mx);
 }
 
@@ -194,7 +202,7 @@ uint64_t sequence_from_degrees(Ctx &c, const uint32_t *deg, uint64_t vs, uint32_
   uint32_t *bcnt = c.get_as<uint32_t>("seq_bcnt", nb + 1);
   unsigned long long *d = (unsigned long long *)c.d_scalars;
   HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
-  hipLaunchKernelGGL(k_compact_count, dim3((unsigned)nb), dim3(BLOCK), 0, c.stream, deg, vs, bcnt, d);
+  hipLaunchKernelGGL(k_compact_count, dim3(grid_for(nb, 1)), dim3(BLOCK), 0, c.stream, deg, vs, bcnt, d);
   LAUNCH_CHECK();
   scan_exclusive_u32(c, bcnt, bcnt, nb, (uint32_t *)(c.d_scalars + 1));
   HIP_CHECK(hipMemcpyAsync(c.h_scalars, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
