@@ -138,6 +138,39 @@ def test_rmat_vs_oracle(gpu_ctx, scale, seed, k):
     assert ev.__dict__ == oev
 
 
+def test_timed_trees_count_their_levels(gpu_ctx):
+    """With timing on, the elimination tree's per-level list sizes travel to a pinned
+    buffer on the stream and are counted into the regions' algorithmic bytes when the
+    timers are read (no host round trip inside the timed trees): the bytes of two identical
+    maps are about twice one map's (the contraction dedup is lossy under races, so a level's
+    list length varies a little between runs), they survive timing being switched off
+    before the read, and a reset clears them.  The trees stay the oracle's."""
+    import sheep_amd
+    ctx = gpu_ctx
+    d = sheep_amd.rmat(17, 16, 13)
+    h = sheep_amd.to_numpy_u32(d).reshape(-1, 3)
+    s = sheep_amd.degree_sequence(d)
+    op, ow = oracle.build_tree(h[:, 0], h[:, 1], oracle.sequence(h[:, 0], h[:, 1]))
+    regions = ("etree_split", "etree_union", "etree_cross", "etree_apply")
+    ctx.timer_reset()
+    ctx.timing(True)
+    try:
+        p, w = _tree_np(sheep_amd.build_tree(d, s))
+        assert np.array_equal(p, op) and np.array_equal(w, ow)
+        one = {r: ctx.timer(r)[2] for r in regions}
+        assert all(v > 0 for v in one.values()), one
+        ctx.timer_reset()
+        for _ in range(2):
+            p, w = _tree_np(sheep_amd.build_tree(d, s))
+            assert np.array_equal(p, op) and np.array_equal(w, ow)
+    finally:
+        ctx.timing(False)
+    two = {r: ctx.timer(r)[2] for r in regions}   # read after timing went off
+    assert all(abs(two[r] - 2 * one[r]) <= 0.05 * 2 * one[r] for r in regions), (one, two)
+    ctx.timer_reset()
+    assert all(ctx.timer(r)[2] == 0 for r in regions)
+
+
 def test_relabel_layout_reuse_and_stale(gpu_ctx):
     """The bucketed relabel reuses the degree pass's head-bucket offsets; records changed
     in place after degree_sequence (same pointer and count, other head buckets) must be
