@@ -850,13 +850,17 @@ constexpr int FIN_LANE_BITS = 8;   // lane-per-block: 2^8 one-byte entries x 64 
 constexpr int FIN_BITS_MAX = 13;   // wave-per-block: 2^13 two-byte entries = 16 KB
 constexpr uint64_t FIN_HEAVY = 256;
 
+// (rb, re) = (seg[sg], seg[L]): the groups left, none when the top block's groups were
+// replaced by its MSF (cut); at most cap entries are written (the caller checks *n_out)
 __global__ void k_fin_gather(const uint64_t *__restrict__ list, const uint64_t *__restrict__ prev,
-                             const uint64_t *__restrict__ r0, uint64_t rb, uint64_t re, uint64_t *__restrict__ out,
-                             uint64_t *__restrict__ n_out) {
+                             const uint64_t *__restrict__ r0, const uint64_t *__restrict__ seg, int sg, int L, bool cut,
+                             uint64_t cap, uint64_t *__restrict__ out, uint64_t *__restrict__ n_out) {
   // out = list ++ r0[rb, re), halves swapped (lo << 32 | hi) so a sort on the low bits sorts by hi
   // (the top block is only ever cut above the finishing levels: prev carries no cut)
-  const uint64_t len = prev ? prev[ST_KEPT] + prev[ST_CONTR] + prev[ST_EXTRA] : 0, m = len + (re - rb);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *n_out = m;
+  const uint64_t re = seg[L], rb = cut ? re : seg[sg];
+  const uint64_t len = prev ? prev[ST_KEPT] + prev[ST_CONTR] + prev[ST_EXTRA] : 0, m0 = len + (re - rb);
+  const uint64_t m = m0 < cap ? m0 : cap;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *n_out = m0;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
     const uint64_t e = i < len ? list[i] : r0[rb + (i - len)];
@@ -2426,24 +2430,23 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     // Liu's algorithm per 2^B-position block
     TimedRegion tr(c, "etree_finish");
     const int sg = (L < FINB ? L : FINB) - 1;   // highest group left
-    uint64_t hseg[2], hrow[ST_ROW] = {};
     const uint64_t *prev = nglobal ? stats + (uint64_t)(nglobal - 1) * ST_ROW : nullptr;
-    HIP_CHECK(hipMemcpyAsync(&hseg[0], seg + sg, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-    HIP_CHECK(hipMemcpyAsync(&hseg[1], seg + L, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-    if (prev) HIP_CHECK(hipMemcpyAsync(hrow, prev, sizeof hrow, hipMemcpyDeviceToHost, c.stream));
-    c.sync();
-    if (gcut > sg) hseg[0] = hseg[1];   // the top block's groups were replaced by its MSF
-    // the finish's input exactly: the last level's list plus the groups left (sized by the
-    // list's worst case, these three buffers took ~48 GB at RMAT-26)
-    const uint64_t cap = hrow[ST_KEPT] + hrow[ST_CONTR] + hrow[ST_EXTRA] + (hseg[1] - hseg[0]) + 1;
-    uint64_t *fin = c.get_as<uint64_t>("et_fin", cap), *fin_alt = c.get_as<uint64_t>("et_fin_alt", cap);
+    // The finish's input, the last level's list plus the groups left (list + groups <= m +
+    // the cuts' MSF edges <= lcap), goes into the list buffer the last level read, and its
+    // sort's other half into lx: both are free now, so nothing is sized from the device's
+    // counts and the gather reads the list length and group bounds on the device (one host
+    // round trip, for the sort's length; buffers of their own sized by the list's worst
+    // case took ~48 GB at RMAT-26)
+    uint64_t *fin = lists[(nglobal + 1) & 1], *fin_alt = lx;
     uint64_t *n_fin = stats + (uint64_t)L * ST_ROW;
-    hipLaunchKernelGGL(k_fin_gather, dim3(grid_for(cap)), dim3(BLOCK), 0, c.stream, (const uint64_t *)lists[nglobal & 1],
-                       prev, r0, hseg[0], hseg[1], fin, n_fin);
+    hipLaunchKernelGGL(k_fin_gather, dim3(grid_for(lcap)), dim3(BLOCK), 0, c.stream, (const uint64_t *)lists[nglobal & 1],
+                       prev, r0, seg, sg, L, gcut > sg, lcap, fin, n_fin);
     LAUNCH_CHECK();
     HIP_CHECK(hipMemcpyAsync(c.h_scalars + 15, n_fin, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
     c.sync();
     const uint64_t nf = c.h_scalars[15];
+    if (nf > lcap) throw Error(SHEEP_ERR_HIP, "etree finish: input beyond the list buffer");
+    const uint64_t cap = nf + 1;
     if (nf) {
       // L + 1 bits: hi < 2^L, and DEAD (all ones) sorts after every edge
       bool in_alt = false;
