@@ -143,6 +143,8 @@ int sheep_ctx_destroy(sheep_ctx *ctx) {
   for (auto &kv : c.pinned) if (kv.second.p) hipHostFree(kv.second.p);
   for (auto &d : c.deferred) hipHostFree(d.host);
   for (auto &d : c.deferred_pool) hipHostFree(d.first);
+  if (c.stage.p) hipHostFree(c.stage.p);
+  for (char *p : c.stage_old) hipHostFree(p);
   for (auto &kv : c.timers) for (auto &p : kv.second.pending) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
   for (hipEvent_t e : c.event_pool) hipEventDestroy(e);
   if (c.h_scalars) hipHostFree(c.h_scalars);
