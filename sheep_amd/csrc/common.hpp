@@ -239,7 +239,9 @@ struct Ctx {
     HIP_CHECK(hipMemcpyAsync(d, s, cnt * sizeof(T), hipMemcpyHostToDevice, stream));
   }
   void sync() {
-    HIP_CHECK(hipStreamSynchronize(stream));
+    const hipError_t e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) after_sync.clear();   // (the vectors they fill may not outlive the error)
+    HIP_CHECK(e);
     for (auto &f : after_sync) f();
     after_sync.clear();
     stage.used = 0;
