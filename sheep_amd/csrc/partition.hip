@@ -248,23 +248,33 @@ constexpr uint64_t RAKE_CNT_MASK = (1ull << RAKE_CNT_BITS) - 1;
 
 // round 1's mark fused in: a leaf finishes when its weight is <= max_component.  lw[v] =
 // the push a round-1 leaf makes on its parent (0 for every other node), for k_rake_pull1.
+// LW: the push word as lw[v] itself (u64), or, when every finishing weight fits 32 bits
+// (max_component < 2^32 - 1), as w + 1 in a u32 (0: no push) — half the bytes for
+// k_rake_pull1's random gather over it.
+template <typename LW>
 __global__ void k_rake_init(const uint32_t *__restrict__ koff, const uint64_t *__restrict__ w, uint64_t n, uint64_t maxc,
-                            bool rake, uint64_t *__restrict__ pk, uint8_t *__restrict__ fin, uint64_t *__restrict__ lw) {
+                            bool rake, uint64_t *__restrict__ pk, uint8_t *__restrict__ fin, LW *__restrict__ lw) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride) {
     const uint32_t nk = koff[v + 1] - koff[v];
     const bool f = rake && nk == 0 && w[v] <= maxc;
     pk[v] = (w[v] << RAKE_CNT_BITS) | nk;
     fin[v] = f;
-    lw[v] = f ? (w[v] << RAKE_CNT_BITS) - 1 : 0;
+    if (sizeof(LW) == 8) lw[v] = f ? (w[v] << RAKE_CNT_BITS) - 1 : 0;
+    else lw[v] = f ? (LW)(w[v] + 1) : 0;
   }
+}
+template <typename LW> __device__ __forceinline__ uint64_t lw_push(LW x) {
+  if (sizeof(LW) == 8) return (uint64_t)x;
+  return x ? ((uint64_t)(x - 1) << RAKE_CNT_BITS) - 1 : 0;
 }
 // Round 1 as a PULL over the kid table: kids[i] sits in the list of kpar[i] (lists are
 // contiguous, parents ascending), so a wave sums its lanes' pushes per parent run and
 // adds each run with one atomic — a few neighbouring lines per wave instead of one
 // scattered atomic per leaf (66% of the nodes; ~1.1 ms of pushes at RMAT-26).
+template <typename LW>
 __global__ __launch_bounds__(BLOCK) void k_rake_pull1(const uint32_t *__restrict__ kids, const uint32_t *__restrict__ kpar,
-                                                      uint64_t nkids, const uint64_t *__restrict__ lw,
+                                                      uint64_t nkids, const LW *__restrict__ lw,
                                                       uint64_t *__restrict__ pk) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   const uint64_t iters = (nkids + stride - 1) / stride;
@@ -273,7 +283,7 @@ __global__ __launch_bounds__(BLOCK) void k_rake_pull1(const uint32_t *__restrict
   for (uint64_t it = 0; it < iters; ++it, i += stride) {   // wave-uniform trip count (shuffles)
     const bool live = i < nkids;
     const uint32_t p = live ? kpar[i] : INVALID;
-    uint64_t x = live ? lw[kids[i]] : 0;
+    uint64_t x = live ? lw_push<LW>(lw[kids[i]]) : 0;
     // inclusive segmented sum over runs of equal p (runs are contiguous lanes)
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -995,9 +1005,14 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   uint64_t *S = c.get_as<uint64_t>("pt_S", n);   // the rake's packed state, then acc, then every node's subtree sum
   uint8_t *fin = c.get_as<uint8_t>("pt_fin", n);
   const bool rake = k->max_kids <= RAKE_CNT_MASK && total < (1ull << (64 - RAKE_CNT_BITS));
-  uint64_t *lw = c.get_as<uint64_t>("pt_lw", n);
-  hipLaunchKernelGGL(k_rake_init, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->koff,
-                     (const uint64_t *)w, n, max_component, rake, S, fin, lw);
+  const bool lw32 = max_component < 0xFFFFFFFFull;   // every finishing leaf's w + 1 fits a u32
+  void *lw = c.get(std::string("pt_lw"), n * (lw32 ? 4 : 8));
+  if (lw32)
+    hipLaunchKernelGGL(k_rake_init<uint32_t>, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->koff,
+                       (const uint64_t *)w, n, max_component, rake, S, fin, (uint32_t *)lw);
+  else
+    hipLaunchKernelGGL(k_rake_init<uint64_t>, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->koff,
+                       (const uint64_t *)w, n, max_component, rake, S, fin, (uint64_t *)lw);
   LAUNCH_CHECK();
   // two rounds (1 / 2 / 3 measured 9.37 / 8.71 / 8.62 ms of partition at RMAT-26), both
   // pulls over the kid table; the second also writes the core table's flags
@@ -1006,8 +1021,12 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
   uint32_t *pref = c.get_as<uint32_t>("pt_cpref", k->nkids + 1);
   if (rake) {
     if (k->nkids) {
-      hipLaunchKernelGGL(k_rake_pull1, dim3(grid_for(k->nkids)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->kids,
-                         (const uint32_t *)k->kpar, (uint64_t)k->nkids, (const uint64_t *)lw, S);
+      if (lw32)
+        hipLaunchKernelGGL(k_rake_pull1<uint32_t>, dim3(grid_for(k->nkids)), dim3(BLOCK), 0, c.stream,
+                           (const uint32_t *)k->kids, (const uint32_t *)k->kpar, (uint64_t)k->nkids, (const uint32_t *)lw, S);
+      else
+        hipLaunchKernelGGL(k_rake_pull1<uint64_t>, dim3(grid_for(k->nkids)), dim3(BLOCK), 0, c.stream,
+                           (const uint32_t *)k->kids, (const uint32_t *)k->kpar, (uint64_t)k->nkids, (const uint64_t *)lw, S);
       LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(k_rake_mark, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, (const uint64_t *)S, n, max_component,
