@@ -334,11 +334,6 @@ __global__ __launch_bounds__(BLOCK) void k_rake_pull2(const uint32_t *__restrict
     if (live && last && x) atomicAdd((unsigned long long *)&pk[p], (unsigned long long)x);
   }
 }
-// acc out of the packed words, in place
-__global__ void k_rake_acc(uint64_t *__restrict__ pk, uint64_t n) {
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  for (uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; v < n; v += stride) pk[v] >>= RAKE_CNT_BITS;
-}
 
 // The core's kid table: the kid table's segments with finished kids dropped (order kept);
 // finished nodes become isolated (parent INVALID, no kids) so the tour skips them.
@@ -350,7 +345,7 @@ __global__ void k_core_flags(const uint32_t *__restrict__ kids, uint64_t nk, con
 __global__ void k_core_build(const uint32_t *__restrict__ kids, uint64_t nk, const uint32_t *__restrict__ koff,
                              const uint32_t *__restrict__ parent, const uint8_t *__restrict__ fin, uint64_t n,
                              const uint32_t *__restrict__ pref, uint32_t *__restrict__ ckids,
-                             uint32_t *__restrict__ ckoff, uint32_t *__restrict__ cparent) {
+                             uint32_t *__restrict__ ckoff, uint32_t *__restrict__ cparent, uint64_t *__restrict__ pk) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   const uint64_t t0 = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
   for (uint64_t j = t0; j < nk; j += stride) {   // the scanned core flags: entry j is core iff pref steps
@@ -359,7 +354,10 @@ __global__ void k_core_build(const uint32_t *__restrict__ kids, uint64_t nk, con
   }
   for (uint64_t v = t0; v <= n; v += stride) {
     ckoff[v] = pref[koff[v]];
-    if (v < n) cparent[v] = fin[v] ? INVALID : parent[v];
+    if (v < n) {
+      cparent[v] = fin[v] ? INVALID : parent[v];
+      pk[v] >>= RAKE_CNT_BITS;   // acc out of the packed rake words (the pulls are done)
+    }
   }
 }
 
@@ -1042,8 +1040,6 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
                        k->nkids, (const uint8_t *)fin, pref);
     LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(k_rake_acc, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, S, n);
-  LAUNCH_CHECK();
   sheep_kids core;
   core.ctx = &c;
   core.n = n;
@@ -1056,7 +1052,7 @@ void partition_tree(Ctx &c, const sheep_jnode *tree, uint64_t n, const uint32_t 
     scan_exclusive_u32(c, pref, pref, k->nkids + 1, tot);
     hipLaunchKernelGGL(k_core_build, dim3(grid_for(n + 1)), dim3(BLOCK), 0, c.stream, (const uint32_t *)k->kids,
                        k->nkids, (const uint32_t *)k->koff, (const uint32_t *)k->parent, (const uint8_t *)fin, n,
-                       (const uint32_t *)pref, core.kids, core.koff, core.parent);
+                       (const uint32_t *)pref, core.kids, core.koff, core.parent, S);
     LAUNCH_CHECK();
     d2h(c, c.h_scalars + 31, c.d_scalars + 31, 1);
     c.sync();
