@@ -149,7 +149,8 @@ typedef struct sheep_tuning {
   int32_t big_hot16;       /* early cut: 1 = u16-distance window over 2^16 positions */
   int32_t relabel_planes;  /* relabel scatter: 1 = stage pairs as two u32 planes, 0 = one u64 array */
   int32_t relabel_per;     /* relabel scatter: records per thread per staged sub-tile, 4, 8, 12 or 15 */
-  int32_t cross_win_levels;/* etree: levels (from the first) whose cross pass keeps minima in an LDS window, 0..8 */
+  int32_t cross_win_levels;/* etree: levels (from the first) whose cross pass keeps minima in an LDS window, 0..8
+                            * (maps too sparse for the early cut: one more) */
   int32_t hook_batch;      /* etree hook rounds find all of a thread's roots at once: 0 never, 1 merges, 2 all */
   int32_t merge_cut_bits;  /* merges: the early MSF cut of the top 2^bits positions, whatever the density: 0 off, 14..30 */
   int32_t event_loop;      /* partition packing events: 0 one launch per event, else one persistent launch while the

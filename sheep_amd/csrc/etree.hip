@@ -2301,6 +2301,11 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     const uint64_t big_dense = (uint64_t)c.tune.big_dense;
     if (n - a >= 2 && (forced || big_g1 - big_g0 >= big_dense * (n - a))) big_lvl = L - 1 - big_bits;
   }
+  // The cross pass's LDS window (k_cross_find_win) for the first cross_win_levels levels; a
+  // map too sparse for the early cut keeps singleton roots in lo order one level longer and
+  // takes one window level more (8 RMAT-26 shard maps 65.3 -> 64.4 ms; a dense map and the
+  // merges lose with it: C3 +0.5 ms, 8-tree merge +0.1 ms)
+  const int win_levels = std::min(8, c.tune.cross_win_levels + (top_bits > 0 && big_lvl < 0 && filt_lvl < 0 ? 1 : 0));
   int cut_lvl = -1;           // the level whose split follows a cut (its list entries dropped)
   uint32_t cut_val = 0;
   // a split reads at most the list plus a bucket: (lcap + m) entries, in SPLIT_TILE tiles
@@ -2344,7 +2349,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     }
     {
       TimedRegion tr(c, "etree_cross");
-      if (lvl < c.tune.cross_win_levels)
+      if (lvl < win_levels)
         hipLaunchKernelGGL(k_cross_find_win, dim3(grid_for(mcap, XW_STEP, 1024)), dim3(XWB),
                            (XW + XWB / WAVE) * 4, c.stream, (const uint64_t *)lx, (const uint64_t *)st, uf,
                            mt, xtop, g);
