@@ -120,7 +120,8 @@ int sheep_ctx_trim(sheep_ctx *ctx) {
   HIP_CHECK(hipStreamSynchronize(c.stream));
   for (auto &kv : c.ws) if (kv.second.p) HIP_CHECK(hipFree(kv.second.p));
   c.ws.clear();
-  c.head_layout = sheep::Ctx::HeadLayout();   // its offsets lived in the workspace
+  for (auto &l : c.layouts) l = sheep::Ctx::HeadLayout();   // their offsets lived in the workspace
+  c.layout_next = 0;
   c.step_edges = sheep::Ctx::StepEdges();     // and the last map's grouped edges
   if (c.kid_spare.parent) {
     hipFree(c.kid_spare.parent); hipFree(c.kid_spare.koff); hipFree(c.kid_spare.kids); hipFree(c.kid_spare.kpar);

@@ -117,11 +117,35 @@ struct Ctx {
   static constexpr int NSCALARS = 72;
   static constexpr int SCAN_TICKET = 64;   // d_scalars word of the scans' last-block ticket (zero between scans)
 
-  // Bucket layout of the last degree_count's head histogram (LLAMA mode): the scanned
-  // (bucket, tile) offsets live in ws["head_offsets"]; relabel_bucketed reuses them when
-  // it sees the same records and key range (and verifies every region's count in-kernel).
-  struct HeadLayout { const void *rec = nullptr; uint64_t nrec = 0, K = 0; std::vector<uint32_t> bstart; bool valid = false; };
-  HeadLayout head_layout;
+  // Bucket layouts of the last degree_count head histograms (LLAMA mode), one per record
+  // buffer (up to NLAYOUT, round robin: the shards of one rank's step each keep theirs):
+  // the scanned (bucket, tile) offsets live in ws[layout_buf(slot)]; relabel_bucketed
+  // reuses them when it sees the same records (and verifies every region's count in-kernel).
+  struct HeadLayout { const void *rec = nullptr; uint64_t nrec = 0, K = 0; std::vector<uint32_t> bstart; bool valid = false; int slot = 0; };
+  static constexpr int NLAYOUT = 8;
+  HeadLayout layouts[NLAYOUT];
+  int layout_next = 0;
+  static std::string layout_buf(int slot) { return slot ? "head_offsets" + std::to_string(slot) : "head_offsets"; }
+  HeadLayout *find_layout(const void *rec, uint64_t nrec) {
+    for (auto &l : layouts)
+      if (l.valid && l.rec == rec && l.nrec == nrec) return &l;
+    return nullptr;
+  }
+  // the slot for this record buffer: its own, else the next one round robin (invalidated)
+  HeadLayout &layout_for(const void *rec, uint64_t nrec) {
+    for (int i = 0; i < NLAYOUT; ++i)
+      if (layouts[i].rec == rec && layouts[i].nrec == nrec) {
+        layouts[i].valid = false;
+        layouts[i].bstart.clear();
+        layouts[i].slot = i;
+        return layouts[i];
+      }
+    const int i = layout_next;
+    layout_next = (layout_next + 1) % NLAYOUT;
+    layouts[i] = HeadLayout();
+    layouts[i].slot = i;
+    return layouts[i];
+  }
   // the degree pass's sortedness probe of the last record buffer (sequence.hip)
   struct SortedProbe { const void *rec = nullptr; uint64_t nrec = 0; bool sorted = true; };
   SortedProbe sorted_probe;

@@ -813,15 +813,13 @@ bool degree_fused(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uint32_
 }
 
 void histogram_heads(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt, bool counted) {
-  Ctx::HeadLayout &hl = c.head_layout;
-  hl.valid = false;
-  hl.bstart.clear();
+  Ctx::HeadLayout &hl = c.layout_for(rec, nrec);
   const uint64_t nb = (K + W - 1) >> WBITS, ntiles = (nrec + TKEYS - 1) >> TLOG;
   if (!llama || nb == 0 || nb > 8192 || ntiles * nb + 1 >= (1ull << 32)) {
     histogram_add(c, HeadKeys{rec, llama}, nrec, K, cnt, nullptr, nullptr, nullptr, nullptr, nullptr, counted);
     return;
   }
-  uint32_t *save = c.get_as<uint32_t>("head_offsets", ntiles * nb + 1);
+  uint32_t *save = c.get_as<uint32_t>(Ctx::layout_buf(hl.slot), ntiles * nb + 1);
   histogram_add(c, HeadKeys{rec, llama}, nrec, K, cnt, nullptr, nullptr, nullptr, save, &hl.bstart, counted);
   hl.rec = rec;
   hl.nrec = nrec;
@@ -842,9 +840,7 @@ bool degree_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int mode, uin
 
 void histogram_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama, uint64_t K, uint32_t *cnt,
                          bool counted) {
-  Ctx::HeadLayout &hl = c.head_layout;
-  hl.valid = false;
-  hl.bstart.clear();
+  Ctx::HeadLayout &hl = c.layout_for(rec, nrec);
   if (!counted) {   // the relabel counts its own head layout
     histogram_add(c, EndpointKeys{rec, nrec, llama}, 2 * nrec, K, cnt);
     return;
@@ -856,7 +852,7 @@ void histogram_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama,
   const uint64_t nt = (nrec + TKEYS - 1) >> TLOG, nb = (K + W - 1) >> WBITS;
   if (llama && nb && nb <= 8192 && nt * nb + 1 < (1ull << 32)) {
     const uint32_t *tile_hist = c.get_as<uint32_t>("hist_tiles", 2 * nt * nb + 1);
-    uint32_t *off = c.get_as<uint32_t>("head_offsets", nt * nb + 1);
+    uint32_t *off = c.get_as<uint32_t>(Ctx::layout_buf(hl.slot), nt * nb + 1);
     hipLaunchKernelGGL(k_head_cols, dim3(grid_for(nt * nb)), dim3(BLOCK), 0, c.stream, tile_hist, nt, (uint32_t)nb, off);
     LAUNCH_CHECK();
     scan_exclusive_u32(c, off, off, nt * nb, off + nt * nb);
@@ -876,6 +872,8 @@ void histogram_endpoints(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, int llama,
                 nullptr, nullptr, true);
 }
 
+void fill_u32(Ctx &c, uint32_t *p, uint64_t n, uint32_t v);   // sequence.hip
+
 uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
                           uint64_t n_tree, uint32_t *pst, uint64_t *edges, unsigned long long *err, const LoGroup *lg,
                           bool *counted) {
@@ -888,10 +886,13 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
                         (const void *)k_relabel_scatter<4, 512, true>,
                         (const void *)k_relabel_gather<false>, (const void *)k_relabel_gather<true>})
     allow_full_lds(f);
-  Ctx::HeadLayout &hl = c.head_layout;
+  Ctx::HeadLayout *found = c.find_layout(rec, nrec);
+  Ctx::HeadLayout *hlp = found;
   unsigned long long *flags = c.get_as<unsigned long long>("rl_flags", 2);
   auto recount = [&]() -> uint32_t * {   // the relabel's own (bucket, tile) offsets
-    uint32_t *off = c.get_as<uint32_t>("head_offsets", ntiles * nb + 1);
+    hlp = &c.layout_for(rec, nrec);
+    Ctx::HeadLayout &hl = *hlp;
+    uint32_t *off = c.get_as<uint32_t>(Ctx::layout_buf(hl.slot), ntiles * nb + 1);
     hipLaunchKernelGGL(k_hist_count<RelabelKeys>, dim3((unsigned)ntiles), dim3(CB), nb * 4, c.stream,
                        RelabelKeys{rec, pos_size}, nrec, (uint32_t)nb, off, ntiles);
     LAUNCH_CHECK();
@@ -909,9 +910,35 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
     hl.valid = true;
     return off;
   };
-  const bool cached = hl.valid && hl.rec == rec && hl.nrec == nrec && hl.K == pos_size && hl.bstart.size() == nb + 1;
-  uint32_t *off = cached ? c.get_as<uint32_t>("head_offsets", ntiles * nb + 1) : recount();
-  const uint64_t total = hl.bstart[nb];
+  // The degree pass's layout serves whenever it has this many buckets: its key range K (the
+  // records' largest slot + 1) may sit below pos_size (a shard's records, the sequence of
+  // all shards), but no head reaches past K, so the buckets and their counts are the same.
+  // (A layout that does not match the records is caught by the scatter's region check.)
+  // A layout with fewer buckets (a shard of tail-sorted records: its largest slot sits below
+  // the sequence's) serves too: the buckets past it are empty, so its offsets are copied
+  // and the missing rows filled with the total (bst: the bucket starts this call uses).
+  const bool cached = found && found->K <= pos_size && found->bstart.size() >= 2 && found->bstart.size() <= nb + 1;
+  std::vector<uint32_t> bst;
+  uint32_t *off;
+  if (cached && found->bstart.size() == nb + 1) {
+    off = c.get_as<uint32_t>(Ctx::layout_buf(found->slot), ntiles * nb + 1);
+    bst = found->bstart;
+  } else if (cached) {
+    const uint64_t nbc = found->bstart.size() - 1;
+    const uint32_t tot = found->bstart[nbc];
+    const uint32_t *src = c.get_as<uint32_t>(Ctx::layout_buf(found->slot), ntiles * nbc + 1);
+    off = c.get_as<uint32_t>("head_offsets_ext", ntiles * nb + 1);
+    HIP_CHECK(hipMemcpyAsync(off, src, ntiles * nbc * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
+    fill_u32(c, off + ntiles * nbc, ntiles * (nb - nbc) + 1, tot);
+    bst = found->bstart;
+    bst.resize(nb + 1, tot);
+  } else {
+    off = recount();
+    bst = hlp->bstart;
+  }
+  Ctx::HeadLayout &hl = *hlp;
+  (void)hl;
+  const uint64_t total = bst[nb];
   // (the pairs die with the gather: their workspace is the elimination tree's first list
   // buffer, et_list1, which the levels fill only after the relabel)
   uint64_t *pairs = c.get_as<uint64_t>("et_list1", total ? total : 1);
@@ -972,10 +999,10 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
   // pst / error counts are cleared.
   const uint64_t ntiles_e_max = (total + TKEYS - 1) >> TLOG;
   auto gather = [&]() -> bool {
-    const uint64_t m = hl.bstart[nb];
+    const uint64_t m = bst[nb];
     const uint64_t chunk = chunk_for(m);
     uint64_t nch = 0;
-    for (uint32_t b = 0; b < nb; ++b) nch += (hl.bstart[b + 1] - hl.bstart[b] + chunk - 1) / chunk;
+    for (uint32_t b = 0; b < nb; ++b) nch += (bst[b + 1] - bst[b] + chunk - 1) / chunk;
     // the grouping's count pass fused in when its bucket counters fit beside the pos slice
     const uint64_t ntiles_e = (m + TKEYS - 1) >> TLOG;
     const bool count = lg && m && lg->nb && ((size_t)W + lg->nb) * 4 <= 160 * 1024 &&
@@ -989,7 +1016,7 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
     Chunk *hch = (Chunk *)c.get_pinned("rl_chunks_host", nch * sizeof(Chunk));
     uint64_t j = 0;
     for (uint32_t b = 0; b < nb; ++b) {
-      const uint64_t beg = hl.bstart[b], end = hl.bstart[b + 1];
+      const uint64_t beg = bst[b], end = bst[b + 1];
       for (uint64_t x = beg; x < end; x += chunk) hch[j++] = {x, x + chunk < end ? x + chunk : end, b, 0};
     }
     Chunk *dch = c.get_as<Chunk>("rl_chunks", nch);
@@ -1014,13 +1041,14 @@ uint64_t relabel_bucketed(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uin
     HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned long long), c.stream));
     if (n_tree) HIP_CHECK(hipMemsetAsync(pst, 0, n_tree * sizeof(uint32_t), c.stream));
     off = recount();
-    if (hl.bstart[nb] > total) pairs = c.get_as<uint64_t>("et_list1", hl.bstart[nb]);
+    bst = hl.bstart;
+    if (bst[nb] > total) pairs = c.get_as<uint64_t>("et_list1", bst[nb]);
     scatter();
     count = gather();
     c.sync();
     if (c.h_scalars[13]) throw Error(SHEEP_ERR_HIP, "relabel: bucket layout inconsistent with its own count");
   }
-  const uint64_t m = hl.bstart[nb];
+  const uint64_t m = bst[nb];
   if (c.h_scalars[12]) HIP_CHECK(hipMemsetAsync(err, 0xFF, 1, c.stream));   // range error (reported by the caller)
   if (counted) *counted = count;
   return m;
