@@ -119,6 +119,8 @@ int sheep_malloc(sheep_ctx *ctx, size_t bytes, void **dev_out);
 int sheep_free(sheep_ctx *ctx, void *dev);
 int sheep_memcpy_h2d(sheep_ctx *ctx, void *dst_dev, const void *src_host, size_t bytes);
 int sheep_memcpy_d2h(sheep_ctx *ctx, void *dst_host, const void *src_dev, size_t bytes);
+/* device to device on the context's stream (asynchronous) */
+int sheep_memcpy_d2d(sheep_ctx *ctx, void *dst_dev, const void *src_dev, size_t bytes);
 /* Device-side timing per instrumented region (HIP events on the context stream; see
  * DESIGN.md §Measurement): name = "degree" | "relabel" | "etree" | ...; returns the
  * accumulated ms, launch count and algorithmic bytes since the last reset. */
@@ -248,8 +250,11 @@ int sheep_evaluate(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec,
  * index pos_dev[0, pos_size)) left grouped in HBM: no pass over the records unless they
  * hold self-loops, and the random side of every edge reads jnid-indexed state (parts: 2 B
  * per node, owner bits: 8 B per node per metric for k <= 64) instead of vid-indexed rows.
- * SHEEP_ERR_ARG when the context's last map ran on other records or another sequence (or
- * the context was trimmed since); the records must be unchanged since that map. */
+ * SHEEP_ERR_ARG when the context's last map ran on other records or another index (or the
+ * context was trimmed since), or when seq_dev is not the sequence pos_dev indexes
+ * (pos[seq[j]] != j, checked on the device); the records must be unchanged since that map.
+ * An edge endpoint without a part is SHEEP_ERR_RANGE, as in sheep_evaluate; a sequenced
+ * vertex that is no endpoint may have none. */
 int sheep_evaluate_step(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec,
                         const uint32_t *seq_dev, uint64_t seq_n, const uint32_t *pos_dev, uint64_t pos_size,
                         const int16_t *parts_vid_dev, int what, sheep_eval *out);
@@ -324,7 +329,16 @@ int sheep_edge_parts(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec, co
  *   sheep_group_transfer        one point-to-point move of `bytes` from rank `from`'s src to
  *                               rank `to`'s dst (ncclSend/ncclRecv in one group under RCCL; the
  *                               hop of mpi_merge's MPI_Reduce, jnode.cpp:238-241); src / dst
- *                               matter only where that rank is local */
+ *                               matter only where that rank is local
+ * Failure (the job-ending behaviour of MPI's default error handler, graph2tree.cpp:134-157):
+ * no call waits on another rank for longer than SHEEP_JOIN_TIMEOUT seconds (default 300).
+ * A joined world's communicator is non-blocking (ncclConfig_t.blocking = 0); every collective
+ * polls ncclCommGetAsyncError and its streams against that deadline, and the TCP links poll
+ * their sockets.  On an RCCL error, a dead peer or an expired deadline the call aborts the
+ * communicators (ncclCommAbort), prints one line per local rank to stderr ("sheep: rank R of
+ * W (bus B): COLLECTIVE of N bytes failed: CAUSE") and returns SHEEP_ERR_HIP; every later
+ * collective of that world fails at once (sheep_group_failed = 1), and destroying it is safe.
+ *   sheep_group_abort           the same on request (reason: the text of the stderr line) */
 typedef struct sheep_group sheep_group;
 #define SHEEP_LINK_AUTO 0
 #define SHEEP_LINK_RCCL 1
@@ -337,6 +351,8 @@ int sheep_group_local_count(const sheep_group *g);         /* ranks held by this
 int sheep_group_rank(const sheep_group *g, int local);     /* global rank of local rank i */
 sheep_ctx *sheep_group_ctx(sheep_group *g, int local);
 int sheep_group_uses_rccl(const sheep_group *g);
+int sheep_group_abort(sheep_group *g, const char *reason);
+int sheep_group_failed(const sheep_group *g);               /* 1 after a failed collective or an abort */
 int sheep_group_barrier(sheep_group *g);
 int sheep_group_allreduce_max_u64(sheep_group *g, uint64_t *value);
 /* sheep_ctx_set_tuning on every context of this process's ranks */
@@ -361,9 +377,28 @@ int sheep_group_evaluate(sheep_group *g, const sheep_xs1 *const *rec_dev, const 
  * own buffer hashes (tests/test_dist.py checks both on CPUs). */
 int sheep_mesh_selftest(int rank, int world, const char *host, int port, uint64_t bytes, uint64_t *checksum_out,
                         uint64_t *max_out);
+/* Host-only check of the links' deadline: rank stall_rank joins and then takes no part; every
+ * other rank's barrier must fail (SHEEP_ERR_HIP, sheep_last_error naming the peer) within
+ * timeout_s.  *waited_s_out = the barrier's wait (0 on the stalled rank, which returns
+ * SHEEP_OK after sleeping past the deadline). */
+int sheep_mesh_selftest_stall(int rank, int world, const char *host, int port, int stall_rank, int timeout_s,
+                              double *waited_s_out);
 
 /* ---- tree facts (TREEFAQS) -------------------------------------------------------- */
 int sheep_facts(sheep_ctx *ctx, const sheep_jnode *tree_dev, uint64_t n, sheep_facts_t *out);
+
+/* ---- .dat partial loads (LLAMAGraph(filename, part, num_parts), graph_wrapper.h:43-63) ----
+ * Host-only.  sheep_dat_range: records [*first_out, *first_out + *count_out) of a .dat file
+ * (R = file size / 12 records) form part `part` of `num_parts` (1-indexed, contiguous:
+ * [(part-1)R/num_parts, part R/num_parts); num_parts = 0: the whole file).
+ * sheep_read_dat: preads exactly records [first, first + count) into out_host (no other byte
+ * of the file is read); *got_out = records read.  An unreadable file is SHEEP_ERR_ARG.
+ * sheep_record_stats (device; synchronises): *max_slot_out = 1 + the largest vid of
+ * rec_dev[0, nrec) (LLAMA max_nodes, 0 for no records), *loops_out = self-loop records. */
+int sheep_dat_range(const char *filename, uint64_t part, uint64_t num_parts, uint64_t *first_out, uint64_t *count_out);
+int sheep_read_dat(const char *filename, uint64_t first, uint64_t count, sheep_xs1 *out_host, uint64_t *got_out);
+int sheep_record_stats(sheep_ctx *ctx, const sheep_xs1 *rec_dev, uint64_t nrec, uint64_t *max_slot_out,
+                       uint64_t *loops_out);
 
 /* ---- .net (SNAP text) ingest ---------------------------------------------------------
  * text_dev[0, bytes): a SNAP text edge list in HBM.  Whitespace-separated unsigned decimal

@@ -151,6 +151,8 @@ def lib() -> ctypes.CDLL:
         "sheep_group_rank": ([P, I32], I32),
         "sheep_group_ctx": ([P, I32], P),
         "sheep_group_uses_rccl": ([P], I32),
+        "sheep_group_abort": ([P, ctypes.c_char_p], I32),
+        "sheep_group_failed": ([P], I32),
         "sheep_group_barrier": ([P], I32),
         "sheep_group_allreduce_max_u64": ([P, ctypes.POINTER(U64)], I32),
         "sheep_group_reduce_trees": ([P, P, U64, I32], I32),
@@ -690,6 +692,16 @@ class Group:
     @property
     def rccl(self) -> bool:
         return bool(lib().sheep_group_uses_rccl(self.handle))
+
+    @property
+    def failed(self) -> bool:
+        """A collective failed or timed out (SHEEP_JOIN_TIMEOUT), or abort() ran: the
+        communicators are aborted and every later collective raises."""
+        return bool(lib().sheep_group_failed(self.handle))
+
+    def abort(self, reason: str = "requested by the caller"):
+        """sheep_group_abort: end the world (ncclCommAbort), one stderr line per local rank."""
+        _check(lib().sheep_group_abort(self.handle, reason.encode()))
 
     def close(self):
         if getattr(self, "handle", None):

@@ -51,37 +51,24 @@ static int run_world(World &w, const char *graph_filename, bool use_mpi_sort, bo
   }
   const bool leader_here = w.rank(0) == 0;   // rank 0 prints (graph2tree.cpp:158-159)
   if (verbose) printf("Loading %s...\n", graph_filename);
-  std::vector<sheep_xs1> all;
-  if (is_dat(graph_filename)) {
-    all = readRecords(graph_filename);
-  } else {   // SNAP text, parsed on the first local rank's GPU
-    uint64_t nr = 0;
-    DeviceArray<sheep_xs1> d = parseNet(graph_filename, true, &nr, w.ctx(0));
-    all.resize(nr);
-    if (nr) d.download(all.data(), nr);
-  }
-  const uint64_t R = all.size();
-  uint64_t cap = 1;   // the degree array's capacity: the same on every rank
-  for (const sheep_xs1 &x : all) cap = std::max<uint64_t>(cap, (uint64_t)std::max(x.tail, x.head) + 1);
   std::vector<RankState> rk(L);
-  for (int i = 0; i < L; ++i) {   // rank r loads part r+1 of P (graph2tree.cpp:137-143, 162)
+  uint64_t cap = 1;   // the degree array's capacity: the same on every rank (the world's max vid + 1)
+  for (int i = 0; i < L; ++i) {   // rank r loads part r+1 of P (graph2tree.cpp:137-143, 162): only its records
     const int r = w.rank(i);
-    const uint64_t beg = (uint64_t)r * R / P, end = (uint64_t)(r + 1) * R / P;
     rk[i].rank = r;
-    rk[i].host.assign(all.begin() + beg, all.begin() + end);
-    rk[i].rec = DeviceArray<sheep_xs1>(end - beg, w.ctx(i));
-    if (end > beg) rk[i].rec.upload(rk[i].host.data(), end - beg);
-    for (const sheep_xs1 &x : rk[i].host)
-      rk[i].max_vid = std::max<uint64_t>(rk[i].max_vid, (uint64_t)std::max(x.tail, x.head) + 1);
+    rk[i].rec = loadRecords(graph_filename, (size_t)r + 1, (size_t)P, w.ctx(i), true, &rk[i].nrec);
+    uint64_t loops = 0;
+    recordStats(w.ctx(i), rk[i].rec.get(), rk[i].nrec, &rk[i].max_vid, &loops);
+    cap = std::max(cap, rk[i].max_vid);
   }
-  std::vector<sheep_xs1>().swap(all);
+  check(sheep_group_allreduce_max_u64(w.handle(), &cap));
   const double load_s = seconds_since(start_point);
   if (leader_here) printf("Loaded graph in: %f seconds\n", load_s);
 
   std::vector<const sheep_xs1 *> recp(L);
   std::vector<uint64_t> nrec(L);
   std::vector<uint32_t *> seqp(L), posp(L), degp(L);
-  for (int i = 0; i < L; ++i) { recp[i] = rk[i].rec.get(); nrec[i] = rk[i].host.size(); }
+  for (int i = 0; i < L; ++i) { recp[i] = rk[i].rec.get(); nrec[i] = rk[i].nrec; }
   uint64_t n = 0, pos_size = 0;
   if (use_mpi_sort) {   // mpiSequence (sequence.h:65-93)
     const std::vector<uint32_t> zero(cap, 0);
@@ -164,7 +151,9 @@ static int run_world(World &w, const char *graph_filename, bool use_mpi_sort, bo
                                ep.get()));
         std::vector<int16_t> eh(nrec[i]);
         if (nrec[i]) ep.download(eh.data(), nrec[i]);
-        write_partition_files(rk[i].host, eh, max_part, rk[i].max_vid, rank_output(rk[i].rank).c_str(), false, false);
+        std::vector<sheep_xs1> host(nrec[i]);   // (the writer's records: read back only to write them)
+        if (nrec[i]) rk[i].rec.download(host.data(), nrec[i]);
+        write_partition_files(host, eh, max_part, rk[i].max_vid, rank_output(rk[i].rank).c_str(), false, false);
       }
     } else if (leader_here) {
       printf("Actually created %d partitions.\n", (int)info.created);

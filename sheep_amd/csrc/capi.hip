@@ -50,6 +50,7 @@ void eval_finish(Ctx &c, const uint64_t *bits, const uint64_t *acc, uint64_t pos
 void tree_facts(Ctx &c, const sheep_jnode *tree, uint64_t n, sheep_facts_t *out);
 void edge_parts(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
                 const int16_t *parts_vid, int16_t *out);
+void record_stats(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, uint64_t *max_slot, uint64_t *loops);
 uint64_t parse_net(Ctx &c, const char *text, uint64_t bytes, int skip_comments, sheep_xs1 *out, uint64_t cap);
 uint64_t rmat_generate(Ctx &c, int scale, int ef, uint64_t seed, sheep_xs1 *out, uint64_t cap);
 uint64_t powerlaw_generate(Ctx &c, uint64_t V, uint64_t M, double gamma, uint64_t seed, sheep_xs1 *out, uint64_t cap);
@@ -204,6 +205,22 @@ int sheep_memcpy_d2h(sheep_ctx *ctx, void *dst, const void *src, size_t bytes) {
   API_END
 }
 
+int sheep_memcpy_d2d(sheep_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  API_BEGIN
+  DeviceGuard dg(ctx);
+  NEED(ctx, "null ctx");
+  if (bytes) HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->c.stream));
+  API_END
+}
+
+int sheep_record_stats(sheep_ctx *ctx, const sheep_xs1 *rec, uint64_t nrec, uint64_t *max_slot_out, uint64_t *loops_out) {
+  API_BEGIN
+  DeviceGuard dg(ctx);
+  NEED(ctx && (rec || !nrec) && max_slot_out && loops_out, "null argument");
+  sheep::record_stats(ctx->c, rec, nrec, max_slot_out, loops_out);
+  API_END
+}
+
 int sheep_timer_enable(sheep_ctx *ctx, int on) {
   API_BEGIN
   DeviceGuard dg(ctx);
@@ -264,8 +281,8 @@ static sheep_tuning resolve_tuning(const sheep_tuning *t) {
 #define SHEEP_TUNE(f, ok)                                                                  \
   if (r.f == SHEEP_TUNE_DEFAULT) r.f = d.f;                                                \
   else if (!(ok)) throw sheep::Error(SHEEP_ERR_ARG, "sheep_tuning: " #f " out of range");
-  SHEEP_TUNE(fin_map_bits, r.fin_map_bits >= 1 && r.fin_map_bits <= 13)
-  SHEEP_TUNE(fin_merge_bits, r.fin_merge_bits >= 1 && r.fin_merge_bits <= 13)
+  SHEEP_TUNE(fin_map_bits, r.fin_map_bits >= 8 && r.fin_map_bits <= 13)
+  SHEEP_TUNE(fin_merge_bits, r.fin_merge_bits >= 8 && r.fin_merge_bits <= 13)
   SHEEP_TUNE(fin_dc, r.fin_dc == 0 || r.fin_dc == 1)
   SHEEP_TUNE(top_bits, r.top_bits == 0 || (r.top_bits >= 9 && r.top_bits <= 16))
   SHEEP_TUNE(top_blocks, r.top_blocks >= 1 && r.top_blocks <= 9)

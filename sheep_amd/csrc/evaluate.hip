@@ -382,14 +382,18 @@ namespace {
 // part to its sets and counts them; an endpoint without a position or a part is the
 // reference's pos.at() throw, as in k_eval_records.
 __global__ void k_parts_jnid(const uint32_t *__restrict__ seq, uint64_t n, const int16_t *__restrict__ parts_vid,
-                             uint64_t pos_size, int16_t *__restrict__ pj, unsigned long long *__restrict__ bad) {
+                             const uint32_t *__restrict__ pos, uint64_t pos_size, int16_t *__restrict__ pj,
+                             unsigned long long *__restrict__ bad) {
+  // pj[x] = the part of seq[x] (-1: none; an error only where x turns out to be an edge
+  // endpoint, as in k_eval_records).  pos[seq[x]] == x checks that seq is the sequence the
+  // map's index (and so its edges) came from.
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   bool b = false;
   for (uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; x < n; x += stride) {
     const uint32_t v = seq[x];
-    const int16_t p = v < pos_size ? parts_vid[v] : (int16_t)-1;
-    b |= p < 0;
-    pj[x] = p;
+    const bool in = v < pos_size;
+    b |= !in || pos[v] != (uint32_t)x;
+    pj[x] = in ? parts_vid[v] : (int16_t)-1;
   }
   if (__any(b) && (threadIdx.x & 63) == 0) atomicAdd(bad, 1ull);
 }
@@ -411,15 +415,19 @@ __global__ __launch_bounds__(BLOCK) void k_eval_edges(const uint64_t *__restrict
   const int au = (what & 4) ? ((what & 2) ? 1 : 0) : -1;
   const int ah = (what & 1) ? M - 2 : -1, av = (what & 1) ? M - 1 : -1;
   const bool need_hi = (what & 5) != 0;   // up, hash and Vcom read the hi end's part
-  uint64_t cut = 0;
+  uint64_t cut = 0, nopart = 0;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   const uint64_t iters = (m + stride - 1) / stride;
   uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
   for (uint64_t it = 0; it < iters; ++it, i += stride) {   // wave-uniform trip count (wave_count)
-    const bool live = i < m;
-    const uint64_t e = live ? __builtin_nontemporal_load(&edges[i]) : 0ull;   // (streamed once: caches kept for the rows)
+    const bool in = i < m;
+    const uint64_t e = in ? __builtin_nontemporal_load(&edges[i]) : 0ull;   // (streamed once: caches kept for the rows)
     const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
-    const int pl = live ? pj[lo] : 0, ph = live && need_hi ? pj[hi] : 0;
+    const int pl = in ? pj[lo] : 0, ph = in && need_hi ? pj[hi] : 0;
+    // an endpoint without a part (-1) is the reference's throw: counted, never an index (a
+    // hi end's part is read here only when a metric needs it; the node pass checks the rest)
+    const bool live = in && pl >= 0 && ph >= 0;
+    nopart += in && !live;
     int po = 0;
     if ((what & 1) && live) {
       po = cormen_hash(seq[lo]) < cormen_hash(seq[hi]) ? pl : ph;
@@ -444,6 +452,7 @@ __global__ __launch_bounds__(BLOCK) void k_eval_edges(const uint64_t *__restrict
     if (au >= 0) up_own[hi] = 1;
   }
   block_atomic_add(&acc[AC_CUT], cut);
+  block_atomic_add(&acc[AC_BAD], nopart);
   __syncthreads();
   if (lds)
     for (int x = threadIdx.x; x < 3 * nparts; x += BLOCK) {
@@ -469,6 +478,7 @@ __global__ __launch_bounds__(BLOCK) void k_eval_loops(const sheep_xs1 *__restric
     if (r.tail != r.head) continue;
     ++loops;
     const int p = pj[pt];
+    if (p < 0) { ++bad; continue; }
     for (int a = 0; a < M; ++a) or_bits(bits, (uint64_t)pt * RW + a * W64 + (p >> 6), 1ull << (p & 63));
   }
   block_atomic_add(&acc[AC_LOOPS], loops);
@@ -482,7 +492,8 @@ __global__ __launch_bounds__(BLOCK) void k_eval_nodes_j(uint64_t n, const int16_
                                                         const uint32_t *__restrict__ pst,
                                                         const uint8_t *__restrict__ up_own,
                                                         unsigned long long *__restrict__ vbal,
-                                                        unsigned long long *__restrict__ out) {
+                                                        unsigned long long *__restrict__ out,
+                                                        unsigned long long *__restrict__ acc) {
   __shared__ uint32_t lv[LDS_PARTS];
   const bool lds = nparts <= LDS_PARTS;
   if (lds)
@@ -491,7 +502,7 @@ __global__ __launch_bounds__(BLOCK) void k_eval_nodes_j(uint64_t n, const int16_
   const int ad = (what & 2) ? 0 : -1;
   const int au = (what & 4) ? ((what & 2) ? 1 : 0) : -1;
   const int ah = (what & 1) ? M - 2 : -1, av = (what & 1) ? M - 1 : -1;
-  uint64_t s[4] = {0, 0, 0, 0}, nodes = 0;
+  uint64_t s[4] = {0, 0, 0, 0}, nodes = 0, nopart = 0;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t x = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; x < n; x += stride) {
     const unsigned long long *b = bits + x * (uint64_t)M * W64;
@@ -501,6 +512,7 @@ __global__ __launch_bounds__(BLOCK) void k_eval_nodes_j(uint64_t n, const int16_
     bool node = own[ad >= 0 ? 0 : 1];   // (the first array: an own entry alone makes a node)
     for (uint32_t w = 0; w < W64; ++w) node |= b[w] != 0;
     if (!node) continue;
+    if (p < 0) { ++nopart; continue; }   // an endpoint without a part (the edge pass skipped it)
     ++nodes;
     const int arr[4] = {ad, au, ah, av};
 #pragma unroll
@@ -521,6 +533,7 @@ __global__ __launch_bounds__(BLOCK) void k_eval_nodes_j(uint64_t n, const int16_
 #pragma unroll
   for (int q = 0; q < 4; ++q) block_atomic_add(&out[q], s[q]);
   block_atomic_add(&out[4], nodes);
+  block_atomic_add(&acc[AC_BAD], nopart);
   __syncthreads();
   if (lds)
     for (int x = threadIdx.x; x < nparts; x += BLOCK)
@@ -561,7 +574,8 @@ void evaluate_step(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *
     HIP_CHECK(hipMemsetAsync(res, 0, 6 * sizeof(uint64_t), c.stream));
     if (what & 4) HIP_CHECK(hipMemsetAsync(up_own, 0, n, c.stream));
     if (n) {
-      hipLaunchKernelGGL(k_parts_jnid, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, seq, n, parts, pos_size, pj, pbad);
+      hipLaunchKernelGGL(k_parts_jnid, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, seq, n, parts, pos, pos_size, pj,
+                         pbad);
       LAUNCH_CHECK();
     }
     if (se.m_valid) {
@@ -577,7 +591,8 @@ void evaluate_step(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *
     }
     if (n) {
       hipLaunchKernelGGL(k_eval_nodes_j, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, n, (const int16_t *)pj, what, M,
-                         W64, nparts, (const unsigned long long *)bits, se.pst, (const uint8_t *)up_own, vbal, res);
+                         W64, nparts, (const unsigned long long *)bits, se.pst, (const uint8_t *)up_own, vbal, res,
+                         (unsigned long long *)acc);
       LAUNCH_CHECK();
     }
     std::vector<uint64_t> ha(aw), hv(nparts);
@@ -585,8 +600,11 @@ void evaluate_step(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *
     HIP_CHECK(hipMemcpyAsync(hv.data(), vbal, (uint64_t)nparts * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
     HIP_CHECK(hipMemcpyAsync(c.h_scalars + 48, res, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
     c.sync();
-    // a DEAD edge (an endpoint without a position), a part < 0, or a bad record
-    if (se.m_valid != se.m_pairs || c.h_scalars[53] || ha[AC_BAD])
+    // another sequence than the map's index came from
+    if (c.h_scalars[53])
+      throw Error(SHEEP_ERR_ARG, "evaluate_step: seq is not the sequence whose index the context's last map used");
+    // a DEAD edge (an endpoint without a position), an endpoint without a part, or a bad record
+    if (se.m_valid != se.m_pairs || ha[AC_BAD])
       throw Error(SHEEP_ERR_RANGE, "evaluate: a vertex is unsequenced or unassigned");
     auto mx = [&](const uint64_t *h) { uint64_t m = 0; for (int p = 0; p < nparts; ++p) m = h[p] > m ? h[p] : m; return m; };
     const uint64_t *bal = ha.data() + AC_SCAL;

@@ -28,8 +28,21 @@
 //   Partition::mpi_sync (partition.cpp:69-79)     sheep_group_broadcast_parts
 //   (evaluate on one rank)                        sheep_group_evaluate: per-shard bitsets,
 //                                                 binomial OR-reduction, node pass on rank 0
+//
+// Failure path (what MPI's default error handler gives graph2tree -ir: a dead or stalled
+// rank ends the job instead of wedging it).  A joined world opens its communicator
+// NON-BLOCKING (ncclConfig_t.blocking = 0) and never waits inside RCCL: after every group
+// of RCCL calls it polls ncclCommGetAsyncError and the ranks' streams against a deadline of
+// SHEEP_JOIN_TIMEOUT seconds (default 300); the TCP links poll their sockets against the
+// same deadline (mesh.hpp).  On an error or an expired deadline the collective aborts the
+// communicators (ncclCommAbort), prints ONE line per local rank to stderr — rank, device bus
+// id, collective, bytes, cause — and returns SHEEP_ERR_HIP through the C ABI; the world is
+// then unusable (every later collective fails at once), and the drivers exit non-zero.
+// sheep_group_abort does the same on request (a driver whose own control plane saw a rank
+// die).
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -48,6 +61,9 @@ struct sheep_group {
   int world = 0;
   std::vector<ncclComm_t> comm;   // per local rank when RCCL carries the data
   std::unique_ptr<sheep::Mesh> mesh;   // one process per rank
+  int timeout_s = 300;            // SHEEP_JOIN_TIMEOUT: the deadline of every wait on other ranks
+  bool failed = false;            // a collective failed or timed out: the communicators are aborted
+  std::string failure;
 };
 
 namespace sheep {
@@ -69,11 +85,54 @@ void set_error(const char *msg);
 
 namespace {
 
+// (ncclInProgress: a non-blocking communicator accepted the call; rccl_wait completes it)
 #define NCCL_CHECK(expr)                                                                  \
   do {                                                                                    \
     ncclResult_t _r = (expr);                                                             \
-    if (_r != ncclSuccess) throw Error(SHEEP_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+    if (_r != ncclSuccess && _r != ncclInProgress)                                        \
+      throw Error(SHEEP_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(_r));     \
   } while (0)
+
+int join_timeout() {
+  // (a run-time setting, not a debug knob: how long the ranks wait for each other)
+  const char *v = getenv("SHEEP_JOIN_TIMEOUT");
+  const int t = v ? atoi(v) : 300;
+  return t > 0 ? t : 300;
+}
+
+std::string bus_id(int device) {
+  char b[64] = {0};
+  if (hipDeviceGetPCIBusId(b, sizeof b, device) != hipSuccess) return "dev" + std::to_string(device);
+  return b;
+}
+
+// Ends the world: one stderr line per local rank, every communicator aborted (its queued
+// and running RCCL kernels stop), later collectives refused.
+void fail_world(sheep_group *g, const char *what, size_t bytes, const std::string &why) {
+  if (g->failed) return;
+  g->failed = true;
+  g->failure = std::string(what) + ": " + why;
+  for (size_t i = 0; i < g->rank.size(); ++i)
+    fprintf(stderr, "sheep: rank %d of %d (bus %s): %s of %zu bytes failed: %s\n", g->rank[i], g->world,
+            bus_id(g->dev[i]).c_str(), what, bytes, why.c_str());
+  fflush(stderr);
+  for (ncclComm_t &c : g->comm)
+    if (c) {
+      (void)ncclCommAbort(c);
+      c = nullptr;
+    }
+}
+
+// Runs one collective; any failure inside it ends the world (above) and is rethrown.
+template <typename F> void collective(sheep_group *g, const char *what, size_t bytes, F &&f) {
+  if (g->failed) throw Error(SHEEP_ERR_HIP, std::string(what) + ": the world failed before (" + g->failure + ")");
+  try {
+    f();
+  } catch (const std::exception &e) {
+    fail_world(g, what, bytes, e.what());
+    throw;
+  }
+}
 
 __global__ void k_add_u32(uint32_t *__restrict__ dst, const uint32_t *__restrict__ src, uint64_t n) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
@@ -119,6 +178,33 @@ void sync_all(sheep_group *g) {
     HIP_CHECK(hipSetDevice(g->dev[i]));
     C(g, i).sync();
   }
+}
+
+// Completes the RCCL calls just grouped: polls every local communicator's async state and
+// stream until all are done, an error shows, or the deadline passes (no blocking wait
+// inside RCCL or HIP, so a peer that never posts its side cannot wedge this rank).
+void rccl_wait(sheep_group *g) {
+  using Clock = std::chrono::steady_clock;
+  const auto t0 = Clock::now(), until = t0 + std::chrono::seconds(g->timeout_s);
+  for (;;) {
+    bool done = true;
+    for (int i = 0; i < nlocal(g); ++i) {
+      ncclResult_t st = ncclSuccess;
+      NCCL_CHECK(ncclCommGetAsyncError(g->comm[i], &st));
+      if (st == ncclInProgress) { done = false; continue; }
+      if (st != ncclSuccess) throw Error(SHEEP_ERR_HIP, std::string("RCCL: ") + ncclGetErrorString(st));
+      HIP_CHECK(hipSetDevice(g->dev[i]));
+      const hipError_t q = hipStreamQuery(C(g, i).stream);
+      if (q == hipErrorNotReady) { done = false; continue; }
+      HIP_CHECK(q);
+    }
+    if (done) break;
+    const auto now = Clock::now();
+    if (now > until) throw Error(SHEEP_ERR_HIP, "timed out after " + std::to_string(g->timeout_s) + " s (SHEEP_JOIN_TIMEOUT)");
+    if (now - t0 > std::chrono::milliseconds(2)) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    else std::this_thread::yield();
+  }
+  sync_all(g);   // (complete: runs the contexts' after-sync work)
 }
 
 // bytes from rank `from` to rank `to` (global ranks): `src` is meaningful where `from` is
@@ -172,8 +258,7 @@ void host_transfer(sheep_group *g, const std::vector<Xfer> &xs) {
 
 // A set of point-to-point transfers issued together (one RCCL group: every pair on its
 // own xGMI link), complete on return.  Every rank calls it with the same list.
-void transfer(sheep_group *g, const std::vector<Xfer> &xs) {
-  if (xs.empty()) return;
+void transfer_now(sheep_group *g, const std::vector<Xfer> &xs) {
   if (!g->comm.empty()) {
     sync_all(g);   // the sources are complete (they may come from other streams)
     NCCL_CHECK(ncclGroupStart());
@@ -183,7 +268,7 @@ void transfer(sheep_group *g, const std::vector<Xfer> &xs) {
       if (lt >= 0) NCCL_CHECK(ncclRecv(x.dst, x.bytes, ncclUint8, x.from, g->comm[lt], C(g, lt).stream));
     }
     NCCL_CHECK(ncclGroupEnd());
-    sync_all(g);
+    rccl_wait(g);
     return;
   }
   if (host_transport(g)) {
@@ -201,17 +286,26 @@ void transfer(sheep_group *g, const std::vector<Xfer> &xs) {
   sync_all(g);
 }
 
+void transfer(sheep_group *g, const std::vector<Xfer> &xs, const char *what = "send/recv") {
+  if (xs.empty()) return;
+  size_t bytes = 0;
+  for (const Xfer &x : xs) bytes += x.bytes;
+  collective(g, what, bytes, [&]() { transfer_now(g, xs); });
+}
+
 // In-place sum of one u32 array per rank (the degree all-reduce); buf[li] per local rank.
 void allreduce_sum_u32(sheep_group *g, uint32_t *const *buf, uint64_t count) {
   const int P = g->world;
   if (count == 0) return;
   if (!g->comm.empty()) {   // (also a world of one that asked for RCCL: the identity, through RCCL)
-    sync_all(g);
-    NCCL_CHECK(ncclGroupStart());
-    for (int i = 0; i < nlocal(g); ++i)
-      NCCL_CHECK(ncclAllReduce(buf[i], buf[i], count, ncclUint32, ncclSum, g->comm[i], C(g, i).stream));
-    NCCL_CHECK(ncclGroupEnd());
-    sync_all(g);
+    collective(g, "all-reduce(sum) of degrees", count * sizeof(uint32_t), [&]() {
+      sync_all(g);
+      NCCL_CHECK(ncclGroupStart());
+      for (int i = 0; i < nlocal(g); ++i)
+        NCCL_CHECK(ncclAllReduce(buf[i], buf[i], count, ncclUint32, ncclSum, g->comm[i], C(g, i).stream));
+      NCCL_CHECK(ncclGroupEnd());
+      rccl_wait(g);
+    });
     return;
   }
   if (P == 1) return;
@@ -224,7 +318,7 @@ void allreduce_sum_u32(sheep_group *g, uint32_t *const *buf, uint64_t count) {
   }
   for (int r = 1; r < P; ++r) {
     const int lr = local_of(g, r);
-    transfer(g, {Xfer{r, 0, lr >= 0 ? buf[lr] : nullptr, tmp, count * sizeof(uint32_t)}});
+    transfer(g, {Xfer{r, 0, lr >= 0 ? buf[lr] : nullptr, tmp, count * sizeof(uint32_t)}}, "all-reduce(sum) of degrees");
     if (l0 >= 0) {
       HIP_CHECK(hipSetDevice(g->dev[l0]));
       hipLaunchKernelGGL(k_add_u32, dim3(grid_for(count)), dim3(BLOCK), 0, C(g, l0).stream, buf[l0],
@@ -237,20 +331,22 @@ void allreduce_sum_u32(sheep_group *g, uint32_t *const *buf, uint64_t count) {
     const int lr = local_of(g, r);
     xs.push_back(Xfer{0, r, l0 >= 0 ? buf[l0] : nullptr, lr >= 0 ? buf[lr] : nullptr, count * sizeof(uint32_t)});
   }
-  transfer(g, xs);
+  transfer(g, xs, "all-reduce(sum) of degrees");
 }
 
 // rank 0's bytes to every rank; buf[li] per local rank
-void broadcast(sheep_group *g, void *const *buf, size_t bytes) {
+void broadcast(sheep_group *g, void *const *buf, size_t bytes, const char *what) {
   const int P = g->world;
   if (bytes == 0) return;
   if (!g->comm.empty()) {
-    sync_all(g);
-    NCCL_CHECK(ncclGroupStart());
-    for (int i = 0; i < nlocal(g); ++i)
-      NCCL_CHECK(ncclBroadcast(buf[i], buf[i], bytes, ncclUint8, 0, g->comm[i], C(g, i).stream));
-    NCCL_CHECK(ncclGroupEnd());
-    sync_all(g);
+    collective(g, what, bytes, [&]() {
+      sync_all(g);
+      NCCL_CHECK(ncclGroupStart());
+      for (int i = 0; i < nlocal(g); ++i)
+        NCCL_CHECK(ncclBroadcast(buf[i], buf[i], bytes, ncclUint8, 0, g->comm[i], C(g, i).stream));
+      NCCL_CHECK(ncclGroupEnd());
+      rccl_wait(g);
+    });
     return;
   }
   if (P == 1) return;
@@ -260,19 +356,18 @@ void broadcast(sheep_group *g, void *const *buf, size_t bytes) {
     const int lr = local_of(g, r);
     xs.push_back(Xfer{0, r, l0 >= 0 ? buf[l0] : nullptr, lr >= 0 ? buf[lr] : nullptr, bytes});
   }
-  transfer(g, xs);
+  transfer(g, xs, what);
 }
 
-uint64_t allreduce_max(sheep_group *g, const std::vector<uint64_t> &local) {
+uint64_t allreduce_max(sheep_group *g, const std::vector<uint64_t> &local, const char *what) {
   uint64_t m = 0;
   for (uint64_t v : local) m = v > m ? v : m;
-  return g->mesh ? g->mesh->allreduce_max(m) : m;
+  if (g->mesh) collective(g, what, sizeof m, [&]() { m = g->mesh->allreduce_max(m); });
+  return m;
 }
 
-std::string bus_id(int device) {
-  char b[64] = {0};
-  if (hipDeviceGetPCIBusId(b, sizeof b, device) != hipSuccess) return "dev" + std::to_string(device);
-  return b;
+void mesh_bcast(sheep_group *g, void *buf, size_t bytes, const char *what) {
+  if (g->mesh) collective(g, what, bytes, [&]() { g->mesh->bcast(buf, bytes); });
 }
 
 }  // namespace
@@ -298,7 +393,7 @@ struct DeviceRestore {
 };
 
 static void group_free(sheep_group *g) {
-  for (ncclComm_t c : g->comm) if (c) ncclCommDestroy(c);
+  for (ncclComm_t c : g->comm) if (c) ncclCommDestroy(c);   // (aborted ones are null)
   for (sheep_ctx *c : g->ctx) sheep_ctx_destroy(c);
   delete g;
 }
@@ -313,6 +408,7 @@ int sheep_group_create(const int *devices, int ndev, sheep_group **out) {
   try {
     bool distinct = true;
     g->world = ndev;
+    g->timeout_s = sheep::join_timeout();
     for (int r = 0; r < ndev; ++r) {
       for (int q = 0; q < r; ++q) distinct &= devices[q] != devices[r];
       sheep_ctx *c = nullptr;
@@ -348,9 +444,8 @@ int sheep_group_join(int device, int rank, int world, const char *host, int port
     g->ctx.push_back(c);
     g->dev.push_back(device);
     g->rank.push_back(rank);
-    // (a run-time setting, not a debug knob: how long the ranks wait for each other)
-    const int timeout = getenv("SHEEP_JOIN_TIMEOUT") ? atoi(getenv("SHEEP_JOIN_TIMEOUT")) : 300;
-    g->mesh.reset(new sheep::Mesh(rank, world, host, port, sheep::bus_id(device), timeout));
+    g->timeout_s = sheep::join_timeout();
+    g->mesh.reset(new sheep::Mesh(rank, world, host, port, sheep::bus_id(device), g->timeout_s));
     bool distinct = true;
     const auto &bus = g->mesh->bus_ids();
     for (int r = 0; r < world; ++r)
@@ -363,10 +458,26 @@ int sheep_group_join(int device, int rank, int world, const char *host, int port
     if (link == SHEEP_LINK_RCCL || (world > 1 && link == SHEEP_LINK_AUTO && distinct)) {
       ncclUniqueId id;
       if (rank == 0) NCCL_CHECK(ncclGetUniqueId(&id));
-      g->mesh->bcast(&id, sizeof id);
+      sheep::mesh_bcast(g, &id, sizeof id, "RCCL bootstrap");
       HIP_CHECK(hipSetDevice(device));
       g->comm.resize(1);
-      NCCL_CHECK(ncclCommInitRank(&g->comm[0], world, id, rank));
+      // non-blocking: the init runs in the background while this rank polls it against the
+      // deadline (a rank that never arrives would otherwise hold ncclCommInitRank forever)
+      sheep::collective(g, "ncclCommInitRank", 0, [&]() {
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        NCCL_CHECK(ncclCommInitRankConfig(&g->comm[0], world, id, rank, &cfg));
+        const auto until = std::chrono::steady_clock::now() + std::chrono::seconds(g->timeout_s);
+        for (;;) {
+          ncclResult_t st = ncclInProgress;
+          NCCL_CHECK(ncclCommGetAsyncError(g->comm[0], &st));
+          if (st == ncclSuccess) break;
+          if (st != ncclInProgress) throw sheep::Error(SHEEP_ERR_HIP, std::string("RCCL: ") + ncclGetErrorString(st));
+          if (std::chrono::steady_clock::now() > until)
+            throw sheep::Error(SHEEP_ERR_HIP, "timed out after " + std::to_string(g->timeout_s) + " s (SHEEP_JOIN_TIMEOUT)");
+          std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+      });
     }
   } catch (...) {
     group_free(g);
@@ -398,17 +509,29 @@ int sheep_group_barrier(sheep_group *g) {
   DeviceRestore dr;
   GAPI_BEGIN
   GNEED(g, "null argument");
-  sheep::sync_all(g);
-  if (g->mesh) g->mesh->barrier();
+  sheep::collective(g, "barrier", 0, [&]() {
+    sheep::sync_all(g);
+    if (g->mesh) g->mesh->barrier();
+  });
   GAPI_END
 }
 
 int sheep_group_allreduce_max_u64(sheep_group *g, uint64_t *v) {
   GAPI_BEGIN
   GNEED(g && v, "null argument");
-  if (g->mesh) *v = g->mesh->allreduce_max(*v);
+  *v = sheep::allreduce_max(g, {*v}, "all-reduce(max)");
   GAPI_END
 }
+
+int sheep_group_abort(sheep_group *g, const char *reason) {
+  DeviceRestore dr;
+  GAPI_BEGIN
+  GNEED(g, "null argument");
+  sheep::fail_world(g, "abort", 0, reason && *reason ? reason : "requested by the caller");
+  GAPI_END
+}
+
+int sheep_group_failed(const sheep_group *g) { return g && g->failed ? 1 : 0; }
 
 int sheep_group_set_tuning(sheep_group *g, const sheep_tuning *t) {
   GAPI_BEGIN
@@ -430,7 +553,7 @@ int sheep_group_sequence(sheep_group *g, const sheep_xs1 *const *rec, const uint
   sheep::per_rank(g, [&](int i) {   // each shard's LLAMA degrees (mpiSequence, sequence.h:76-77)
     sheep::degree_count(sheep::C(g, i), rec[i], nrec[i], SHEEP_DEGREE_LLAMA, deg[i], cap, &ms[i]);
   });
-  const uint64_t vs = sheep::allreduce_max(g, ms);                   // MPI_Allreduce(MAX), sequence.h:72
+  const uint64_t vs = sheep::allreduce_max(g, ms, "all-reduce(max) of max_slot");   // MPI_Allreduce(MAX), sequence.h:72
   sheep::allreduce_sum_u32(g, deg, vs);                              // MPI_Allreduce(SUM), sequence.h:78
   sheep::per_rank(g, [&](int i) {
     n[i] = sheep::sequence_from_degrees(sheep::C(g, i), deg[i], vs, seq[i], pos[i]);
@@ -470,7 +593,7 @@ int sheep_group_reduce_trees(sheep_group *g, sheep_jnode *const *tree, uint64_t 
         HIP_CHECK(hipSetDevice(g->dev[i]));
         tr.emplace_back(new sheep::TimedRegion(sheep::C(g, i), "gather", tb));
       }
-      sheep::transfer(g, xs);
+      sheep::transfer(g, xs, "gather of partial trees");
       for (int i = 0; i < sheep::nlocal(g); ++i) {
         HIP_CHECK(hipSetDevice(g->dev[i]));
         tr[i].reset();
@@ -495,7 +618,7 @@ int sheep_group_reduce_trees(sheep_group *g, sheep_jnode *const *tree, uint64_t 
       }
       xs.push_back(sheep::Xfer{i + d, i, ls >= 0 ? tree[ls] : nullptr, in, tb});
     }
-    sheep::transfer(g, xs);
+    sheep::transfer(g, xs, "binomial hop of partial trees");
     sheep::per_rank(g, [&](int li) {
       const int r = g->rank[li];
       if (r % (2 * d) != 0 || r + d >= P) return;
@@ -532,7 +655,7 @@ int sheep_group_transfer(sheep_group *g, int from, int to, const void *src, void
   GNEED(g && from >= 0 && from < g->world && to >= 0 && to < g->world, "bad argument");
   const int lf = sheep::local_of(g, from), lt = sheep::local_of(g, to);
   GNEED((lf < 0 || src) && (lt < 0 || dst), "null buffer on a local rank");
-  sheep::transfer(g, {sheep::Xfer{from, to, src, dst, (size_t)bytes}});
+  sheep::transfer(g, {sheep::Xfer{from, to, src, dst, (size_t)bytes}}, "send/recv");
   GAPI_END
 }
 
@@ -548,7 +671,7 @@ int sheep_group_broadcast_parts(sheep_group *g, int16_t *const *parts, uint64_t 
   GAPI_BEGIN
   GNEED(g && parts, "null argument");
   sheep::sync_all(g);
-  sheep::broadcast(g, (void *const *)parts, pos_size * sizeof(int16_t));
+  sheep::broadcast(g, (void *const *)parts, pos_size * sizeof(int16_t), "broadcast of parts");
   GAPI_END
 }
 
@@ -566,7 +689,7 @@ int sheep_group_evaluate(sheep_group *g, const sheep_xs1 *const *rec, const uint
     HIP_CHECK(hipSetDevice(g->dev[l0]));
     np = (uint64_t)sheep::eval_num_parts(sheep::C(g, l0), parts[l0], pos_size);
   }
-  if (g->mesh) g->mesh->bcast(&np, sizeof np);
+  sheep::mesh_bcast(g, &np, sizeof np, "broadcast of the part count");
   const int nparts = (int)np;
   uint64_t words = 0, aw = 0;
   sheep::eval_sizes(what, nparts, pos_size, &words, &aw);
@@ -592,7 +715,7 @@ int sheep_group_evaluate(sheep_group *g, const sheep_xs1 *const *rec, const uint
       xs.push_back(sheep::Xfer{i + d, i, ls >= 0 ? acc[ls] : nullptr, li >= 0 ? ra[li] : nullptr,
                                aw * sizeof(uint64_t)});
     }
-    sheep::transfer(g, xs);
+    sheep::transfer(g, xs, "evaluator state reduction");
     sheep::per_rank(g, [&](int li) {
       const int r = g->rank[li];
       if (r % (2 * d) != 0 || r + d >= P) return;

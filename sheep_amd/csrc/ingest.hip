@@ -17,6 +17,10 @@
 // a number followed by other characters: k_tok_parse); pinned by the reference's own
 // SNAPReader on tests/golden/snap_cases.json.  Not followed: a token that holds two
 // numbers glued by a sign ("4-5": istream reads 4 and then -5) ends the input after 4.
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include "common.hpp"
 
 namespace sheep {
@@ -150,7 +154,35 @@ __global__ void k_add_u32_inplace(uint32_t *__restrict__ dst, const uint32_t *__
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) dst[i] += add[i];
 }
 
+// 1 + the largest vid of the records (LLAMA max_nodes) and the self-loop count
+__global__ __launch_bounds__(BLOCK) void k_record_stats(const sheep_xs1 *__restrict__ rec, uint64_t nrec,
+                                                        unsigned long long *__restrict__ out) {
+  uint64_t mx = 0, loops = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nrec; i += stride) {
+    const sheep_xs1 r = rec[i];
+    const uint64_t v = (uint64_t)(r.tail > r.head ? r.tail : r.head) + 1;
+    mx = v > mx ? v : mx;
+    loops += r.tail == r.head;
+  }
+  block_atomic_max(&out[0], mx);
+  block_atomic_add(&out[1], loops);
+}
+
 }  // namespace
+
+void record_stats(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, uint64_t *max_slot, uint64_t *loops) {
+  unsigned long long *d = (unsigned long long *)c.d_scalars + 56;
+  HIP_CHECK(hipMemsetAsync(d, 0, 2 * sizeof(uint64_t), c.stream));
+  if (nrec) {
+    hipLaunchKernelGGL(k_record_stats, dim3(grid_for(nrec)), dim3(BLOCK), 0, c.stream, rec, nrec, d);
+    LAUNCH_CHECK();
+  }
+  HIP_CHECK(hipMemcpyAsync(c.h_scalars + 56, d, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  *max_slot = c.h_scalars[56];
+  *loops = c.h_scalars[57];
+}
 
 uint64_t parse_net(Ctx &c, const char *text, uint64_t bytes, int skip_comments, sheep_xs1 *out, uint64_t cap) {
   if (bytes == 0) return 0;
@@ -213,3 +245,57 @@ uint64_t parse_net(Ctx &c, const char *text, uint64_t bytes, int skip_comments, 
 }
 
 }  // namespace sheep
+
+// ---- .dat partial loads (graph_wrapper.h:43-63: LLAMAGraph(filename, part, num_parts) hands
+// lc_partial_load_part / num_parts to the loader, which reads only that part) -------------
+// Part p of k is the contiguous record range [(p-1)R/k, pR/k) of the R = size / 12 records;
+// the host reads exactly those bytes with pread, never the rest of the file.
+extern "C" int sheep_dat_range(const char *filename, uint64_t part, uint64_t num_parts, uint64_t *first_out,
+                               uint64_t *count_out) {
+  try {
+    if (!filename || !first_out || !count_out) throw sheep::Error(SHEEP_ERR_ARG, "null argument");
+    if (num_parts != 0 && (part < 1 || part > num_parts)) throw sheep::Error(SHEEP_ERR_ARG, "part must be in 1..num_parts");
+    struct stat st;
+    if (stat(filename, &st) != 0) throw sheep::Error(SHEEP_ERR_ARG, std::string("cannot open ") + filename);
+    const uint64_t R = (uint64_t)st.st_size / sizeof(sheep_xs1);
+    uint64_t beg = 0, end = R;
+    if (num_parts != 0) {
+      beg = (part - 1) * R / num_parts;   // (R < 2^40: no overflow for any part count < 2^24)
+      end = part * R / num_parts;
+    }
+    *first_out = beg;
+    *count_out = end - beg;
+    return SHEEP_OK;
+  } catch (const sheep::Error &e) {
+    sheep::set_error(e.what());
+    return e.code;
+  }
+}
+
+extern "C" int sheep_read_dat(const char *filename, uint64_t first, uint64_t count, sheep_xs1 *out, uint64_t *got_out) {
+  int fd = -1;
+  try {
+    if (!filename || !got_out || (count && !out)) throw sheep::Error(SHEEP_ERR_ARG, "null argument");
+    *got_out = 0;
+    fd = open(filename, O_RDONLY);
+    if (fd < 0) throw sheep::Error(SHEEP_ERR_ARG, std::string("cannot open ") + filename);
+    char *dst = (char *)out;
+    uint64_t left = count * sizeof(sheep_xs1), off = first * sizeof(sheep_xs1);
+    while (left) {
+      const ssize_t r = pread(fd, dst, left > (1ull << 30) ? (1ull << 30) : left, (off_t)off);
+      if (r < 0 && errno == EINTR) continue;
+      if (r < 0) throw sheep::Error(SHEEP_ERR_ARG, std::string("read ") + filename + ": " + strerror(errno));
+      if (r == 0) break;   // (the file shrank)
+      dst += r;
+      off += (uint64_t)r;
+      left -= (uint64_t)r;
+    }
+    close(fd);
+    *got_out = (count * sizeof(sheep_xs1) - left) / sizeof(sheep_xs1);
+    return SHEEP_OK;
+  } catch (const sheep::Error &e) {
+    if (fd >= 0) close(fd);
+    sheep::set_error(e.what());
+    return e.code;
+  }
+}

@@ -32,24 +32,45 @@ void tune(int fd) {
   setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof buf);
 }
 
-void put(int fd, const void *p, size_t n) {
+using Clock = std::chrono::steady_clock;
+constexpr Clock::time_point NO_DEADLINE = Clock::time_point::max();
+
+// waits until fd is ready for `events` or the deadline passes (then fails naming `who`)
+void wait_ready(int fd, short events, Clock::time_point until, const std::string &who) {
+  for (;;) {
+    int ms = 1000;
+    if (until != NO_DEADLINE) {
+      const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(until - Clock::now()).count();
+      if (left <= 0) { errno = 0; fail("timed out waiting for " + who); }
+      ms = (int)std::min<long long>(left, 1000);
+    }
+    pollfd p{fd, events, 0};
+    const int r = poll(&p, 1, ms);
+    if (r < 0 && errno != EINTR) fail("poll");
+    if (r > 0) return;   // ready, or an error / hang-up the next send / recv reports
+  }
+}
+
+void put(int fd, const void *p, size_t n, Clock::time_point until = NO_DEADLINE, const std::string &who = "a peer") {
   const char *c = (const char *)p;
   while (n) {
-    const ssize_t w = ::send(fd, c, n, MSG_NOSIGNAL);
-    if (w < 0 && errno == EINTR) continue;
-    if (w <= 0) fail("send");
+    wait_ready(fd, POLLOUT, until, who);
+    const ssize_t w = ::send(fd, c, n, MSG_NOSIGNAL | MSG_DONTWAIT);
+    if (w < 0 && (errno == EINTR || errno == EAGAIN || errno == EWOULDBLOCK)) continue;
+    if (w <= 0) fail("send to " + who);
     c += w;
     n -= (size_t)w;
   }
 }
 
-void get(int fd, void *p, size_t n) {
+void get(int fd, void *p, size_t n, Clock::time_point until = NO_DEADLINE, const std::string &who = "a peer") {
   char *c = (char *)p;
   while (n) {
-    const ssize_t r = ::recv(fd, c, n, 0);
-    if (r < 0 && errno == EINTR) continue;
-    if (r == 0) { errno = 0; fail("peer closed the connection"); }
-    if (r < 0) fail("recv");
+    wait_ready(fd, POLLIN, until, who);
+    const ssize_t r = ::recv(fd, c, n, MSG_DONTWAIT);
+    if (r < 0 && (errno == EINTR || errno == EAGAIN || errno == EWOULDBLOCK)) continue;
+    if (r == 0) { errno = 0; fail(who + " closed the connection"); }
+    if (r < 0) fail("recv from " + who);
     c += r;
     n -= (size_t)r;
   }
@@ -125,7 +146,7 @@ int connect_within(const sockaddr_in &a, std::chrono::steady_clock::time_point u
 }  // namespace
 
 Mesh::Mesh(int rank, int world, const std::string &host, int port, const std::string &bus_id, int timeout_s)
-    : rank_(rank), world_(world), fd_(world, -1), bus_(world) {
+    : rank_(rank), world_(world), timeout_s_(timeout_s), fd_(world, -1), bus_(world) {
   if (world < 1 || rank < 0 || rank >= world) { errno = 0; fail("bad rank / world"); }
   bus_[rank] = bus_id;
   if (world == 1) return;
@@ -192,24 +213,37 @@ Mesh::~Mesh() {
   for (int f : fd_) if (f >= 0) close(f);
 }
 
-void Mesh::send(int peer, const void *buf, size_t bytes) { put(fd_.at(peer), buf, bytes); }
-void Mesh::recv(int peer, void *buf, size_t bytes) { get(fd_.at(peer), buf, bytes); }
+namespace {
+Clock::time_point deadline(int timeout_s) {
+  return timeout_s > 0 ? Clock::now() + std::chrono::seconds(timeout_s) : NO_DEADLINE;
+}
+std::string peer_name(int r) { return "rank " + std::to_string(r); }
+}  // namespace
+
+void Mesh::send(int peer, const void *buf, size_t bytes) {
+  put(fd_.at(peer), buf, bytes, deadline(timeout_s_), peer_name(peer));
+}
+void Mesh::recv(int peer, void *buf, size_t bytes) {
+  get(fd_.at(peer), buf, bytes, deadline(timeout_s_), peer_name(peer));
+}
 
 void Mesh::bcast(void *buf, size_t bytes) {
-  if (rank_ == 0) for (int r = 1; r < world_; ++r) put(fd_[r], buf, bytes);
-  else get(fd_[0], buf, bytes);
+  const auto until = deadline(timeout_s_);
+  if (rank_ == 0) for (int r = 1; r < world_; ++r) put(fd_[r], buf, bytes, until, peer_name(r));
+  else get(fd_[0], buf, bytes, until, peer_name(0));
 }
 
 uint64_t Mesh::allreduce(uint64_t v, bool is_max) {
   if (world_ == 1) return v;
+  const auto until = deadline(timeout_s_);
   if (rank_ == 0) {
     for (int r = 1; r < world_; ++r) {
       uint64_t x;
-      get(fd_[r], &x, 8);
+      get(fd_[r], &x, 8, until, peer_name(r));
       v = is_max ? (x > v ? x : v) : v + x;
     }
   } else {
-    put(fd_[0], &v, 8);
+    put(fd_[0], &v, 8, until, peer_name(0));
   }
   bcast(&v, 8);
   return v;
@@ -267,6 +301,36 @@ extern "C" int sheep_mesh_selftest(int rank, int world, const char *host, int po
     return SHEEP_OK;
   } catch (const std::exception &e) {
     fprintf(stderr, "sheep_mesh_selftest: %s\n", e.what());
+    return SHEEP_ERR_HIP;
+  }
+}
+
+// The deadline of a joined world's links: rank `stall_rank` joins and then takes no part
+// (it sleeps past the deadline); every other rank enters a barrier, which must fail within
+// timeout_s instead of hanging.  *waited_s_out = how long the barrier waited (the stalled
+// rank reports 0).  Returns SHEEP_OK on the stalled rank and the barrier's status (an
+// error, with sheep_last_error naming the peer) on the others.  Host-only.
+extern "C" int sheep_mesh_selftest_stall(int rank, int world, const char *host, int port, int stall_rank, int timeout_s,
+                                         double *waited_s_out) {
+  try {
+    sheep::Mesh m(rank, world, host ? host : "127.0.0.1", port, "host" + std::to_string(rank), timeout_s);
+    *waited_s_out = 0;
+    if (rank == stall_rank) {
+      std::this_thread::sleep_for(std::chrono::seconds(timeout_s + 3));
+      return SHEEP_OK;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    try {
+      m.barrier();
+    } catch (const sheep::Error &e) {
+      *waited_s_out = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      sheep::set_error(e.what());
+      return e.code;
+    }
+    *waited_s_out = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return SHEEP_OK;
+  } catch (const std::exception &e) {
+    sheep::set_error(e.what());
     return SHEEP_ERR_HIP;
   }
 }

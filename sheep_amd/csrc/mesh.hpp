@@ -6,6 +6,10 @@
 // Rendezvous: rank 0 listens on host:port; every rank listens on an ephemeral port of its
 // own and reports (rank, port, device bus id) to rank 0, which sends the table back; then
 // rank j connects to every rank i < j.  Every pair of ranks has its own socket.
+//
+// Deadlines: every operation waits at most timeout_s seconds for its peer (poll on the
+// socket, not a blocking send/recv), so a rank that stops taking part surfaces as an
+// error on the others (naming the peer) instead of a hang.
 #pragma once
 
 #include <cstddef>
@@ -28,6 +32,7 @@ class Mesh {
   // every rank's device bus id, by rank (known after the rendezvous)
   const std::vector<std::string> &bus_ids() const { return bus_; }
 
+  int timeout_s() const { return timeout_s_; }
   void send(int peer, const void *buf, size_t bytes);
   void recv(int peer, void *buf, size_t bytes);
   // rank 0's bytes to every rank (star)
@@ -38,7 +43,7 @@ class Mesh {
 
  private:
   uint64_t allreduce(uint64_t v, bool is_max);
-  int rank_, world_;
+  int rank_, world_, timeout_s_;
   std::vector<int> fd_;           // socket per peer rank (-1 for self)
   std::vector<std::string> bus_;
 };

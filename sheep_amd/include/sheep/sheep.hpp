@@ -94,6 +94,9 @@ class DeviceArray {
   T *get() const { return p_; }
   size_t size() const { return n_; }
   void upload(const T *h, size_t cnt) { check(sheep_memcpy_h2d(c_, p_, h, cnt * sizeof(T))); }
+  void upload_at(size_t off, const T *h, size_t cnt) { check(sheep_memcpy_h2d(c_, p_ + off, h, cnt * sizeof(T))); }
+  void copy_from(const T *dev, size_t cnt) { check(sheep_memcpy_d2d(c_, p_, dev, cnt * sizeof(T))); }
+  sheep_ctx *context() const { return c_; }
   void download(T *h, size_t cnt) const { check(sheep_memcpy_d2h(c_, h, p_, cnt * sizeof(T))); }
 
  private:
@@ -105,38 +108,6 @@ class DeviceArray {
 inline bool is_dat(const char *filename) {
   const size_t l = strlen(filename);
   return l >= 4 && strcmp(".dat", filename + l - 4) == 0;
-}
-
-// XS1 records of a .dat file, or pairs of a SNAP text file read the way SNAPReader does
-// (readerwriter.h:78-90: whitespace-separated pairs, stop at the first pair that does not
-// parse).  skip_comments: lines starting with '#' or '%' are skipped first, as the graph
-// loader does for SNAP / edge-list headers (LLAMA's text loader is un-vendored: that
-// behaviour is parity-unpinned); SNAPReader itself (fileSequence) does not skip them.
-inline std::vector<sheep_xs1> readRecords(const char *filename, bool skip_comments = false) {
-  std::vector<sheep_xs1> rec;
-  if (is_dat(filename)) {
-    FILE *f = fopen(filename, "rb");
-    if (!f) throw std::bad_alloc();   // the reference's loaders fail with bad_alloc / abort
-    fseek(f, 0, SEEK_END);
-    const long bytes = ftell(f);
-    fseek(f, 0, SEEK_SET);
-    rec.resize((size_t)bytes / sizeof(sheep_xs1));
-    const size_t got = rec.empty() ? 0 : fread(rec.data(), sizeof(sheep_xs1), rec.size(), f);
-    fclose(f);
-    rec.resize(got);
-  } else {
-    std::ifstream s(filename);
-    if (!s) throw std::bad_alloc();
-    if (skip_comments) {
-      for (int ch = (s >> std::ws).peek(); ch == '#' || ch == '%'; ch = (s >> std::ws).peek()) {
-        std::string line;
-        std::getline(s, line);
-      }
-    }
-    vid_t X, Y;
-    while ((s >> X) && (s >> Y)) rec.push_back(sheep_xs1{X, Y, 1.0f});
-  }
-  return rec;
 }
 
 inline std::vector<char> readBytes(const char *filename) {
@@ -163,34 +134,62 @@ inline DeviceArray<sheep_xs1> parseNet(const char *filename, bool skip_comments,
   return rec;
 }
 
+// The records of part `part` of `num_parts` (1-indexed contiguous record ranges, LLAMA's
+// partial load: LLAMAGraph(filename, part, num_parts), graph_wrapper.h:43-63; num_parts = 0:
+// the whole file) in HBM on context c.  A .dat file is read with pread over exactly the
+// part's byte range (sheep_dat_range / sheep_read_dat), in 48-MB chunks uploaded as they
+// arrive: no other byte of the file is read and no whole-part host copy is kept.  A SNAP
+// text file is parsed whole on the GPU (record boundaries are only known after parsing;
+// skip_comments: the graph loader's '#' / '%' lines) and the part's range kept.
+inline DeviceArray<sheep_xs1> loadRecords(const char *filename, size_t part, size_t num_parts, sheep_ctx *c,
+                                          bool skip_comments, uint64_t *nrec) {
+  if (is_dat(filename)) {
+    uint64_t first = 0, count = 0;
+    if (sheep_dat_range(filename, part, num_parts, &first, &count) != SHEEP_OK)
+      throw std::bad_alloc();   // the reference's loaders fail with bad_alloc / abort
+    DeviceArray<sheep_xs1> rec(count, c);
+    const uint64_t chunk = 1ull << 22;   // records (48 MB)
+    std::vector<sheep_xs1> buf((size_t)std::min(count, chunk));
+    uint64_t done = 0;
+    while (done < count) {
+      const uint64_t want = std::min(chunk, count - done);
+      uint64_t got = 0;
+      if (sheep_read_dat(filename, first + done, want, buf.data(), &got) != SHEEP_OK) throw std::bad_alloc();
+      if (got) rec.upload_at(done, buf.data(), got);
+      done += got;
+      if (got < want) break;   // (the file shrank under us)
+    }
+    *nrec = done;
+    return rec;
+  }
+  uint64_t n = 0;
+  DeviceArray<sheep_xs1> all = parseNet(filename, skip_comments, &n, c);
+  if (num_parts == 0) {
+    *nrec = n;
+    return all;
+  }
+  if (part < 1 || part > num_parts) throw std::bad_alloc();
+  const uint64_t beg = (part - 1) * n / num_parts, end = part * n / num_parts;
+  DeviceArray<sheep_xs1> rec(end - beg, c);
+  if (end > beg) rec.copy_from(all.get() + beg, end - beg);
+  *nrec = end - beg;
+  return rec;
+}
+
+// 1 + the largest vid (max_nodes) and the self-loop count of records in HBM (one device pass)
+inline void recordStats(sheep_ctx *c, const sheep_xs1 *rec, uint64_t nrec, uint64_t *max_slot, uint64_t *loops) {
+  check(sheep_record_stats(c, rec, nrec, max_slot, loops));
+}
+
 // The graph of one (optionally partial, `part`/`num_parts` 1-indexed, contiguous record
 // ranges like LLAMA's partial load) edge file, resident in HBM.  LLAMA semantics:
 // undirected doubling, a self-loop stored once, degree-0 slots are not nodes.
 class GraphWrapper {
  public:
   GraphWrapper(const char *filename, size_t part = 0, size_t num_parts = 0) {
-    std::vector<sheep_xs1> all;
-    if (is_dat(filename)) {
-      all = readRecords(filename);
-    } else {   // SNAP text: parsed on the GPU, the records brought back for the metadata
-      uint64_t n = 0;
-      DeviceArray<sheep_xs1> d = parseNet(filename, true, &n);
-      all.resize(n);
-      if (n) d.download(all.data(), n);
-    }
-    size_t beg = 0, end = all.size();
-    if (num_parts != 0) {
-      beg = (part - 1) * all.size() / num_parts;
-      end = part * all.size() / num_parts;
-    }
-    nrec_ = end - beg;
-    rec_ = DeviceArray<sheep_xs1>(nrec_);
-    if (nrec_) rec_.upload(all.data() + beg, nrec_);
+    rec_ = loadRecords(filename, part, num_parts, ctx(), true, &nrec_);
     uint64_t loops = 0;
-    for (size_t i = beg; i < end; ++i) {
-      max_nodes_ = std::max<uint64_t>(max_nodes_, (uint64_t)std::max(all[i].tail, all[i].head) + 1);
-      loops += all[i].tail == all[i].head;
-    }
+    recordStats(ctx(), rec_.get(), nrec_, &max_nodes_, &loops);
     edges_ = (2 * nrec_ - loops) / 2;   // max_edges / 2 (graph_wrapper.h:79-81)
     dat_ = is_dat(filename);
   }
@@ -252,25 +251,16 @@ inline size_t GraphWrapper::getNodes() const {
 // fileSequence (sequence.h:95-128): degrees straight from the file records (self-loop
 // +2; XS1Reader hands the last record out twice, readerwriter.h:138-146).
 inline std::vector<vid_t> fileSequence(const char *filename) {
-  std::vector<sheep_xs1> all;
-  DeviceArray<sheep_xs1> rec;
-  if (is_dat(filename)) {
-    all = readRecords(filename);
-    rec = DeviceArray<sheep_xs1>(all.size());
-    if (!all.empty()) rec.upload(all.data(), all.size());
-  } else {   // SNAPReader semantics, parsed on the GPU
-    uint64_t n = 0;
-    rec = parseNet(filename, false, &n);
-    all.resize(n);
-    if (n) rec.download(all.data(), n);
-  }
-  uint64_t cap = 1;
-  for (const sheep_xs1 &r : all) cap = std::max<uint64_t>(cap, (uint64_t)std::max(r.tail, r.head) + 1);
+  uint64_t nrec = 0, cap = 0, loops = 0;
+  // SNAPReader semantics for text (no comment skipping), parsed on the GPU
+  DeviceArray<sheep_xs1> rec = loadRecords(filename, 0, 0, ctx(), false, &nrec);
+  recordStats(ctx(), rec.get(), nrec, &cap, &loops);
+  cap = std::max<uint64_t>(cap, 1);
   DeviceArray<uint32_t> deg(cap);
   std::vector<uint32_t> zero(cap, 0);
   deg.upload(zero.data(), cap);
   uint64_t vs = 0;
-  check(sheep_degree_count(ctx(), rec.get(), all.size(), is_dat(filename) ? SHEEP_DEGREE_FILE_DAT : SHEEP_DEGREE_FILE_NET,
+  check(sheep_degree_count(ctx(), rec.get(), nrec, is_dat(filename) ? SHEEP_DEGREE_FILE_DAT : SHEEP_DEGREE_FILE_NET,
                            deg.get(), cap, &vs));
   return sequenceFromDegrees(deg, vs).host();
 }

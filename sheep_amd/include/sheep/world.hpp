@@ -100,8 +100,8 @@ class World {
 // semantics) and its copy of the sequence, on its device.
 struct RankState {
   int rank = 0;
-  std::vector<sheep_xs1> host;   // the shard's records (the partition-file writer reads them)
-  DeviceArray<sheep_xs1> rec;
+  DeviceArray<sheep_xs1> rec;    // the shard's records, read straight into HBM (loadRecords)
+  uint64_t nrec = 0;
   DeviceArray<uint32_t> seq, pos, deg;
   DeviceArray<sheep_jnode> tree;
   DeviceArray<int16_t> parts;

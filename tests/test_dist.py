@@ -81,6 +81,46 @@ def test_mesh_links(world):
         assert mx == max(h), rank
 
 
+def _stall_rank(rank, world, port, stall, timeout_s, q):
+    L = ctypes.CDLL(LIB)
+    L.sheep_mesh_selftest_stall.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    L.sheep_last_error.restype = ctypes.c_char_p
+    waited = ctypes.c_double()
+    rc = L.sheep_mesh_selftest_stall(rank, world, b"127.0.0.1", port, stall, timeout_s, ctypes.byref(waited))
+    q.put((rank, rc, waited.value, L.sheep_last_error().decode() if rc else ""))
+
+
+@pytest.mark.parametrize("world,stall", [(2, 1), (3, 1), (3, 0)])
+def test_mesh_deadline_when_a_rank_stalls(world, stall):
+    """A rank that joins and then stops taking part (alive, sockets open) must surface as an
+    error on the others within SHEEP_JOIN_TIMEOUT, not as a hang: rank 0 waiting on the
+    stalled rank times out naming it; a rank waiting on rank 0 instead learns when rank 0
+    gives up and closes its links (or times out itself when rank 0 is the stalled one)."""
+    if not os.path.exists(LIB):
+        pytest.skip("libsheep_hip.so not built")
+    timeout_s = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stall_rank, args=(r, world, port, stall, timeout_s, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for rank, rc, waited, msg in got:
+        if rank == stall:
+            assert rc == 0
+            continue
+        assert rc != 0, rank
+        assert waited <= timeout_s + 1.5, (rank, waited)
+        if rank == 0 or stall == 0:   # the waiter on the stalled rank itself: a timeout naming it
+            assert f"timed out waiting for rank {stall}" in msg, msg
+        else:                         # rank 0 gave up and closed its links
+            assert "rank 0" in msg, msg
+
+
 def _control_rank(rank, world, port, q):
     import torch.distributed as dist
     from sheep_amd import dist as sdist

@@ -485,9 +485,43 @@ def test_evaluate_from_step_edges_needs_that_map(gpu_ctx):
         sheep_amd.evaluate(d, s, res.parts, from_step=True)
     res2 = sheep_amd.partition(s2, tree2, 4)
     assert sheep_amd.evaluate(d2, s2, res2.parts, from_step=True) == sheep_amd.evaluate(d2, s2, res2.parts)
+    # the same index with another sequence of the same length (two entries swapped)
+    sw = golden_seq("rmat14").copy()
+    sw[[0, 1]] = sw[[1, 0]]
+    s2x = sheep_amd.Sequence(sheep_amd.sequence_from_host(sw).seq, s2.pos, s2.n, s2.pos_size)
+    with pytest.raises(ValueError):
+        sheep_amd.evaluate(d2, s2x, res2.parts, from_step=True)
     gpu_ctx.trim()
     with pytest.raises(ValueError):
         sheep_amd.evaluate(d2, s2, res2.parts, from_step=True)
+
+
+@pytest.mark.parametrize("what", [0, 1, 2, 4])
+def test_evaluate_unassigned_part(gpu_ctx, what):
+    """A part of -1 (INVALID_PART) on an edge endpoint is the reference's throw in both
+    evaluators (the step-edge one must not index with it); on a sequenced vertex that is no
+    endpoint it is ignored by both, with the same counts."""
+    import sheep_amd
+    rec = golden_records("rmat12")
+    seq = golden_seq("rmat12")
+    d = _dev_records(rec)
+    # one extra sequenced vid past every record: sequenced, never an endpoint
+    extra = np.uint32(int(seq.max()) + 5)
+    s = sheep_amd.sequence_from_host(np.concatenate([seq, [extra]]))
+    tree = sheep_amd.build_tree(d, s)
+    res = sheep_amd.partition(s, tree, 8)
+    for victim in (int(rec["tail"][0]), int(rec["head"][0]), int(rec["head"][-1])):   # a tail, a head, another head
+        parts = res.parts.clone()
+        parts[victim] = -1
+        with pytest.raises(IndexError):
+            sheep_amd.evaluate(d, s, parts, what=what)
+        with pytest.raises(IndexError):
+            sheep_amd.evaluate(d, s, parts, what=what, from_step=True)
+    parts = res.parts.clone()
+    parts[int(extra)] = -1
+    a = sheep_amd.evaluate(d, s, parts, what=what)
+    assert a == sheep_amd.evaluate(d, s, parts, what=what, from_step=True)
+    assert a == sheep_amd.evaluate(d, s, res.parts, what=what)
 
 
 @pytest.mark.parametrize("scale,seed,k", [(16, 5, 16), (18, 7, 64)])
@@ -634,6 +668,58 @@ def test_rccl_world_of_one(gpu_ctx):
         out[link] = g.evaluate([d], seqs, parts)
         g.close()
     assert out["rccl"] == out["host"] == ev
+
+
+def test_rccl_world_of_one_abort(gpu_ctx, capfd):
+    """The failure path's RCCL side on one GPU: a non-blocking one-rank communicator runs a
+    collective through the polled wait, then sheep_group_abort ends the world
+    (ncclCommAbort): one stderr line names the rank, bus id and cause, every later
+    collective raises at once, and destroying the world does not hang."""
+    import time
+    import sheep_amd
+    d = sheep_amd.rmat(12, 16, 12)
+    g = sheep_amd.Group.join(0, 0, 1, link="rccl")
+    assert g.rccl and not g.failed
+    seqs = g.sequence([d], 1 << 12)
+    assert seqs[0].n == sheep_amd.degree_sequence(d).n
+    g.abort("test abort")
+    assert g.failed
+    t0 = time.time()
+    with pytest.raises(RuntimeError, match="failed before"):
+        g.sequence([d], 1 << 12)
+    with pytest.raises(RuntimeError, match="failed before"):
+        g.barrier()
+    assert time.time() - t0 < 5
+    g.close()
+    err = capfd.readouterr().err
+    assert "sheep: rank 0 of 1 (bus " in err and "abort of 0 bytes failed: test abort" in err, err
+
+
+def test_group_join_rank_stalls(gpu_ctx, tmp_path):
+    """A joined world of 3 processes on one GPU (host links) whose rank 2 joins and then
+    never takes part: ranks 0 and 1 get an error from their first collective within
+    SHEEP_JOIN_TIMEOUT instead of hanging, print the one-line report (rank, bus id,
+    collective, bytes), and then every call is refused at once."""
+    import socket
+    import subprocess
+    import sys
+    timeout = 4
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "group_worker.py")
+    env = dict(os.environ, SHEEP_JOIN_TIMEOUT=str(timeout))
+    procs = [subprocess.Popen([sys.executable, worker, str(r), "3", str(port), str(tmp_path), "stall"],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env) for r in range(3)]
+    outs = [p.communicate(timeout=240)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    for r in (0, 1):
+        out = outs[r]
+        waited = float(out.split("failed after ")[1].split(" s")[0])
+        assert waited <= timeout + 2, out
+        assert f"sheep: rank {r} of 3 (bus " in out and "failed: mesh:" in out, out
+        assert "refused after" in out and "failed before" in out, out
+    assert "timed out waiting for rank 2" in outs[0], outs[0]
 
 
 @pytest.mark.parametrize("ranks", [2, 3])
