@@ -190,6 +190,9 @@ def main():
         # barriers and the max over ranks of the wall time.  The data path is the world of
         # include/sheep_hip.h (sheep_group_join, group.hip): RCCL over xGMI between the
         # ranks' GPUs, the same code graph2tree -i -r runs under mpiexec.
+        # a rank that dies or stalls ends the run within this many seconds (group.hip's RCCL
+        # failure path: abort, one stderr line per rank, non-zero exit) instead of wedging it
+        os.environ.setdefault("SHEEP_JOIN_TIMEOUT", "180")
         sdist.init_control()
         group = sheep_amd.Group.join(local, rank, world, "127.0.0.1", sdist.shared_port(),
                                      link="host" if a.same_device else "rccl")
@@ -459,6 +462,14 @@ def time_evaluator(a, ctx, group, shard, subs, s, res, rank, world, dev, barrier
             out["device_ms"] = round(ms / launches, 3)
     if world == 1 and a.shards == 1:
         out["source"] = "the step's position-space edges (sheep_evaluate_step)"
+        # the bytes this form moves: per edge the 8-B edge, the lo's 2-B part and the hi's 8-B
+        # owner word; per node the part lookup (seq 4 + pos check 4 + part 2 + pj 2) and the
+        # node pass (owner word 8 + pj 2 + pst 4)
+        b_step = 18 * R_total + 26 * s.n
+        out["own_model"] = {"alg_bytes": b_step, "achieved_GBs": round(b_step / best / 1e9, 2),
+                            "frac": round(b_step / best / 1e9 / HBM_PEAK_GBS, 4),
+                            "model": "18 B per edge + 26 B per tree node (what sheep_evaluate_step reads and "
+                                     "writes; B_eval above prices the record evaluator's reads)"}
         if a.eval_records:   # the record evaluator (sheep_evaluate) on the same parts, for comparison
             rt = []
             for _ in range(a.eval_reps):
@@ -545,6 +556,27 @@ def cpu_info():
     return model, os.cpu_count(), usable
 
 
+def run_group(cmd, env, timeout):
+    """Runs cmd in a process group of its own and kills whatever of the group is left when it
+    returns (mpiexec's hydra proxies can outlive it): nothing the baseline started survives
+    bench.py."""
+    import signal
+    import subprocess
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, err = p.communicate()
+    finally:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)   # (the group's leftovers; the leader has exited)
+        except (ProcessLookupError, PermissionError):
+            pass
+    return subprocess.CompletedProcess(cmd, p.returncode, out, err)
+
+
 def cpu_baseline(a, ctx):
     """The reference CPU path on the same workload (RMAT-26 by default), on this host.
 
@@ -590,8 +622,7 @@ def cpu_baseline(a, ctx):
         ctx.sync()
         for p, th in configs:
             env = dict(os.environ, OMP_NUM_THREADS=str(th))
-            r = subprocess.run([mpiexec, "-n", str(p), harness, "mpi", path, str(a.k)], capture_output=True,
-                               text=True, timeout=900, env=env)
+            r = run_group([mpiexec, "-n", str(p), harness, "mpi", path, str(a.k)], env, 900)
             if r.returncode != 0:
                 runs.append({"ranks": p, "threads": th, "error": r.stderr.strip()[-300:]})
                 continue

@@ -41,6 +41,12 @@
 extern "C" {
 #endif
 
+/* ABI version: raised whenever a public struct changes size or layout or an entry point its
+ * signature (INTEGRATION.md "ABI versions" lists the changes).  sheep_abi_version() returns the
+ * library's; a caller built against another header should refuse to run. */
+#define SHEEP_ABI_VERSION 6
+int sheep_abi_version(void);
+
 #define SHEEP_OK 0
 #define SHEEP_ERR_ARG (-1)     /* bad argument (null pointer, size mismatch)          */
 #define SHEEP_ERR_HIP (-2)     /* HIP runtime error (no device, launch failure, ...)  */

@@ -40,6 +40,7 @@ INVALID_PART = -1
 DEGREE_MODES = {"llama": 0, "dat": 1, "net": 2}
 EVAL_GRAPH, EVAL_DOWN, EVAL_UP = 1, 2, 4
 
+ABI_VERSION = 6   # include/sheep_hip.h SHEEP_ABI_VERSION
 _ERRORS = {-1: ValueError, -2: RuntimeError, -3: IndexError, -4: RuntimeError, -5: MemoryError}
 
 
@@ -104,6 +105,7 @@ def lib() -> ctypes.CDLL:
     P, U64, I32, I16, D = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int16, ctypes.c_double
     sig = {
         "sheep_last_error": ([], ctypes.c_char_p),
+        "sheep_abi_version": ([], I32),
         "sheep_ctx_create": ([I32, P, ctypes.POINTER(P)], I32),
         "sheep_ctx_destroy": ([P], I32),
         "sheep_ctx_trim": ([P], I32),
@@ -170,6 +172,8 @@ def lib() -> ctypes.CDLL:
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
+    if L.sheep_abi_version() != ABI_VERSION:   # (struct layouts below are this header's)
+        raise ImportError(f"{LIB_PATH}: ABI version {L.sheep_abi_version()}, this binding expects {ABI_VERSION}")
     _lib = L
     return L
 

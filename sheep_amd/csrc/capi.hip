@@ -90,6 +90,8 @@ extern "C" {
 
 const char *sheep_last_error(void) { return sheep::g_last_error.c_str(); }
 
+int sheep_abi_version(void) { return SHEEP_ABI_VERSION; }
+
 int sheep_ctx_create(int device, void *hip_stream, sheep_ctx **out) {
   API_BEGIN
   NEED(out, "null out");

@@ -14,6 +14,8 @@ reduce and the parts broadcast — and uses torch.distributed over gloo (host TC
 """
 from __future__ import annotations
 
+import datetime
+import os
 import socket
 
 import torch
@@ -25,7 +27,11 @@ def shard_bounds(nrec: int, rank: int, world: int) -> tuple[int, int]:
 
 
 def init_control(**kw) -> None:
+    """The gloo group; its collectives give up after max(300 s, SHEEP_JOIN_TIMEOUT) instead of
+    torch's 30 minutes, so a dead rank ends the run (the sheep world has its own deadline)."""
     if not dist.is_initialized():
+        t = max(300, int(os.environ.get("SHEEP_JOIN_TIMEOUT", "300")))
+        kw.setdefault("timeout", datetime.timedelta(seconds=t))
         dist.init_process_group("gloo", **kw)
 
 

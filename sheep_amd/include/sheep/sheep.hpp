@@ -62,6 +62,9 @@ class Context {
 
  private:
   Context() {
+    if (sheep_abi_version() != SHEEP_ABI_VERSION)   // built against another header: struct layouts differ
+      throw std::runtime_error("libsheep_hip.so ABI version " + std::to_string(sheep_abi_version()) +
+                               ", this build expects " + std::to_string(SHEEP_ABI_VERSION));
     const char *d = getenv("SHEEP_DEVICE");
     check(sheep_ctx_create(d ? atoi(d) : 0, SHEEP_OWN_STREAM, &h_));
   }
