@@ -163,6 +163,8 @@ typedef struct sheep_tuning {
   int32_t merge_cut_bits;  /* merges: the early MSF cut of the top 2^bits positions, whatever the density: 0 off, 14..30 */
   int32_t event_loop;      /* partition packing events: 0 one launch per event, else one persistent launch while the
                               event table fits this many entries (in LDS), 1..4096 */
+  int32_t hook_up;         /* etree hook rounds hook the smaller root under the larger (root = top, no light-top
+                              pass): 0 never, 1 merges, 2 all */
 } sheep_tuning;
 int sheep_tuning_default(sheep_tuning *out);
 int sheep_ctx_set_tuning(sheep_ctx *ctx, const sheep_tuning *t);

@@ -74,7 +74,8 @@ class Tuning(ctypes.Structure):
                 ("big_dense", ctypes.c_int64), ("big_hot_bits", ctypes.c_int32), ("big_hot16", ctypes.c_int32),
                 ("relabel_planes", ctypes.c_int32), ("relabel_per", ctypes.c_int32),
                 ("cross_win_levels", ctypes.c_int32), ("hook_batch", ctypes.c_int32),
-                ("merge_cut_bits", ctypes.c_int32), ("event_loop", ctypes.c_int32)]
+                ("merge_cut_bits", ctypes.c_int32), ("event_loop", ctypes.c_int32),
+                ("hook_up", ctypes.c_int32)]
 
     @classmethod
     def of(cls, **kw):

@@ -296,6 +296,7 @@ static sheep_tuning resolve_tuning(const sheep_tuning *t) {
   SHEEP_TUNE(relabel_per, r.relabel_per == 4 || r.relabel_per == 8 || r.relabel_per == 12 || r.relabel_per == 15)
   SHEEP_TUNE(cross_win_levels, r.cross_win_levels >= 0 && r.cross_win_levels <= 8)
   SHEEP_TUNE(hook_batch, r.hook_batch >= 0 && r.hook_batch <= 2)
+  SHEEP_TUNE(hook_up, r.hook_up >= 0 && r.hook_up <= 2)
   SHEEP_TUNE(merge_cut_bits, r.merge_cut_bits == 0 || (r.merge_cut_bits >= 14 && r.merge_cut_bits <= 30))
   SHEEP_TUNE(event_loop, r.event_loop >= 0 && r.event_loop <= 4096)
 #undef SHEEP_TUNE

@@ -96,6 +96,7 @@ inline sheep_tuning default_tuning() {
   t.relabel_per = 8;
   t.cross_win_levels = 2;   // RMAT-26: level 0/1 1.30/2.46 -> 0.77/1.16 ms; level 2 1.60 -> 1.74 ms
   t.hook_batch = 0;        // merges 14.0 -> 18.0 ms, maps no better (RMAT-26, 8 shards)
+  t.hook_up = 0;
   t.merge_cut_bits = 0;
   t.event_loop = 4096;
   return t;
@@ -572,11 +573,13 @@ uint64_t group_edges_by_lo(Ctx &c, const uint64_t *edges, uint64_t m, const LoGr
 // subproblem of a split merge; the caller cuts the later groups to it).  top_bits > 0: the
 // block of the 2^top_bits highest positions is replaced by its minimum spanning forest when
 // dense (maps; etree.hip "the dense top block").
-// hook_batch: the hook rounds find all of a thread's edges' roots at once (merges: chains
-// of tree edges, little contention) instead of one edge after another (maps: hub pile-ups).
+// hook_mode: HOOK_BATCH — the hook rounds find all of a thread's edges' roots at once
+// (merges: chains of tree edges, little contention) instead of one edge after another (maps:
+// hub pile-ups); HOOK_UP — the smaller root is hooked under the larger (root = top).
 void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
                       int fin_bits, int filt_lvl = -1, uint32_t ylo = 0, uint32_t yhi = 0, int top_bits = 0,
-                      bool hook_batch = false, int force_big_bits = 0);
+                      int hook_mode = 0, int force_big_bits = 0);
+constexpr int HOOK_BATCH = 1, HOOK_UP = 2;
 void spread_params(uint64_t n, int *L, uint32_t *clo);
 // append.hip — sharded appends: counters (NSHARD * SHARD_STRIDE u64, zeroed).  The pack
 // step moves the shard regions of a producer that streamed *n_in items together in dst

@@ -239,6 +239,14 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint32_t *__restrict__ uf, uint
 // values — entry by entry when the level's lists are short against n (only light
 // endpoints, cross roots and cross hi ends were written), else densely; the choice is
 // made on the device from the level's counts (no host round trip).
+// Where the adoption parent(top(r)) = m_r runs for tagged state: a level with few cross
+// edges against n adopts in k_cross_apply, from the edges with b == m_r (a random top read
+// and parent store each, for one edge per root), instead of k_level_clean's dense pass over
+// all n words of mt (~26 us at RMAT-26 even when a late level has a few thousand roots).
+// Both kernels decide from the same device counts.
+// (8 RMAT-26 shard maps + merge 122.4 -> 121.7 ms, C3 and C2 unchanged: profiles/r6/README.md)
+__host__ __device__ inline bool sparse_adopt(uint64_t nx, uint64_t n) { return nx * 8 < n; }
+
 struct LevelClean {   // what k_level_clean needs of the level it closes
   const uint64_t *lx;   // the level's light entries, then its cross entries (st[ST_NL] on)
   const uint32_t *xtop;
@@ -265,7 +273,7 @@ __device__ void level_clean(const LevelClean &lc) {
   for (uint64_t i = t0; i < NCSET * CSET_WORDS; i += stride) csets[i] = 0;
   if (tagged) {   // parent(top(r)) = m_r for every root r with a cross edge (jnode.h:158-162 adopt)
     const Tg g = make_tag(lvl, true);
-    if (nx == 0) return;
+    if (nx == 0 || sparse_adopt(nx, n)) return;   // (adopted by k_cross_apply's edges)
     for (uint64_t i = t0; i < n; i += stride) {
       const uint32_t m = g.m_get(mt[i]);
       if (m != INVALID) parent[g.get(top[i], (uint32_t)i)] = m;
@@ -345,6 +353,12 @@ __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict_
 // another round trip); rounds instead resolve such a pile-up in a few passes.
 // (Batched finds of all the thread's edges before any hook left more hooks to later
 // rounds: 21-22 ms against 10.8 ms at RMAT-26.)
+// UP (sheep_tuning hook_up): the smaller root is hooked under the larger, so a component's
+// root IS its top (its largest id) and k_light_top does not run.  Any hook direction leaves
+// the same components; the forest stays a forest of ancestors (a link only ever attaches a
+// root, path splitting only ever names an ancestor), so every read — stale or not — is an
+// ancestor of x.  The maps keep the smaller root (a hub component's root is then the few low
+// ids every hook agrees on; root = top measured 2x slower hooking there).
 // BATCH (sheep_tuning hook_batch): the roots of all the thread's edges are found at once
 // (2 x TILE_ITEMS chains in flight, find_many) and then hooked.  A root found this way may
 // be stale by its turn — hook() then fails on the hi side and the edge goes to the next
@@ -352,7 +366,7 @@ __global__ __launch_bounds__(BLOCK) void k_light_top(const uint64_t *__restrict_
 // the result is the same; it pays where the edges are chains (merges: one dependent load
 // after another, little contention) and not where a forming hub component takes every
 // hook (maps: more stale roots, more rounds).
-template <bool BATCH>
+template <bool BATCH, bool UP>
 __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict__ in, const uint64_t *__restrict__ n_in,
                                                       uint32_t *uf, Tg g, uint64_t *__restrict__ out,
                                                       unsigned long long *__restrict__ counter) {
@@ -382,7 +396,7 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
         uint32_t a = r[2 * j], b = r[2 * j + 1];
         if (a == b) continue;
         const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-        if (!hook(uf, g, hi, lo)) keep |= 1u << j;
+        if (!(UP ? hook(uf, g, lo, hi) : hook(uf, g, hi, lo))) keep |= 1u << j;
       }
     } else {
 #pragma unroll
@@ -392,7 +406,7 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
         find2(uf, g, a, b);
         if (a == b) continue;
         const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-        if (!hook(uf, g, hi, lo)) keep |= 1u << j;
+        if (!(UP ? hook(uf, g, lo, hi) : hook(uf, g, hi, lo))) keep |= 1u << j;
       }
     }
     uint64_t slot = shard_reserve((uint32_t)__popc(keep), counter, tile, ntiles, 1);
@@ -405,6 +419,7 @@ __global__ __launch_bounds__(BLOCK) void k_hook_round(const uint64_t *__restrict
 // The edges still unresolved after HOOK_ROUNDS rounds (few: the pile-ups are gone) are
 // hooked in place, retrying until each one's roots agree.  Lock-free: a failed CAS
 // means another hook made progress.
+template <bool UP>
 __global__ __launch_bounds__(BLOCK) void k_hook_finish(const uint64_t *__restrict__ src, const uint64_t *__restrict__ n_in,
                                                        const unsigned long long *__restrict__ counters, uint32_t *uf, Tg g,
                                                        uint64_t *__restrict__ n_left) {
@@ -440,7 +455,7 @@ __global__ __launch_bounds__(BLOCK) void k_hook_finish(const uint64_t *__restric
       find2(uf, g, a, b);
       if (a == b) break;
       const uint32_t l = a < b ? a : b, h = a < b ? b : a;
-      if (hook(uf, g, h, l)) break;
+      if (UP ? hook(uf, g, l, h) : hook(uf, g, h, l)) break;
     }
   }
 }
@@ -595,8 +610,9 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restric
                                                        const uint32_t *__restrict__ top, uint32_t *__restrict__ claim,
                                                        uint64_t *__restrict__ scratch,
                                                        unsigned long long *__restrict__ counters,
-                                                       uint32_t *__restrict__ parent, Tg g) {
+                                                       uint32_t *__restrict__ parent, Tg g, uint64_t n) {
   const uint64_t nx = st[ST_NX];
+  const bool adopt_here = !g.on || sparse_adopt(nx, n);   // (uniform)
   const uint64_t *__restrict__ xbuf = lx + st[ST_NL];
   const uint64_t ntiles = (nx + TILE - 1) / TILE;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -622,10 +638,10 @@ __global__ __launch_bounds__(BLOCK) void k_cross_apply(const uint64_t *__restric
     for (int k = 0; k < TILE_ITEMS; ++k) m[k] = r[k] != INVALID ? g.m_get(m[k]) : INVALID;
 #pragma unroll
     for (int k = 0; k < TILE_ITEMS; ++k) cl[k] = claim[b[k]];
-    if (!g.on) {   // untagged state: the adoption here (tagged: k_level_clean)
+    if (adopt_here) {   // untagged state, or a level with few cross edges (else k_level_clean)
 #pragma unroll
       for (int k = 0; k < TILE_ITEMS; ++k)
-        if (r[k] != INVALID && b[k] == m[k]) parent[top[r[k]]] = m[k];
+        if (r[k] != INVALID && b[k] == m[k]) parent[g.get(top[r[k]], r[k])] = m[k];
     }
 #pragma unroll
     for (int k = 0; k < TILE_ITEMS; ++k) {
@@ -2201,8 +2217,9 @@ static bool big_cut(Ctx &c, uint64_t *next, uint64_t *st, const uint64_t *r0, ui
 }
 
 void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uint32_t *parent, const uint64_t *seg,
-                      int fin_bits, int filt_lvl, uint32_t ylo, uint32_t yhi, int top_bits, bool hook_batch,
+                      int fin_bits, int filt_lvl, uint32_t ylo, uint32_t yhi, int top_bits, int hook_mode,
                       int force_big_bits) {
+  const bool hook_batch = (hook_mode & HOOK_BATCH) != 0, hook_up = (hook_mode & HOOK_UP) != 0;
   fill_u32(c, parent, n, INVALID);
   if (n < 2 || m == 0) return;
   if (m >= 0xFFFFFFFFull) throw Error(SHEEP_ERR_ARG, "too many edges for one shard");
@@ -2337,15 +2354,20 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
     {
       TimedRegion tr(c, "etree_union");
       static_assert(HOOK_ROUNDS == 1, "k_hook_finish reads the one round's shard regions");
-      hipLaunchKernelGGL(hook_batch ? k_hook_round<true> : k_hook_round<false>, dim3(gt), dim3(BLOCK), 0, c.stream,
-                         (const uint64_t *)lx, (const uint64_t *)(st + ST_NL), uf, g, alt, cset(CSET_HOOK));
+      auto round = hook_up ? (hook_batch ? k_hook_round<true, true> : k_hook_round<false, true>)
+                           : (hook_batch ? k_hook_round<true, false> : k_hook_round<false, false>);
+      hipLaunchKernelGGL(round, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)lx, (const uint64_t *)(st + ST_NL),
+                         uf, g, alt, cset(CSET_HOOK));
       LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_hook_finish, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)alt,
-                         (const uint64_t *)(st + ST_NL), (const unsigned long long *)cset(CSET_HOOK), uf, g, st + ST_HOOK);
+      hipLaunchKernelGGL(hook_up ? k_hook_finish<true> : k_hook_finish<false>, dim3(gf), dim3(BLOCK), 0, c.stream,
+                         (const uint64_t *)alt, (const uint64_t *)(st + ST_NL), (const unsigned long long *)cset(CSET_HOOK),
+                         uf, g, st + ST_HOOK);
       LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_light_top, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)lx,
-                         (const uint64_t *)(st + ST_NL), uf, top, g);
-      LAUNCH_CHECK();
+      if (!hook_up) {   // (hook_up: every root is its component's top already)
+        hipLaunchKernelGGL(k_light_top, dim3(gf), dim3(BLOCK), 0, c.stream, (const uint64_t *)lx,
+                           (const uint64_t *)(st + ST_NL), uf, top, g);
+        LAUNCH_CHECK();
+      }
     }
     {
       TimedRegion tr(c, "etree_cross");
@@ -2362,7 +2384,7 @@ void etree_from_edges(Ctx &c, const uint64_t *edges, uint64_t m, uint64_t n, uin
       TimedRegion tr(c, "etree_apply");
       hipLaunchKernelGGL(k_cross_apply, dim3(gt), dim3(BLOCK), 0, c.stream, (const uint64_t *)lx,
                          (const uint32_t *)xtop, (const uint64_t *)st, (const uint32_t *)mt, (const uint32_t *)top, claim,
-                         alt, cset(CSET_APPLY), parent, g);
+                         alt, cset(CSET_APPLY), parent, g, n);
       LAUNCH_CHECK();
       pack_shards<uint64_t>(c, alt, next, st + ST_NX, cset(CSET_APPLY), st + ST_CONTR, nullptr, nullptr, st + ST_KEPT);
     }
@@ -2617,7 +2639,8 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
       }
     }
     TimedRegion tr(c, "etree", 8 * m);
-    etree_from_edges(c, r0, m, n, parent, seg, c.tune.fin_map_bits, -1, 0, 0, c.tune.top_bits, c.tune.hook_batch >= 2);
+    etree_from_edges(c, r0, m, n, parent, seg, c.tune.fin_map_bits, -1, 0, 0, c.tune.top_bits,
+                     (c.tune.hook_batch >= 2 ? HOOK_BATCH : 0) | (c.tune.hook_up >= 2 ? HOOK_UP : 0));
   } else {
     fill_u32(c, parent, n, INVALID);
   }
@@ -2742,8 +2765,8 @@ static void merge_set(Ctx &c, const TreeSet &ts, uint32_t K, uint64_t n, sheep_j
     TimedRegion tr(c, "merge", 8 * (uint64_t)K * n);   // the K trees
     // groups activated at levels >= l are b < L - l
     const uint64_t m = merge_edges(c, ts, K, n, pst, &edges, &seg, &L, l > 0 ? L - l : 0, lo, hi);
-    etree_from_edges(c, edges, m, n, parent, seg, fin_merge, l > 0 ? l : -1, ylo, yhi, 0, c.tune.hook_batch >= 1,
-                     c.tune.merge_cut_bits);
+    etree_from_edges(c, edges, m, n, parent, seg, fin_merge, l > 0 ? l : -1, ylo, yhi, 0,
+                     (c.tune.hook_batch >= 1 ? HOOK_BATCH : 0) | (c.tune.hook_up >= 1 ? HOOK_UP : 0), c.tune.merge_cut_bits);
   }
   hipLaunchKernelGGL(k_pack_tree, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, parent, pst, n, out);
   LAUNCH_CHECK();

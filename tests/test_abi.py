@@ -77,7 +77,7 @@ def test_tuning_defaults_without_a_device():
     assert t.as_dict() == {"fin_map_bits": 13, "fin_merge_bits": 12, "fin_dc": 1, "top_bits": 16, "top_blocks": 4,
                            "big_bits": 21, "big_dense": 256, "big_hot_bits": 15, "big_hot16": 0, "relabel_planes": 1,
                            "relabel_per": 8, "cross_win_levels": 2, "hook_batch": 0,
-                           "merge_cut_bits": 0, "event_loop": 4096}
+                           "merge_cut_bits": 0, "event_loop": 4096, "hook_up": 0}
     with pytest.raises(KeyError):
         sheep_amd.Tuning.of(no_such_field=1)
 

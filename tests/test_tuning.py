@@ -95,6 +95,8 @@ CASES = {
         {"tune": {"cross_win_levels": 8}, "merge": True, "expect": []},
         {"tune": {"hook_batch": 1}, "merge": True, "expect": []},
         {"tune": {"hook_batch": 2}, "merge": True, "expect": []},
+        {"tune": {"hook_up": 1}, "merge": True, "expect": []},
+        {"tune": {"hook_up": 2, "hook_batch": 2}, "merge": True, "expect": []},
         {"tune": {"merge_cut_bits": 16}, "merge": True, "expect": [r"etree big cut after s 16:"]},
     ]),
     # four times denser: the blocks right below the top one pass the density rule too

@@ -1,15 +1,16 @@
-# Round-5 final measurement set, part 2 (see profiles/r5/README.md): the sparse-input etree
+# Final measurement set, part 2 (see profiles/rN/README.md): the sparse-input etree
 # phase by phase (one 1/8 shard map, the 8-tree merge, the binomial schedule's hops), the
 # 8-shard RMAT-26 bench with one step's kernel trace, shuffled RMAT-26, C4, C5 and the
-# 2-rank rehearsal.  gpurun_out/r5fin/.
+# 2-rank rehearsal.  gpurun_out/$FIN/.
 set -o pipefail
 R=$(pwd)
-mkdir -p gpurun_out/r5fin/s8 && export HSA_ENABLE_IPC_MODE_LEGACY=0 && export TMPDIR=/tmp
+FIN=${FIN:-fin}
+mkdir -p gpurun_out/$FIN/s8 && export HSA_ENABLE_IPC_MODE_LEGACY=0 && export TMPDIR=/tmp
 ( while true; do date >> gpurun_out/heartbeat.txt; sleep 50; done ) &
 HB=$!
 trap 'kill $HB' EXIT
-O=gpurun_out/r5fin
-OUT=r5fin/shard bash tools/gpu/r5_shard.sh || exit 1
+O=gpurun_out/$FIN
+OUT=$FIN/shard bash tools/gpu/shard_phases.sh || exit 1
 cd $O/s8 && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d ks -o run --output-format csv -- \
   python $R/bench.py --scale 26 --k 64 --shards 8 --steps 3 --warmup 1 --eval-reps 1 --no-cpu-baseline > ks.log 2>&1 || exit 1
 python $R/tools/trace_step.py $(find ks -name '*kernel_trace.csv' | head -1) --levels > step_trace.txt || exit 1
