@@ -67,6 +67,10 @@ def parse():
     ap.add_argument("--shards", type=int, default=1,
                     help="one GPU: edge shards mapped one after another and merged K-way (graphs of >= 2^32 "
                          "records, e.g. RMAT-28; C5 on one GPU)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="one GPU with --shards: the shards' degree counts and maps run on this many contexts, each "
+                         "on a stream of its own driven by a host thread of its own (independent shards overlap on "
+                         "the GPU, as the ranks of an N-GPU run do across GPUs); the merge runs on the first")
     ap.add_argument("--shuffle", action="store_true",
                     help="records in a random order, half with tail/head swapped (a generic edge list)")
     ap.add_argument("--eval-reps", type=int, default=3, help="timed evaluator runs (0: skip)")
@@ -212,6 +216,12 @@ def main():
     del rec
     torch.cuda.empty_cache()
     dev = f"cuda:{local}"
+    ctxs = [ctx]   # --streams: more contexts on this device, each with a stream of its own
+    if a.shards > 1 and world == 1:
+        ctxs += [sheep_amd.Context(local, stream=torch.cuda.Stream(local)) for _ in range(max(1, a.streams) - 1)]
+        for cx in ctxs[1:]:
+            if tune:
+                cx.set_tuning(**tune)
     deg = torch.zeros(vs_cap, dtype=torch.int32, device=dev)
     subs = [shard[i * shard.shape[0] // a.shards:(i + 1) * shard.shape[0] // a.shards] for i in range(a.shards)]
     stack = [None]
@@ -222,6 +232,33 @@ def main():
         t1 = time.perf_counter()
         walls[name] = walls.get(name, 0.0) + (t1 - t0)
         return t1
+
+    def on_contexts(fn):
+        """fn(i) for every shard i, shard i on context i mod len(ctxs): one host thread per
+        context (the library's calls release the GIL and synchronise their own stream), the
+        contexts' streams complete on return."""
+        if len(ctxs) == 1:
+            for i in range(len(subs)):
+                fn(i)
+            return
+        import threading
+        torch.cuda.synchronize()                                 # inputs written on other streams
+        err = []
+
+        def run(j):
+            try:
+                for i in range(j, len(subs), len(ctxs)):
+                    fn(i)
+                ctxs[j].sync()
+            except Exception as e:                               # (re-raised below)
+                err.append(e)
+        th = [threading.Thread(target=run, args=(j,)) for j in range(len(ctxs))]
+        for t_ in th:
+            t_.start()
+        for t_ in th:
+            t_.join()
+        if err:
+            raise err[0]
 
     def step():
         deg.zero_()
@@ -239,16 +276,17 @@ def main():
             tree = group.reduce_trees([bufs["tree"][:s.n]], a.reduce)[0]
             t0 = lap("reduce", t0)                              # gather + merge on rank 0, the send elsewhere
         else:
-            vs = 0
-            for sub in subs:                                    # shards accumulate into one histogram
-                _, max_slot = sheep_amd.degree_count(sub, mode="llama", deg=deg, ctx=ctx)
-                vs = max(vs, max_slot)
-            s = sheep_amd.sequence_from_degrees(deg, vs, ctx=ctx)
+            slots = [0] * len(subs)
+
+            def count(i):                                       # shards accumulate into one histogram
+                slots[i] = sheep_amd.degree_count(subs[i], mode="llama", deg=deg, ctx=ctxs[i % len(ctxs)])[1]
+
+            on_contexts(count)
+            s = sheep_amd.sequence_from_degrees(deg, max(slots), ctx=ctx)
             if a.shards > 1:                                    # map per shard, then ONE K-way merge
                 if stack[0] is None or stack[0].shape[1] != s.n:
                     stack[0] = torch.empty((a.shards, s.n, 2), dtype=torch.int32, device=dev)
-                for i, sub in enumerate(subs):
-                    sheep_amd.build_tree(sub, s, ctx=ctx, out=stack[0][i])
+                on_contexts(lambda i: sheep_amd.build_tree(subs[i], s, ctx=ctxs[i % len(ctxs)], out=stack[0][i]))
                 tree = sheep_amd.merge_trees_many(stack[0], ctx=ctx)
             else:
                 tree = sheep_amd.build_tree(shard, s, ctx=ctx)
@@ -272,8 +310,9 @@ def main():
     for _ in range(a.warmup):
         step()
     barrier()
-    ctx.timing(True)
-    ctx.timer_reset()
+    for cx in ctxs:
+        cx.timing(True)
+        cx.timer_reset()
     walls.clear()
     barrier()
     t0 = time.perf_counter()
@@ -287,11 +326,18 @@ def main():
     hbm_used = total_b - free_b
 
     # per-region device timings (HIP events on the context stream), timed steps only
+    # (--streams: summed over the contexts; their regions overlap in time)
     phases = {}
-    for name in ctx.timer_names():
-        ms, launches, nbytes = ctx.timer(name)
-        phases[name] = {"ms_per_step": round(ms / a.steps, 4), "launches": launches, "alg_bytes": nbytes}
-    ctx.timer_reset()
+    for cx in ctxs:
+        for name in cx.timer_names():
+            ms, launches, nbytes = cx.timer(name)
+            p = phases.setdefault(name, {"ms_per_step": 0.0, "launches": 0, "alg_bytes": 0})
+            p["ms_per_step"] = round(p["ms_per_step"] + ms / a.steps, 4)
+            p["launches"] += launches
+            p["alg_bytes"] += nbytes
+        cx.timer_reset()
+    for cx in ctxs[1:]:
+        cx.timing(False)
     per_rank = None
     if world > 1:   # every rank's split of the step, for diagnosing the N-rank run (rank 0 reports)
         mine = {"rank": rank, "wall_ms_per_step": {k: round(1e3 * v / a.steps, 3) for k, v in walls.items()},
@@ -353,7 +399,8 @@ def main():
                      f"synthetic (Chung-Lu power law, gamma 1.9, {sheep_amd.TWITTER_VERTICES} vertices, seeded")
                     + ", self-loops/duplicates removed"
                     + (", records shuffled and half of them reversed)" if a.shuffle else ", records (tail, head)-sorted)"),
-            "config": {"workload": workload, "records": R, "vertex_slots": s.pos_size,
+            "config": {"workload": workload + (f", {len(ctxs)} streams" if len(ctxs) > 1 else ""), "records": R,
+                       "vertex_slots": s.pos_size,
                        "tree_nodes": n, "k": a.k, "created": res.created, "packing_nodes": res.packing_nodes,
                        "heavy_nodes": res.heavy_nodes, "event_launches": res.event_launches, "seed": seed, "shuffled": a.shuffle, "shards": a.shards,
                        "tuning": ctx.tuning() if tune else "defaults",

@@ -1,6 +1,14 @@
-# Round-6 probe: the tuning suite (hook_up branches against the oracle) and the sparse-etree
-# tuning A/B (tools/tune_ab.py: one 1/8 shard's map and the 8-tree K-way merge per variant).
+# Round-6 probe: the one-GPU shard forms with the shards' maps on 1 / 2 / 4 streams
+# (bench.py --streams): the 8-shard RMAT-26 line and C5.
 set -o pipefail
-mkdir -p gpurun_out/r6 && export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 300 python -u -m pytest tests/test_tuning.py -x -q --timeout 240 --timeout-method thread > gpurun_out/r6/tuning_c.log 2>&1 || exit 1
-timeout -k 10 400 python -u tools/tune_ab.py 26 5 8 up1:hook_up=1 up1b:hook_up=1,hook_batch=1 up2:hook_up=2 > gpurun_out/r6/tune_ab_hookup.json 2> gpurun_out/r6/tune_ab_hookup.err || exit 1
+O=gpurun_out/r6/streams
+mkdir -p $O && export HSA_ENABLE_IPC_MODE_LEGACY=0
+( while true; do date >> gpurun_out/heartbeat.txt; sleep 50; done ) &
+HB=$!
+trap 'kill $HB' EXIT
+for st in 1 2 4 2 1; do
+  timeout -k 10 300 python -u bench.py --scale 26 --k 64 --shards 8 --streams $st --steps 3 --warmup 1 --no-cpu-baseline \
+    --eval-reps 1 > $O/s8_st${st}_$RANDOM.json 2> $O/s8_st$st.err || exit 1
+done
+timeout -k 10 600 python -u bench.py --scale 28 --k 256 --shards 8 --streams 2 --steps 2 --warmup 1 --no-cpu-baseline \
+  --eval-reps 1 > $O/c5_st2.json 2> $O/c5_st2.err || exit 1
