@@ -811,3 +811,47 @@ def test_parse_net_large_vs_dat(gpu_ctx):
     text = "".join(f"{t} {u}\n" for t, u in h[:, :2]).encode()
     got = sheep_amd.to_numpy_u32(sheep_amd.parse_net(text)).reshape(-1, 3)
     assert np.array_equal(got[:, :2], h[:, :2])
+
+
+def test_shard_maps_on_concurrent_contexts(gpu_ctx):
+    """bench.py --streams: the shards' degree counts and maps on two contexts of one device,
+    each on a stream of its own driven by a host thread of its own, at the same time: the
+    shard trees and their K-way merge equal the one-context results (and the whole graph's
+    tree)."""
+    import threading
+    import torch
+    import sheep_amd
+    d = sheep_amd.rmat(17, 16, 17)
+    R, K = d.shape[0], 4
+    subs = [d[i * R // K:(i + 1) * R // K] for i in range(K)]
+    s = sheep_amd.degree_sequence(d)
+    want = [sheep_amd.build_tree(x, s) for x in subs]
+    whole = sheep_amd.build_tree(d, s)
+    ctxs = [sheep_amd.Context(0, stream=torch.cuda.Stream(0)) for _ in range(2)]
+    torch.cuda.synchronize()
+    degs = [torch.zeros(1 << 17, dtype=torch.int32, device="cuda") for _ in range(2)]
+    out = torch.empty((K, s.n, 2), dtype=torch.int32, device="cuda")
+    err = []
+
+    def run(j):
+        try:
+            for i in range(j, K, 2):
+                sheep_amd.degree_count(subs[i], mode="llama", deg=degs[j], ctx=ctxs[j])
+                sheep_amd.build_tree(subs[i], s, ctx=ctxs[j], out=out[i])
+            ctxs[j].sync()
+        except Exception as e:
+            err.append(e)
+    th = [threading.Thread(target=run, args=(j,)) for j in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not err, err
+    torch.cuda.synchronize()
+    for i in range(K):
+        assert torch.equal(out[i], want[i]), i
+    assert torch.equal(sheep_amd.merge_trees_many(out), whole)
+    deg_all = degs[0] + degs[1]
+    assert torch.equal(sheep_amd.sequence_from_degrees(deg_all, s.pos_size).seq[: s.n], s.seq[: s.n])
+    for c in ctxs:
+        c.close()
