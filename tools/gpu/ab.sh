@@ -14,7 +14,7 @@ for c in "${CF[@]}"; do
     for v in base $VARIANTS; do
       lib=""
       [ "$v" != base ] && lib=sheep_amd/lib/variants/libsheep_hip_$v.so
-      SHEEP_HIP_LIB=$lib timeout -k 10 ${LIMIT:-400} python -u bench.py $c --no-cpu-baseline --eval-reps 1 \
+      SHEEP_HIP_LIB=$lib timeout -k 10 ${LIMIT:-400} python -u bench.py $c --no-cpu-baseline ${EVAL:---eval-reps 1} \
         > $O/c${i}_${v}_$r.json 2> $O/c${i}_${v}_$r.err || exit 1
     done
   done
