@@ -47,7 +47,7 @@ REGION_KERNELS = {"degree": ["k_degree_fused"], "relabel": ["k_relabel_scatter",
                   "evaluate": ["k_pp", "k_eval_records", "k_eval_nodes", "k_parts_jnid", "k_eval_edges", "k_eval_loops",
                                "k_eval_nodes_j"]}
 # the newest round's profile of this workload (profiles/rNN/), collected by tools/gpu/gpuprof.sh
-PMC_DIRS = ("r5", "r4", "r3")
+PMC_DIRS = ("r6", "r5", "r4", "r3")
 PMC_FILE = os.path.join(ROOT, "profiles", "{round}", "pmc_traffic_rmat{scale}_k{k}.json")
 
 

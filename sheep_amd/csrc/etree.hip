@@ -1274,9 +1274,13 @@ __global__ __launch_bounds__(FDC_T) void k_fin_dc(const uint64_t *__restrict__ f
 // first-activity groups are ranges of them (seg from the node offsets, k_seg_at).  The
 // parents are deduplicated in registers; most of the K x n slots are empty or repeats
 // (RMAT-26, 8 shard trees: ~47M edges in 262M slots), which the levels no longer read.
+// Or parent planes (planes != nullptr): tree k's parents at planes + k * stride (u32 each)
+// with the trees' pst already summed in pst_sum — the form the multi-GPU reduce gathers
+// (half the bytes of whole trees; the pst sum travels as one RCCL reduce).
 struct TreeSet {
   const sheep_jnode *t0, *t1;
   uint64_t stride;
+  const uint32_t *planes = nullptr, *pst_sum = nullptr;
   __device__ __forceinline__ const sheep_jnode *at(uint32_t k) const { return k == 0 ? t0 : t1 + (uint64_t)(k - 1) * stride; }
 };
 constexpr uint32_t MERGE_KMAX = 64;   // trees per pass (a larger K is merged in passes)
@@ -1287,13 +1291,19 @@ template <int KM>
 __device__ __forceinline__ uint32_t tree_parents(const TreeSet &ts, uint32_t K, uint64_t n, uint64_t i,
                                                  uint32_t (&p)[KM], bool &bad) {
   uint32_t w = 0;
+  if (ts.planes) {
+    w = ts.pst_sum[i];
 #pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    p[k] = INVALID;
-    if ((uint32_t)k < K) {
-      const sheep_jnode x = ts.at(k)[i];
-      w += x.pst_weight;
-      p[k] = x.parent;
+    for (int k = 0; k < KM; ++k) p[k] = (uint32_t)k < K ? ts.planes[(uint64_t)k * ts.stride + i] : INVALID;
+  } else {
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      p[k] = INVALID;
+      if ((uint32_t)k < K) {
+        const sheep_jnode x = ts.at(k)[i];
+        w += x.pst_weight;
+        p[k] = x.parent;
+      }
     }
   }
 #pragma unroll
@@ -1345,6 +1355,17 @@ __global__ __launch_bounds__(BLOCK) void k_tree_write(TreeSet ts, uint32_t K, ui
 struct SegNodes { uint32_t node[64]; };
 __global__ void k_seg_at(const uint32_t *__restrict__ off, SegNodes sn, int cnt, uint64_t *__restrict__ seg) {
   if ((int)threadIdx.x < cnt) seg[threadIdx.x] = off[sn.node[threadIdx.x]];
+}
+
+// a tree's parents and pst as two planes (the multi-GPU reduce's send buffers)
+__global__ void k_tree_planes(const sheep_jnode *__restrict__ tree, uint64_t n, uint32_t *__restrict__ parent,
+                              uint32_t *__restrict__ pst) {
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
+    const sheep_jnode j = tree[i];
+    parent[i] = j.parent;
+    pst[i] = j.pst_weight;
+  }
 }
 
 __global__ void k_pack_tree(const uint32_t *__restrict__ parent, const uint32_t *__restrict__ pst, uint64_t n,
@@ -2772,6 +2793,12 @@ static void merge_set(Ctx &c, const TreeSet &ts, uint32_t K, uint64_t n, sheep_j
   LAUNCH_CHECK();
 }
 
+void tree_planes(Ctx &c, const sheep_jnode *tree, uint64_t n, uint32_t *parent, uint32_t *pst) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_tree_planes, dim3(grid_for(n)), dim3(BLOCK), 0, c.stream, tree, n, parent, pst);
+  LAUNCH_CHECK();
+}
+
 void merge_trees_part(Ctx &c, const sheep_jnode *trees, uint32_t K, uint64_t n, uint32_t part, uint32_t nparts,
                       sheep_jnode *out, uint64_t *v_lo, uint64_t *v_hi) {
   if (K == 0) throw Error(SHEEP_ERR_ARG, "merge: no trees");
@@ -2786,6 +2813,18 @@ void merge_trees_part(Ctx &c, const sheep_jnode *trees, uint32_t K, uint64_t n, 
 void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n, sheep_jnode *out) {
   if (n == 0) return;
   merge_set(c, TreeSet{a, b, 0}, 2, n, out);
+}
+
+// The K-way merge from parent planes (planes[k * n + i] = node i's parent in tree k) and the
+// trees' summed pst (pst_sum[i]): the same tree as merge_trees_many over the whole trees.
+void merge_parent_planes(Ctx &c, const uint32_t *planes, const uint32_t *pst_sum, uint32_t K, uint64_t n,
+                         sheep_jnode *out) {
+  if (n == 0) return;
+  if (K == 0 || K > MERGE_KMAX) throw Error(SHEEP_ERR_ARG, "merge: 1..64 parent planes per pass");
+  TreeSet ts{nullptr, nullptr, n};
+  ts.planes = planes;
+  ts.pst_sum = pst_sum;
+  merge_set(c, ts, K, n, out);
 }
 
 void merge_trees_many(Ctx &c, const sheep_jnode *trees, uint32_t K, uint64_t n, sheep_jnode *out) {

@@ -73,6 +73,9 @@ void relabel_and_tree(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_
                       sheep_jnode *tree);
 void merge_trees(Ctx &c, const sheep_jnode *a, const sheep_jnode *b, uint64_t n, sheep_jnode *out);
 void merge_trees_many(Ctx &c, const sheep_jnode *trees, uint32_t k, uint64_t n, sheep_jnode *out);
+void merge_parent_planes(Ctx &c, const uint32_t *planes, const uint32_t *pst_sum, uint32_t K, uint64_t n,
+                         sheep_jnode *out);
+void tree_planes(Ctx &c, const sheep_jnode *tree, uint64_t n, uint32_t *parent, uint32_t *pst);
 void eval_sizes(int what, int nparts, uint64_t pos_size, uint64_t *bits_words, uint64_t *acc_words);
 int eval_num_parts(Ctx &c, const int16_t *parts, uint64_t pos_size);
 void eval_shard(Ctx &c, const sheep_xs1 *rec, uint64_t nrec, const uint32_t *pos, uint64_t pos_size,
@@ -334,6 +337,40 @@ void allreduce_sum_u32(sheep_group *g, uint32_t *const *buf, uint64_t count) {
   transfer(g, xs, "all-reduce(sum) of degrees");
 }
 
+// Sum of one u32 array per rank into rank 0's (in place there); buf[li] per local rank.
+void reduce_sum_u32_to0(sheep_group *g, uint32_t *const *buf, uint64_t count, const char *what) {
+  const int P = g->world;
+  if (count == 0) return;
+  if (!g->comm.empty()) {
+    collective(g, what, count * sizeof(uint32_t), [&]() {
+      sync_all(g);
+      NCCL_CHECK(ncclGroupStart());
+      for (int i = 0; i < nlocal(g); ++i)
+        NCCL_CHECK(ncclReduce(buf[i], buf[i], count, ncclUint32, ncclSum, 0, g->comm[i], C(g, i).stream));
+      NCCL_CHECK(ncclGroupEnd());
+      rccl_wait(g);
+    });
+    return;
+  }
+  if (P == 1) return;
+  const int l0 = local_of(g, 0);
+  uint32_t *tmp = nullptr;
+  if (l0 >= 0) {
+    HIP_CHECK(hipSetDevice(g->dev[l0]));
+    tmp = C(g, l0).get_as<uint32_t>("grp_reduce_tmp", count);
+  }
+  for (int r = 1; r < P; ++r) {
+    const int lr = local_of(g, r);
+    transfer(g, {Xfer{r, 0, lr >= 0 ? buf[lr] : nullptr, tmp, count * sizeof(uint32_t)}}, what);
+    if (l0 >= 0) {
+      HIP_CHECK(hipSetDevice(g->dev[l0]));
+      hipLaunchKernelGGL(k_add_u32, dim3(grid_for(count)), dim3(BLOCK), 0, C(g, l0).stream, buf[l0],
+                         (const uint32_t *)tmp, count);
+      LAUNCH_CHECK();
+    }
+  }
+}
+
 // rank 0's bytes to every rank; buf[li] per local rank
 void broadcast(sheep_group *g, void *const *buf, size_t bytes, const char *what) {
   const int P = g->world;
@@ -570,38 +607,56 @@ int sheep_group_reduce_trees(sheep_group *g, sheep_jnode *const *tree, uint64_t 
   GNEED(g && tree, "null argument");
   GNEED(reduce >= 0 && reduce <= 2, "bad reduce mode");
   const int P = g->world;
-  if (P == 1 || reduce == 0 || n == 0) return SHEEP_OK;
+  // (a world of one over RCCL still runs the K-way path: its RCCL reduce and the parent-plane
+  // merge, the one-GPU check of them; the merged tree of one tree is that tree)
+  if ((P == 1 && g->comm.empty()) || reduce == 0 || n == 0) return SHEEP_OK;
+  GNEED(reduce != 1 || P <= 64, "K-way reduce: at most 64 ranks (one merge pass)");
   const size_t tb = n * sizeof(sheep_jnode);
   const int l0 = sheep::local_of(g, 0);
-  if (reduce == 1) {   // gather + one K-way merge on rank 0 (every transfer on its own link)
-    sheep_jnode *stack = nullptr;
-    if (l0 >= 0) {
-      HIP_CHECK(hipSetDevice(g->dev[l0]));
-      stack = sheep::C(g, l0).get_as<sheep_jnode>("grp_stack", (uint64_t)P * n);
-      HIP_CHECK(hipMemcpyAsync(stack, tree[l0], tb, hipMemcpyDeviceToDevice, sheep::C(g, l0).stream));
-    }
+  if (reduce == 1) {
+    // gather + one K-way merge on rank 0.  Only the parents travel (n x 4 B per rank, every
+    // transfer on its own link): the merge needs each tree's parents and the SUM of their pst
+    // weights, which is one RCCL reduce to rank 0 instead of P - 1 more planes.
+    const int L = sheep::nlocal(g);
+    std::vector<uint32_t *> par(L), pst(L);
+    uint32_t *planes = nullptr;
+    sheep::per_rank(g, [&](int i) {
+      sheep::Ctx &c = sheep::C(g, i);
+      pst[i] = c.get_as<uint32_t>("grp_pst", n);
+      if (i == l0) {   // rank 0's own parents straight into plane 0 of the stack
+        planes = c.get_as<uint32_t>("grp_planes", (uint64_t)P * n);
+        par[i] = planes;
+      } else {
+        par[i] = c.get_as<uint32_t>("grp_par", n);
+      }
+      sheep::tree_planes(c, tree[i], n, par[i], pst[i]);
+      c.sync();
+    });
     std::vector<sheep::Xfer> xs;
     for (int r = 1; r < P; ++r) {
       const int lr = sheep::local_of(g, r);
-      xs.push_back(sheep::Xfer{r, 0, lr >= 0 ? tree[lr] : nullptr, stack ? stack + (uint64_t)r * n : nullptr, tb});
+      xs.push_back(sheep::Xfer{r, 0, lr >= 0 ? par[lr] : nullptr, planes ? planes + (uint64_t)r * n : nullptr,
+                               n * sizeof(uint32_t)});
     }
     {
-      // the gather as a timed region of every local rank's context ("gather": send on the
-      // others, receive on rank 0; the host link's copies fall inside the events too)
+      // the gather (and the pst reduce) as a timed region of every local rank's context
+      // ("gather": send on the others, receive on rank 0; the host link's copies fall inside
+      // the events too)
       std::vector<std::unique_ptr<sheep::TimedRegion>> tr;
-      for (int i = 0; i < sheep::nlocal(g); ++i) {
+      for (int i = 0; i < L; ++i) {
         HIP_CHECK(hipSetDevice(g->dev[i]));
-        tr.emplace_back(new sheep::TimedRegion(sheep::C(g, i), "gather", tb));
+        tr.emplace_back(new sheep::TimedRegion(sheep::C(g, i), "gather", tb / 2 + n * sizeof(uint32_t)));
       }
-      sheep::transfer(g, xs, "gather of partial trees");
-      for (int i = 0; i < sheep::nlocal(g); ++i) {
+      sheep::transfer(g, xs, "gather of partial trees' parents");
+      sheep::reduce_sum_u32_to0(g, pst.data(), n, "reduce of partial trees' pst");
+      for (int i = 0; i < L; ++i) {
         HIP_CHECK(hipSetDevice(g->dev[i]));
         tr[i].reset();
       }
     }
     if (l0 >= 0) {
       HIP_CHECK(hipSetDevice(g->dev[l0]));
-      sheep::merge_trees_many(sheep::C(g, l0), stack, (uint32_t)P, n, tree[l0]);
+      sheep::merge_parent_planes(sheep::C(g, l0), planes, pst[l0], (uint32_t)P, n, tree[l0]);
       sheep::C(g, l0).sync();
     }
     return SHEEP_OK;

@@ -1,5 +1,5 @@
-# Round-6 probe: the direct relabel (random pos[head] gathers, k_relabel) against the
-# head-bucketed one, C3 and C2 (no evaluator leg: the direct form leaves no step edges).
+# Round-6: the group tests after the parent-plane reduce, then final set part 2.
 set -o pipefail
 mkdir -p gpurun_out/r6 && export HSA_ENABLE_IPC_MODE_LEGACY=0
-EVAL="--eval-reps 0" OUT=r6/ab_direct VARIANTS="direct" REPS=2 CONFIGS="--steps 5;--scale 22 --k 16 --steps 10" bash tools/gpu/ab.sh
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 240 --timeout-method thread -k "group or rccl or concurrent" > gpurun_out/r6/group_tests.log 2>&1 || exit 1
+FIN=r6fin bash tools/gpu/final_set2.sh

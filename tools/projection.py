@@ -47,9 +47,12 @@ def main():
     ]
     tail = [("kids + partition", "rank 0", ph.get("kids", 0.0) + ph.get("partition", 0.0),
              f"`kids` {ph.get('kids', 0):.2f} + `partition` {ph.get('partition', 0):.2f}")]
+    par_mb = n * 4 / 1e6
     kway = rows + [
-        (f"gather of {P - 1} partial trees, {P - 1} x {tree_mb:.0f} MB", "into rank 0", tree_mb / LINK_GBS,
+        (f"gather of {P - 1} partial trees' parents, {P - 1} x {par_mb:.0f} MB", "into rank 0", par_mb / LINK_GBS,
          f"model: one transfer per xGMI link at {LINK_GBS:.0f} GB/s"),
+        (f"pst reduce to rank 0, {par_mb:.0f} MB", "all (RCCL)", (P - 1) / P * par_mb / RING_GBS,
+         f"model: {P - 1}/{P} x {par_mb:.0f} MB at {RING_GBS:.0f} GB/s per GPU"),
         (f"K-way merge of {P} trees", "rank 0", ph.get("merge", 0.0), f"`merge` {ph.get('merge', 0):.2f}"),
     ] + tail
     hops = t.get("binomial_hop_ms", [])
