@@ -336,6 +336,24 @@ class TestC5:
             d *= 2
         assert torch.equal(cur[0], c5["tree"])
 
+    def test_c5_two_shards_same_tree(self, c5):
+        """The one-GPU bench line's form: the fewest shards the 32-bit record index allows
+        (2 x 2.1e9 records), mapped under the same sequence and merged K-way (K = 2): the
+        same tree as the 8 shards' (the elimination tree is unique), against the oracle."""
+        import sheep_amd
+        import torch
+        d, s = c5["d"], c5["s"]
+        R = d.shape[0]
+        halves = [d[:R // 2], d[R // 2:]]
+        assert all(h.shape[0] < (1 << 32) for h in halves)
+        two = torch.empty((2, s.n, 2), dtype=torch.int32, device="cuda")
+        for i, h in enumerate(halves):
+            sheep_amd.build_tree(h, s, out=two[i])
+        tree = sheep_amd.merge_trees_many(two)
+        del two
+        _check_tree_digest(tree, c5["g"])
+        assert torch.equal(tree, c5["tree"])
+
     def test_c5_partition_and_full_evaluator_vs_oracle(self, c5):
         import sheep_amd
         g = c5["g"]
