@@ -71,11 +71,9 @@ def parse():
                     help="one GPU with --shards: the shards' degree counts and maps run on this many contexts, each "
                          "on a stream of its own driven by a host thread of its own (independent shards overlap on "
                          "the GPU, as the ranks of an N-GPU run do across GPUs); the merge runs on the first")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="one GPU, one shard: consecutive steps overlap — step i's kids + partition (its packing "
-                         "events are paced by host round trips) run in a host thread on one context while step i+1's "
-                         "sequence and tree run on another (a stream of graphs to partition; by default the steps run "
-                         "one after another)")
+    ap.add_argument("--concurrent", type=int, default=0, metavar="N",
+                    help="one GPU, one shard: whole steps on N contexts at once, each context's steps in a host "
+                         "thread of its own (a stream of graphs; 0: off)")
     ap.add_argument("--shuffle", action="store_true",
                     help="records in a random order, half with tail/head swapped (a generic edge list)")
     ap.add_argument("--eval-reps", type=int, default=3, help="timed evaluator runs (0: skip)")
@@ -185,8 +183,8 @@ def main():
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
     if a.shards > 1 and world > 1:
         raise SystemExit("--shards is the one-GPU form of the edge-shard path")
-    if a.pipeline and (world > 1 or a.shards > 1):
-        raise SystemExit("--pipeline is a one-GPU, one-shard form")
+    if a.concurrent and (world > 1 or a.shards > 1):
+        raise SystemExit("--concurrent is a one-GPU, one-shard form")
     torch.cuda.set_device(local)
     seed = (a.scale if a.graph == "rmat" else 2010) if a.seed is None else a.seed
     group = None
@@ -229,15 +227,15 @@ def main():
         for cx in ctxs[1:]:
             if tune:
                 cx.set_tuning(**tune)
-    pipe = None   # --pipeline: two contexts on streams of their own, one host thread per step's partition
-    if a.pipeline:
-        pstreams = [torch.cuda.Stream(local) for _ in range(2)]
-        ctxs = [sheep_amd.Context(local, stream=st) for st in pstreams]
+    conc = None   # --concurrent N: N contexts, each running whole steps in a host thread of its own
+    if a.concurrent > 0:
+        cstreams = [torch.cuda.Stream(local) for _ in range(a.concurrent)]
+        ctxs = [sheep_amd.Context(local, stream=st) for st in cstreams]
         for cx in ctxs:
             if tune:
                 cx.set_tuning(**tune)
-        pipe = {"i": 0, "th": [None, None], "err": [], "last": None, "streams": pstreams,
-                "deg": [torch.zeros(vs_cap, dtype=torch.int32, device=dev) for _ in range(2)]}
+        conc = {"streams": cstreams, "last": [None] * a.concurrent,
+                "deg": [torch.zeros(vs_cap, dtype=torch.int32, device=dev) for _ in range(a.concurrent)]}
     deg = torch.zeros(vs_cap, dtype=torch.int32, device=dev)
     subs = [shard[i * shard.shape[0] // a.shards:(i + 1) * shard.shape[0] // a.shards] for i in range(a.shards)]
     stack = [None]
@@ -276,43 +274,7 @@ def main():
         if err:
             raise err[0]
 
-    def pipe_join(j):
-        if pipe["th"][j] is not None:
-            pipe["th"][j].join()
-            pipe["th"][j] = None
-        if pipe["err"]:
-            raise pipe["err"][0]
-
-    def pipe_step():
-        """Step i on context i mod 2: sequence and tree here, kids + partition in a thread that
-        the step two later joins before it reuses the context."""
-        import threading
-        j = pipe["i"] % 2
-        pipe["i"] += 1
-        c, dg = ctxs[j], pipe["deg"][j]
-        pipe_join(j)
-        with torch.cuda.stream(pipe["streams"][j]):
-            dg.zero_()
-        s = sheep_amd.sequence_from_degrees(dg, sheep_amd.degree_count(shard, mode="llama", deg=dg, ctx=c)[1], ctx=c)
-        tree = sheep_amd.build_tree(shard, s, ctx=c)
-        box = {}
-
-        def part():
-            try:
-                kids = sheep_amd.KidTable(tree, c)
-                box["res"] = sheep_amd.partition(s, tree, a.k, kids=kids, ctx=c)
-                kids.close()
-            except Exception as e:                              # (re-raised by the joining step)
-                pipe["err"].append(e)
-        th = threading.Thread(target=part)
-        th.start()
-        pipe["th"][j] = th
-        pipe["last"] = (s, tree, box, c)
-        return s, tree, box
-
     def step():
-        if pipe is not None:
-            return pipe_step()
         deg.zero_()
         if group is not None:                                   # graph2tree -i -r over the world
             t0 = time.perf_counter()
@@ -353,17 +315,46 @@ def main():
                 lap("kids_partition", t0)
         return s, tree, res
 
+    def conc_run(nsteps):
+        """nsteps whole steps, step i on context i mod N, each context's steps in a thread."""
+        import threading
+        N, err = len(ctxs), []
+
+        def worker(j):
+            try:
+                c, dg = ctxs[j], conc["deg"][j]
+                for _ in range(j, nsteps, N):
+                    with torch.cuda.stream(conc["streams"][j]):
+                        dg.zero_()
+                    s_ = sheep_amd.sequence_from_degrees(
+                        dg, sheep_amd.degree_count(shard, mode="llama", deg=dg, ctx=c)[1], ctx=c)
+                    tree_ = sheep_amd.build_tree(shard, s_, ctx=c)
+                    kids = sheep_amd.KidTable(tree_, c)
+                    res_ = sheep_amd.partition(s_, tree_, a.k, kids=kids, ctx=c)
+                    kids.close()
+                    conc["last"][j] = (s_, tree_, res_, c)
+                c.sync()
+            except Exception as e:                              # (re-raised below)
+                err.append(e)
+        th = [threading.Thread(target=worker, args=(j,)) for j in range(N)]
+        for t_ in th:
+            t_.start()
+        for t_ in th:
+            t_.join()
+        if err:
+            raise err[0]
+
     def barrier():
-        if pipe is not None:                                    # the steps' partitions are part of the steps
-            pipe_join(0)
-            pipe_join(1)
         torch.cuda.synchronize()
         ctx.sync()
         if world > 1:
             sdist.barrier()
 
-    for _ in range(a.warmup):
-        step()
+    if conc is not None:
+        conc_run(max(a.warmup, len(ctxs)))                      # every context warmed up
+    else:
+        for _ in range(a.warmup):
+            step()
     barrier()
     for cx in ctxs:
         cx.timing(True)
@@ -371,8 +362,11 @@ def main():
     walls.clear()
     barrier()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        s, tree, res = step()
+    if conc is not None:
+        conc_run(a.steps)
+    else:
+        for _ in range(a.steps):
+            s, tree, res = step()
     barrier()
     t = sdist.max_over_ranks(time.perf_counter() - t0) if world > 1 else time.perf_counter() - t0
     # device memory in use after the timed steps: the library's workspaces only grow and
@@ -391,9 +385,8 @@ def main():
             p["launches"] += launches
             p["alg_bytes"] += nbytes
         cx.timer_reset()
-    if pipe is not None:                                        # the last step's results and context
-        s, tree, box, ctx_last = pipe["last"]
-        res = box["res"]
+    if conc is not None:                                        # context 0's last step
+        s, tree, res, ctx_last = conc["last"][0]
     for cx in ctxs[1:]:
         cx.timing(False)
     per_rank = None
@@ -405,10 +398,10 @@ def main():
 
     evaluator = None
     if a.eval_reps > 0:
-        evaluator = time_evaluator(a, ctx_last if pipe is not None else ctx, group, shard, subs, s, res, rank, world,
+        evaluator = time_evaluator(a, ctx_last if conc is not None else ctx, group, shard, subs, s, res, rank, world,
                                    dev, barrier)
     ctx.timing(False)
-    if pipe is not None:
+    if conc is not None:
         ctxs[0].timing(False)
 
     verified = None
@@ -460,7 +453,7 @@ def main():
                      f"synthetic (Chung-Lu power law, gamma 1.9, {sheep_amd.TWITTER_VERTICES} vertices, seeded")
                     + ", self-loops/duplicates removed"
                     + (", records shuffled and half of them reversed)" if a.shuffle else ", records (tail, head)-sorted)"),
-            "config": {"workload": workload + (", steps pipelined on 2 contexts" if pipe is not None else
+            "config": {"workload": workload + (f", steps on {len(ctxs)} concurrent contexts" if conc is not None else
                                                f", {len(ctxs)} streams" if len(ctxs) > 1 else ""), "records": R,
                        "vertex_slots": s.pos_size,
                        "tree_nodes": n, "k": a.k, "created": res.created, "packing_nodes": res.packing_nodes,
@@ -474,7 +467,7 @@ def main():
             "evaluator": evaluator,
             "phases": phases,
             "hbm_peak_bytes": hbm_used,
-            "hbm_workspace_top": dict(list((ctxs[0] if pipe is not None else ctx).workspace().items())[:12]),
+            "hbm_workspace_top": dict(list((ctxs[0] if conc is not None else ctx).workspace().items())[:12]),
             "hbm_peak_note": "device memory in use after the timed steps (hipMemGetInfo: total - free); the "
                              "library's workspaces only grow, so this is the step's high-water mark",
         }

@@ -857,10 +857,10 @@ def test_shard_maps_on_concurrent_contexts(gpu_ctx):
         c.close()
 
 
-def test_pipelined_steps_on_two_contexts(gpu_ctx):
-    """bench.py --pipeline: step i's kids + partition run in a host thread on one context
-    while step i + 1's degree count, sequence and tree run on the other; every step's
-    sequence, tree and parts equal the one-context results."""
+def test_steps_on_concurrent_contexts(gpu_ctx):
+    """bench.py --concurrent N: whole steps (degree count, sequence, tree, kids, partition) on
+    three contexts of one device at once, each context's steps in a host thread of its own:
+    every step's sequence, tree and parts equal the one-context results."""
     import threading
     import torch
     import sheep_amd
@@ -871,34 +871,33 @@ def test_pipelined_steps_on_two_contexts(gpu_ctx):
     kids = sheep_amd.KidTable(t0)
     want = sheep_amd.partition(s0, t0, k, kids=kids)
     kids.close()
-    streams = [torch.cuda.Stream(0) for _ in range(2)]
+    N = 3
+    streams = [torch.cuda.Stream(0) for _ in range(N)]
     ctxs = [sheep_amd.Context(0, stream=st) for st in streams]
-    degs = [torch.zeros(1 << 18, dtype=torch.int32, device="cuda") for _ in range(2)]
+    degs = [torch.zeros(1 << 18, dtype=torch.int32, device="cuda") for _ in range(N)]
     torch.cuda.synchronize()
-    th, got, err = [None, None], [], []
+    got, err = [], []
 
-    def part(c, s, tree):
+    def worker(j):
         try:
-            kt = sheep_amd.KidTable(tree, c)
-            got.append((s, tree, sheep_amd.partition(s, tree, k, kids=kt, ctx=c)))
-            kt.close()
+            for _ in range(2):
+                with torch.cuda.stream(streams[j]):
+                    degs[j].zero_()
+                ms = sheep_amd.degree_count(d, mode="llama", deg=degs[j], ctx=ctxs[j])[1]
+                s = sheep_amd.sequence_from_degrees(degs[j], ms, ctx=ctxs[j])
+                tree = sheep_amd.build_tree(d, s, ctx=ctxs[j])
+                kt = sheep_amd.KidTable(tree, ctxs[j])
+                got.append((s, tree, sheep_amd.partition(s, tree, k, kids=kt, ctx=ctxs[j])))
+                kt.close()
         except Exception as e:
             err.append(e)
-    for i in range(5):
-        j = i % 2
-        if th[j] is not None:
-            th[j].join()
-        with torch.cuda.stream(streams[j]):
-            degs[j].zero_()
-        ms = sheep_amd.degree_count(d, mode="llama", deg=degs[j], ctx=ctxs[j])[1]
-        s = sheep_amd.sequence_from_degrees(degs[j], ms, ctx=ctxs[j])
-        tree = sheep_amd.build_tree(d, s, ctx=ctxs[j])
-        th[j] = threading.Thread(target=part, args=(ctxs[j], s, tree))
-        th[j].start()
+    th = [threading.Thread(target=worker, args=(j,)) for j in range(N)]
+    for t in th:
+        t.start()
     for t in th:
         t.join()
     assert not err, err
-    assert len(got) == 5
+    assert len(got) == 2 * N
     for s, tree, res in got:
         assert torch.equal(s.seq[: s0.n], s0.seq[: s0.n])
         assert torch.equal(tree, t0)
