@@ -475,7 +475,7 @@ def main():
             out["per_rank"] = per_rank
         out.update(checks)   # verified_vs_whole_graph / verified_vs_pairwise_merges: the checks that ran
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(a, ctx)
+        out["cpu_baseline"] = cpu_baseline(a, ctx, (s, tree, res), seed)
     del shard
     if group is not None:
         sdist.barrier()
@@ -679,7 +679,7 @@ def run_group(cmd, env, timeout):
     return subprocess.CompletedProcess(cmd, p.returncode, out, err)
 
 
-def cpu_baseline(a, ctx):
+def cpu_baseline(a, ctx, gpu=None, seed=None):
     """The reference CPU path on the same workload (RMAT-26 by default), on this host.
 
     kind "reference": the reference's own lib/ code, compiled from /root/reference into
@@ -690,7 +690,10 @@ def cpu_baseline(a, ctx):
     MPI_Reduce), makeKids + Partition(k) + mpi_sync on rank 0.  The timed region starts at
     a barrier after the load.  (P ranks, T OpenMP threads each) runs over --cpu-configs,
     P x T capped by the cores this process may run on (os.sched_getaffinity); the fastest
-    is the value and `cores` = its P x T.  The literal `-ir` is not used: its sort copies
+    is the value and `cores` = its P x T.  When the sample is the bench's own graph, the
+    reference flow's sequence, merged tree and parts (the harness's FNV-1a digests) are
+    compared with the GPU step's (`matches_gpu`): a full-size check against the reference's
+    own code in every bench run.  The literal `-ir` is not used: its sort copies
     the whole degree vector with every comparator copy (sequence.h:85; its box record is
     profiles/r4/cpu_ir_literal.json, tools/cpu_ir.py).  Test infrastructure timed as a baseline; never the measured path."""
     import shutil
@@ -731,12 +734,22 @@ def cpu_baseline(a, ctx):
             res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
             runs.append({"ranks": p, "threads": th, "seconds": round(res["seconds"], 3),
                          "edges_per_s": round(R / res["seconds"], 1),
-                         "phases_s": {k: round(v, 3) for k, v in res.get("phases", {}).items()}})
+                         "phases_s": {k: round(v, 3) for k, v in res.get("phases", {}).items()},
+                         "fnv": res.get("fnv")})
             print(f"cpu_baseline: {p} ranks x {th} threads {res['seconds']:.2f} s", file=sys.stderr, flush=True)
     ok = [x for x in runs if "seconds" in x]
     if not ok:
         return {"value": None, "unit": "edges/s", "cores": 0, "kind": "reference", "sample": f"failed: {runs}"}
     best = min(ok, key=lambda x: x["seconds"])
+    matches = None
+    if gpu is not None and a.graph == "rmat" and sc == a.scale and seed == sc and all(x.get("fnv") for x in ok):
+        import oracle                                            # (the checker: FNV-1a over the GPU's arrays)
+        gs, gtree, gres = gpu
+        mine = {"seq": oracle.fnv1a(sheep_amd.to_numpy_u32(gs.seq[:gs.n])),
+                "tree": oracle.fnv1a(gtree.cpu().numpy()),
+                "parts": oracle.fnv1a(gres.parts.cpu().numpy())}
+        matches = {k: all(x["fnv"][k] == v for x in ok) for k, v in mine.items()}
+        matches["gpu_fnv"] = mine
     return {"value": best["edges_per_s"], "unit": "edges/s", "cores": best["ranks"] * best["threads"],
             "kind": "reference", "cpu_model": model, "host_cpus": ncpu, "usable_cpus": usable,
             "sample": f"RMAT-{sc} ef{a.ef} seed {sc} ({R} records), k={a.k}: reference lib/ graph2tree -r -p flow "
@@ -744,7 +757,7 @@ def cpu_baseline(a, ctx):
                       f"makeKids + Partition + mpi_sync) on P MPI ranks x T OpenMP threads, PxT in "
                       f"{['%dx%d' % c for c in configs]} (best {best['ranks']}x{best['threads']}, "
                       f"{best['seconds']:.2f} s), shards loaded untimed",
-            "phases_s": best["phases_s"], "sweep": runs}
+            "phases_s": best["phases_s"], "sweep": runs, "matches_gpu": matches}
 
 
 if __name__ == "__main__":

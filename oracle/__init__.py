@@ -39,6 +39,8 @@ def lib():
         L.or_evaluate.argtypes = [P, P, U64, P, U64, P, U64, P]
         L.or_facts_text.argtypes = [P, P, U64, P, U64]
         L.or_eval_text.argtypes = [P, ctypes.c_int16, P, U64]
+        L.or_fnv1a.argtypes = [P, U64]
+        L.or_fnv1a.restype = U64
         _lib = L
     return _lib
 
@@ -54,6 +56,12 @@ def _u32(a):
 
 def _p(a):
     return a.ctypes.data
+
+
+def fnv1a(a) -> str:
+    """FNV-1a of an array's bytes as 16 hex digits (oracle/ref/ref_harness's digests)."""
+    a = np.ascontiguousarray(a)
+    return "%016x" % lib().or_fnv1a(_p(a), a.nbytes)
 
 
 def set_threads(n: int):

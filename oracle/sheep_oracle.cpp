@@ -738,6 +738,14 @@ static thread_local std::string g_err;
 extern "C" {
 const char *or_last_error() { return g_err.c_str(); }
 
+// FNV-1a over n bytes: the digest oracle/ref/ref_harness prints of the reference flow's
+// sequence, merged tree and parts, so a GPU result can be compared with it.
+uint64_t or_fnv1a(const unsigned char *p, uint64_t n) {
+  uint64_t h = 1469598103934665603ull;
+  for (uint64_t i = 0; i < n; ++i) h = (h ^ p[i]) * 1099511628211ull;
+  return h;
+}
+
 // OpenMP threads for the graph build and the evaluators (default 1; tests raise it for
 // BASELINE-size parity checks).
 void or_set_threads(int n) { omp_set_num_threads(n < 1 ? 1 : n); }

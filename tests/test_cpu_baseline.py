@@ -47,3 +47,26 @@ def test_literal_ir_matches_by_reference_and_golden(name, k):
             got = _run(mode, path, k, p)["fnv"]
             for key, v in want.items():
                 assert got[key] == v, (mode, p, key)
+
+
+def test_reference_flow_on_rmat_matches_the_restatement(tmp_path):
+    """The reference flow (2 MPI ranks) on an RMAT-14 graph gives the oracle restatement's
+    sequence, tree and parts (k = 8), compared through the harness's FNV-1a digests — the
+    digests bench.py's cpu_baseline compares with the GPU's results (`matches_gpu`); and
+    oracle.fnv1a is that digest."""
+    import oracle
+    import sheep_amd
+    b = np.random.default_rng(3).integers(0, 256, 1000, dtype=np.uint8)
+    assert oracle.fnv1a(b) == _fnv(b.tobytes())
+    r = sheep_amd.rmat_host(14, 16, 14).astype(np.uint32)
+    path = str(tmp_path / "r14.dat")
+    r.tofile(path)
+    got = _run("mpi", path, 8, 2)["fnv"]
+    t, h = r[:, 0], r[:, 1]
+    seq = oracle.sequence(t, h)
+    p, w = oracle.build_tree(t, h, seq)
+    tw = np.empty(2 * len(p), np.uint32)
+    tw[0::2], tw[1::2] = p, w
+    parts, _ = oracle.partition(p, w, seq, 8)
+    assert got == {"seq": oracle.fnv1a(seq.astype(np.uint32)), "tree": oracle.fnv1a(tw),
+                   "parts": oracle.fnv1a(np.asarray(parts, np.int16))}
