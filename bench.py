@@ -81,6 +81,9 @@ def parse():
                     help="one GPU: also time the record evaluator (sheep_evaluate) beside the step-edge one")
     ap.add_argument("--cpu-scale", type=int, default=None,
                     help="RMAT scale of the CPU-baseline sample (default: the bench's own RMAT scale up to 26, else 22)")
+    ap.add_argument("--cpu-same-graph", action="store_true",
+                    help="run the CPU baseline on the bench's own records (any graph or scale; C4, C5) instead of "
+                         "an RMAT sample, so `matches_gpu` compares the reference's results with this run's")
     ap.add_argument("--cpu-configs", nargs="+", default=["8x1", "16x1"],
                     help="PxT configurations of the reference CPU baseline: P MPI ranks x T OpenMP threads each "
                          "(the threads serve the reference's __gnu_parallel::sort, sequence.h:55,85); P x T is capped "
@@ -475,7 +478,7 @@ def main():
             out["per_rank"] = per_rank
         out.update(checks)   # verified_vs_whole_graph / verified_vs_pairwise_merges: the checks that ran
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(a, ctx, (s, tree, res), seed)
+        out["cpu_baseline"] = cpu_baseline(a, ctx, (s, tree, res), seed, shard)
     del shard
     if group is not None:
         sdist.barrier()
@@ -679,7 +682,7 @@ def run_group(cmd, env, timeout):
     return subprocess.CompletedProcess(cmd, p.returncode, out, err)
 
 
-def cpu_baseline(a, ctx, gpu=None, seed=None):
+def cpu_baseline(a, ctx, gpu=None, seed=None, records=None):
     """The reference CPU path on the same workload (RMAT-26 by default), on this host.
 
     kind "reference": the reference's own lib/ code, compiled from /root/reference into
@@ -715,9 +718,10 @@ def cpu_baseline(a, ctx, gpu=None, seed=None):
         if (p, t) not in configs:
             configs.append((p, t))
     runs = []
+    same = a.cpu_same_graph and records is not None
     with tempfile.TemporaryDirectory(dir="/tmp") as td:
-        path = os.path.join(td, f"rmat{sc}.dat")
-        d = sheep_amd.rmat(sc, a.ef, sc, ctx=ctx)
+        path = os.path.join(td, "same.dat" if same else f"rmat{sc}.dat")
+        d = records if same else sheep_amd.rmat(sc, a.ef, sc, ctx=ctx)
         R = d.shape[0]
         with open(path, "wb") as f:                               # XS1 records, streamed in chunks
             step = 1 << 26
@@ -742,7 +746,8 @@ def cpu_baseline(a, ctx, gpu=None, seed=None):
         return {"value": None, "unit": "edges/s", "cores": 0, "kind": "reference", "sample": f"failed: {runs}"}
     best = min(ok, key=lambda x: x["seconds"])
     matches = None
-    if gpu is not None and a.graph == "rmat" and sc == a.scale and seed == sc and all(x.get("fnv") for x in ok):
+    if gpu is not None and (same or (a.graph == "rmat" and sc == a.scale and seed == sc)) and \
+            all(x.get("fnv") for x in ok):
         import oracle                                            # (the checker: FNV-1a over the GPU's arrays)
         gs, gtree, gres = gpu
         mine = {"seq": oracle.fnv1a(sheep_amd.to_numpy_u32(gs.seq[:gs.n])),
@@ -752,7 +757,8 @@ def cpu_baseline(a, ctx, gpu=None, seed=None):
         matches["gpu_fnv"] = mine
     return {"value": best["edges_per_s"], "unit": "edges/s", "cores": best["ranks"] * best["threads"],
             "kind": "reference", "cpu_model": model, "host_cpus": ncpu, "usable_cpus": usable,
-            "sample": f"RMAT-{sc} ef{a.ef} seed {sc} ({R} records), k={a.k}: reference lib/ graph2tree -r -p flow "
+            "sample": (f"the bench's own records ({R})" if same else f"RMAT-{sc} ef{a.ef} seed {sc} ({R} records)")
+                      + f", k={a.k}: reference lib/ graph2tree -r -p flow "
                       f"(mpiSequence all-reduce + degreeSequence sort, JTree per shard, JNodeTable::mpi_merge, "
                       f"makeKids + Partition + mpi_sync) on P MPI ranks x T OpenMP threads, PxT in "
                       f"{['%dx%d' % c for c in configs]} (best {best['ranks']}x{best['threads']}, "
